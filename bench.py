@@ -1,0 +1,290 @@
+#!/usr/bin/env python3
+"""bench.py -- PhysGaussian simulate+render loop (lego.json, 128^3) on MI355X.
+
+One bench *step* = one lego frame exactly as main.py runs it (main.py:303-326):
+steps_per_frame (= 100) MPM substeps, postprocess (cov/R), fused
+grid2world + render-space transform, and the rasterizer forward of the frame
+(800x800, SH degree 3).  PNG encoding is host I/O and not timed.
+
+Workload (BASELINE.json configs[1]): lego.json, 100k synthetic lego-like
+Gaussians (the lego PLY in the reference is a git-LFS pointer),
+n_grid 128 (--n_grid override), jelly as written.
+
+    python bench.py [--gpus N --steps K --warmup W]
+
+Multi-GPU (torch.distributed.run, one rank per GPU): spatial-slab weak
+scaling through gsmpm.dist (each rank owns one lego-sized slab of a grid
+stacked along x; halo planes exchanged over RCCL every substep).
+
+Prints ONE JSON line (rank 0).  value = particle-substeps/s over all ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "gaussian-splatting-mpm_amd")
+sys.path.insert(0, PKG)
+
+METRIC = "MPM substeps/sec (and particles·steps/sec) + rendered fps, lego 128³ grid"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--particles", type=int, default=100_000)
+    ap.add_argument("--n_grid", type=int, default=128)
+    ap.add_argument("--config", default="lego.json")
+    ap.add_argument("--material", default=None, help="override (e.g. metal) -- not the headline config")
+    ap.add_argument("--no-render", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    return ap.parse_args()
+
+
+def build_scene(args, dev, rank=0):
+    import torch
+    from arguments import MPMParams, ModelParams, RenderParams
+    from argparse import ArgumentParser
+    from gaussian_splatting.scene import GaussianModel
+    from internel_filling.filling import get_particle_volume
+    from utils.transform_utils import get_center_view_worldspace_and_observant_coordinate, world2grid
+    import main as drv
+
+    with open(os.path.join(PKG, "configs", args.config)) as f:
+        cfg = json.load(f)
+    parser = ArgumentParser()
+    mp, sp, rp = ModelParams(parser, cfg["model"]), MPMParams(parser, cfg["mpm"]), RenderParams(parser, cfg["render"])
+    cli = ["--n_grid", str(args.n_grid)] + (["--material", args.material] if args.material else [])
+    a = parser.parse_args(cli)
+    margs, sargs, rargs = mp.extract(a), sp.extract(a), rp.extract(a)
+    g = GaussianModel(3, device=dev).init_synthetic(args.particles, seed=rank)
+    bound = torch.tensor(sargs.sim_area, device=dev)
+    xyz = g.get_xyz
+    mask = torch.logical_and((xyz <= bound[1]).all(1), (xyz >= bound[0]).all(1))
+    means = xyz[mask]
+    covs = g.get_covariance()[mask]
+    xg, c, s = world2grid(means, sargs)
+    vols = get_particle_volume(xg, sargs)
+    center_w, obs = get_center_view_worldspace_and_observant_coordinate(
+        torch.tensor([[0.5, 0.5, 0.5]], device=dev), torch.tensor([[0, 0, 1]], device=dev), [], s, c)
+    margs.model_path = "/nonexistent"  # -> lego camera 0 record (800x800, fx 1111.11)
+    cam = drv.modify_cam(drv.load_cameras(margs)[0], center_w, obs, device=dev)
+    cam.toCuda(dev)
+    return dict(g=g, mask=mask, xg=xg, covs=covs * (s * s), vols=vols, c=c, s=s, cam=cam, sargs=sargs, rargs=rargs)
+
+
+def make_sim(scene, dev, use_graph=True):
+    from gsmpm.bc import BCSpec
+    from gsmpm.sim import Simulator
+    sa = scene["sargs"]
+    n = scene["xg"].shape[0]
+    sim = Simulator(n, n_grid=sa.n_grid, grid_extent=sa.grid_extent, material=sa.material, E=sa.E, nu=sa.nu,
+                    density=sa.density, gravity=sa.gravity, jelly_fcr=sa.jelly_fcr, use_graph=use_graph, device=dev)
+    sim.set_particles(scene["xg"], scene["covs"], scene["vols"])
+    specs = []
+    for d in sa.boundary_conditions:
+        end = d["start_time"] + sa.substep_dt * d["num_dt"]
+        if d["type"] == "fixed_cube":
+            specs.append(BCSpec("fixed_cube", sim.add_fixed_cube(d["center"], d["size"]), d["start_time"], end))
+        elif d["type"] == "impulse":
+            specs.append(BCSpec("impulse", sim.add_impulse(d["center"], d["size"], d["force"], sa.substep_dt),
+                                d["start_time"], end))
+    specs.append(BCSpec("collider", sim.add_plane_collider((0.0, 0.0, 0.4), (0.0, 0.0, 1.0), 0.0)))
+    return sim, specs
+
+
+def algorithmic_bytes(n, live_nodes, material):
+    """Per-launch algorithmic bytes of the three fused kernels."""
+    stress = material != "jelly"
+    p2g = n * (64 + (48 + 40 if stress else 0)) + 16 * live_nodes
+    grid = 48 * live_nodes
+    g2p = n * 144 + 16 * live_nodes
+    return {"k_p2g": p2g, "k_grid": grid, "k_g2p": g2p}
+
+
+def cpu_baseline(scene, args, budget_s):
+    """The CPU oracle (scalar C restatement, 1 thread) on a bounded sample of
+    the same workload: as many lego substeps at N particles / 128^3 as fit in
+    ~budget_s, timed on this host."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+    import oracle as O  # cpu_baseline leg only
+    sa = scene["sargs"]
+    x = scene["xg"].cpu().numpy()
+    sim = O.OracleMPM(x, scene["covs"].cpu().numpy(), scene["vols"].cpu().numpy(), n_grid=sa.n_grid,
+                      grid_extent=sa.grid_extent, material=sa.material, E=sa.E, nu=sa.nu, density=sa.density,
+                      gravity=sa.gravity, jelly_quirk=not sa.jelly_fcr)
+    ops = []
+    for d in sa.boundary_conditions:
+        if d["type"] == "fixed_cube":
+            sim.add_fixed_box(d["center"], d["size"])
+            ops.append((d["start_time"], d["start_time"] + sa.substep_dt * d["num_dt"]))
+    sim.add_collider([0.0, 0.0, 0.4], [0.0, 0.0, 1.0])
+    ops.append(None)
+    t, n_done = 0.0, 0
+    t0 = time.perf_counter()
+    while True:
+        oa = [1 if o is None else int(o[0] <= t < o[1]) for o in ops]
+        sim.substep(sa.substep_dt, None, oa)
+        t += sa.substep_dt
+        n_done += 1
+        el = time.perf_counter() - t0
+        if el > budget_s or n_done >= 2000:
+            break
+    return {"value": n_done * x.shape[0] / el, "unit": "particle-substeps/s", "cores": 1, "kind": "port",
+            "sample": f"{n_done} lego substeps of the same workload ({x.shape[0]} particles, {sa.n_grid}^3), "
+                      f"scalar C oracle (oracle/mpm_oracle.c), {el:.1f}s",
+            "substeps_per_s": n_done / el}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from gsmpm import raster
+    from gsmpm.bc import substep_masks
+
+    scene = build_scene(args, dev, rank=0)
+    sa = scene["sargs"]
+    dt, spf = sa.substep_dt, sa.steps_per_frame
+    if world > 1:
+        from gsmpm.dist import SlabSimulator
+        sim = SlabSimulator.from_scene(scene, dev, rank, world)
+        specs = sim.specs
+    else:
+        sim, specs = make_sim(scene, dev)
+    n_local = sim.n
+    g, mask, cam = scene["g"], scene["mask"], scene["cam"]
+    feats = g.get_features[mask].contiguous()
+    opac = g.get_opacity[mask].reshape(-1).contiguous()
+    bg = torch.zeros(3, device=dev)
+    tanx, tany = math.tan(cam.FovX * 0.5), math.tan(cam.FovY * 0.5)
+    state = {"t": 0.0, "K": 0}
+
+    def frame(render=True):
+        masks, state["t"] = substep_masks(specs, state["t"], dt, spf)
+        sim.step(dt, masks)
+        sim.postprocess()
+        if render and not args.no_render:
+            means_r, covs_r = sim.world_outputs(scene["s"], scene["c"].tolist(), render_space=True)
+            if world > 1:
+                means_r, covs_r, fe, op = sim.gather_for_render(means_r, covs_r, feats, opac)
+            else:
+                fe, op = feats, opac
+            if rank == 0:
+                K, _, _ = raster.forward(means_r, op, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg,
+                                         cam.height, cam.width, tanx, tany, sh_degree=3, shs=fe,
+                                         cov3D_precomp=covs_r)
+                state["K"] = K
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        frame()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        frame()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        nt = torch.tensor([n_local], device=dev, dtype=torch.float64)
+        dist.all_reduce(nt)
+        n_total = int(nt.item())
+    else:
+        n_total = n_local
+
+    # ---- breakdown (untimed by the contract; measured on the same stream) ----
+    ev = lambda: torch.cuda.Event(enable_timing=True)
+    e0, e1 = ev(), ev()
+    masks, t_after = substep_masks(specs, state["t"], dt, spf)
+    e0.record()
+    sim.step(dt, masks)
+    e1.record()
+    barrier()
+    sim_ms = e0.elapsed_time(e1)
+    state["t"] = t_after
+    render_ms = None
+    if not args.no_render and rank == 0 and world == 1:
+        means_r, covs_r = sim.world_outputs(scene["s"], scene["c"].tolist(), render_space=True)
+        torch.cuda.synchronize()
+        r0 = time.perf_counter()
+        for _ in range(5):
+            raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg, cam.height, cam.width,
+                           tanx, tany, sh_degree=3, shs=feats, cov3D_precomp=covs_r)
+        torch.cuda.synchronize()
+        render_ms = (time.perf_counter() - r0) / 5 * 1e3
+    kern = None
+    if world == 1:
+        masks, state["t"] = substep_masks(specs, state["t"], dt, spf)
+        lo, hi = sim.live_box()
+        live = max(0, hi[0] - lo[0] + 1) * max(0, hi[1] - lo[1] + 1) * max(0, hi[2] - lo[2] + 1)
+        kms = sim.profile(dt, masks)
+        kern = {k: kms[i] / spf for i, k in enumerate(("k_p2g", "k_grid", "k_g2p"))}
+        abytes = algorithmic_bytes(n_local, live, sa.material)
+
+    out = {
+        "metric": METRIC,
+        "value": n_total * spf * args.steps / elapsed,
+        "unit": "particle-substeps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (lego-like Gaussians, seed 0; lego PLY is an LFS pointer in the reference)",
+        "config": {"workload": f"{args.config} frame: {spf} substeps + postprocess + render "
+                               f"{cam.width}x{cam.height} SH3", "particles_per_gpu": n_local,
+                   "particles_total": n_total, "n_grid": sa.n_grid, "material": sa.material,
+                   "substep_dt": dt, "parallelism": f"slab{world}" if world > 1 else "single"},
+        "substeps_per_s": spf * args.steps / elapsed,
+        "frames_per_s": args.steps / elapsed,
+        "sim_ms_per_frame": sim_ms,
+        "sim_substeps_per_s": spf / (sim_ms / 1e3),
+        "render_ms_per_frame": render_ms,
+        "num_rendered": state["K"],
+    }
+    if kern is not None:
+        dom = max(kern, key=kern.get)
+        ach = abytes[dom] / (kern[dom] * 1e-3) / 1e9
+        out["kernels_ms_per_launch"] = {k: round(v, 5) for k, v in kern.items()}
+        out["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                           "algorithmic_bytes_per_launch": abytes[dom], "live_nodes": live}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(scene, args, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,493 @@
+// raster.hip -- 3D Gaussian splatting forward for MI355X (gfx950).
+//
+// Drop-in for diff_gaussian_rasterization._C.rasterize_gaussians (forward), the
+// third-party CUDA extension the reference calls at main.py:148-156 (pre-2024
+// API: returns color [3,H,W] and radii [P]).  Pipeline:
+//
+//   k_preprocess   one lane per Gaussian: frustum test (view z > 0.2), EWA 2D
+//                  covariance (+0.3 low-pass), conic, 3-sigma radius, 16x16
+//                  tile rect, SH(deg<=3) -> RGB, depth, tiles touched
+//   scan           inclusive sum of tiles touched (rocPRIM), one D2H of K
+//   k_duplicate    emit (tile<<32 | depth bits, idx) per touched tile
+//   sort           stable LSD radix sort over 32 + msb(#tiles) key bits
+//   k_ranges       per-tile [start, end) in the sorted list
+//   k_render       one 256-lane workgroup (4 wave64) per 16x16 tile; batches of
+//                  256 Gaussians staged in LDS (xy, conic/opacity, rgb) and
+//                  front-to-back alpha blending with the upstream cut-offs
+//                  (alpha < 1/255 skip, alpha <= 0.99, T < 1e-4 stop), block
+//                  early exit via __syncthreads_count.
+#include <hip/hip_runtime.h>
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include <cstring>
+#include <string>
+
+#include "common.h"
+
+namespace gsmpm {
+
+constexpr int kBX = 16, kBY = 16, kBlock = kBX * kBY;
+
+__constant__ float kSH_C0 = 0.28209479177387814f;
+__constant__ float kSH_C1 = 0.4886025119029199f;
+__constant__ float kSH_C2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f, -1.0925484305920792f,
+                                0.5462742152960396f};
+__constant__ float kSH_C3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f, 0.3731763325901154f,
+                                -0.4570457994644658f, 1.445305721320277f, -0.5900435899266435f};
+
+struct RasterDev {
+  int P, D, M, W, H;
+  const float *means3D, *shs, *colors_precomp, *opacities, *scales, *rotations, *cov3D_precomp;
+  float scale_modifier;
+  const float *viewmatrix, *projmatrix, *campos, *bg;
+  float tanfovx, tanfovy, focal_x, focal_y;
+  int grid_x, grid_y;
+};
+
+__device__ __forceinline__ void xform4x3(const float* p, const float* m, float o[3]) {
+  o[0] = m[0] * p[0] + m[4] * p[1] + m[8] * p[2] + m[12];
+  o[1] = m[1] * p[0] + m[5] * p[1] + m[9] * p[2] + m[13];
+  o[2] = m[2] * p[0] + m[6] * p[1] + m[10] * p[2] + m[14];
+}
+
+__device__ __forceinline__ float ndc2pix(float v, int S) { return ((v + 1.0f) * S - 1.0f) * 0.5f; }
+
+__device__ __forceinline__ void get_rect(float px, float py, int r, int gx, int gy, int rmin[2], int rmax[2]) {
+  rmin[0] = min(gx, max(0, (int)((px - r) / kBX)));
+  rmin[1] = min(gy, max(0, (int)((py - r) / kBY)));
+  rmax[0] = min(gx, max(0, (int)((px + r + kBX - 1) / kBX)));
+  rmax[1] = min(gy, max(0, (int)((py + r + kBY - 1) / kBY)));
+}
+
+// computeCov3D: Sigma = R diag(s*mod)^2 R^T, R from the (unnormalised) quaternion (r,x,y,z)
+__device__ __forceinline__ void cov3d_from_sr(const float* s, float mod, const float* rot, float c6[6]) {
+  const float S0 = mod * s[0], S1 = mod * s[1], S2 = mod * s[2];
+  const float r = rot[0], x = rot[1], y = rot[2], z = rot[3];
+  const float R[3][3] = {{1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y)},
+                         {2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x)},
+                         {2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y)}};
+  float M[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    M[i][0] = R[i][0] * S0;
+    M[i][1] = R[i][1] * S1;
+    M[i][2] = R[i][2] * S2;
+  }
+  float Sg[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) Sg[i][j] = M[i][0] * M[j][0] + M[i][1] * M[j][1] + M[i][2] * M[j][2];
+  c6[0] = Sg[0][0];
+  c6[1] = Sg[0][1];
+  c6[2] = Sg[0][2];
+  c6[3] = Sg[1][1];
+  c6[4] = Sg[1][2];
+  c6[5] = Sg[2][2];
+}
+
+// computeCov2D: EWA projection J W Vrk W^T J^T with the 1.3 x fov clamp and +0.3 low-pass
+__device__ __forceinline__ void cov2d(const float* mean, const RasterDev& a, const float* c3, float out[3]) {
+  float t[3];
+  xform4x3(mean, a.viewmatrix, t);
+  const float limx = 1.3f * a.tanfovx, limy = 1.3f * a.tanfovy;
+  const float txtz = t[0] / t[2], tytz = t[1] / t[2];
+  t[0] = fminf(limx, fmaxf(-limx, txtz)) * t[2];
+  t[1] = fminf(limy, fmaxf(-limy, tytz)) * t[2];
+  const float J00 = a.focal_x / t[2], J02 = -(a.focal_x * t[0]) / (t[2] * t[2]);
+  const float J11 = a.focal_y / t[2], J12 = -(a.focal_y * t[1]) / (t[2] * t[2]);
+  const float* vm = a.viewmatrix;
+  const float W[3][3] = {{vm[0], vm[4], vm[8]}, {vm[1], vm[5], vm[9]}, {vm[2], vm[6], vm[10]}};
+  float T[2][3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    T[0][c] = J00 * W[0][c] + J02 * W[2][c];
+    T[1][c] = J11 * W[1][c] + J12 * W[2][c];
+  }
+  const float V[3][3] = {{c3[0], c3[1], c3[2]}, {c3[1], c3[3], c3[4]}, {c3[2], c3[4], c3[5]}};
+  float TV[2][3];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) TV[r][c] = T[r][0] * V[0][c] + T[r][1] * V[1][c] + T[r][2] * V[2][c];
+  const float ca = TV[0][0] * T[0][0] + TV[0][1] * T[0][1] + TV[0][2] * T[0][2];
+  const float cb = TV[0][0] * T[1][0] + TV[0][1] * T[1][1] + TV[0][2] * T[1][2];
+  const float cc = TV[1][0] * T[1][0] + TV[1][1] * T[1][1] + TV[1][2] * T[1][2];
+  out[0] = ca + 0.3f;
+  out[1] = cb;
+  out[2] = cc + 0.3f;
+}
+
+__device__ __forceinline__ void sh_rgb(const RasterDev& a, int idx, const float* pos, float rgb[3]) {
+  float dir[3] = {pos[0] - a.campos[0], pos[1] - a.campos[1], pos[2] - a.campos[2]};
+  const float len = sqrtf(dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2]);
+  dir[0] /= len;
+  dir[1] /= len;
+  dir[2] /= len;
+  const float* sh = a.shs + (size_t)idx * a.M * 3;
+  const float x = dir[0], y = dir[1], z = dir[2];
+  const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    float r = kSH_C0 * sh[0 * 3 + ch];
+    if (a.D > 0) {
+      r = r - kSH_C1 * y * sh[1 * 3 + ch] + kSH_C1 * z * sh[2 * 3 + ch] - kSH_C1 * x * sh[3 * 3 + ch];
+      if (a.D > 1) {
+        r = r + kSH_C2[0] * xy * sh[4 * 3 + ch] + kSH_C2[1] * yz * sh[5 * 3 + ch] +
+            kSH_C2[2] * (2.0f * zz - xx - yy) * sh[6 * 3 + ch] + kSH_C2[3] * xz * sh[7 * 3 + ch] +
+            kSH_C2[4] * (xx - yy) * sh[8 * 3 + ch];
+        if (a.D > 2) {
+          r = r + kSH_C3[0] * y * (3.0f * xx - yy) * sh[9 * 3 + ch] + kSH_C3[1] * xy * z * sh[10 * 3 + ch] +
+              kSH_C3[2] * y * (4.0f * zz - xx - yy) * sh[11 * 3 + ch] +
+              kSH_C3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * sh[12 * 3 + ch] +
+              kSH_C3[4] * x * (4.0f * zz - xx - yy) * sh[13 * 3 + ch] + kSH_C3[5] * z * (xx - yy) * sh[14 * 3 + ch] +
+              kSH_C3[6] * x * (xx - 3.0f * yy) * sh[15 * 3 + ch];
+        }
+      }
+    }
+    r += 0.5f;
+    rgb[ch] = fmaxf(r, 0.0f);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_preprocess(RasterDev a, int* __restrict__ radii, float* __restrict__ depth,
+                                                    float2* __restrict__ xy, float4* __restrict__ conic_o,
+                                                    float4* __restrict__ rgbo, unsigned* __restrict__ tiles) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= a.P) return;
+  radii[idx] = 0;
+  tiles[idx] = 0;
+  const float* p = a.means3D + (size_t)idx * 3;
+  float pv[3];
+  xform4x3(p, a.viewmatrix, pv);
+  if (pv[2] <= 0.2f) return;
+  const float* pm = a.projmatrix;
+  const float hx = pm[0] * p[0] + pm[4] * p[1] + pm[8] * p[2] + pm[12];
+  const float hy = pm[1] * p[0] + pm[5] * p[1] + pm[9] * p[2] + pm[13];
+  const float hw = pm[3] * p[0] + pm[7] * p[1] + pm[11] * p[2] + pm[15];
+  const float pw = 1.0f / (hw + 0.0000001f);
+  const float ppx = hx * pw, ppy = hy * pw;
+  float c6[6];
+  const float* c3;
+  if (a.cov3D_precomp) {
+    c3 = a.cov3D_precomp + (size_t)idx * 6;
+  } else {
+    cov3d_from_sr(a.scales + (size_t)idx * 3, a.scale_modifier, a.rotations + (size_t)idx * 4, c6);
+    c3 = c6;
+  }
+  float cv[3];
+  cov2d(p, a, c3, cv);
+  const float det = cv[0] * cv[2] - cv[1] * cv[1];
+  if (det == 0.0f) return;
+  const float di = 1.f / det;
+  const float mid = 0.5f * (cv[0] + cv[2]);
+  const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+  const float l2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+  const int rad = (int)ceilf(3.f * sqrtf(fmaxf(l1, l2)));
+  const float px = ndc2pix(ppx, a.W), py = ndc2pix(ppy, a.H);
+  int rmin[2], rmax[2];
+  get_rect(px, py, rad, a.grid_x, a.grid_y, rmin, rmax);
+  if ((rmax[0] - rmin[0]) * (rmax[1] - rmin[1]) == 0) return;
+  float rgb[3];
+  if (a.colors_precomp) {
+    rgb[0] = a.colors_precomp[(size_t)idx * 3 + 0];
+    rgb[1] = a.colors_precomp[(size_t)idx * 3 + 1];
+    rgb[2] = a.colors_precomp[(size_t)idx * 3 + 2];
+  } else {
+    sh_rgb(a, idx, p, rgb);
+  }
+  depth[idx] = pv[2];
+  radii[idx] = rad;
+  xy[idx] = make_float2(px, py);
+  conic_o[idx] = make_float4(cv[2] * di, -cv[1] * di, cv[0] * di, a.opacities[idx]);
+  rgbo[idx] = make_float4(rgb[0], rgb[1], rgb[2], 0.f);
+  tiles[idx] = (unsigned)((rmax[1] - rmin[1]) * (rmax[0] - rmin[0]));
+}
+
+__global__ __launch_bounds__(256) void k_duplicate(int P, const float2* __restrict__ xy, const float* __restrict__ depth,
+                                                   const unsigned* __restrict__ offsets, const int* __restrict__ radii,
+                                                   int gx, int gy, unsigned long long* __restrict__ keys,
+                                                   unsigned* __restrict__ vals) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= P || radii[idx] <= 0) return;
+  unsigned off = idx == 0 ? 0u : offsets[idx - 1];
+  int rmin[2], rmax[2];
+  get_rect(xy[idx].x, xy[idx].y, radii[idx], gx, gy, rmin, rmax);
+  const unsigned dbits = __float_as_uint(depth[idx]);
+  for (int y = rmin[1]; y < rmax[1]; ++y)
+    for (int x = rmin[0]; x < rmax[0]; ++x) {
+      keys[off] = ((unsigned long long)(unsigned)(y * gx + x) << 32) | dbits;
+      vals[off] = (unsigned)idx;
+      ++off;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_ranges(int L, const unsigned long long* __restrict__ keys,
+                                                uint2* __restrict__ ranges) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= L) return;
+  const unsigned cur = (unsigned)(keys[idx] >> 32);
+  if (idx == 0) {
+    ranges[cur].x = 0;
+  } else {
+    const unsigned prev = (unsigned)(keys[idx - 1] >> 32);
+    if (cur != prev) {
+      ranges[prev].y = idx;
+      ranges[cur].x = idx;
+    }
+  }
+  if (idx == L - 1) ranges[cur].y = L;
+}
+
+__global__ __launch_bounds__(kBlock) void k_render(const uint2* __restrict__ ranges, const unsigned* __restrict__ list,
+                                                   int W, int H, int gx, const float2* __restrict__ xy,
+                                                   const float4* __restrict__ conic_o, const float4* __restrict__ rgbo,
+                                                   const float* __restrict__ bg, float* __restrict__ out) {
+  __shared__ float2 s_xy[kBlock];
+  __shared__ float4 s_co[kBlock];
+  __shared__ float4 s_rgb[kBlock];
+  const int tx = threadIdx.x % kBX, ty = threadIdx.x / kBX;
+  const int px = blockIdx.x * kBX + tx, py = blockIdx.y * kBY + ty;
+  const bool inside = px < W && py < H;
+  bool done = !inside;
+  const uint2 range = ranges[blockIdx.y * gx + blockIdx.x];
+  const int rounds = (int)((range.y - range.x + kBlock - 1) / kBlock);
+  int todo = (int)(range.y - range.x);
+  const float pfx = (float)px, pfy = (float)py;
+  float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f;
+  for (int i = 0; i < rounds; ++i, todo -= kBlock) {
+    if (__syncthreads_count(done) == kBlock) break;
+    const int prog = i * kBlock + threadIdx.x;
+    if ((int)range.x + prog < (int)range.y) {
+      const unsigned id = list[range.x + prog];
+      s_xy[threadIdx.x] = xy[id];
+      s_co[threadIdx.x] = conic_o[id];
+      s_rgb[threadIdx.x] = rgbo[id];
+    }
+    __syncthreads();
+    const int nb = min(kBlock, todo);
+    for (int j = 0; !done && j < nb; ++j) {
+      const float2 g = s_xy[j];
+      const float dx = g.x - pfx, dy = g.y - pfy;
+      const float4 co = s_co[j];
+      const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+      if (power > 0.0f) continue;
+      const float alpha = fminf(0.99f, co.w * expf(power));
+      if (alpha < 1.0f / 255.0f) continue;
+      const float test_T = T * (1 - alpha);
+      if (test_T < 0.0001f) {
+        done = true;
+        continue;
+      }
+      const float4 c = s_rgb[j];
+      C0 += c.x * alpha * T;
+      C1 += c.y * alpha * T;
+      C2 += c.z * alpha * T;
+      T = test_T;
+    }
+  }
+  if (inside) {
+    const size_t pix = (size_t)py * W + px, HW = (size_t)H * W;
+    out[pix] = C0 + T * bg[0];
+    out[HW + pix] = C1 + T * bg[1];
+    out[2 * HW + pix] = C2 + T * bg[2];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_mark_visible(const float* __restrict__ m, int P, const float* __restrict__ vm,
+                                                      uint8_t* __restrict__ vis) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= P) return;
+  float pv[3];
+  xform4x3(m + (size_t)idx * 3, vm, pv);
+  vis[idx] = pv[2] > 0.2f ? 1 : 0;
+}
+
+static int msb_bits(unsigned n) {
+  int b = 0;
+  while (n > 0) {
+    ++b;
+    n >>= 1;
+  }
+  return b;
+}
+
+}  // namespace gsmpm
+
+using namespace gsmpm;
+
+struct gsmpm_raster {
+  // per-Gaussian buffers
+  size_t capP = 0;
+  int* radii_tmp = nullptr;
+  float* depth = nullptr;
+  float2* xy = nullptr;
+  float4* conic = nullptr;
+  float4* rgb = nullptr;
+  unsigned* tiles = nullptr;
+  unsigned* offsets = nullptr;
+  void* scan_tmp = nullptr;
+  size_t scan_tmp_bytes = 0;
+  // binning buffers
+  size_t capK = 0;
+  unsigned long long *keys = nullptr, *keys_sorted = nullptr;
+  unsigned *vals = nullptr, *vals_sorted = nullptr;
+  void* sort_tmp = nullptr;
+  size_t sort_tmp_bytes = 0;
+  // tile ranges
+  size_t capT = 0;
+  uint2* ranges = nullptr;
+  unsigned* h_count = nullptr;  // pinned
+};
+
+static int grow(void** p, size_t bytes) {
+  if (*p) hipFree(*p);
+  *p = nullptr;
+  GSMPM_HIP(hipMalloc(p, bytes ? bytes : 16));
+  return GSMPM_OK;
+}
+
+extern "C" {
+
+int gsmpm_raster_create(gsmpm_raster** out) {
+  GSMPM_REQUIRE(out, "gsmpm_raster_create: null argument");
+  auto* r = new gsmpm_raster();
+  hipError_t e = hipHostMalloc((void**)&r->h_count, sizeof(unsigned));
+  if (e != hipSuccess) {
+    delete r;
+    set_error(std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    return GSMPM_EHIP;
+  }
+  *out = r;
+  return GSMPM_OK;
+}
+
+int gsmpm_raster_destroy(gsmpm_raster* r) {
+  if (!r) return GSMPM_OK;
+  for (void* p : {(void*)r->radii_tmp, (void*)r->depth, (void*)r->xy, (void*)r->conic, (void*)r->rgb, (void*)r->tiles,
+                  (void*)r->offsets, r->scan_tmp, (void*)r->keys, (void*)r->keys_sorted, (void*)r->vals,
+                  (void*)r->vals_sorted, r->sort_tmp, (void*)r->ranges})
+    if (p) hipFree(p);
+  if (r->h_count) hipHostFree(r->h_count);
+  delete r;
+  return GSMPM_OK;
+}
+
+int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* out_color, int32_t* out_radii,
+                         int32_t* num_rendered, void* stream) {
+  GSMPM_REQUIRE(r && in && out_color && out_radii, "gsmpm_raster_forward: null argument");
+  GSMPM_REQUIRE(in->P >= 0 && in->W > 0 && in->H > 0, "gsmpm_raster_forward: bad sizes");
+  GSMPM_REQUIRE((in->shs != nullptr) != (in->colors_precomp != nullptr),
+                "Please provide excatly one of either SHs or precomputed colors!");
+  GSMPM_REQUIRE((in->cov3D_precomp != nullptr) != (in->scales != nullptr && in->rotations != nullptr),
+                "Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
+  GSMPM_REQUIRE(in->means3D && in->opacities && in->viewmatrix && in->projmatrix && in->campos && in->bg,
+                "gsmpm_raster_forward: null tensor");
+  GSMPM_REQUIRE(in->shs == nullptr || in->M >= 1, "gsmpm_raster_forward: shs needs M >= 1");
+  GSMPM_REQUIRE(in->shs == nullptr || in->D < 1 || in->M >= (in->D + 1) * (in->D + 1),
+                "gsmpm_raster_forward: too few SH coefficients for sh_degree");
+  GSMPM_REQUIRE(!in->prefiltered, "gsmpm_raster_forward: prefiltered=True is not supported (upstream traps too)");
+  hipStream_t st = (hipStream_t)stream;
+  RasterDev a;
+  a.P = in->P;
+  a.D = in->D;
+  a.M = in->M;
+  a.W = in->W;
+  a.H = in->H;
+  a.means3D = in->means3D;
+  a.shs = in->shs;
+  a.colors_precomp = in->colors_precomp;
+  a.opacities = in->opacities;
+  a.scales = in->scales;
+  a.rotations = in->rotations;
+  a.cov3D_precomp = in->cov3D_precomp;
+  a.scale_modifier = in->scale_modifier;
+  a.viewmatrix = in->viewmatrix;
+  a.projmatrix = in->projmatrix;
+  a.campos = in->campos;
+  a.bg = in->bg;
+  a.tanfovx = in->tanfovx;
+  a.tanfovy = in->tanfovy;
+  a.focal_x = in->W / (2.0f * in->tanfovx);
+  a.focal_y = in->H / (2.0f * in->tanfovy);
+  a.grid_x = (in->W + kBX - 1) / kBX;
+  a.grid_y = (in->H + kBY - 1) / kBY;
+  const int P = in->P;
+  const size_t ntiles = (size_t)a.grid_x * a.grid_y;
+  if ((size_t)P > r->capP || r->capP == 0) {
+    const size_t cap = std::max<size_t>(P, 1024);
+    int rc;
+    if ((rc = grow((void**)&r->depth, cap * sizeof(float)))) return rc;
+    if ((rc = grow((void**)&r->xy, cap * sizeof(float2)))) return rc;
+    if ((rc = grow((void**)&r->conic, cap * sizeof(float4)))) return rc;
+    if ((rc = grow((void**)&r->rgb, cap * sizeof(float4)))) return rc;
+    if ((rc = grow((void**)&r->tiles, cap * sizeof(unsigned)))) return rc;
+    if ((rc = grow((void**)&r->offsets, cap * sizeof(unsigned)))) return rc;
+    size_t bytes = 0;
+    GSMPM_HIP(rocprim::inclusive_scan(nullptr, bytes, r->tiles, r->offsets, cap, rocprim::plus<unsigned>(), st));
+    if ((rc = grow(&r->scan_tmp, bytes))) return rc;
+    r->scan_tmp_bytes = bytes;
+    r->capP = cap;
+  }
+  if (ntiles > r->capT) {
+    int rc;
+    if ((rc = grow((void**)&r->ranges, ntiles * sizeof(uint2)))) return rc;
+    r->capT = ntiles;
+  }
+  GSMPM_HIP(hipMemsetAsync(r->ranges, 0, ntiles * sizeof(uint2), st));
+  unsigned K = 0;
+  if (P > 0) {
+    hipLaunchKernelGGL(k_preprocess, dim3(div_up(P, 256)), dim3(256), 0, st, a, out_radii, r->depth, r->xy, r->conic,
+                       r->rgb, r->tiles);
+    GSMPM_LAUNCH_CHECK();
+    size_t bytes = r->scan_tmp_bytes;
+    GSMPM_HIP(rocprim::inclusive_scan(r->scan_tmp, bytes, r->tiles, r->offsets, (size_t)P, rocprim::plus<unsigned>(), st));
+    GSMPM_HIP(hipMemcpyAsync(r->h_count, r->offsets + (P - 1), sizeof(unsigned), hipMemcpyDeviceToHost, st));
+    GSMPM_HIP(hipStreamSynchronize(st));
+    K = *r->h_count;
+  }
+  if (K > 0) {
+    if (K > r->capK) {
+      const size_t cap = (size_t)K + K / 4 + 1024;
+      int rc;
+      if ((rc = grow((void**)&r->keys, cap * 8))) return rc;
+      if ((rc = grow((void**)&r->keys_sorted, cap * 8))) return rc;
+      if ((rc = grow((void**)&r->vals, cap * 4))) return rc;
+      if ((rc = grow((void**)&r->vals_sorted, cap * 4))) return rc;
+      size_t bytes = 0;
+      GSMPM_HIP(rocprim::radix_sort_pairs(nullptr, bytes, r->keys, r->keys_sorted, r->vals, r->vals_sorted, cap, 0,
+                                          64, st));
+      if ((rc = grow(&r->sort_tmp, bytes))) return rc;
+      r->sort_tmp_bytes = bytes;
+      r->capK = cap;
+    }
+    hipLaunchKernelGGL(k_duplicate, dim3(div_up(P, 256)), dim3(256), 0, st, P, r->xy, r->depth, r->offsets, out_radii,
+                       a.grid_x, a.grid_y, r->keys, r->vals);
+    GSMPM_LAUNCH_CHECK();
+    const int bits = msb_bits((unsigned)ntiles);
+    size_t bytes = r->sort_tmp_bytes;
+    GSMPM_HIP(rocprim::radix_sort_pairs(r->sort_tmp, bytes, r->keys, r->keys_sorted, r->vals, r->vals_sorted,
+                                        (size_t)K, 0, 32 + bits, st));
+    hipLaunchKernelGGL(k_ranges, dim3(div_up(K, 256)), dim3(256), 0, st, (int)K, r->keys_sorted, r->ranges);
+    GSMPM_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(k_render, dim3(a.grid_x, a.grid_y), dim3(kBlock), 0, st, r->ranges, r->vals_sorted, a.W, a.H,
+                     a.grid_x, r->xy, r->conic, r->rgb, in->bg, out_color);
+  GSMPM_LAUNCH_CHECK();
+  if (num_rendered) *num_rendered = (int32_t)K;
+  return GSMPM_OK;
+}
+
+int gsmpm_raster_mark_visible(const float* means3D, int32_t P, const float* vm, const float* pm, uint8_t* vis,
+                              void* stream) {
+  GSMPM_REQUIRE(means3D && vm && vis && P >= 0, "gsmpm_raster_mark_visible: bad argument");
+  (void)pm;
+  if (P == 0) return GSMPM_OK;
+  hipLaunchKernelGGL(k_mark_visible, dim3(div_up(P, 256)), dim3(256), 0, (hipStream_t)stream, means3D, P, vm, vis);
+  GSMPM_LAUNCH_CHECK();
+  return GSMPM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,141 @@
+// svd3.h -- 3x3 f32 SVD for the constitutive kernels, register-resident.
+//
+// Same published algorithm as Taichi's ti.svd for f32 (McAdams, Selle, Tamstorf,
+// Teran, Sifakis 2011, "Computing the SVD of 3x3 matrices with minimal branching
+// and elementary floating point operations"), which the reference calls at
+// mpm_solver/utils.py:33,385 and constitutive_models.py:64,107,218:
+//   1. Jacobi eigen-analysis of S = A^T A with approximate Givens quaternions,
+//      5 sweeps of the (0,1),(1,2),(2,0) pivots (f32 setting);
+//   2. V from the accumulated quaternion, B = A V;
+//   3. sort B's columns by decreasing norm, negating the swapped-in column so
+//      V stays a rotation;
+//   4. Givens QR of B: U = G1 G2 G3, sigma = diag(R) (sigma3 carries sign(det A)).
+// Written branch-free for the wavefront: every select is a v_cndmask.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace gsmpm {
+
+struct M3 {
+  float m[3][3];
+};
+
+__device__ __forceinline__ void svd_jacobi(float (&S)[3][3], float (&q)[4], int p, int r) {
+  constexpr float kGamma = 5.828427124746190f;  // 3 + 2 sqrt(2)
+  constexpr float kCStar = 0.923879532511287f;  // cos(pi/8)
+  constexpr float kSStar = 0.382683432365090f;  // sin(pi/8)
+  float ch = 2.0f * (S[p][p] - S[r][r]);
+  float sh = S[r][p];
+  const bool b = (kGamma * sh * sh) < (ch * ch);
+  const float w = 1.0f / sqrtf(ch * ch + sh * sh);
+  ch = b ? w * ch : kCStar;
+  sh = b ? w * sh : kSStar;
+  const float c = ch * ch - sh * sh, s = 2.0f * sh * ch;
+  // S <- R^T S R with R the (p,r)-plane rotation [[c,-s],[s,c]]
+  const int k = 3 - p - r;
+  const float spp = S[p][p], srr = S[r][r], spr = S[p][r], spk = S[p][k], srk = S[r][k];
+  const float npp = c * (c * spp + s * spr) + s * (c * spr + s * srr);
+  const float nrr = -s * (-s * spp + c * spr) + c * (-s * spr + c * srr);
+  const float npr = c * (-s * spp + c * spr) + s * (-s * spr + c * srr);
+  const float npk = c * spk + s * srk;
+  const float nrk = -s * spk + c * srk;
+  S[p][p] = npp; S[r][r] = nrr;
+  S[p][r] = npr; S[r][p] = npr;
+  S[p][k] = npk; S[k][p] = npk;
+  S[r][k] = nrk; S[k][r] = nrk;
+  // q <- q * (ch, sh e_k)
+  float rq[4] = {ch, 0.f, 0.f, 0.f};
+  rq[1 + k] = sh;
+  const float a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
+  q[0] = a0 * rq[0] - a1 * rq[1] - a2 * rq[2] - a3 * rq[3];
+  q[1] = a0 * rq[1] + a1 * rq[0] + a2 * rq[3] - a3 * rq[2];
+  q[2] = a0 * rq[2] - a1 * rq[3] + a2 * rq[0] + a3 * rq[1];
+  q[3] = a0 * rq[3] + a1 * rq[2] - a2 * rq[1] + a3 * rq[0];
+}
+
+__device__ __forceinline__ void svd_cond_swap(bool c, float (&B)[3][3], float (&V)[3][3], float (&rho)[3], int i, int j) {
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const float bi = B[r][i], bj = B[r][j];
+    B[r][i] = c ? bj : bi;
+    B[r][j] = c ? -bi : bj;
+    const float vi = V[r][i], vj = V[r][j];
+    V[r][i] = c ? vj : vi;
+    V[r][j] = c ? -vi : vj;
+  }
+  const float ri = rho[i], rj = rho[j];
+  rho[i] = c ? rj : ri;
+  rho[j] = c ? ri : rj;
+}
+
+__device__ __forceinline__ void svd_qr_givens(float (&B)[3][3], float (&U)[3][3], int p, int r) {
+  constexpr float kEps = 1.0e-12f;
+  const float a1 = B[p][p], a2 = B[r][p];
+  const float rho = sqrtf(a1 * a1 + a2 * a2);
+  float sh = rho > kEps ? a2 : 0.0f;
+  float ch = fabsf(a1) + fmaxf(rho, kEps);
+  const bool neg = a1 < 0.0f;
+  const float t = sh;
+  sh = neg ? ch : sh;
+  ch = neg ? t : ch;
+  const float w = 1.0f / sqrtf(ch * ch + sh * sh);
+  ch *= w;
+  sh *= w;
+  const float c = ch * ch - sh * sh, s = 2.0f * sh * ch;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const float bp = B[p][j], br = B[r][j];
+    B[p][j] = c * bp + s * br;
+    B[r][j] = -s * bp + c * br;
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const float up = U[i][p], ur = U[i][r];
+    U[i][p] = c * up + s * ur;
+    U[i][r] = -s * up + c * ur;
+  }
+}
+
+// A = U diag(sig) V^T
+__device__ __forceinline__ void svd3(const float (&A)[3][3], float (&U)[3][3], float (&sig)[3], float (&V)[3][3]) {
+  float S[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) S[i][j] = A[0][i] * A[0][j] + A[1][i] * A[1][j] + A[2][i] * A[2][j];
+  float q[4] = {1.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int it = 0; it < 5; ++it) {
+    svd_jacobi(S, q, 0, 1);
+    svd_jacobi(S, q, 1, 2);
+    svd_jacobi(S, q, 2, 0);
+  }
+  const float qn = 1.0f / sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  const float w = q[0] * qn, x = q[1] * qn, y = q[2] * qn, z = q[3] * qn;
+  V[0][0] = 1.f - 2.f * (y * y + z * z); V[0][1] = 2.f * (x * y - w * z); V[0][2] = 2.f * (x * z + w * y);
+  V[1][0] = 2.f * (x * y + w * z); V[1][1] = 1.f - 2.f * (x * x + z * z); V[1][2] = 2.f * (y * z - w * x);
+  V[2][0] = 2.f * (x * z - w * y); V[2][1] = 2.f * (y * z + w * x); V[2][2] = 1.f - 2.f * (x * x + y * y);
+  float B[3][3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) B[i][j] = A[i][0] * V[0][j] + A[i][1] * V[1][j] + A[i][2] * V[2][j];
+  float rho[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) rho[c] = B[0][c] * B[0][c] + B[1][c] * B[1][c] + B[2][c] * B[2][c];
+  svd_cond_swap(rho[0] < rho[1], B, V, rho, 0, 1);
+  svd_cond_swap(rho[0] < rho[2], B, V, rho, 0, 2);
+  svd_cond_swap(rho[1] < rho[2], B, V, rho, 1, 2);
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) U[i][j] = (i == j) ? 1.f : 0.f;
+  svd_qr_givens(B, U, 0, 1);
+  svd_qr_givens(B, U, 0, 2);
+  svd_qr_givens(B, U, 1, 2);
+  sig[0] = B[0][0];
+  sig[1] = B[1][1];
+  sig[2] = B[2][2];
+}
+
+}  // namespace gsmpm

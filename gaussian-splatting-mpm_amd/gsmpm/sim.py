@@ -1,0 +1,166 @@
+"""Torch-facing wrapper of the MPM C-ABI (gsmpm_mpm_*).
+
+All tensors live on the current HIP device; every call is asynchronous on
+torch's current stream.  This is plumbing: the math runs in libgsmpm.so.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+
+from . import _lib
+from ._lib import LIB, check, ptr, stream_of
+
+MATERIALS = {"jelly": 0, "metal": 1, "sand": 2, "foam": 3}  # mpm_solver/utils.py:5-10
+
+_WIDTH = {"x": 3, "v": 3, "C": 9, "F_trial": 9, "cov": 6, "init_cov": 6, "R": 9, "mass": 1, "vol": 1, "mu": 1,
+          "lam": 1, "yield_stress": 1}
+
+
+def _d3(v):
+    return (ctypes.c_double * 3)(*[float(a) for a in v])
+
+
+class Simulator:
+    """One MPM domain: particle state + dense n^3 grid on one GPU."""
+
+    def __init__(self, n_particles: int, *, n_grid: int, grid_extent: float = 2.0, material: str | int = "jelly",
+                 E: float = 2e6, nu: float = 0.4, density: float = 1000.0, gravity=(0.0, -9.81, 0.0),
+                 yield_stress: float = 0.005, hardening: float = 1.0, xi: float = 1.0,
+                 plastic_viscosity: float = 0.008, friction_angle: float = 25.0, jelly_fcr: bool = False,
+                 keep_grid: bool = False, use_graph: bool = True, sort: bool = True, device=None):
+        code = MATERIALS.get(material, -1) if isinstance(material, str) else int(material)
+        if code not in (0, 1, 2, 3):
+            raise TypeError("Material not supported yet")  # model.py:27-30
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        self.n = int(n_particles)
+        self.n_grid = int(n_grid)
+        self.grid_extent = float(grid_extent)
+        p = _lib.MpmParams()
+        p.n_particles = self.n
+        p.n_grid = self.n_grid
+        p.grid_extent = self.grid_extent
+        p.material = code
+        p.E, p.nu, p.density = float(E), float(nu), float(density)
+        p.gravity[:] = [float(g) for g in gravity]
+        p.yield_stress, p.hardening, p.xi = float(yield_stress), float(hardening), float(xi)
+        p.plastic_viscosity, p.friction_angle_deg = float(plastic_viscosity), float(friction_angle)
+        flags = 0
+        if jelly_fcr:
+            flags |= _lib.FLAG_JELLY_FCR
+        if keep_grid:
+            flags |= _lib.FLAG_KEEP_GRID
+        if not use_graph:
+            flags |= _lib.FLAG_NO_GRAPH
+        if not sort:
+            flags |= _lib.FLAG_NO_SORT
+        p.flags = flags
+        self.params = p
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            check(LIB.gsmpm_mpm_create(ctypes.byref(p), ctypes.byref(h)), "gsmpm_mpm_create")
+        self._h = h
+
+    # -------------------------------------------------------------- setup --
+    def set_particles(self, x, cov6, vol, v=None):
+        f = lambda t: None if t is None else t.detach().to(self.device, torch.float32).contiguous()
+        x, cov6, vol, v = f(x), f(cov6), f(vol), f(v)
+        assert x.numel() == 3 * self.n and cov6.numel() == 6 * self.n and vol.numel() == self.n
+        assert v is None or v.numel() == 3 * self.n
+        check(LIB.gsmpm_mpm_set_particles(self._h, ptr(x), ptr(cov6), ptr(vol), ptr(v), stream_of(self.device)),
+              "gsmpm_mpm_set_particles")
+
+    def add_fixed_cube(self, center, size) -> int:
+        return check(LIB.gsmpm_mpm_add_fixed_cube(self._h, _d3(center), _d3(size)), "add_fixed_cube")
+
+    def add_impulse(self, center, size, force, substep_dt) -> int:
+        return check(LIB.gsmpm_mpm_add_impulse(self._h, _d3(center), _d3(size), _d3(force), float(substep_dt)),
+                     "add_impulse")
+
+    def add_plane_collider(self, point, normal, friction=0.0) -> int:
+        return check(LIB.gsmpm_mpm_add_plane_collider(self._h, _d3(point), _d3(normal), float(friction)),
+                     "add_plane_collider")
+
+    # ------------------------------------------------------------ stepping --
+    def step(self, dt: float, masks):
+        n = len(masks)
+        if n == 0:
+            return
+        arr = (ctypes.c_uint32 * n)(*[int(m) & 0xFFFFFFFF for m in masks])
+        check(LIB.gsmpm_mpm_step(self._h, ctypes.c_float(dt), n, arr, stream_of(self.device)), "gsmpm_mpm_step")
+
+    def profile(self, dt: float, masks):
+        """Eager substeps with hipEvents between kernels -> (p2g_ms, grid_ms, g2p_ms) summed."""
+        n = len(masks)
+        arr = (ctypes.c_uint32 * max(1, n))(*[int(m) & 0xFFFFFFFF for m in masks])
+        out = (ctypes.c_float * 3)()
+        check(LIB.gsmpm_mpm_profile_substeps(self._h, ctypes.c_float(dt), n, arr, out, stream_of(self.device)),
+              "gsmpm_mpm_profile_substeps")
+        return tuple(float(v) for v in out)
+
+    def live_box(self):
+        b = (ctypes.c_int32 * 6)()
+        check(LIB.gsmpm_mpm_live_box(self._h, b, stream_of(self.device)), "gsmpm_mpm_live_box")
+        return list(b[:3]), list(b[3:])
+
+    def postprocess(self):
+        check(LIB.gsmpm_mpm_postprocess(self._h, stream_of(self.device)), "gsmpm_mpm_postprocess")
+
+    # ------------------------------------------------------------------ io --
+    def get(self, name: str) -> torch.Tensor:
+        w = _WIDTH[name]
+        out = torch.empty((self.n, w) if w > 1 else (self.n,), dtype=torch.float32, device=self.device)
+        check(LIB.gsmpm_mpm_get(self._h, _lib.FIELD[name], ptr(out), stream_of(self.device)), f"get {name}")
+        return out
+
+    def set(self, name: str, t: torch.Tensor):
+        t = t.detach().to(self.device, torch.float32).contiguous()
+        assert t.numel() == self.n * _WIDTH[name]
+        check(LIB.gsmpm_mpm_set(self._h, _lib.FIELD[name], ptr(t), stream_of(self.device)), f"set {name}")
+
+    def get_grid(self, which: str) -> torch.Tensor:
+        code = {"mass": 0, "v_in": 1, "v_out": 2}[which]
+        ng = self.n_grid
+        shape = (ng, ng, ng) if code == 0 else (ng, ng, ng, 3)
+        out = torch.empty(shape, dtype=torch.float32, device=self.device)
+        check(LIB.gsmpm_mpm_get_grid(self._h, code, ptr(out), stream_of(self.device)), f"get_grid {which}")
+        return out
+
+    def world_outputs(self, scale, center, render_space: bool, means_out=None, cov_out=None):
+        """Fused grid2world (+ render shift) of x and cov, in caller order."""
+        means_out = torch.empty((self.n, 3), dtype=torch.float32, device=self.device) if means_out is None else means_out
+        cov_out = torch.empty((self.n, 6), dtype=torch.float32, device=self.device) if cov_out is None else cov_out
+        c = (ctypes.c_float * 3)(*[float(a) for a in center])
+        check(LIB.gsmpm_mpm_world_outputs(self._h, ctypes.c_float(float(scale)), c, int(bool(render_space)),
+                                          ptr(means_out), ptr(cov_out), stream_of(self.device)), "world_outputs")
+        return means_out, cov_out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            LIB.gsmpm_mpm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def particle_volume(x: torch.Tensor, n_grid: int, grid_extent: float) -> torch.Tensor:
+    """internel_filling/filling.py:27-42 on the GPU (i32 atomics, floor cells)."""
+    x = x.detach().to(torch.float32).contiguous()
+    n = x.shape[0]
+    scratch = torch.empty(n_grid ** 3, dtype=torch.int32, device=x.device)
+    vol = torch.empty(n, dtype=torch.float32, device=x.device)
+    check(LIB.gsmpm_particle_volume(ptr(x), n, n_grid, float(grid_extent), ptr(scratch), ptr(vol),
+                                    stream_of(x.device)), "gsmpm_particle_volume")
+    return vol
+
+
+def alpha_from_friction(friction_angle_deg: float) -> float:
+    """model.py:48-51 (f64)."""
+    s = math.sin(friction_angle_deg / 180.0 * 3.141592653589793)
+    return math.sqrt(2.0 / 3.0) * 2.0 * s / (3.0 - s)

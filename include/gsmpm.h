@@ -1,0 +1,192 @@
+/*
+ * gsmpm.h -- C-ABI of the MI355X-native PhysGaussian hot path (libgsmpm.so).
+ *
+ * Plain C types only: device pointers are `float*`/`int32_t*` allocated by
+ * the caller (e.g. torch tensors' data_ptr()), streams are `void*`
+ * (hipStream_t).  Every entry point returns 0 on success or a negative
+ * status; gsmpm_last_error() then holds a thread-local message.
+ *
+ * Each declaration names the reference interface it replaces
+ * (ranrandy/gaussian-splatting-mpm @ 2024-12-18, file:line).
+ */
+#ifndef GSMPM_H
+#define GSMPM_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSMPM_OK 0
+#define GSMPM_EINVAL -1
+#define GSMPM_EHIP -2
+#define GSMPM_ESTATE -3
+
+/* ------------------------------------------------------------ common --- */
+const char* gsmpm_last_error(void);
+int gsmpm_version(void);
+
+/* --------------------------------------------------------------- MPM ---
+ * Replaces mpm_solver.MPM_Simulator (mpm_solver/solver.py:9-177) with its
+ * MPM_model / MPM_state (mpm_solver/model.py:6-132).
+ */
+typedef struct gsmpm_mpm gsmpm_mpm;
+
+#define GSMPM_MAT_JELLY 0
+#define GSMPM_MAT_METAL 1
+#define GSMPM_MAT_SAND 2
+#define GSMPM_MAT_FOAM 3
+
+/* flags */
+#define GSMPM_FLAG_JELLY_FCR 1u   /* fix SURVEY F3: run FCR elasticity for jelly (utils.py:37-38) */
+#define GSMPM_FLAG_KEEP_GRID 2u   /* keep m / m*v of the last substep readable (debug, slower) */
+#define GSMPM_FLAG_NO_GRAPH 4u    /* launch substeps eagerly instead of through a cached hipGraph */
+#define GSMPM_FLAG_NO_SORT 8u     /* keep particles in input order (no spatial sort) */
+
+typedef struct {
+  int32_t n_particles;
+  int32_t n_grid;               /* MPMParams.n_grid (arguments/__init__.py:66) */
+  double grid_extent;           /* MPMParams.grid_extent */
+  int32_t material;             /* GSMPM_MAT_*; model.py:24-31 */
+  double E, nu, density;        /* model.py:42-44, 100-102 */
+  double gravity[3];            /* model.py:32 */
+  double yield_stress;          /* 0.005, model.py:55-56 */
+  double hardening, xi;         /* 1, 1, model.py:57-58 */
+  double plastic_viscosity;     /* 0.008, model.py:59 */
+  double friction_angle_deg;    /* 25, model.py:48 */
+  uint32_t flags;
+} gsmpm_mpm_params;
+
+/* MPM_Simulator.__init__ -> MPM_model.__init__ (model.py:8-22) */
+int gsmpm_mpm_create(const gsmpm_mpm_params* params, gsmpm_mpm** out);
+int gsmpm_mpm_destroy(gsmpm_mpm* h);
+
+/* MPM_state.__init__ (model.py:78-122): x [N,3] grid space, cov6 [N,6]
+ * (becomes particle_init_cov and particle_cov), vol [N]; v [N,3] or NULL
+ * (MPM_state_opt init_vel, model.py:160-167).  Device pointers, f32. */
+int gsmpm_mpm_set_particles(gsmpm_mpm* h, const float* x, const float* cov6, const float* vol,
+                            const float* v_or_null, void* stream);
+
+/* Boundary conditions (mpm_solver/boundary_conditions.py, solver.py:110-167).
+ * Each returns (>=0) a bc id; ids index the bit of the per-substep activity mask.
+ *   fixed_cube  -> BasicBC.apply           (boundary_conditions.py:23-27)
+ *   impulse     -> ImpulseBC.apply         (boundary_conditions.py:41-45)
+ *   plane       -> MPM_Collider.collide    (collider.py:13-44), always active;
+ *                  normal is normalised in f64 as solver.py:153-154 does. */
+int gsmpm_mpm_add_fixed_cube(gsmpm_mpm* h, const double center[3], const double size[3]);
+int gsmpm_mpm_add_impulse(gsmpm_mpm* h, const double center[3], const double size[3], const double force[3],
+                          double substep_dt);
+int gsmpm_mpm_add_plane_collider(gsmpm_mpm* h, const double point[3], const double normal[3], double friction);
+
+/* MPM_Simulator.p2g2p (solver.py:27-52) x n_substeps.  bc_active[s] holds
+ * the activity bits of substep s, decided by the caller from the f64 host
+ * clock exactly as BasicBC.isActive (boundary_conditions.py:30-31); NULL =
+ * all active.  Asynchronous on `stream`. */
+int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t n_substeps, const uint32_t* bc_active, void* stream);
+
+/* MPM_Simulator.postprocess (solver.py:135-137): compute_cov_from_F and
+ * compute_R_from_F (utils.py:376-433). */
+int gsmpm_mpm_postprocess(gsmpm_mpm* h, void* stream);
+
+/* Field readback / write in the reference layout (Taichi to_torch shapes):
+ * rows follow the caller's original particle order. */
+#define GSMPM_FIELD_X 0        /* particle_xyz      [N,3]   */
+#define GSMPM_FIELD_V 1        /* particle_vel      [N,3]   */
+#define GSMPM_FIELD_C 2        /* particle_C        [N,3,3] */
+#define GSMPM_FIELD_F_TRIAL 3  /* particle_F_trial  [N,3,3] */
+#define GSMPM_FIELD_COV 4      /* particle_cov      [6N]    */
+#define GSMPM_FIELD_INIT_COV 5 /* particle_init_cov [6N]    */
+#define GSMPM_FIELD_R 6        /* particle_R        [N,3,3] */
+#define GSMPM_FIELD_MASS 7     /* particle_mass     [N]     */
+#define GSMPM_FIELD_VOL 8      /* particle_vol      [N]     */
+#define GSMPM_FIELD_MU 9       /* mpm_model.mu      [N]     */
+#define GSMPM_FIELD_LAM 10     /* mpm_model.lam     [N]     */
+#define GSMPM_FIELD_YIELD 11   /* mpm_model.yield_stress [N] */
+#define GSMPM_FIELD_COUNT 12
+int gsmpm_mpm_field_width(int32_t field);
+int gsmpm_mpm_get(gsmpm_mpm* h, int32_t field, float* out, void* stream);
+int gsmpm_mpm_set(gsmpm_mpm* h, int32_t field, const float* in, void* stream);
+
+/* Grid readback [n^3] / [n^3,3] (grid_mass / grid_v_in / grid_v_out,
+ * model.py:117-121).  mass and v_in need GSMPM_FLAG_KEEP_GRID. */
+#define GSMPM_GRID_MASS 0
+#define GSMPM_GRID_V_IN 1
+#define GSMPM_GRID_V_OUT 2
+int gsmpm_mpm_get_grid(gsmpm_mpm* h, int32_t which, float* out, void* stream);
+
+/* Fused frame output (main.py:310-313 + render_frame 139-146), f32 as torch does it:
+ * means_out[N,3] = (x - extent/2)/s + c            (grid2world, transform_utils.py:18-21)
+ *                  and, if render_space != 0, then c + (means - 1)/1.0
+ *                  (undoshift2center111 + undotransform2origin with scale 1.0);
+ * cov_out[N,6]   = cov / (s*s).   Rows in original particle order. */
+int gsmpm_mpm_world_outputs(gsmpm_mpm* h, float scale, const float center[3], int32_t render_space,
+                            float* means_out, float* cov_out, void* stream);
+
+/* Measurement: run n substeps eagerly with hipEvents between the three fused
+ * kernels on `stream`; kernel_ms[0..2] = summed time of k_p2g, k_grid, k_g2p.
+ * Synchronises `stream`. */
+int gsmpm_mpm_profile_substeps(gsmpm_mpm* h, float dt, int32_t n_substeps, const uint32_t* bc_active,
+                               float* kernel_ms, void* stream);
+/* Current live-node box (lo[3], hi[3]) that k_grid sweeps; synchronises `stream`. */
+int gsmpm_mpm_live_box(gsmpm_mpm* h, int32_t* box6, void* stream);
+
+/* Device 3x3 SVD (the ti.svd restatement used by the constitutive kernels) on
+ * n row-major matrices: A[n*9] -> U[n*9], sig[n*3], V[n*9].  Test entry point. */
+int gsmpm_svd3(const float* A, int32_t n, float* U, float* sig, float* V, void* stream);
+
+/* Constitutive step alone (compute_stress_from_F_trial, utils.py:13-54) on n
+ * particles: F_trial[n*9], mu[n], lam[n], yield[n] (updated in place for
+ * metal) -> F[n*9] (return-mapped), tau[n*9] (symmetrised Kirchhoff stress).
+ * material: GSMPM_MAT_*, or 4 = jelly with FCR (F3 fixed).  Test entry point. */
+int gsmpm_constitutive(int32_t material, const float* F_trial, int32_t n, const float* mu, const float* lam,
+                       float* yield, float dt, float* F_out, float* tau_out, void* stream);
+
+/* get_particle_volume (internel_filling/filling.py:27-42): vol[N] from
+ * x[N,3] (grid space) with an n^3 i32 count grid in `scratch` (>= 4*n^3 B). */
+int gsmpm_particle_volume(const float* x, int32_t n, int32_t n_grid, double grid_extent, int32_t* scratch,
+                          float* vol_out, void* stream);
+
+/* -------------------------------------------------------- rasterizer ---
+ * Replaces diff_gaussian_rasterization._C.rasterize_gaussians (forward;
+ * called via GaussianRasterizer.forward at main.py:148-156).  Upstream
+ * third-party, pre-2024 API; not vendored in the reference.
+ */
+typedef struct gsmpm_raster gsmpm_raster;
+
+typedef struct {
+  int32_t P;                 /* number of Gaussians */
+  int32_t D;                 /* sh degree */
+  int32_t M;                 /* SH coefficients per Gaussian (shs.size(1)), 0 if colors_precomp */
+  int32_t W, H;
+  const float* means3D;      /* [P,3] */
+  const float* shs;          /* [P,M,3] or NULL */
+  const float* colors_precomp; /* [P,3] or NULL */
+  const float* opacities;    /* [P] */
+  const float* scales;       /* [P,3] or NULL */
+  const float* rotations;    /* [P,4] or NULL */
+  const float* cov3D_precomp;/* [P,6] or NULL */
+  float scale_modifier;
+  const float* viewmatrix;   /* [4,4] (transposed world->view, as upstream) */
+  const float* projmatrix;   /* [4,4] */
+  const float* campos;       /* [3] */
+  const float* bg;           /* [3] */
+  float tanfovx, tanfovy;
+  int32_t prefiltered;
+} gsmpm_raster_args;
+
+int gsmpm_raster_create(gsmpm_raster** out);
+int gsmpm_raster_destroy(gsmpm_raster* r);
+/* out_color [3,H,W] f32, out_radii [P] i32 (device).  *num_rendered gets K.
+ * The binning buffers grow inside the context (not graph-capturable: the
+ * upstream forward also syncs on num_rendered). */
+int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* a, float* out_color, int32_t* out_radii,
+                         int32_t* num_rendered, void* stream);
+/* GaussianRasterizer.markVisible -> _C.mark_visible: visible[P] (u8) = view z > 0.2 */
+int gsmpm_raster_mark_visible(const float* means3D, int32_t P, const float* viewmatrix, const float* projmatrix,
+                              uint8_t* visible, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

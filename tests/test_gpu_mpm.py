@@ -1,0 +1,119 @@
+"""MPM parity: HIP path (through the drop-in MPM_Simulator / C-ABI) vs the CPU oracle.
+
+Tolerance (BASELINE north_star): 1e-4 relative on particle positions and
+covariances, err = max|gpu - oracle| / max|oracle| per field.  Float atomics
+make the HIP sum order differ from the oracle's serial order, so other fields
+are checked at the same scale-relative bound.
+"""
+import numpy as np
+import pytest
+
+from conftest import rel_err
+from scenarios import build_oracle_sim, lego_problem, oracle_run
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+# v and C are grid-velocity gradients (C = sum v_i dpos^T w 4/dx^2): with a stiff
+# stress model they amplify the float-atomic summation order by ~1/dx, so they get
+# their own bound; x / F_trial / cov carry the north_star 1e-4.
+TOL_DERIVED = {"v": 2e-3, "C": 5e-3}
+
+
+# Two reference-algorithm conditioning limits (documented in DESIGN.md §Parity):
+#  * metal yield_stress grows by 2*mu*xi*dgamma with dgamma from log(sigma),
+#    sigma ~ 1 + 1e-4: f32 log near 1 carries ~1e-3 relative noise;
+#  * foam's F = U * diag * V^T is element-wise (constitutive_models.py:256, F13):
+#    it depends on the SVD basis itself, which is ill-defined for F ~ I, so
+#    F_trial (not x) inherits the float-atomic noise amplified.
+MATERIAL_TOL = {"metal": {"yield": 5e-3}, "foam": {"F_trial": 2e-2}}
+
+
+def _compare(s, ref, fields=("x", "v", "C", "F_trial"), tol=TOL, extra=None):
+    st = s.mpm_state
+    got = {
+        "x": st.particle_xyz.to_torch().cpu().numpy(),
+        "v": st.particle_vel.to_torch().cpu().numpy(),
+        "C": st.particle_C.to_torch().cpu().numpy().reshape(-1, 9),
+        "F_trial": st.particle_F_trial.to_torch().cpu().numpy().reshape(-1, 9),
+    }
+    exp = {"x": ref.x, "v": ref.v, "C": ref.C, "F_trial": ref.F_trial}
+    errs = {k: rel_err(got[k], exp[k]) for k in fields}
+    for k, e in errs.items():
+        bound = (extra or {}).get(k, TOL_DERIVED.get(k, tol))
+        assert e < bound, f"{k}: rel err {e:.3e} (all: {errs})"
+    return errs
+
+
+def test_lego_config_A_parity(dev):
+    """configs[0]: lego.json jelly (as written), 5k Gaussians, 64^3, 50 substeps."""
+    from gpu_helpers import dropin_sim
+    prob = lego_problem(5000, 64)
+    ref, imps, ops = build_oracle_sim(prob)
+    dt = prob["cfg"]["substep_dt"]
+    s, args = dropin_sim(prob, dev)
+    t = oracle_run(ref, imps, ops, dt, 50)
+    for _ in range(50):
+        s.p2g2p(dt)
+    assert abs(s.time - t) == 0.0
+    _compare(s, ref)
+    s.postprocess()
+    ref.postprocess()
+    cov = s.mpm_state.particle_cov.to_torch().cpu().numpy().reshape(-1, 6)
+    R = s.mpm_state.particle_R.to_torch().cpu().numpy().reshape(-1, 9)
+    assert rel_err(cov, ref.cov) < TOL
+    assert rel_err(R, ref.R) < TOL
+
+
+@pytest.mark.parametrize("material,quirk", [("metal", True), ("sand", True), ("foam", True), ("jelly", False)])
+def test_materials_parity(dev, material, quirk):
+    """Return maps + SVD stress (metal/sand/foam) and FCR jelly (F3 fixed), 30 substeps."""
+    from gpu_helpers import dropin_sim
+    prob = lego_problem(4000, 48)
+    ref, imps, ops = build_oracle_sim(prob, material=material, jelly_quirk=quirk)
+    dt = prob["cfg"]["substep_dt"]
+    s, _ = dropin_sim(prob, dev, material=material, jelly_fcr=not quirk)
+    oracle_run(ref, imps, ops, dt, 30)
+    for _ in range(30):
+        s.p2g2p(dt)
+    extra = MATERIAL_TOL.get(material, {})
+    _compare(s, ref, extra=extra)
+    if material == "metal":
+        y = s.mpm_model.yield_stress.to_torch().cpu().numpy()
+        assert rel_err(y, ref.yield_stress) < extra["yield"]
+
+
+def test_impulse_window(dev):
+    """ImpulseBC active on a host-decided window mid-run (boundary_conditions.py:41-45)."""
+    from gpu_helpers import dropin_sim
+    prob = lego_problem(3000, 48)
+    for d in prob["cfg"]["boundary_conditions"]:
+        if d["type"] == "impulse":
+            d["start_time"] = 0.0015
+            d["force"] = [-80.0, 0.0, 30.0]
+    ref, imps, ops = build_oracle_sim(prob)
+    dt = prob["cfg"]["substep_dt"]
+    s, _ = dropin_sim(prob, dev)
+    oracle_run(ref, imps, ops, dt, 40)
+    for _ in range(40):
+        s.p2g2p(dt)
+    _compare(s, ref)
+
+
+def test_eager_equals_graph(dev):
+    """Per-substep launches and the cached hipGraph replay give identical state."""
+    import torch
+    from gsmpm.sim import Simulator
+    prob = lego_problem(3000, 48)
+    cfg = prob["cfg"]
+    outs = []
+    for graph in (False, True):
+        sim = Simulator(len(prob["x"]), n_grid=48, material="metal", E=cfg["E"], nu=cfg["nu"],
+                        density=cfg["density"], gravity=cfg["gravity"], use_graph=graph)
+        t = lambda a: torch.from_numpy(a).to(dev)
+        sim.set_particles(t(prob["x"]), t(prob["cov"]), t(prob["vol"]))
+        b = sim.add_fixed_cube([1.0, 1.2, 0.5], [1.0, 0.8, 0.3])
+        sim.add_plane_collider([0, 0, 0.4], [0, 0, 1])
+        sim.step(1e-4, [1 << b] * 20)
+        outs.append(sim.get("x").cpu().numpy())
+    assert rel_err(outs[0], outs[1]) < 1e-6
