@@ -6,283 +6,102 @@
 // BasicBC.apply / MPM_Collider.collide, g2p -- ~10 launches per substep -- by
 // three fused kernels per substep, replayed from a cached hipGraph:
 //
-//   k_p2g   particle-parallel: impulse kick + return map + SVD stress +
-//           APIC scatter of (m*v, m) into the node accumulator (f32 atomics)
-//   k_grid  node-parallel over the live node box: normalise + gravity + the
-//           grid BC list in order, writes v_out, and re-zeroes the accumulator
-//           (that re-zero replaces reset_grid_state's three full fills)
-//   k_g2p   particle-parallel: 27-node gather, v/x/C/F_trial update, and the
-//           live-node box for the next substep (wave-reduced atomics)
+//   k_p2g   one workgroup per 8^3-cell tile: impulse kick, return map + SVD
+//           stress, APIC scatter of (m*v, m) into the tile's 10^3-node window
+//           with LDS float atomics; the window is written to the tile's slot
+//           with plain coalesced stores (no global atomics)
+//   k_grid  node-parallel over the live node box: pulls the <= 8 tile windows
+//           covering each node in a fixed order (deterministic sum), then
+//           normalise + gravity + the grid BC list in order -> v_out
+//   k_g2p   one workgroup per tile: stage the tile window of v_out in LDS,
+//           gather the 27-node stencil, update v / x / C / F_trial, and
+//           re-bucket every particle into its next tile (LDS-aggregated
+//           counters: <= 27 global atomics per workgroup)
 //
 // Layout in HBM: particle state is SoA (one f32 plane per scalar component,
-// stride np = N rounded to 256) so every particle-parallel load/store is a
-// coalesced dword per lane; particles are stored in Morton order of their cell
-// (rows map back to the caller's order through `orig`).  The grid is a dense
-// n^3 array of float4 {m*v, m} plus a float4 {v_out} array: 32 B/node.
+// stride np = N rounded up to 256), stored in Morton order of the particles'
+// cells and re-sorted every `resort_interval` substeps for locality (rows map
+// back to the caller's order through `orig`).  Grid: v_out dense float4 n^3;
+// tile slots float4[ntiles][1000]; per-tile buckets int[2][ntiles][cap].
 #include <hip/hip_runtime.h>
+
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <climits>
 #include <cmath>
 #include <cstring>
 #include <map>
-#include <mutex>
 #include <numeric>
 #include <vector>
 
 #include "common.h"
+#include "constitutive.h"
+#include "mpm_common.h"
 #include "svd3.h"
 
 namespace gsmpm {
 
-// ------------------------------------------------------------------ layout --
-enum Plane : int {
-  PX = 0,      // x y z
-  PV = 3,      // v
-  PC = 6,      // C (row-major 3x3)
-  PF = 15,     // F_trial between substeps; return-mapped F inside p2g
-  PMASS = 24,
-  PVOL = 25,
-  PMU = 26,
-  PLAM = 27,
-  PYLD = 28,
-  PICOV = 29,  // init cov (upper 6)
-  PCOV = 35,   // cov (upper 6)
-  PR = 41,     // particle_R
-  NPLANES = 50
+constexpr int kChunk = 256;  // particles per work chunk (one per lane of a 256-lane workgroup)
+
+// Workgroup timeline stamps (diagnostics): [kernel][wg][start, end] in
+// s_memrealtime ticks (100 MHz), written by lane 0 of the first 4096 workgroups.
+__device__ unsigned long long g_stamps[2][4096][8];
+__device__ __forceinline__ void stamp(int kern, int slot) {
+  if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[kern][blockIdx.x][slot] = __builtin_amdgcn_s_memrealtime();
+}
+
+// Chunk work lists (one set per parity).  Every substep G2P re-bins each
+// particle into the tile of its new base cell (LDS-aggregated counters), a
+// one-workgroup scan turns the per-tile counts into list offsets and a list of
+// <= 256-particle chunks, and a scatter writes the per-tile particle lists.
+// Particles whose base leaves the grid go to the extra pseudo-tile `ntiles`
+// (their transfers take the global, bounds-checked path).
+struct Tiles {
+  int td;      // tiles per axis
+  int ntiles;  // td^3 (the pseudo-tile "outside" is index ntiles)
+  int max_chunks;
+};
+struct ChunkIn {
+  const int* count;   // [ntiles + 1] particles per tile
+  const int* cbase;   // [ntiles + 1] first chunk of each tile
+  const int* ctile;   // [max_chunks] tile of each chunk
+  const int* cfirst;  // [max_chunks] first list entry of each chunk
+  const int* nchunk;  // [1]
+  const int* list;    // [n] particle (storage) indices grouped by tile
+};
+struct BinOut {
+  int* count;  // [ntiles + 1], zeroed before G2P
+  int* ptile;  // [n] next tile of each particle (storage index)
+  int* pslot;  // [n] rank of the particle inside that tile
 };
 
-constexpr int kMaxBC = 32;
-
-struct Impulse {
-  float c[3], s[3], f[3], sdt;
-  int bit;
-};
-struct GridOp {
-  int kind;  // 0 fixed cube, 1 plane collider
-  int bit;
-  float a[3], b[3], friction;
-};
-struct BcTable {
-  int n_imp, n_ops;
-  Impulse imp[kMaxBC];
-  GridOp op[kMaxBC];
-};
-
-struct Particles {
-  float* P;
-  int n, np;
-  __device__ __forceinline__ float& at(int plane, int i) const { return P[(size_t)plane * np + i]; }
-};
-
-struct GridDims {
-  int ng;
-  float dx, inv_dx;
-};
-
-struct MatConsts {
-  float alpha, hardening, xi, pvisc;
-};
-
-// live node box [lo, hi] of the last G2P (int x3 lo, x3 hi), used by k_grid
-struct Box {
-  int lo[3], hi[3];
-};
-
-// -------------------------------------------------------- device helpers --
-__device__ __forceinline__ void bspline(const float x[3], float inv_dx, int base[3], float fx[3], float w[3][3],
-                                        float dw[3][3]) {
-  // utils.py:92-109: base = (x*inv_dx - 0.5).cast(int) (truncation), quadratic B-spline
+__device__ __forceinline__ int tile_of(const float (&x)[3], const GridDims& g, const Tiles& tl, int (&tc)[3]) {
+  bool ok = true;
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
-    const float gp = x[d] * inv_dx;
-    base[d] = (int)(gp - 0.5f);
-    fx[d] = gp - (float)base[d];
-    const float wa = 1.5f - fx[d], wb = fx[d] - 1.0f, wc = fx[d] - 0.5f;
-    w[d][0] = wa * wa * 0.5f;
-    w[d][1] = 0.75f - wb * wb;
-    w[d][2] = wc * wc * 0.5f;
-    dw[d][0] = fx[d] - 1.5f;
-    dw[d][1] = -2.0f * (fx[d] - 1.0f);
-    dw[d][2] = fx[d] - 0.5f;
+    const float gp = x[d] * g.inv_dx - 0.5f;
+    ok = ok && (gp >= 0.0f) && (gp < (float)g.ng);  // false for NaN
+    const int b = ok ? (int)gp : 0;
+    tc[d] = b / kTile;
   }
+  return ok ? (tc[0] * tl.td + tc[1]) * tl.td + tc[2] : tl.ntiles;
 }
 
-__device__ __forceinline__ float det3(const float (&A)[3][3]) {
-  return A[0][0] * (A[1][1] * A[2][2] - A[1][2] * A[2][1]) - A[0][1] * (A[1][0] * A[2][2] - A[1][2] * A[2][0]) +
-         A[0][2] * (A[1][0] * A[2][1] - A[1][1] * A[2][0]);
-}
-
-// U diag(d) V^T
-__device__ __forceinline__ void usv(const float (&U)[3][3], const float (&d)[3], const float (&V)[3][3],
-                                    float (&O)[3][3]) {
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) O[i][j] = (U[i][0] * d[0]) * V[j][0] + (U[i][1] * d[1]) * V[j][1] + (U[i][2] * d[2]) * V[j][2];
-}
-
-// A B^T
-__device__ __forceinline__ void mmT(const float (&A)[3][3], const float (&B)[3][3], float (&O)[3][3]) {
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) O[i][j] = A[i][0] * B[j][0] + A[i][1] * B[j][1] + A[i][2] * B[j][2];
-}
-
-// ---------------------------------------------------- constitutive models --
-// Material codes as template: 0 = jelly as written (zero stress),
-// 1 metal, 2 sand, 3 foam, 4 = jelly with FCR (F3 fixed).
+// ------------------------------------------------------- particle front --
+// loads + ImpulseBC.apply + compute_stress_from_F_trial for one particle
 template <int MAT>
-__device__ __forceinline__ void return_map_and_stress(float (&F)[3][3], float mu, float lam, float& yld, float dt,
-                                                      const MatConsts& mc, float (&tau)[3][3]) {
-  float U[3][3], V[3][3], s[3];
-  if constexpr (MAT == 1) {
-    // von_mises_return_mapping, constitutive_models.py:62-103
-    svd3(F, U, s, V);
-    float eps[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) eps[d] = logf(fmaxf(s[d], 0.01f));
-    const float tr = eps[0] + eps[1] + eps[2];
-    const float temp = tr / 3.0f;
-    float t3[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) t3[d] = 2.0f * mu * eps[d] + lam * tr * 1.0f;
-    const float st = t3[0] + t3[1] + t3[2];
-    float cond[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) cond[d] = t3[d] - st / 3.0f;
-    const float cn = sqrtf(cond[0] * cond[0] + cond[1] * cond[1] + cond[2] * cond[2]);
-    if (cn > yld) {
-      float eh[3];
-#pragma unroll
-      for (int d = 0; d < 3; ++d) eh[d] = eps[d] - temp;
-      const float ehn = sqrtf(eh[0] * eh[0] + eh[1] * eh[1] + eh[2] * eh[2]) + 1e-6f;
-      const float dg = ehn - yld / (2.0f * mu);
-      float se[3];
-#pragma unroll
-      for (int d = 0; d < 3; ++d) se[d] = expf(eps[d] - (dg / ehn) * eh[d]);
-      usv(U, se, V, F);
-      if (mc.hardening == 1.0f) yld += 2.0f * mu * mc.xi * dg;
-    }
-  } else if constexpr (MAT == 2) {
-    // sand_return_mapping, constitutive_models.py:105-140
-    svd3(F, U, s, V);
-    float eps[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) eps[d] = logf(fmaxf(fabsf(s[d]), 1e-14f));
-    const float tr = eps[0] + eps[1] + eps[2];
-    float eh[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) eh[d] = eps[d] - tr / 3.0f;
-    const float ehn = sqrtf(eh[0] * eh[0] + eh[1] * eh[1] + eh[2] * eh[2]);
-    const float dg = ehn + (3.0f * lam + 2.0f * mu) / (2.0f * mu) * tr * mc.alpha;
-    if (dg > 0.0f) {
-      if (tr > 0.0f) {
-        mmT(U, V, F);
-      } else {
-        float sn[3];
-#pragma unroll
-        for (int d = 0; d < 3; ++d) sn[d] = expf(eps[d] - eh[d] * (dg / ehn));
-        usv(U, sn, V, F);
-      }
-    }
-  } else if constexpr (MAT == 3) {
-    // viscoplasticity_return_mapping_with_StVK, constitutive_models.py:216-259
-    svd3(F, U, s, V);
-    float sg[3], eps[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      sg[d] = fmaxf(s[d], 0.01f);
-      eps[d] = logf(sg[d]);
-    }
-    const float tr = eps[0] + eps[1] + eps[2];
-    float stv[3];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) stv[d] = 2.0f * mu * (eps[d] - tr / 3.0f);
-    const float stn = sqrtf(stv[0] * stv[0] + stv[1] * stv[1] + stv[2] * stv[2]);
-    const float y = stn - 0.8f * sqrtf(2.0f / 3.0f) * yld;
-    if (y > 0.0f) {
-      const float mu_hat = mu * (sg[0] * sg[0] + sg[1] * sg[1] + sg[2] * sg[2]) / 3.0f;
-      const float snn = stn - y / (1.0f + mc.pvisc * 2.0f / (2.0f * mu_hat * dt));
-      // element-wise U * diag * V^T (constitutive_models.py:256)
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          const float en = 1.0f / (2.0f * mu) * ((snn / stn) * stv[i]) + tr / 3.0f;
-          const float se = (i == j) ? expf(en) : 0.0f;
-          F[i][j] = U[i][j] * se * V[j][i];
-        }
-    }
-  }
-  // Kirchhoff stress of the (returned) F, utils.py:32-52
-  float T[3][3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) T[i][j] = 0.0f;
-  if constexpr (MAT != 0) {
-    svd3(F, U, s, V);
-    if constexpr (MAT == 1 || MAT == 3) {
-      // kirchoff_stress_StVK, constitutive_models.py:23-38
-      float tv[3];
-      float ls[3];
-#pragma unroll
-      for (int d = 0; d < 3; ++d) ls[d] = logf(fmaxf(s[d], 0.01f));
-      const float lss = ls[0] + ls[1] + ls[2];
-#pragma unroll
-      for (int d = 0; d < 3; ++d) tv[d] = 2.0f * mu * ls[d] + lam * lss * 1.0f;
-      float W[3][3];
-      usv(U, tv, V, W);
-      mmT(W, F, T);
-    } else if constexpr (MAT == 2) {
-      // kirchoff_stress_Drucker_Prager, constitutive_models.py:41-58
-      const float lss = logf(s[0]) + logf(s[1]) + logf(s[2]);
-      float cv[3];
-#pragma unroll
-      for (int d = 0; d < 3; ++d) cv[d] = 2.0f * mu * logf(s[d]) / s[d] + lam * lss / s[d];
-      float W[3][3];
-      usv(U, cv, V, W);
-      mmT(W, F, T);
-    } else if constexpr (MAT == 4) {
-      // kirchoff_stress_FCR, constitutive_models.py:10-20
-      const float J = det3(F);
-      float R[3][3], D[3][3];
-      mmT(U, V, R);
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) D[i][j] = 2.0f * mu * (F[i][j] - R[i][j]);
-      mmT(D, F, T);
-      const float l = lam * J * (J - 1.0f);
-      T[0][0] += l;
-      T[1][1] += l;
-      T[2][2] += l;
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) tau[i][j] = (T[i][j] + T[j][i]) / 2.0f;
-}
-
-// ------------------------------------------------------------------- P2G --
-template <int MAT>
-__global__ __launch_bounds__(256) void k_p2g(Particles ps, GridDims g, const BcTable* __restrict__ bct,
-                                             uint32_t mask, float dt, MatConsts mc, float4* __restrict__ gacc) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= ps.n) return;
-  float x[3], v[3], C[3][3];
+__device__ __forceinline__ void particle_front(const Particles& ps, int p, const BcTable* __restrict__ bct,
+                                               uint32_t mask, float dt, const MatConsts& mc, float (&x)[3],
+                                               float (&v)[3], float (&C)[3][3], float& m, float (&nvt)[3][3]) {
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
-    x[d] = ps.at(PX + d, p);
-    v[d] = ps.at(PV + d, p);
+    x[d] = ps.ld(PX + d, p);
+    v[d] = ps.ld(PV + d, p);
   }
 #pragma unroll
-  for (int i = 0; i < 9; ++i) C[i / 3][i % 3] = ps.at(PC + i, p);
-  const float m = ps.at(PMASS, p);
-
+  for (int i = 0; i < 9; ++i) C[i / 3][i % 3] = ps.ld(PC + i, p);
+  m = ps.ld(PMASS, p);
   // ImpulseBC.apply (boundary_conditions.py:41-45), host-decided activity.
   // G2P overwrites particle_vel, so the kick only needs to live in registers.
   if (mask) {
@@ -298,103 +117,271 @@ __global__ __launch_bounds__(256) void k_p2g(Particles ps, GridDims g, const BcT
       }
     }
   }
-
   // compute_stress_from_F_trial (utils.py:13-54), fused: stress never leaves registers
-  float nvt[3][3];  // -vol * tau
+#pragma unroll
+  for (int i = 0; i < 9; ++i) nvt[i / 3][i % 3] = 0.f;
   if constexpr (MAT != 0) {
     float F[3][3], tau[3][3];
 #pragma unroll
-    for (int i = 0; i < 9; ++i) F[i / 3][i % 3] = ps.at(PF + i, p);
-    float yld = ps.at(PYLD, p);
-    const float mu = ps.at(PMU, p), lam = ps.at(PLAM, p);
+    for (int i = 0; i < 9; ++i) F[i / 3][i % 3] = ps.ld(PF + i, p);
+    float yld = ps.ld(PYLD, p);
+    const float mu = ps.ld(PMU, p), lam = ps.ld(PLAM, p);
     return_map_and_stress<MAT>(F, mu, lam, yld, dt, mc, tau);
     if constexpr (MAT == 1 || MAT == 2 || MAT == 3) {
 #pragma unroll
-      for (int i = 0; i < 9; ++i) ps.at(PF + i, p) = F[i / 3][i % 3];
+      for (int i = 0; i < 9; ++i) ps.st(PF + i, p, F[i / 3][i % 3]);
     }
-    if constexpr (MAT == 1) ps.at(PYLD, p) = yld;
-    const float nvol = -ps.at(PVOL, p);
+    if constexpr (MAT == 1) ps.st(PYLD, p, yld);
+    const float nvol = -ps.ld(PVOL, p);
 #pragma unroll
     for (int i = 0; i < 3; ++i)
 #pragma unroll
       for (int j = 0; j < 3; ++j) nvt[i][j] = nvol * tau[i][j];
   }
+}
 
-  int base[3];
-  float fx[3], w[3][3], dw[3][3];
-  bspline(x, g.inv_dx, base, fx, w, dw);
+// One P2G contribution (utils.py:110-134) of a particle to the stencil node at
+// offset (i,j,k): the reference's expression, in its operation order.
+template <int MAT>
+__device__ __forceinline__ void p2g_term(int i, int j, int k, const float (&fx)[3], const float (&v)[3],
+                                         const float (&C)[3][3], float m, const float (&nvt)[3][3], const GridDims& g,
+                                         float dt, float4& acc) {
+  float w[3], dw[3];
+  const int o[3] = {i, j, k};
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    const float f = fx[d];
+    const float wa = 1.5f - f, wb = f - 1.0f, wc = f - 0.5f;
+    w[d] = o[d] == 0 ? wa * wa * 0.5f : (o[d] == 1 ? 0.75f - wb * wb : wc * wc * 0.5f);
+    dw[d] = o[d] == 0 ? f - 1.5f : (o[d] == 1 ? -2.0f * (f - 1.0f) : f - 0.5f);
+  }
+  const float dpos0 = ((float)i - fx[0]) * g.dx;
+  const float dpos1 = ((float)j - fx[1]) * g.dx;
+  const float dpos2 = ((float)k - fx[2]) * g.dx;
+  const float weight = w[0] * w[1] * w[2];
+  const float wm = weight * m;
+  float add[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) add[r] = wm * (v[r] + (C[r][0] * dpos0 + C[r][1] * dpos1 + C[r][2] * dpos2));
+  if constexpr (MAT != 0) {
+    const float dw0 = dw[0] * w[1] * w[2] * g.inv_dx;
+    const float dw1 = w[0] * dw[1] * w[2] * g.inv_dx;
+    const float dw2 = w[0] * w[1] * dw[2] * g.inv_dx;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) add[r] = add[r] + dt * (nvt[r][0] * dw0 + nvt[r][1] * dw1 + nvt[r][2] * dw2);
+  }
+  acc.x += add[0];
+  acc.y += add[1];
+  acc.z += add[2];
+  acc.w += wm;
+}
+
+// ------------------------------------------------------------------- P2G --
+// One workgroup per <= 256-particle chunk of one tile, one particle per lane.
+// Contributions are accumulated into the tile's 10^3-node window in LDS as
+// 64-bit fixed point with ds_add_u64: on gfx950 an f32 LDS atomic to distinct
+// addresses costs ~192 cycles per wave-instruction, the u64 integer add ~9
+// (tools/ubench/lds_atomics.hip).  The scale 2^S is chosen per chunk from a
+// bound on its contributions so that no node sum can overflow and every
+// contribution keeps >= 2^53 relative resolution; integer sums are exact and
+// order-independent.  The window is converted back to f32 once and written to
+// the chunk's slot with plain coalesced stores (no global atomics); k_grid sums
+// the <= 8 windows covering each node.
+__device__ __forceinline__ long long to_fixed(float v, int S) {
+  const unsigned b = __float_as_uint(v);
+  const int e = (int)((b >> 23) & 0xffu);
+  const long long mant = (long long)((b & 0x7fffffu) | 0x800000u);
+  const int sh = e - 150 + S;  // |v| = mant * 2^(e-150)
+  long long r = sh >= 0 ? (mant << min(sh, 39)) : (sh > -25 ? (mant >> (-sh)) : 0LL);
+  r = (e == 0) ? 0LL : r;  // zero / denormal
+  return (b >> 31) ? -r : r;
+}
+
+template <int MAT>
+__global__ __launch_bounds__(256) void k_p2g(Particles ps, GridDims g, Tiles tl, ChunkIn ck,
+                                             const BcTable* __restrict__ bct, uint32_t mask, float dt, MatConsts mc,
+                                             float4* __restrict__ slots, float4* __restrict__ gacc) {
+  __shared__ unsigned long long s_acc[kWin * 4];
+  __shared__ float s_max[4];
   const int ng = g.ng;
+  const int nch = *ck.nchunk;
+  for (int w = blockIdx.x; w < nch; w += gridDim.x) {
+    const int t = ck.ctile[w];
+    const int first = ck.cfirst[w];
+    const int cnt = min(kChunk, ck.count[t] - (first - (ck.cfirst[ck.cbase[t]])));
+    const int k = threadIdx.x;
+    if (t == tl.ntiles) {
+      // particles outside the grid: bounds-checked global f32 atomics (reference UB region)
+      if (k < cnt) {
+        const int p = ck.list[first + k];
+        float x[3], v[3], C[3][3], m, nvt[3][3];
+        particle_front<MAT>(ps, p, bct, mask, dt, mc, x, v, C, m, nvt);
+        int base[3];
+        float fx[3], ww[3][3], dw[3][3];
+        bspline(x, g.inv_dx, base, fx, ww, dw);
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
+        for (int i = 0; i < 3; ++i)
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
+          for (int j = 0; j < 3; ++j)
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const int ix = base[0] + i, iy = base[1] + j, iz = base[2] + k;
-        const float dpos0 = ((float)i - fx[0]) * g.dx;
-        const float dpos1 = ((float)j - fx[1]) * g.dx;
-        const float dpos2 = ((float)k - fx[2]) * g.dx;
-        const float weight = w[0][i] * w[1][j] * w[2][k];
-        const float wm = weight * m;
-        float add[3];
+            for (int kk = 0; kk < 3; ++kk) {
+              const int ix = base[0] + i, iy = base[1] + j, iz = base[2] + kk;
+              if ((unsigned)ix < (unsigned)ng && (unsigned)iy < (unsigned)ng && (unsigned)iz < (unsigned)ng) {
+                float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+                p2g_term<MAT>(i, j, kk, fx, v, C, m, nvt, g, dt, a);
+                float* cell = reinterpret_cast<float*>(gacc + (((size_t)ix * ng + iy) * ng + iz));
+                unsafeAtomicAdd(cell + 0, a.x);
+                unsafeAtomicAdd(cell + 1, a.y);
+                unsafeAtomicAdd(cell + 2, a.z);
+                unsafeAtomicAdd(cell + 3, a.w);
+              }
+            }
+      }
+      continue;  // workgroup-uniform
+    }
+    const int tx = t / (tl.td * tl.td), ty = (t / tl.td) % tl.td, tz = t % tl.td;
+    for (int q = k; q < kWin * 4; q += kChunk) s_acc[q] = 0ull;
+    float x[3], v[3], C[3][3], m = 0.f, nvt[3][3];
+    int base[3] = {0, 0, 0};
+    float fx[3] = {1.f, 1.f, 1.f}, ww[3][3], dw[3][3];
+    float bound = 0.f;
+    if (k < cnt) {
+      const int p = ck.list[first + k];
+      particle_front<MAT>(ps, p, bct, mask, dt, mc, x, v, C, m, nvt);
+      bspline(x, g.inv_dx, base, fx, ww, dw);
+      float vm = 0.f, cm = 0.f, sm = 0.f;
 #pragma unroll
-        for (int r = 0; r < 3; ++r) add[r] = wm * (v[r] + (C[r][0] * dpos0 + C[r][1] * dpos1 + C[r][2] * dpos2));
-        if constexpr (MAT != 0) {
-          const float dw0 = dw[0][i] * w[1][j] * w[2][k] * g.inv_dx;
-          const float dw1 = w[0][i] * dw[1][j] * w[2][k] * g.inv_dx;
-          const float dw2 = w[0][i] * w[1][j] * dw[2][k] * g.inv_dx;
+      for (int r = 0; r < 3; ++r) {
+        vm = fmaxf(vm, fabsf(v[r]));
 #pragma unroll
-          for (int r = 0; r < 3; ++r) add[r] = add[r] + dt * (nvt[r][0] * dw0 + nvt[r][1] * dw1 + nvt[r][2] * dw2);
-        }
-        if ((unsigned)ix < (unsigned)ng && (unsigned)iy < (unsigned)ng && (unsigned)iz < (unsigned)ng) {
-          float* cell = reinterpret_cast<float*>(gacc + (((size_t)ix * ng + iy) * ng + iz));
-          unsafeAtomicAdd(cell + 0, add[0]);
-          unsafeAtomicAdd(cell + 1, add[1]);
-          unsafeAtomicAdd(cell + 2, add[2]);
-          unsafeAtomicAdd(cell + 3, wm);
+        for (int c = 0; c < 3; ++c) {
+          cm = fmaxf(cm, fabsf(C[r][c]));
+          sm = fmaxf(sm, fabsf(nvt[r][c]));
         }
       }
+      // |m v + m C dpos| <= m (|v| + 3 * 1.5 dx |C|), |dt nvt dweight| <= dt * 3 * 1.5 inv_dx |nvt|
+      bound = fmaxf(m, m * (vm + 4.5f * g.dx * cm) + dt * 4.5f * g.inv_dx * sm) * 1.01f;
     }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) bound = fmaxf(bound, __shfl_xor(bound, o));
+    if ((k & 63) == 0) s_max[k >> 6] = bound;
+    __syncthreads();  // also orders the window zeroing before the adds
+    const float bmax = fmaxf(fmaxf(s_max[0], s_max[1]), fmaxf(s_max[2], s_max[3]));
+    int ebits;
+    frexpf(bmax, &ebits);                     // bmax < 2^ebits
+    const int S = bmax > 0.f ? 53 - ebits : 0;  // 256 * bmax * 2^S < 2^62
+    if (k < cnt) {
+      const int l0 = base[0] - tx * kTile, l1 = base[1] - ty * kTile, l2 = base[2] - tz * kTile;
+      unsigned long long* cell0 = s_acc + 4 * ((l0 * kTW + l1) * kTW + l2);
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+          for (int kk = 0; kk < 3; ++kk) {
+            float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+            p2g_term<MAT>(i, j, kk, fx, v, C, m, nvt, g, dt, a);
+            unsigned long long* cell = cell0 + 4 * ((i * kTW + j) * kTW + kk);
+            __hip_atomic_fetch_add(cell + 0, (unsigned long long)to_fixed(a.x, S), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(cell + 1, (unsigned long long)to_fixed(a.y, S), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(cell + 2, (unsigned long long)to_fixed(a.z, S), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(cell + 3, (unsigned long long)to_fixed(a.w, S), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+    }
+    __syncthreads();
+    float* dst = reinterpret_cast<float*>(slots + (size_t)w * kWin);
+    for (int q = k; q < kWin * 4; q += kChunk) dst[q] = (float)ldexp((double)(long long)s_acc[q], -S);
+    __syncthreads();  // LDS reuse by the next chunk
   }
 }
 
 // ------------------------------------------------------------------ grid --
-// grid_normalization_and_gravity (utils.py:177-183) + grid_postprocess list
-// (solver.py:41-46): BasicBC.apply (boundary_conditions.py:23-27) and
-// MPM_Collider.collide (collider.py:13-44), pointwise, in list order.
-__global__ __launch_bounds__(256) void k_grid(float4* __restrict__ gacc, float4* __restrict__ gvel, GridDims g,
-                                              const BcTable* __restrict__ bct, uint32_t mask, float dt, float gx,
-                                              float gy, float gz, int keep, const Box* __restrict__ box,
-                                              Box* __restrict__ next_box) {
-  // reset the box the following G2P accumulates into (stream order makes this safe)
+// Sum of the chunk windows covering each node (fixed order: deterministic),
+// then grid_normalization_and_gravity (utils.py:177-183) and the
+// grid_postprocess list (solver.py:41-46): BasicBC.apply
+// (boundary_conditions.py:23-27) / MPM_Collider.collide (collider.py:13-44),
+// pointwise, in list order.
+struct GridStep {
+  float dt, gx, gy, gz;
+  uint32_t mask;
+  int keep;
+};
+
+__global__ __launch_bounds__(256) void k_grid(GridDims g, Tiles tl, ChunkIn ck, const float4* __restrict__ slots,
+                                              float4* __restrict__ gacc, float4* __restrict__ gvel,
+                                              const BcTable* __restrict__ bct, GridStep gs,
+                                              const Box* __restrict__ box, Box* __restrict__ next_box,
+                                              int* __restrict__ count_next) {
+  // housekeeping for the G2P that follows (stream order makes this safe)
   if (blockIdx.x == 0 && threadIdx.x < 3) {
     next_box->lo[threadIdx.x] = INT_MAX;
     next_box->hi[threadIdx.x] = INT_MIN;
   }
-  const int ng = g.ng;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t <= tl.ntiles; t += gridDim.x * blockDim.x) count_next[t] = 0;
+
+  const int ng = g.ng, td = tl.td;
+  const bool outside = ck.count[tl.ntiles] > 0;
   const int lo0 = box->lo[0], lo1 = box->lo[1], lo2 = box->lo[2];
   const int e0 = box->hi[0] - lo0 + 1, e1 = box->hi[1] - lo1 + 1, e2 = box->hi[2] - lo2 + 1;
   if (e0 <= 0 || e1 <= 0 || e2 <= 0) return;
   const long total = (long)e0 * e1 * e2;
-  for (long t = (long)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-    const int k = lo2 + (int)(t % e2);
-    const long t2 = t / e2;
-    const int j = lo1 + (int)(t2 % e1);
-    const int i = lo0 + (int)(t2 / e1);
+  for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
+    const int k = lo2 + (int)(q % e2);
+    const long q2 = q / e2;
+    const int j = lo1 + (int)(q2 % e1);
+    const int i = lo0 + (int)(q2 / e1);
     const size_t idx = ((size_t)i * ng + j) * ng + k;
-    const float4 a = gacc[idx];
-    if (!keep) gacc[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int ti = i / kTile, tj = j / kTile, tk = k / kTile;
+    const int li = i - ti * kTile, lj = j - tj * kTile, lk = k - tk * kTile;
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int ax = 0; ax < 2; ++ax) {
+      if (ax && !(li < 2 && ti > 0)) continue;
+#pragma unroll
+      for (int ay = 0; ay < 2; ++ay) {
+        if (ay && !(lj < 2 && tj > 0)) continue;
+#pragma unroll
+        for (int az = 0; az < 2; ++az) {
+          if (az && !(lk < 2 && tk > 0)) continue;
+          const int t = ((ti - ax) * td + (tj - ay)) * td + (tk - az);
+          const int c = ck.count[t];
+          if (c > 0) {
+            const int loc = ((li + kTile * ax) * kTW + (lj + kTile * ay)) * kTW + (lk + kTile * az);
+            const int c0 = ck.cbase[t], nc = (c + kChunk - 1) / kChunk;
+            for (int w = c0; w < c0 + nc; ++w) {
+              const float4 s = slots[(size_t)w * kWin + loc];
+              a.x += s.x;
+              a.y += s.y;
+              a.z += s.z;
+              a.w += s.w;
+            }
+          }
+        }
+      }
+    }
+    if (outside || gs.keep) {
+      const float4 o = gacc[idx];
+      a.x += o.x;
+      a.y += o.y;
+      a.z += o.z;
+      a.w += o.w;
+      gacc[idx] = gs.keep ? a : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     float v[3] = {0.f, 0.f, 0.f};
     if (a.w > 1e-15f) {
-      v[0] = a.x / a.w + dt * gx;
-      v[1] = a.y / a.w + dt * gy;
-      v[2] = a.z / a.w + dt * gz;
+      v[0] = a.x / a.w + gs.dt * gs.gx;
+      v[1] = a.y / a.w + gs.dt * gs.gy;
+      v[2] = a.z / a.w + gs.dt * gs.gz;
       const int nops = bct->n_ops;
       for (int o = 0; o < nops; ++o) {
         const GridOp& op = bct->op[o];
         const float p0 = (float)i * g.dx, p1 = (float)j * g.dx, p2 = (float)k * g.dx;
         if (op.kind == 0) {
-          if (!((mask >> op.bit) & 1u)) continue;
+          if (!((gs.mask >> op.bit) & 1u)) continue;
           if (fabsf(p0 - op.a[0]) < op.b[0] && fabsf(p1 - op.a[1]) < op.b[1] && fabsf(p2 - op.a[2]) < op.b[2]) {
             v[0] = 0.f;
             v[1] = 0.f;
@@ -425,95 +412,90 @@ __global__ __launch_bounds__(256) void k_grid(float4* __restrict__ gacc, float4*
 }
 
 // ------------------------------------------------------------------- G2P --
-__device__ __forceinline__ int wave_min(int v) {
+// g2p (utils.py:218-282) without the dead update_cov; the gather
+// reads through `fetch(base, i, j, k)` (LDS window or global v_out).
+template <typename Fetch>
+__device__ __forceinline__ void g2p_particle(const Particles& ps, int p, const GridDims& g, float dt, Fetch fetch,
+                                             float (&xn)[3]) {
+  float x[3];
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
-  return v;
-}
-__device__ __forceinline__ int wave_max(int v) {
+  for (int d = 0; d < 3; ++d) x[d] = ps.ld(PX + d, p);
+  int base[3];
+  float fx[3], w[3][3], dw[3][3];
+  bspline(x, g.inv_dx, base, fx, w, dw);
+  float nv[3] = {0.f, 0.f, 0.f}, nC[3][3], nF[3][3];
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
-  return v;
-}
-
-// g2p (utils.py:218-282) without the dead update_cov
-__global__ __launch_bounds__(256) void k_g2p(Particles ps, GridDims g, const float4* __restrict__ gvel, float dt,
-                                             Box* __restrict__ next_box) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool live = p < ps.n;
-  int blo[3] = {INT_MAX, INT_MAX, INT_MAX}, bhi[3] = {INT_MIN, INT_MIN, INT_MIN};
-  if (live) {
-    float x[3];
+  for (int r = 0; r < 3; ++r)
 #pragma unroll
-    for (int d = 0; d < 3; ++d) x[d] = ps.at(PX + d, p);
-    int base[3];
-    float fx[3], w[3][3], dw[3][3];
-    bspline(x, g.inv_dx, base, fx, w, dw);
-    const int ng = g.ng;
-    float nv[3] = {0.f, 0.f, 0.f}, nC[3][3], nF[3][3];
+    for (int c = 0; c < 3; ++c) {
+      nC[r][c] = 0.f;
+      nF[r][c] = 0.f;
+    }
+  // The i-slab loop stays rolled (weights picked by select) so that only one
+  // 9-node slab of gathers is live: the fully unrolled 27-node form hoists all
+  // 27 loads and needs > 256 VGPRs (1 wave/SIMD).  Same operations and
+  // accumulation order (i, j, k) as the reference.
+#pragma unroll 1
+  for (int i = 0; i < 3; ++i) {
+    const float w0 = i == 0 ? w[0][0] : (i == 1 ? w[0][1] : w[0][2]);
+    const float dw0 = i == 0 ? dw[0][0] : (i == 1 ? dw[0][1] : dw[0][2]);
+    const float dp0 = (float)i - fx[0];
 #pragma unroll
-    for (int r = 0; r < 3; ++r)
+    for (int j = 0; j < 3; ++j) {
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        nC[r][c] = 0.f;
-        nF[r][c] = 0.f;
-      }
+      for (int k = 0; k < 3; ++k) {
+        const float4 gv = fetch(base, i, j, k);
+        const float gvv[3] = {gv.x, gv.y, gv.z};
+        const float dpos[3] = {dp0, (float)j - fx[1], (float)k - fx[2]};
+        const float weight = w0 * w[1][j] * w[2][k];
+        const float cw = weight * g.inv_dx * 4.0f;
+        const float dwt[3] = {dw0 * w[1][j] * w[2][k] * g.inv_dx, w0 * dw[1][j] * w[2][k] * g.inv_dx,
+                              w0 * w[1][j] * dw[2][k] * g.inv_dx};
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+        for (int r = 0; r < 3; ++r) {
+          nv[r] += gvv[r] * weight;
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const int ix = base[0] + i, iy = base[1] + j, iz = base[2] + k;
-          float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
-          if ((unsigned)ix < (unsigned)ng && (unsigned)iy < (unsigned)ng && (unsigned)iz < (unsigned)ng)
-            gv = gvel[((size_t)ix * ng + iy) * ng + iz];
-          const float gvv[3] = {gv.x, gv.y, gv.z};
-          const float dpos[3] = {(float)i - fx[0], (float)j - fx[1], (float)k - fx[2]};
-          const float weight = w[0][i] * w[1][j] * w[2][k];
-          const float cw = weight * g.inv_dx * 4.0f;
-          const float dwt[3] = {dw[0][i] * w[1][j] * w[2][k] * g.inv_dx, w[0][i] * dw[1][j] * w[2][k] * g.inv_dx,
-                                w[0][i] * w[1][j] * dw[2][k] * g.inv_dx};
-#pragma unroll
-          for (int r = 0; r < 3; ++r) {
-            nv[r] += gvv[r] * weight;
-#pragma unroll
-            for (int c = 0; c < 3; ++c) {
-              nC[r][c] += gvv[r] * dpos[c] * cw;
-              nF[r][c] += gvv[r] * dwt[c];
-            }
+          for (int c = 0; c < 3; ++c) {
+            nC[r][c] += gvv[r] * dpos[c] * cw;
+            nF[r][c] += gvv[r] * dwt[c];
           }
         }
       }
     }
-    float F[3][3];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) F[i / 3][i % 3] = ps.at(PF + i, p);
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      ps.at(PV + d, p) = nv[d];
-      x[d] += dt * nv[d];
-      ps.at(PX + d, p) = x[d];
-    }
-#pragma unroll
-    for (int i = 0; i < 9; ++i) ps.at(PC + i, p) = nC[i / 3][i % 3];
-#pragma unroll
-    for (int r = 0; r < 3; ++r)
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const float a0 = (r == 0 ? 1.0f : 0.0f) + nF[r][0] * dt;
-        const float a1 = (r == 1 ? 1.0f : 0.0f) + nF[r][1] * dt;
-        const float a2 = (r == 2 ? 1.0f : 0.0f) + nF[r][2] * dt;
-        ps.at(PF + r * 3 + c, p) = a0 * F[0][c] + a1 * F[1][c] + a2 * F[2][c];
-      }
-    // node box touched by the next P2G (base..base+2 of the new position)
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      const int b = (int)(x[d] * g.inv_dx - 0.5f);
-      blo[d] = max(0, b);
-      bhi[d] = min(g.ng - 1, b + 2);
-    }
   }
+  float F[3][3];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) F[i / 3][i % 3] = ps.ld(PF + i, p);
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    ps.st(PV + d, p, nv[d]);
+    xn[d] = x[d] + dt * nv[d];
+    ps.st(PX + d, p, xn[d]);
+  }
+#pragma unroll
+  for (int i = 0; i < 9; ++i) ps.st(PC + i, p, nC[i / 3][i % 3]);
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float a0 = (r == 0 ? 1.0f : 0.0f) + nF[r][0] * dt;
+      const float a1 = (r == 1 ? 1.0f : 0.0f) + nF[r][1] * dt;
+      const float a2 = (r == 2 ? 1.0f : 0.0f) + nF[r][2] * dt;
+      ps.st(PF + r * 3 + c, p, a0 * F[0][c] + a1 * F[1][c] + a2 * F[2][c]);
+    }
+}
+
+// node box the next P2G touches (base..base+2 of the new position)
+__device__ __forceinline__ void box_accumulate(const float (&xn)[3], const GridDims& g, int (&blo)[3], int (&bhi)[3]) {
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    const int b = (int)(xn[d] * g.inv_dx - 0.5f);
+    blo[d] = min(blo[d], max(0, b));
+    bhi[d] = max(bhi[d], min(g.ng - 1, b + 2));
+  }
+}
+
+__device__ __forceinline__ void box_flush(const int (&blo)[3], const int (&bhi)[3], Box* next_box) {
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
     const int lo = wave_min(blo[d]);
@@ -525,7 +507,173 @@ __global__ __launch_bounds__(256) void k_g2p(Particles ps, GridDims g, const flo
   }
 }
 
-// box ping-pong: the box written by G2P of substep s is read by k_grid of s+1
+// One workgroup per chunk: stage the tile's 10^3 window of v_out in LDS,
+// gather, update the particle, and bin it into the tile of its new base cell.
+// Moves to the 27 neighbour tiles are counted in LDS and reserved with <= 27
+// global atomics per chunk; farther moves / leaving the grid use one atomic.
+__global__ __launch_bounds__(256) void k_g2p(Particles ps, GridDims g, Tiles tl, ChunkIn ck, BinOut bo,
+                                                const float4* __restrict__ gvel, float dt,
+                                                Box* __restrict__ next_box) {
+  __shared__ float4 s_win[kWin];
+  __shared__ int s_cnt[27];
+  __shared__ int s_base[27];
+  const int ng = g.ng;
+  int blo[3] = {INT_MAX, INT_MAX, INT_MAX}, bhi[3] = {INT_MIN, INT_MIN, INT_MIN};
+  stamp(1, 0);
+  const int nch = *ck.nchunk;
+  for (int w = blockIdx.x; w < nch; w += gridDim.x) {
+    const int t = ck.ctile[w];
+    const int first = ck.cfirst[w];
+    const int cnt = min(kChunk, ck.count[t] - (first - (ck.cfirst[ck.cbase[t]])));
+    const int k = threadIdx.x;
+    if (t == tl.ntiles) {
+      if (k < cnt) {
+        const int p = ck.list[first + k];
+        float xn[3];
+        g2p_particle(ps, p, g, dt,
+                     [&](const int (&base)[3], int i, int j, int kk) {
+                       const int ix = base[0] + i, iy = base[1] + j, iz = base[2] + kk;
+                       float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
+                       if ((unsigned)ix < (unsigned)ng && (unsigned)iy < (unsigned)ng && (unsigned)iz < (unsigned)ng)
+                         gv = gvel[((size_t)ix * ng + iy) * ng + iz];
+                       return gv;
+                     },
+                     xn);
+        box_accumulate(xn, g, blo, bhi);
+        int tc[3];
+        const int nt = tile_of(xn, g, tl, tc);
+        bo.ptile[p] = nt;
+        bo.pslot[p] = atomicAdd(&bo.count[nt], 1);
+      }
+      continue;  // workgroup-uniform
+    }
+    const int tx = t / (tl.td * tl.td), ty = (t / tl.td) % tl.td, tz = t % tl.td;
+    const int lo0 = tx * kTile, lo1 = ty * kTile, lo2 = tz * kTile;
+    for (int q = k; q < kWin; q += kChunk) {
+      const int a = q / (kTW * kTW), b = (q / kTW) % kTW, c = q % kTW;
+      const int ix = lo0 + a, iy = lo1 + b, iz = lo2 + c;
+      float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ix < ng && iy < ng && iz < ng) gv = gvel[((size_t)ix * ng + iy) * ng + iz];
+      s_win[q] = gv;
+    }
+    if (k < 27) s_cnt[k] = 0;
+    __syncthreads();
+    if (w == (int)blockIdx.x) stamp(1, 2);
+    int p = -1, code = -1, lslot = 0, nt = -1;
+    if (k < cnt) {
+      p = ck.list[first + k];
+      float xn[3];
+      g2p_particle(ps, p, g, dt,
+                   [&](const int (&base)[3], int i, int j, int kk) {
+                     const float4* wb = s_win + ((base[0] - lo0) * kTW + (base[1] - lo1)) * kTW + (base[2] - lo2);
+                     return wb[(i * kTW + j) * kTW + kk];
+                   },
+                   xn);
+      box_accumulate(xn, g, blo, bhi);
+      int tc[3];
+      nt = tile_of(xn, g, tl, tc);
+      if (nt < tl.ntiles) {
+        const int d0 = tc[0] - tx, d1 = tc[1] - ty, d2 = tc[2] - tz;
+        if (abs(d0) <= 1 && abs(d1) <= 1 && abs(d2) <= 1) {
+          code = (d0 + 1) * 9 + (d1 + 1) * 3 + (d2 + 1);
+          lslot = atomicAdd(&s_cnt[code], 1);
+        }
+      }
+    }
+    __syncthreads();
+    if (w == (int)blockIdx.x) stamp(1, 3);
+    if (k < 27) {
+      const int c = s_cnt[k];
+      if (c > 0) {
+        const int ntile = ((tx + k / 9 - 1) * tl.td + (ty + (k / 3) % 3 - 1)) * tl.td + (tz + k % 3 - 1);
+        s_base[k] = atomicAdd(&bo.count[ntile], c);
+      }
+    }
+    __syncthreads();
+    if (w == (int)blockIdx.x) stamp(1, 4);
+    if (p >= 0) {
+      bo.ptile[p] = nt;
+      bo.pslot[p] = code >= 0 ? s_base[code] + lslot : atomicAdd(&bo.count[nt], 1);
+    }
+    __syncthreads();  // LDS reuse by the next chunk
+  }
+  box_flush(blo, bhi, next_box);
+  stamp(1, 1);
+}
+
+// ------------------------------------------------------- binning passes --
+// bin every particle by its current x (set_particles / resort / set x) and
+// accumulate the live node box
+__global__ __launch_bounds__(256) void k_bin_all(Particles ps, GridDims g, Tiles tl, BinOut bo, Box* box) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  int blo[3] = {INT_MAX, INT_MAX, INT_MAX}, bhi[3] = {INT_MIN, INT_MIN, INT_MIN};
+  if (p < ps.n) {
+    float x[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) x[d] = ps.ld(PX + d, p);
+    box_accumulate(x, g, blo, bhi);
+    int tc[3];
+    const int t = tile_of(x, g, tl, tc);
+    bo.ptile[p] = t;
+    bo.pslot[p] = atomicAdd(&bo.count[t], 1);
+  }
+  box_flush(blo, bhi, box);
+}
+
+// One workgroup (1024 lanes): per-tile counts -> list offsets (exclusive scan)
+// and the chunk list (ceil(count/256) chunks per tile, pseudo-tile last).
+struct ChunkOut {
+  int* cstart;  // [ntiles + 1] first list entry of each tile
+  int* cbase;   // [ntiles + 1]
+  int* ctile;   // [max_chunks]
+  int* cfirst;  // [max_chunks]
+  int* nchunk;  // [1]
+};
+__global__ __launch_bounds__(1024) void k_scan_tiles(Tiles tl, const int* __restrict__ count, ChunkOut co) {
+  __shared__ int s_a[1024], s_b[1024];
+  const int E = tl.ntiles + 1;
+  const int per = (E + 1023) / 1024;
+  const int t0 = threadIdx.x * per, t1 = min(E, t0 + per);
+  int sa = 0, sb = 0;
+  for (int t = t0; t < t1; ++t) {
+    const int c = count[t];
+    sa += c;
+    sb += (c + kChunk - 1) / kChunk;
+  }
+  s_a[threadIdx.x] = sa;
+  s_b[threadIdx.x] = sb;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
+    const int xa = threadIdx.x >= o ? s_a[threadIdx.x - o] : 0;
+    const int xb = threadIdx.x >= o ? s_b[threadIdx.x - o] : 0;
+    __syncthreads();
+    s_a[threadIdx.x] += xa;
+    s_b[threadIdx.x] += xb;
+    __syncthreads();
+  }
+  int oa = s_a[threadIdx.x] - sa, ob = s_b[threadIdx.x] - sb;
+  for (int t = t0; t < t1; ++t) {
+    const int c = count[t];
+    const int nc = (c + kChunk - 1) / kChunk;
+    co.cstart[t] = oa;
+    co.cbase[t] = ob;
+    for (int k = 0; k < nc; ++k) {
+      co.ctile[ob + k] = t;
+      co.cfirst[ob + k] = oa + k * kChunk;
+    }
+    oa += c;
+    ob += nc;
+  }
+  if (threadIdx.x == 1023) *co.nchunk = s_b[1023];
+}
+
+__global__ __launch_bounds__(256) void k_scatter(int n, const int* __restrict__ ptile, const int* __restrict__ pslot,
+                                                 const int* __restrict__ cstart, int* __restrict__ list) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  list[cstart[ptile[p]] + pslot[p]] = p;
+}
+
 __global__ void k_box_reset(Box* b) {
   if (threadIdx.x < 3) {
     b->lo[threadIdx.x] = INT_MAX;
@@ -540,29 +688,6 @@ __global__ void k_box_full(Box* b, int ng) {
   }
 }
 
-// particle box from the current positions (used after set/set_field)
-__global__ __launch_bounds__(256) void k_box_from_x(Particles ps, GridDims g, Box* box) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  int blo[3] = {INT_MAX, INT_MAX, INT_MAX}, bhi[3] = {INT_MIN, INT_MIN, INT_MIN};
-  if (p < ps.n) {
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-      const int b = (int)(ps.at(PX + d, p) * g.inv_dx - 0.5f);
-      blo[d] = max(0, b);
-      bhi[d] = min(g.ng - 1, b + 2);
-    }
-  }
-#pragma unroll
-  for (int d = 0; d < 3; ++d) {
-    const int lo = wave_min(blo[d]);
-    const int hi = wave_max(bhi[d]);
-    if ((threadIdx.x & 63) == 0 && lo <= hi) {
-      atomicMin(&box->lo[d], lo);
-      atomicMax(&box->hi[d], hi);
-    }
-  }
-}
-
 // ------------------------------------------------------------ postprocess --
 // compute_cov_from_F (utils.py:401-433) + compute_R_from_F (utils.py:376-398)
 __global__ __launch_bounds__(256) void k_postprocess(Particles ps) {
@@ -570,9 +695,9 @@ __global__ __launch_bounds__(256) void k_postprocess(Particles ps) {
   if (p >= ps.n) return;
   float F[3][3];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) F[i / 3][i % 3] = ps.at(PF + i, p);
-  const float a0 = ps.at(PICOV + 0, p), a1 = ps.at(PICOV + 1, p), a2 = ps.at(PICOV + 2, p);
-  const float a3 = ps.at(PICOV + 3, p), a4 = ps.at(PICOV + 4, p), a5 = ps.at(PICOV + 5, p);
+  for (int i = 0; i < 9; ++i) F[i / 3][i % 3] = ps.ld(PF + i, p);
+  const float a0 = ps.ld(PICOV + 0, p), a1 = ps.ld(PICOV + 1, p), a2 = ps.ld(PICOV + 2, p);
+  const float a3 = ps.ld(PICOV + 3, p), a4 = ps.ld(PICOV + 4, p), a5 = ps.ld(PICOV + 5, p);
   const float A[3][3] = {{a0, a1, a2}, {a1, a3, a4}, {a2, a4, a5}};
   float T[3][3], Cv[3][3];
 #pragma unroll
@@ -580,12 +705,12 @@ __global__ __launch_bounds__(256) void k_postprocess(Particles ps) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) T[i][j] = F[i][0] * A[0][j] + F[i][1] * A[1][j] + F[i][2] * A[2][j];
   mmT(T, F, Cv);
-  ps.at(PCOV + 0, p) = Cv[0][0];
-  ps.at(PCOV + 1, p) = Cv[0][1];
-  ps.at(PCOV + 2, p) = Cv[0][2];
-  ps.at(PCOV + 3, p) = Cv[1][1];
-  ps.at(PCOV + 4, p) = Cv[1][2];
-  ps.at(PCOV + 5, p) = Cv[2][2];
+  ps.st(PCOV + 0, p, Cv[0][0]);
+  ps.st(PCOV + 1, p, Cv[0][1]);
+  ps.st(PCOV + 2, p, Cv[0][2]);
+  ps.st(PCOV + 3, p, Cv[1][1]);
+  ps.st(PCOV + 4, p, Cv[1][2]);
+  ps.st(PCOV + 5, p, Cv[2][2]);
   float U[3][3], V[3][3], s[3];
   svd3(F, U, s, V);
   if (det3(U) < 0.f) {
@@ -603,7 +728,7 @@ __global__ __launch_bounds__(256) void k_postprocess(Particles ps) {
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
-    for (int j = 0; j < 3; ++j) ps.at(PR + i * 3 + j, p) = R[j][i];  // particle_R = (U V^T)^T
+    for (int j = 0; j < 3; ++j) ps.st(PR + i * 3 + j, p, R[j][i]);  // particle_R = (U V^T)^T
 }
 
 // ------------------------------------------------------------ init / io --
@@ -620,30 +745,30 @@ __global__ __launch_bounds__(256) void k_init(Particles ps, InitArgs a) {
   const int o = a.orig[p];
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
-    ps.at(PX + d, p) = a.x[(size_t)o * 3 + d];
-    ps.at(PV + d, p) = a.v ? a.v[(size_t)o * 3 + d] : 0.0f;
+    ps.st(PX + d, p, a.x[(size_t)o * 3 + d]);
+    ps.st(PV + d, p, a.v ? a.v[(size_t)o * 3 + d] : 0.0f);
   }
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
-    ps.at(PC + i, p) = 0.0f;
-    ps.at(PF + i, p) = (i % 4 == 0) ? 1.0f : 0.0f;
-    ps.at(PR + i, p) = 0.0f;
+    ps.st(PC + i, p, 0.0f);
+    ps.st(PF + i, p, (i % 4 == 0) ? 1.0f : 0.0f);
+    ps.st(PR + i, p, 0.0f);
   }
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     const float c = a.cov6[(size_t)o * 6 + i];
-    ps.at(PICOV + i, p) = c;
-    ps.at(PCOV + i, p) = c;
+    ps.st(PICOV + i, p, c);
+    ps.st(PCOV + i, p, c);
   }
   const float vol = a.vol[o];
-  ps.at(PVOL, p) = vol;
-  ps.at(PMASS, p) = a.density * vol;
+  ps.st(PVOL, p, vol);
+  ps.st(PMASS, p, a.density * vol);
   // utils.py:349-362 in f32
   const float E = powf(10.0f, a.logE);
   const float nu = 0.49f / (1.0f + expf(-a.y));
-  ps.at(PMU, p) = E / (2.0f * (1.0f + nu));
-  ps.at(PLAM, p) = E * nu / ((1.0f + nu) * (1.0f - 2.0f * nu));
-  ps.at(PYLD, p) = a.yield0;
+  ps.st(PMU, p, E / (2.0f * (1.0f + nu)));
+  ps.st(PLAM, p, E * nu / ((1.0f + nu) * (1.0f - 2.0f * nu)));
+  ps.st(PYLD, p, a.yield0);
 }
 
 __global__ __launch_bounds__(256) void k_get(Particles ps, const int* __restrict__ orig, int plane0, int width,
@@ -651,7 +776,7 @@ __global__ __launch_bounds__(256) void k_get(Particles ps, const int* __restrict
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= ps.n) return;
   const size_t o = (size_t)orig[p] * width;
-  for (int j = 0; j < width; ++j) out[o + j] = ps.at(plane0 + j, p);
+  for (int j = 0; j < width; ++j) out[o + j] = ps.ld(plane0 + j, p);
 }
 
 __global__ __launch_bounds__(256) void k_set(Particles ps, const int* __restrict__ orig, int plane0, int width,
@@ -659,7 +784,7 @@ __global__ __launch_bounds__(256) void k_set(Particles ps, const int* __restrict
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= ps.n) return;
   const size_t o = (size_t)orig[p] * width;
-  for (int j = 0; j < width; ++j) ps.at(plane0 + j, p) = in[o + j];
+  for (int j = 0; j < width; ++j) ps.st(plane0 + j, p, in[o + j]);
 }
 
 __global__ __launch_bounds__(256) void k_world_out(Particles ps, const int* __restrict__ orig, float half, float s,
@@ -671,13 +796,13 @@ __global__ __launch_bounds__(256) void k_world_out(Particles ps, const int* __re
   const float c[3] = {c0, c1, c2};
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
-    float w = (ps.at(PX + d, p) - half) / s + c[d];  // grid2world, transform_utils.py:19
+    float w = (ps.ld(PX + d, p) - half) / s + c[d];  // grid2world, transform_utils.py:19
     if (render) w = c[d] + (w - 1.0f) / 1.0f;        // render_frame, main.py:139-144 (scale 1.0)
     mo[o * 3 + d] = w;
   }
   const float ss = s * s;
 #pragma unroll
-  for (int i = 0; i < 6; ++i) co[o * 6 + i] = ps.at(PCOV + i, p) / ss;  // transform_utils.py:20
+  for (int i = 0; i < 6; ++i) co[o * 6 + i] = ps.ld(PCOV + i, p) / ss;  // transform_utils.py:20
 }
 
 __global__ void k_grid_get(const float4* __restrict__ src, size_t nn, int which, float* __restrict__ out) {
@@ -691,6 +816,47 @@ __global__ void k_grid_get(const float4* __restrict__ src, size_t nn, int which,
       out[i * 3 + 2] = a.z;
     }
   }
+}
+
+// ------------------------------------------------------- spatial resort --
+__device__ __forceinline__ uint32_t spread10(uint32_t v) {
+  v &= 0x3ffu;
+  v = (v | (v << 16)) & 0x030000ffu;
+  v = (v | (v << 8)) & 0x0300f00fu;
+  v = (v | (v << 4)) & 0x030c30c3u;
+  v = (v | (v << 2)) & 0x09249249u;
+  return v;
+}
+
+// 30-bit Morton key of each particle's base cell (clamped to [0, 1023]^3)
+__global__ __launch_bounds__(256) void k_morton(Particles ps, float inv_dx, uint32_t* __restrict__ keys,
+                                                int* __restrict__ idx) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= ps.n) return;
+  uint32_t c[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    const float gp = ps.ld(PX + d, p) * inv_dx - 0.5f;
+    c[d] = (uint32_t)min(1023.0f, fmaxf(0.0f, gp));  // NaN -> 0
+  }
+  keys[p] = (spread10(c[0]) << 2) | (spread10(c[1]) << 1) | spread10(c[2]);
+  idx[p] = p;
+}
+
+// dst[plane][i] = src[plane][perm[i]] for every plane (blockIdx.y = plane)
+__global__ __launch_bounds__(256) void k_permute(const float* __restrict__ src, float* __restrict__ dst, int n, int np,
+                                                 const int* __restrict__ perm) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const size_t off = (size_t)blockIdx.y * np;
+  dst[off + i] = src[off + perm[i]];
+}
+
+__global__ __launch_bounds__(256) void k_permute_i(const int* __restrict__ src, int* __restrict__ dst, int n,
+                                                   const int* __restrict__ perm) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  dst[i] = src[perm[i]];
 }
 
 __global__ __launch_bounds__(256) void k_svd3(const float* __restrict__ A, int n, float* __restrict__ U,
@@ -765,19 +931,40 @@ struct gsmpm_mpm {
   gsmpm_mpm_params prm{};
   GridDims g{};
   MatConsts mc{};
+  Tiles tl{};
   int mat_kernel = 0;  // template code of k_p2g
   int n = 0, np = 0;
   float* planes = nullptr;
   int* orig = nullptr;
-  float4* gacc = nullptr;
-  float4* gvel = nullptr;
+  float4* gacc = nullptr;   // dense accumulator: outside-grid particles + KEEP_GRID readback
+  float4* gvel = nullptr;   // dense v_out
+  float4* slots = nullptr;  // [max_chunks][kWin] per-chunk P2G windows
+  // chunk work lists, one set per parity
+  int* count[2] = {nullptr, nullptr};   // [ntiles + 1]
+  int* cstart[2] = {nullptr, nullptr};  // [ntiles + 1]
+  int* cbase[2] = {nullptr, nullptr};   // [ntiles + 1]
+  int* ctile[2] = {nullptr, nullptr};   // [max_chunks]
+  int* cfirst[2] = {nullptr, nullptr};  // [max_chunks]
+  int* nchunk[2] = {nullptr, nullptr};  // [1]
+  int* list[2] = {nullptr, nullptr};    // [np]
+  int* ptile = nullptr;                 // [np]
+  int* pslot = nullptr;                 // [np]
   Box* boxes = nullptr;  // [0],[1] ping-pong live-node boxes, [2] whole grid
-  int cur_box = 0;
+  int cur_box = 0;       // parity of the boxes / buckets the next substep reads
   BcTable host_bc{};
   BcTable* dev_bc = nullptr;
   int n_bc = 0;
   bool has_particles = false;
   hipStream_t cap = nullptr;
+  // spatial resort (Morton order of the current cells), every resort_interval substeps
+  int resort_interval = 100;
+  long since_sort = 0;
+  float* planes_tmp = nullptr;
+  int* orig_tmp = nullptr;
+  uint32_t* sort_keys = nullptr;  // [2][np]
+  int* sort_idx = nullptr;        // [2][np]
+  void* sort_tmp = nullptr;
+  size_t sort_tmp_bytes = 0;
   std::map<std::vector<uint32_t>, hipGraphExec_t> graphs;
   std::map<std::vector<uint32_t>, int> graph_box_parity;
 };
@@ -788,42 +975,81 @@ void set_error(const std::string& m) { g_err = m; }
 
 static Particles particles_of(gsmpm_mpm* h) { return Particles{h->planes, h->n, h->np}; }
 
+static ChunkIn chunk_in(gsmpm_mpm* h, int c) {
+  return ChunkIn{h->count[c], h->cbase[c], h->ctile[c], h->cfirst[c], h->nchunk[c], h->list[c]};
+}
+static ChunkOut chunk_out(gsmpm_mpm* h, int c) {
+  return ChunkOut{h->cstart[c], h->cbase[c], h->ctile[c], h->cfirst[c], h->nchunk[c]};
+}
+static BinOut bin_out(gsmpm_mpm* h, int c) { return BinOut{h->count[c], h->ptile, h->pslot}; }
+
+static int p2g_grid(gsmpm_mpm* h) { return std::min(h->tl.max_chunks, 1024); }
+static int g2p_grid(gsmpm_mpm* h) { return std::min(h->tl.max_chunks, 512); }
+
 template <int MAT>
-static void launch_p2g(gsmpm_mpm* h, uint32_t mask, float dt, hipStream_t st) {
-  const int blocks = div_up(h->n, 256);
-  hipLaunchKernelGGL(k_p2g<MAT>, dim3(blocks), dim3(256), 0, st, particles_of(h), h->g, h->dev_bc, mask, dt, h->mc,
-                     h->gacc);
+static void launch_p2g(gsmpm_mpm* h, int c, uint32_t mask, float dt, hipStream_t st) {
+  hipLaunchKernelGGL(k_p2g<MAT>, dim3(p2g_grid(h)), dim3(kChunk), 0, st, particles_of(h), h->g, h->tl, chunk_in(h, c),
+                     h->dev_bc, mask, dt, h->mc, h->slots, h->gacc);
 }
 
-static int launch_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc, hipStream_t st, int& box_parity,
+// counts of parity c -> list offsets + chunk list, then the per-tile lists
+static int finish_binning(gsmpm_mpm* h, int c, hipStream_t st) {
+  hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, st, h->tl, h->count[c], chunk_out(h, c));
+  hipLaunchKernelGGL(k_scatter, dim3(div_up(h->n, 256)), dim3(256), 0, st, h->n, h->ptile, h->pslot, h->cstart[c],
+                     h->list[c]);
+  GSMPM_LAUNCH_CHECK();
+  return GSMPM_OK;
+}
+
+// (Re)build the chunk lists and the live box of parity `cur_box` from the current x.
+static int rebin(gsmpm_mpm* h, hipStream_t st) {
+  const int c = h->cur_box;
+  GSMPM_HIP(hipMemsetAsync(h->count[c], 0, sizeof(int) * (h->tl.ntiles + 1), st));
+  hipLaunchKernelGGL(k_box_reset, dim3(1), dim3(64), 0, st, h->boxes + c);
+  hipLaunchKernelGGL(k_bin_all, dim3(div_up(h->n, 256)), dim3(256), 0, st, particles_of(h), h->g, h->tl,
+                     bin_out(h, c), h->boxes + c);
+  GSMPM_LAUNCH_CHECK();
+  return finish_binning(h, c, st);
+}
+
+static int launch_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc, hipStream_t st, int& parity,
                            hipEvent_t* ev = nullptr, float* kernel_ms = nullptr) {
   const size_t nn = (size_t)h->g.ng * h->g.ng * h->g.ng;
   const bool keep = (h->prm.flags & GSMPM_FLAG_KEEP_GRID) != 0;
-  const float gx = (float)h->prm.gravity[0], gy = (float)h->prm.gravity[1], gz = (float)h->prm.gravity[2];
-  const int pblocks = div_up(h->n, 256);
-  // the node box is small in practice; cap the grid-stride launch at 8 blocks/CU
+  // the live node box is far smaller than n^3 in practice; cap the grid-stride launch
   const int gblocks = (int)std::min<long>(div_up((long)nn, 256), 2048);
+  GridStep gs;
+  gs.dt = dt;
+  gs.gx = (float)h->prm.gravity[0];
+  gs.gy = (float)h->prm.gravity[1];
+  gs.gz = (float)h->prm.gravity[2];
+  gs.keep = keep ? 1 : 0;
   for (int s = 0; s < nsub; ++s) {
     const uint32_t mask = bc ? bc[s] : 0xffffffffu;
-    Box* cur = h->boxes + box_parity;
-    Box* nxt = h->boxes + (box_parity ^ 1);
+    gs.mask = mask;
+    const int c = parity, nx = parity ^ 1;
     if (keep) GSMPM_HIP(hipMemsetAsync(h->gacc, 0, nn * sizeof(float4), st));
     if (ev) GSMPM_HIP(hipEventRecord(ev[0], st));
     switch (h->mat_kernel) {
-      case 0: launch_p2g<0>(h, mask, dt, st); break;
-      case 1: launch_p2g<1>(h, mask, dt, st); break;
-      case 2: launch_p2g<2>(h, mask, dt, st); break;
-      case 3: launch_p2g<3>(h, mask, dt, st); break;
-      default: launch_p2g<4>(h, mask, dt, st); break;
+      case 0: launch_p2g<0>(h, c, mask, dt, st); break;
+      case 1: launch_p2g<1>(h, c, mask, dt, st); break;
+      case 2: launch_p2g<2>(h, c, mask, dt, st); break;
+      case 3: launch_p2g<3>(h, c, mask, dt, st); break;
+      default: launch_p2g<4>(h, c, mask, dt, st); break;
     }
     GSMPM_LAUNCH_CHECK();
     if (ev) GSMPM_HIP(hipEventRecord(ev[1], st));
-    hipLaunchKernelGGL(k_grid, dim3(gblocks), dim3(256), 0, st, h->gacc, h->gvel, h->g, h->dev_bc, mask, dt, gx, gy,
-                       gz, keep ? 1 : 0, keep ? h->boxes + 2 : cur, nxt);
+    hipLaunchKernelGGL(k_grid, dim3(gblocks), dim3(256), 0, st, h->g, h->tl, chunk_in(h, c), h->slots, h->gacc, h->gvel,
+                       h->dev_bc, gs, keep ? h->boxes + 2 : h->boxes + c, h->boxes + nx, h->count[nx]);
     GSMPM_LAUNCH_CHECK();
     if (ev) GSMPM_HIP(hipEventRecord(ev[2], st));
-    hipLaunchKernelGGL(k_g2p, dim3(pblocks), dim3(256), 0, st, particles_of(h), h->g, h->gvel, dt, nxt);
+    hipLaunchKernelGGL(k_g2p, dim3(g2p_grid(h)), dim3(kChunk), 0, st, particles_of(h), h->g, h->tl, chunk_in(h, c),
+                       bin_out(h, nx), h->gvel, dt, h->boxes + nx);
     GSMPM_LAUNCH_CHECK();
+    {
+      int rc = finish_binning(h, nx, st);
+      if (rc) return rc;
+    }
     if (ev) {
       GSMPM_HIP(hipEventRecord(ev[3], st));
       GSMPM_HIP(hipEventSynchronize(ev[3]));
@@ -833,7 +1059,7 @@ static int launch_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc,
         kernel_ms[k] += ms;
       }
     }
-    box_parity ^= 1;
+    parity = nx;
   }
   return GSMPM_OK;
 }
@@ -881,12 +1107,37 @@ static uint64_t morton3(uint32_t a, uint32_t b, uint32_t c) {
   return (spread(a) << 2) | (spread(b) << 1) | spread(c);
 }
 
-static int refresh_box(gsmpm_mpm* h, hipStream_t st) {
-  Box* cur = h->boxes + h->cur_box;
-  hipLaunchKernelGGL(k_box_reset, dim3(1), dim3(64), 0, st, cur);
-  hipLaunchKernelGGL(k_box_from_x, dim3(div_up(h->n, 256)), dim3(256), 0, st, particles_of(h), h->g, cur);
+// Re-establish Morton order of the particles' current cells so the transfer
+// kernels' per-workgroup windows stay compact.  Only the storage order (and so
+// the float-atomic summation order) changes; `orig` keeps rows in caller order.
+static int resort(gsmpm_mpm* h, hipStream_t st) {
+  const int n = h->n, np = h->np;
+  if (!h->planes_tmp) {
+    GSMPM_HIP(hipMalloc(&h->planes_tmp, sizeof(float) * (size_t)NPLANES * np));
+    GSMPM_HIP(hipMalloc(&h->orig_tmp, sizeof(int) * (size_t)np));
+    GSMPM_HIP(hipMalloc(&h->sort_keys, sizeof(uint32_t) * 2 * (size_t)np));
+    GSMPM_HIP(hipMalloc(&h->sort_idx, sizeof(int) * 2 * (size_t)np));
+    size_t bytes = 0;
+    GSMPM_HIP(rocprim::radix_sort_pairs(nullptr, bytes, h->sort_keys, h->sort_keys + np, h->sort_idx,
+                                        h->sort_idx + np, (size_t)n, 0, 30, st));
+    GSMPM_HIP(hipMalloc(&h->sort_tmp, bytes ? bytes : 16));
+    h->sort_tmp_bytes = bytes;
+  }
+  const dim3 pb(div_up(n, 256));
+  hipLaunchKernelGGL(k_morton, pb, dim3(256), 0, st, particles_of(h), h->g.inv_dx, h->sort_keys, h->sort_idx);
   GSMPM_LAUNCH_CHECK();
-  return GSMPM_OK;
+  size_t bytes = h->sort_tmp_bytes;
+  GSMPM_HIP(rocprim::radix_sort_pairs(h->sort_tmp, bytes, h->sort_keys, h->sort_keys + np, h->sort_idx,
+                                      h->sort_idx + np, (size_t)n, 0, 30, st));
+  const int* perm = h->sort_idx + np;
+  hipLaunchKernelGGL(k_permute, dim3(div_up(n, 256), NPLANES), dim3(256), 0, st, h->planes, h->planes_tmp, n, np, perm);
+  hipLaunchKernelGGL(k_permute_i, pb, dim3(256), 0, st, h->orig, h->orig_tmp, n, perm);
+  GSMPM_LAUNCH_CHECK();
+  // copy back so pointers baked into cached graphs stay valid
+  GSMPM_HIP(hipMemcpyAsync(h->planes, h->planes_tmp, sizeof(float) * (size_t)NPLANES * np, hipMemcpyDeviceToDevice, st));
+  GSMPM_HIP(hipMemcpyAsync(h->orig, h->orig_tmp, sizeof(int) * (size_t)n, hipMemcpyDeviceToDevice, st));
+  h->since_sort = 0;
+  return rebin(h, st);  // list entries are storage indices
 }
 
 }  // namespace gsmpm
@@ -899,6 +1150,9 @@ int gsmpm_version(void) { return 1; }
 int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
   GSMPM_REQUIRE(prm && out, "gsmpm_mpm_create: null argument");
   GSMPM_REQUIRE(prm->n_particles > 0, "gsmpm_mpm_create: n_particles must be > 0");
+  // particle planes are addressed with 32-bit buffer offsets (mpm_common.h)
+  GSMPM_REQUIRE((long long)NPLANES * ((prm->n_particles + 255) / 256 * 256) * 4 < (1LL << 31),
+                "gsmpm_mpm_create: n_particles too large for one domain (use slabs, < 10.7M)");
   GSMPM_REQUIRE(prm->n_grid > 0 && prm->n_grid <= 2048, "gsmpm_mpm_create: n_grid out of range");
   GSMPM_REQUIRE(prm->grid_extent > 0, "gsmpm_mpm_create: grid_extent must be > 0");
   // model.py:27-30: anything but jelly/metal/sand/foam raises TypeError
@@ -932,6 +1186,26 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
   if ((e = hipMalloc(&h->gacc, sizeof(float4) * nn)) != hipSuccess) return fail(e, "hipMalloc grid acc");
   if ((e = hipMalloc(&h->gvel, sizeof(float4) * nn)) != hipSuccess) return fail(e, "hipMalloc grid vel");
   if ((e = hipMalloc(&h->boxes, sizeof(Box) * 3)) != hipSuccess) return fail(e, "hipMalloc boxes");
+  h->tl.td = (h->g.ng + kTile - 1) / kTile;
+  h->tl.ntiles = h->tl.td * h->tl.td * h->tl.td;
+  // every chunk but the last of each tile is full: <= n/256 + occupied tiles
+  h->tl.max_chunks = h->n / kChunk + std::min(h->tl.ntiles + 1, h->n) + 1;
+  if ((e = hipMalloc(&h->slots, sizeof(float4) * (size_t)h->tl.max_chunks * kWin)) != hipSuccess)
+    return fail(e, "hipMalloc chunk slots");
+  for (int c = 0; c < 2; ++c) {
+    const size_t E = (size_t)h->tl.ntiles + 1;
+    if ((e = hipMalloc(&h->count[c], sizeof(int) * E)) != hipSuccess) return fail(e, "hipMalloc count");
+    if ((e = hipMalloc(&h->cstart[c], sizeof(int) * E)) != hipSuccess) return fail(e, "hipMalloc cstart");
+    if ((e = hipMalloc(&h->cbase[c], sizeof(int) * E)) != hipSuccess) return fail(e, "hipMalloc cbase");
+    if ((e = hipMalloc(&h->ctile[c], sizeof(int) * (size_t)h->tl.max_chunks)) != hipSuccess) return fail(e, "hipMalloc ctile");
+    if ((e = hipMalloc(&h->cfirst[c], sizeof(int) * (size_t)h->tl.max_chunks)) != hipSuccess) return fail(e, "hipMalloc cfirst");
+    if ((e = hipMalloc(&h->nchunk[c], sizeof(int))) != hipSuccess) return fail(e, "hipMalloc nchunk");
+    if ((e = hipMalloc(&h->list[c], sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc list");
+    if ((e = hipMemset(h->count[c], 0, sizeof(int) * E)) != hipSuccess) return fail(e, "hipMemset");
+    if ((e = hipMemset(h->nchunk[c], 0, sizeof(int))) != hipSuccess) return fail(e, "hipMemset");
+  }
+  if ((e = hipMalloc(&h->ptile, sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc ptile");
+  if ((e = hipMalloc(&h->pslot, sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc pslot");
   if ((e = hipMalloc(&h->dev_bc, sizeof(BcTable))) != hipSuccess) return fail(e, "hipMalloc bc table");
   if ((e = hipMemset(h->gacc, 0, sizeof(float4) * nn)) != hipSuccess) return fail(e, "hipMemset");
   if ((e = hipMemset(h->gvel, 0, sizeof(float4) * nn)) != hipSuccess) return fail(e, "hipMemset");
@@ -959,6 +1233,23 @@ int gsmpm_mpm_destroy(gsmpm_mpm* h) {
   hipFree(h->gvel);
   hipFree(h->boxes);
   hipFree(h->dev_bc);
+  hipFree(h->slots);
+  for (int c = 0; c < 2; ++c) {
+    hipFree(h->count[c]);
+    hipFree(h->cstart[c]);
+    hipFree(h->cbase[c]);
+    hipFree(h->ctile[c]);
+    hipFree(h->cfirst[c]);
+    hipFree(h->nchunk[c]);
+    hipFree(h->list[c]);
+  }
+  hipFree(h->ptile);
+  hipFree(h->pslot);
+  hipFree(h->planes_tmp);
+  hipFree(h->orig_tmp);
+  hipFree(h->sort_keys);
+  hipFree(h->sort_idx);
+  hipFree(h->sort_tmp);
   delete h;
   return GSMPM_OK;
 }
@@ -1003,7 +1294,7 @@ int gsmpm_mpm_set_particles(gsmpm_mpm* h, const float* x, const float* cov6, con
   const size_t nn = (size_t)h->g.ng * h->g.ng * h->g.ng;
   GSMPM_HIP(hipMemsetAsync(h->gacc, 0, nn * sizeof(float4), st));
   GSMPM_HIP(hipMemsetAsync(h->gvel, 0, nn * sizeof(float4), st));
-  int rc = refresh_box(h, st);
+  int rc = rebin(h, st);
   if (rc) return rc;
   GSMPM_HIP(hipStreamSynchronize(st));
   h->has_particles = true;
@@ -1078,6 +1369,11 @@ int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t nsub, const uint32_t* bc, voi
   GSMPM_REQUIRE(nsub >= 0, "gsmpm_mpm_step: n_substeps < 0");
   if (nsub == 0) return GSMPM_OK;
   hipStream_t st = (hipStream_t)stream;
+  if (!(h->prm.flags & GSMPM_FLAG_NO_SORT) && h->resort_interval > 0 && h->since_sort >= h->resort_interval) {
+    int rc = resort(h, st);
+    if (rc) return rc;
+  }
+  h->since_sort += nsub;
   const bool use_graph = !(h->prm.flags & GSMPM_FLAG_NO_GRAPH) && nsub >= 2;
   if (!use_graph) {
     int parity = h->cur_box;
@@ -1121,6 +1417,13 @@ int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t nsub, const uint32_t* bc, voi
   return GSMPM_OK;
 }
 
+int gsmpm_mpm_resort(gsmpm_mpm* h, int32_t interval, void* stream) {
+  GSMPM_REQUIRE(h, "gsmpm_mpm_resort: null handle");
+  if (interval >= 0) h->resort_interval = interval;
+  if (!h->has_particles || (h->prm.flags & GSMPM_FLAG_NO_SORT)) return GSMPM_OK;
+  return resort(h, (hipStream_t)stream);
+}
+
 int gsmpm_mpm_postprocess(gsmpm_mpm* h, void* stream) {
   GSMPM_REQUIRE(h, "gsmpm_mpm_postprocess: null handle");
   hipLaunchKernelGGL(k_postprocess, dim3(div_up(h->n, 256)), dim3(256), 0, (hipStream_t)stream, particles_of(h));
@@ -1153,7 +1456,7 @@ int gsmpm_mpm_set(gsmpm_mpm* h, int32_t field, const float* in, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_set, dim3(div_up(h->n, 256)), dim3(256), 0, st, particles_of(h), h->orig, p0, w, in);
   GSMPM_LAUNCH_CHECK();
-  if (field == GSMPM_FIELD_X) return refresh_box(h, st);
+  if (field == GSMPM_FIELD_X) return rebin(h, st);
   return GSMPM_OK;
 }
 
@@ -1198,6 +1501,39 @@ int gsmpm_mpm_profile_substeps(gsmpm_mpm* h, float dt, int32_t nsub, const uint3
   h->cur_box = parity;
   for (int k = 0; k < 4; ++k) hipEventDestroy(ev[k]);
   return rc;
+}
+
+int gsmpm_mpm_debug_stats(gsmpm_mpm* h, int32_t* out8, void* stream) {
+  GSMPM_REQUIRE(h && out8, "gsmpm_mpm_debug_stats: null argument");
+  hipStream_t st = (hipStream_t)stream;
+  std::vector<int> hc(h->tl.ntiles + 1);
+  int nch = 0;
+  GSMPM_HIP(hipMemcpyAsync(hc.data(), h->count[h->cur_box], sizeof(int) * hc.size(), hipMemcpyDeviceToHost, st));
+  GSMPM_HIP(hipMemcpyAsync(&nch, h->nchunk[h->cur_box], sizeof(int), hipMemcpyDeviceToHost, st));
+  GSMPM_HIP(hipStreamSynchronize(st));
+  int active = 0, mx = 0;
+  long tot = 0;
+  for (int t = 0; t < h->tl.ntiles; ++t) {
+    active += hc[t] > 0;
+    mx = std::max(mx, hc[t]);
+    tot += hc[t];
+  }
+  out8[0] = active;
+  out8[1] = mx;
+  out8[2] = hc[h->tl.ntiles];  // particles outside the grid
+  out8[3] = nch;
+  out8[4] = h->tl.ntiles;
+  out8[5] = (int)tot;
+  out8[6] = h->cur_box;
+  out8[7] = (int)h->since_sort;
+  return GSMPM_OK;
+}
+
+int gsmpm_debug_stamps(uint64_t* out, void* stream) {
+  GSMPM_REQUIRE(out, "gsmpm_debug_stamps: null argument");
+  GSMPM_HIP(hipStreamSynchronize((hipStream_t)stream));
+  GSMPM_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 2 * 4096 * 8));
+  return GSMPM_OK;
 }
 
 int gsmpm_mpm_live_box(gsmpm_mpm* h, int32_t* box6, void* stream) {

@@ -1,0 +1,136 @@
+// mpm_common.h -- particle/grid layout, BC tables and small device helpers
+// shared by the MPM kernels (mpm.hip) and the constitutive models.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cstdint>
+
+namespace gsmpm {
+
+// ------------------------------------------------------------------ layout --
+enum Plane : int {
+  PX = 0,      // x y z
+  PV = 3,      // v
+  PC = 6,      // C (row-major 3x3)
+  PF = 15,     // F_trial between substeps; return-mapped F inside p2g
+  PMASS = 24,
+  PVOL = 25,
+  PMU = 26,
+  PLAM = 27,
+  PYLD = 28,
+  PICOV = 29,  // init cov (upper 6)
+  PCOV = 35,   // cov (upper 6)
+  PR = 41,     // particle_R
+  NPLANES = 50
+};
+
+constexpr int kMaxBC = 32;
+
+// Tiles: the grid is cut into kTile^3-cell tiles; a particle belongs to the
+// tile of its base cell, so its 3x3x3 stencil lies in the tile's
+// (kTile+2)^3-node window.
+constexpr int kTile = 8;
+constexpr int kTW = kTile + 2;          // window edge
+constexpr int kWin = kTW * kTW * kTW;   // window nodes (1000)
+
+struct Impulse {
+  float c[3], s[3], f[3], sdt;
+  int bit;
+};
+struct GridOp {
+  int kind;  // 0 fixed cube, 1 plane collider
+  int bit;
+  float a[3], b[3], friction;
+};
+struct BcTable {
+  int n_imp, n_ops;
+  Impulse imp[kMaxBC];
+  GridOp op[kMaxBC];
+};
+
+struct Particles {
+  float* P;
+  int n, np;
+  // Plane access through a buffer resource: SGPR descriptor + SGPR plane
+  // offset + ONE 32-bit VGPR lane offset for all 50 planes (a flat access
+  // holds a 64-bit VGPR address per plane, which costs the transfer kernels
+  // ~48 VGPRs).  Requires NPLANES * np * 4 < 2^32 (np < 10.7M), checked on the host.
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const {
+    return __builtin_amdgcn_make_buffer_rsrc(P, (short)0, NPLANES * np * 4, 0x00020000);
+  }
+  __device__ __forceinline__ float ld(int plane, int i) const {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc(), i * 4, plane * np * 4, 0));
+  }
+  __device__ __forceinline__ void st(int plane, int i, float v) const {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rsrc(), i * 4, plane * np * 4, 0);
+  }
+};
+
+struct GridDims {
+  int ng;
+  float dx, inv_dx;
+};
+
+struct MatConsts {
+  float alpha, hardening, xi, pvisc;
+};
+
+// live node box [lo, hi] of the last G2P (int x3 lo, x3 hi), used by k_grid
+struct Box {
+  int lo[3], hi[3];
+};
+
+// -------------------------------------------------------- device helpers --
+__device__ __forceinline__ void bspline(const float x[3], float inv_dx, int base[3], float fx[3], float w[3][3],
+                                        float dw[3][3]) {
+  // utils.py:92-109: base = (x*inv_dx - 0.5).cast(int) (truncation), quadratic B-spline
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    const float gp = x[d] * inv_dx;
+    base[d] = (int)(gp - 0.5f);
+    fx[d] = gp - (float)base[d];
+    const float wa = 1.5f - fx[d], wb = fx[d] - 1.0f, wc = fx[d] - 0.5f;
+    w[d][0] = wa * wa * 0.5f;
+    w[d][1] = 0.75f - wb * wb;
+    w[d][2] = wc * wc * 0.5f;
+    dw[d][0] = fx[d] - 1.5f;
+    dw[d][1] = -2.0f * (fx[d] - 1.0f);
+    dw[d][2] = fx[d] - 0.5f;
+  }
+}
+
+__device__ __forceinline__ float det3(const float (&A)[3][3]) {
+  return A[0][0] * (A[1][1] * A[2][2] - A[1][2] * A[2][1]) - A[0][1] * (A[1][0] * A[2][2] - A[1][2] * A[2][0]) +
+         A[0][2] * (A[1][0] * A[2][1] - A[1][1] * A[2][0]);
+}
+
+// U diag(d) V^T
+__device__ __forceinline__ void usv(const float (&U)[3][3], const float (&d)[3], const float (&V)[3][3],
+                                    float (&O)[3][3]) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) O[i][j] = (U[i][0] * d[0]) * V[j][0] + (U[i][1] * d[1]) * V[j][1] + (U[i][2] * d[2]) * V[j][2];
+}
+
+// A B^T
+__device__ __forceinline__ void mmT(const float (&A)[3][3], const float (&B)[3][3], float (&O)[3][3]) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) O[i][j] = A[i][0] * B[j][0] + A[i][1] * B[j][1] + A[i][2] * B[j][2];
+}
+
+__device__ __forceinline__ int wave_min(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
+
+}  // namespace gsmpm

@@ -100,10 +100,20 @@ class Simulator:
               "gsmpm_mpm_profile_substeps")
         return tuple(float(v) for v in out)
 
+    def debug_stats(self):
+        b = (ctypes.c_int32 * 8)()
+        check(LIB.gsmpm_mpm_debug_stats(self._h, b, stream_of(self.device)), "gsmpm_mpm_debug_stats")
+        keys = ("active_tiles", "max_per_tile", "outside", "chunks", "tiles", "binned", "parity", "since_sort")
+        return dict(zip(keys, list(b)))
+
     def live_box(self):
         b = (ctypes.c_int32 * 6)()
         check(LIB.gsmpm_mpm_live_box(self._h, b, stream_of(self.device)), "gsmpm_mpm_live_box")
         return list(b[:3]), list(b[3:])
+
+    def resort(self, interval: int = -1):
+        """Re-sort storage into Morton order now; interval >= 0 sets the automatic period."""
+        check(LIB.gsmpm_mpm_resort(self._h, int(interval), stream_of(self.device)), "gsmpm_mpm_resort")
 
     def postprocess(self):
         check(LIB.gsmpm_mpm_postprocess(self._h, stream_of(self.device)), "gsmpm_mpm_postprocess")

@@ -85,6 +85,12 @@ int gsmpm_mpm_add_plane_collider(gsmpm_mpm* h, const double point[3], const doub
  * all active.  Asynchronous on `stream`. */
 int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t n_substeps, const uint32_t* bc_active, void* stream);
 
+/* Re-sort particle storage into Morton order of the current cells now (only
+ * summation order changes; rows stay in caller order).  interval >= 0 also sets
+ * how many substeps gsmpm_mpm_step lets pass between automatic re-sorts
+ * (0 = never; default 100).  No counterpart in the reference. */
+int gsmpm_mpm_resort(gsmpm_mpm* h, int32_t interval, void* stream);
+
 /* MPM_Simulator.postprocess (solver.py:135-137): compute_cov_from_F and
  * compute_R_from_F (utils.py:376-433). */
 int gsmpm_mpm_postprocess(gsmpm_mpm* h, void* stream);
@@ -128,6 +134,13 @@ int gsmpm_mpm_world_outputs(gsmpm_mpm* h, float scale, const float center[3], in
  * Synchronises `stream`. */
 int gsmpm_mpm_profile_substeps(gsmpm_mpm* h, float dt, int32_t n_substeps, const uint32_t* bc_active,
                                float* kernel_ms, void* stream);
+/* Diagnostics of the tile buckets the next substep reads: {active tiles, max
+ * particles in a tile, particles outside the grid, chunks, tiles, binned total,
+ * parity, substeps since the last re-sort}.  Synchronises `stream`. */
+int gsmpm_mpm_debug_stats(gsmpm_mpm* h, int32_t* out8, void* stream);
+/* Workgroup timeline of the last k_p2g / k_g2p launches: out[2][4096][2]
+ * (start, end) in s_memrealtime ticks (100 MHz).  Diagnostics. */
+int gsmpm_debug_stamps(uint64_t* out, void* stream);  /* out[2][4096][8] */
 /* Current live-node box (lo[3], hi[3]) that k_grid sweeps; synchronises `stream`. */
 int gsmpm_mpm_live_box(gsmpm_mpm* h, int32_t* box6, void* stream);
 

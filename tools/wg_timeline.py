@@ -1,0 +1,40 @@
+"""Workgroup timeline of one eager substep (GPU diagnostic)."""
+import os, sys, ctypes
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'gaussian-splatting-mpm_amd'))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
+import numpy as np, torch
+import bench
+from gsmpm.bc import substep_masks
+from gsmpm._lib import LIB, stream_of
+class A: particles = 100000; n_grid = 128; config = 'lego.json'; material = None
+dev = torch.device('cuda:0')
+scene = bench.build_scene(A, dev)
+sim, specs = bench.make_sim(scene, dev)
+sa = scene['sargs']
+masks, t = substep_masks(specs, 0.0, sa.substep_dt, 20)
+sim.profile(sa.substep_dt, masks)
+ms = sim.profile(sa.substep_dt, masks[:1])
+buf = np.zeros((2, 4096, 8), np.uint64)
+LIB.gsmpm_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), stream_of(dev))
+print('event ms p2g/grid/g2p', ms)
+for k, name in enumerate(('p2g', 'g2p')):
+    st = buf[k, :, 0].astype(np.int64); en = buf[k, :, 1].astype(np.int64)
+    valid = st > 0
+    n = int(valid.sum())
+    st, en = st[:n], en[:n]
+    t0 = st.min()
+    dur = (en - st) / 100.0  # us
+    print(f"{name}: {n} WGs; start spread {(st.max()-t0)/100:.1f} us; end {(en.max()-t0)/100:.1f} us; WG dur us: min {dur.min():.1f} med {np.median(dur):.1f} max {dur.max():.1f}")
+    order = np.argsort(st)
+    print('  first starts (us):', ((st[order[:8]] - t0) / 100).round(1), ' last starts:', ((st[order[-8:]] - t0) / 100).round(1))
+    hist = np.histogram((st - t0) / 100, bins=10)
+    print('  start histogram', hist[0].tolist(), 'edges', hist[1].round(1).tolist())
+
+st = buf[1, :, :].astype(np.int64)
+v = st[:, 0] > 0
+st = st[v]
+seg = lambda a, b: (st[:, b] - st[:, a]) / 100.0
+ok = st[:, 2] > 0
+print('g2p first-chunk segments (us): start->staged', np.median(seg(0, 2)[ok]), ' staged->particles', np.median(seg(2, 3)[ok]),
+      ' particles->reserved', np.median(seg(3, 4)[ok]), ' reserved->end', np.median(seg(4, 1)[ok]))
+print('  max:', seg(0, 2)[ok].max(), seg(2, 3)[ok].max(), seg(3, 4)[ok].max(), seg(4, 1)[ok].max())
