@@ -241,8 +241,8 @@ def main():
     kern = None
     if world == 1:
         masks, state["t"] = substep_masks(specs, state["t"], dt, spf)
-        lo, hi = sim.live_box()
-        live = max(0, hi[0] - lo[0] + 1) * max(0, hi[1] - lo[1] + 1) * max(0, hi[2] - lo[2] + 1)
+        # nodes owned by the grid update: 8^3 per touched tile (Roofline)
+        live = sim.debug_stats()["touched_tiles"] * 512
         kms = sim.profile(dt, masks)
         kern = {k: kms[i] / spf for i, k in enumerate(("k_p2g", "k_grid", "k_g2p"))}
         abytes = algorithmic_bytes(n_local, live, sa.material)

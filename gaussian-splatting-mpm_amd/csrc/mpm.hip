@@ -63,12 +63,12 @@ struct Tiles {
   int max_chunks;
 };
 struct ChunkIn {
-  const int* count;   // [ntiles + 1] particles per tile
-  const int* cbase;   // [ntiles + 1] first chunk of each tile
-  const int* ctile;   // [max_chunks] tile of each chunk
-  const int* cfirst;  // [max_chunks] first list entry of each chunk
-  const int* nchunk;  // [1]
-  const int* list;    // [n] particle (storage) indices grouped by tile
+  const int* count;    // [ntiles + 1] particles per tile
+  const int* cbase;    // [ntiles + 1] first chunk of each tile
+  const int4* chunk;   // [max_chunks] {tile, first list entry, particles, 0}
+  const int* nchunk;   // [2] {chunks, touched tiles}
+  const int* list;     // [n] particle (storage) indices grouped by tile
+  const int* touched;  // [ntiles] tiles whose nodes the next grid update owns
 };
 struct BinOut {
   int* count;  // [ntiles + 1], zeroed before G2P
@@ -204,11 +204,10 @@ __global__ __launch_bounds__(256) void k_p2g(Particles ps, GridDims g, Tiles tl,
   __shared__ unsigned long long s_acc[kWin * 4];
   __shared__ float s_max[4];
   const int ng = g.ng;
-  const int nch = *ck.nchunk;
+  const int nch = ck.nchunk[0];
   for (int w = blockIdx.x; w < nch; w += gridDim.x) {
-    const int t = ck.ctile[w];
-    const int first = ck.cfirst[w];
-    const int cnt = min(kChunk, ck.count[t] - (first - (ck.cfirst[ck.cbase[t]])));
+    const int4 cr = ck.chunk[w];
+    const int t = cr.x, first = cr.y, cnt = cr.z;
     const int k = threadIdx.x;
     if (t == tl.ntiles) {
       // particles outside the grid: bounds-checked global f32 atomics (reference UB region)
@@ -314,29 +313,22 @@ struct GridStep {
 __global__ __launch_bounds__(256) void k_grid(GridDims g, Tiles tl, ChunkIn ck, const float4* __restrict__ slots,
                                               float4* __restrict__ gacc, float4* __restrict__ gvel,
                                               const BcTable* __restrict__ bct, GridStep gs,
-                                              const Box* __restrict__ box, Box* __restrict__ next_box,
                                               int* __restrict__ count_next) {
   // housekeeping for the G2P that follows (stream order makes this safe)
-  if (blockIdx.x == 0 && threadIdx.x < 3) {
-    next_box->lo[threadIdx.x] = INT_MAX;
-    next_box->hi[threadIdx.x] = INT_MIN;
-  }
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t <= tl.ntiles; t += gridDim.x * blockDim.x) count_next[t] = 0;
 
   const int ng = g.ng, td = tl.td;
   const bool outside = ck.count[tl.ntiles] > 0;
-  const int lo0 = box->lo[0], lo1 = box->lo[1], lo2 = box->lo[2];
-  const int e0 = box->hi[0] - lo0 + 1, e1 = box->hi[1] - lo1 + 1, e2 = box->hi[2] - lo2 + 1;
-  if (e0 <= 0 || e1 <= 0 || e2 <= 0) return;
-  const long total = (long)e0 * e1 * e2;
-  for (long q = (long)blockIdx.x * blockDim.x + threadIdx.x; q < total; q += (long)gridDim.x * blockDim.x) {
-    const int k = lo2 + (int)(q % e2);
-    const long q2 = q / e2;
-    const int j = lo1 + (int)(q2 % e1);
-    const int i = lo0 + (int)(q2 / e1);
+  const int ntouch = ck.nchunk[1];
+  // one touched tile (8^3 owned nodes) per workgroup iteration, two nodes per lane
+  for (int wt = blockIdx.x; wt < ntouch; wt += gridDim.x)
+  for (int q = threadIdx.x; q < kTile * kTile * kTile; q += blockDim.x) {
+    const int T = ck.touched[wt];
+    const int ti = T / (td * td), tj = (T / td) % td, tk = T % td;
+    const int li = q >> 6, lj = (q >> 3) & 7, lk = q & 7;
+    const int i = ti * kTile + li, j = tj * kTile + lj, k = tk * kTile + lk;
+    if (i >= ng || j >= ng || k >= ng) continue;
     const size_t idx = ((size_t)i * ng + j) * ng + k;
-    const int ti = i / kTile, tj = j / kTile, tk = k / kTile;
-    const int li = i - ti * kTile, lj = j - tj * kTile, lk = k - tk * kTile;
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
     for (int ax = 0; ax < 2; ++ax) {
@@ -485,46 +477,21 @@ __device__ __forceinline__ void g2p_particle(const Particles& ps, int p, const G
     }
 }
 
-// node box the next P2G touches (base..base+2 of the new position)
-__device__ __forceinline__ void box_accumulate(const float (&xn)[3], const GridDims& g, int (&blo)[3], int (&bhi)[3]) {
-#pragma unroll
-  for (int d = 0; d < 3; ++d) {
-    const int b = (int)(xn[d] * g.inv_dx - 0.5f);
-    blo[d] = min(blo[d], max(0, b));
-    bhi[d] = max(bhi[d], min(g.ng - 1, b + 2));
-  }
-}
-
-__device__ __forceinline__ void box_flush(const int (&blo)[3], const int (&bhi)[3], Box* next_box) {
-#pragma unroll
-  for (int d = 0; d < 3; ++d) {
-    const int lo = wave_min(blo[d]);
-    const int hi = wave_max(bhi[d]);
-    if ((threadIdx.x & 63) == 0 && lo <= hi) {
-      atomicMin(&next_box->lo[d], lo);
-      atomicMax(&next_box->hi[d], hi);
-    }
-  }
-}
-
 // One workgroup per chunk: stage the tile's 10^3 window of v_out in LDS,
 // gather, update the particle, and bin it into the tile of its new base cell.
 // Moves to the 27 neighbour tiles are counted in LDS and reserved with <= 27
 // global atomics per chunk; farther moves / leaving the grid use one atomic.
 __global__ __launch_bounds__(256) void k_g2p(Particles ps, GridDims g, Tiles tl, ChunkIn ck, BinOut bo,
-                                                const float4* __restrict__ gvel, float dt,
-                                                Box* __restrict__ next_box) {
+                                                const float4* __restrict__ gvel, float dt) {
   __shared__ float4 s_win[kWin];
   __shared__ int s_cnt[27];
   __shared__ int s_base[27];
   const int ng = g.ng;
-  int blo[3] = {INT_MAX, INT_MAX, INT_MAX}, bhi[3] = {INT_MIN, INT_MIN, INT_MIN};
   stamp(1, 0);
-  const int nch = *ck.nchunk;
+  const int nch = ck.nchunk[0];
   for (int w = blockIdx.x; w < nch; w += gridDim.x) {
-    const int t = ck.ctile[w];
-    const int first = ck.cfirst[w];
-    const int cnt = min(kChunk, ck.count[t] - (first - (ck.cfirst[ck.cbase[t]])));
+    const int4 cr = ck.chunk[w];
+    const int t = cr.x, first = cr.y, cnt = cr.z;
     const int k = threadIdx.x;
     if (t == tl.ntiles) {
       if (k < cnt) {
@@ -539,7 +506,6 @@ __global__ __launch_bounds__(256) void k_g2p(Particles ps, GridDims g, Tiles tl,
                        return gv;
                      },
                      xn);
-        box_accumulate(xn, g, blo, bhi);
         int tc[3];
         const int nt = tile_of(xn, g, tl, tc);
         bo.ptile[p] = nt;
@@ -558,7 +524,14 @@ __global__ __launch_bounds__(256) void k_g2p(Particles ps, GridDims g, Tiles tl,
     }
     if (k < 27) s_cnt[k] = 0;
     __syncthreads();
-    if (w == (int)blockIdx.x) stamp(1, 2);
+    if (w == (int)blockIdx.x) {
+      stamp(1, 2);
+      if (threadIdx.x == 0 && blockIdx.x < 4096) {
+        g_stamps[1][blockIdx.x][5] = cnt;
+        g_stamps[1][blockIdx.x][6] = t;
+        g_stamps[1][blockIdx.x][7] = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));  // HW_ID
+      }
+    }
     int p = -1, code = -1, lslot = 0, nt = -1;
     if (k < cnt) {
       p = ck.list[first + k];
@@ -569,7 +542,6 @@ __global__ __launch_bounds__(256) void k_g2p(Particles ps, GridDims g, Tiles tl,
                      return wb[(i * kTW + j) * kTW + kk];
                    },
                    xn);
-      box_accumulate(xn, g, blo, bhi);
       int tc[3];
       nt = tile_of(xn, g, tl, tc);
       if (nt < tl.ntiles) {
@@ -597,74 +569,122 @@ __global__ __launch_bounds__(256) void k_g2p(Particles ps, GridDims g, Tiles tl,
     }
     __syncthreads();  // LDS reuse by the next chunk
   }
-  box_flush(blo, bhi, next_box);
   stamp(1, 1);
 }
 
 // ------------------------------------------------------- binning passes --
-// bin every particle by its current x (set_particles / resort / set x) and
-// accumulate the live node box
-__global__ __launch_bounds__(256) void k_bin_all(Particles ps, GridDims g, Tiles tl, BinOut bo, Box* box) {
+// bin every particle by its current x (set_particles / resort / set x)
+__global__ __launch_bounds__(256) void k_bin_all(Particles ps, GridDims g, Tiles tl, BinOut bo) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  int blo[3] = {INT_MAX, INT_MAX, INT_MAX}, bhi[3] = {INT_MIN, INT_MIN, INT_MIN};
   if (p < ps.n) {
     float x[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) x[d] = ps.ld(PX + d, p);
-    box_accumulate(x, g, blo, bhi);
     int tc[3];
     const int t = tile_of(x, g, tl, tc);
     bo.ptile[p] = t;
     bo.pslot[p] = atomicAdd(&bo.count[t], 1);
   }
-  box_flush(blo, bhi, box);
 }
 
-// One workgroup (1024 lanes): per-tile counts -> list offsets (exclusive scan)
-// and the chunk list (ceil(count/256) chunks per tile, pseudo-tile last).
+// One workgroup (1024 lanes): per-tile counts -> list offsets (exclusive
+// scan), the chunk records (ceil(count/256) per tile, pseudo-tile last), the
+// list of tiles the next grid update owns and their node bounding box.  A tile
+// is touched when it or one of its 7 lower neighbours holds particles: those
+// are exactly the owners of the nodes inside the occupied tiles' 10^3 windows.
+// Particles outside the grid (or KEEP_GRID) make every tile touched.
 struct ChunkOut {
-  int* cstart;  // [ntiles + 1] first list entry of each tile
-  int* cbase;   // [ntiles + 1]
-  int* ctile;   // [max_chunks]
-  int* cfirst;  // [max_chunks]
-  int* nchunk;  // [1]
+  int* cstart;   // [ntiles + 1] first list entry of each tile
+  int* cbase;    // [ntiles + 1]
+  int4* chunk;   // [max_chunks]
+  int* nchunk;   // [2]
+  int* touched;  // [ntiles]
+  Box* box;      // node box of the touched tiles (diagnostics)
 };
-__global__ __launch_bounds__(1024) void k_scan_tiles(Tiles tl, const int* __restrict__ count, ChunkOut co) {
-  __shared__ int s_a[1024], s_b[1024];
-  const int E = tl.ntiles + 1;
+__device__ __forceinline__ bool tile_touched(const int* __restrict__ count, int t, int td) {
+  const int ti = t / (td * td), tj = (t / td) % td, tk = t % td;
+  bool any = false;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+        if (ti >= a && tj >= b && tk >= c) any = any || count[((ti - a) * td + (tj - b)) * td + (tk - c)] > 0;
+  return any;
+}
+
+__global__ __launch_bounds__(1024) void k_scan_tiles(Tiles tl, GridDims g, const int* __restrict__ count, ChunkOut co,
+                                                     int all_touched) {
+  __shared__ int s_a[1024], s_b[1024], s_c[1024];
+  __shared__ int s_box[6];
+  const int E = tl.ntiles + 1, td = tl.td;
+  const bool all = all_touched || count[tl.ntiles] > 0;
   const int per = (E + 1023) / 1024;
   const int t0 = threadIdx.x * per, t1 = min(E, t0 + per);
-  int sa = 0, sb = 0;
+  if (threadIdx.x < 3) {
+    s_box[threadIdx.x] = INT_MAX;
+    s_box[3 + threadIdx.x] = INT_MIN;
+  }
+  int sa = 0, sb = 0, sc = 0;
   for (int t = t0; t < t1; ++t) {
     const int c = count[t];
     sa += c;
     sb += (c + kChunk - 1) / kChunk;
+    sc += (t < tl.ntiles && (all || tile_touched(count, t, td))) ? 1 : 0;
   }
   s_a[threadIdx.x] = sa;
   s_b[threadIdx.x] = sb;
+  s_c[threadIdx.x] = sc;
   __syncthreads();
   for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
     const int xa = threadIdx.x >= o ? s_a[threadIdx.x - o] : 0;
     const int xb = threadIdx.x >= o ? s_b[threadIdx.x - o] : 0;
+    const int xc = threadIdx.x >= o ? s_c[threadIdx.x - o] : 0;
     __syncthreads();
     s_a[threadIdx.x] += xa;
     s_b[threadIdx.x] += xb;
+    s_c[threadIdx.x] += xc;
     __syncthreads();
   }
-  int oa = s_a[threadIdx.x] - sa, ob = s_b[threadIdx.x] - sb;
+  int oa = s_a[threadIdx.x] - sa, ob = s_b[threadIdx.x] - sb, oc = s_c[threadIdx.x] - sc;
+  int blo[3] = {INT_MAX, INT_MAX, INT_MAX}, bhi[3] = {INT_MIN, INT_MIN, INT_MIN};
   for (int t = t0; t < t1; ++t) {
     const int c = count[t];
     const int nc = (c + kChunk - 1) / kChunk;
     co.cstart[t] = oa;
     co.cbase[t] = ob;
-    for (int k = 0; k < nc; ++k) {
-      co.ctile[ob + k] = t;
-      co.cfirst[ob + k] = oa + k * kChunk;
-    }
+    for (int k = 0; k < nc; ++k) co.chunk[ob + k] = make_int4(t, oa + k * kChunk, min(kChunk, c - k * kChunk), 0);
     oa += c;
     ob += nc;
+    if (t < tl.ntiles && (all || tile_touched(count, t, td))) {
+      co.touched[oc++] = t;
+      const int tc[3] = {t / (td * td), (t / td) % td, t % td};
+#pragma unroll
+      for (int d = 0; d < 3; ++d) {
+        blo[d] = min(blo[d], tc[d] * kTile);
+        bhi[d] = max(bhi[d], min(g.ng - 1, tc[d] * kTile + kTile - 1));
+      }
+    }
   }
-  if (threadIdx.x == 1023) *co.nchunk = s_b[1023];
+  __syncthreads();
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    const int lo = wave_min(blo[d]), hi = wave_max(bhi[d]);
+    if ((threadIdx.x & 63) == 0) {
+      atomicMin(&s_box[d], lo);
+      atomicMax(&s_box[3 + d], hi);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 1023) {
+    co.nchunk[0] = s_b[1023];
+    co.nchunk[1] = s_c[1023];
+  }
+  if (threadIdx.x < 3) {
+    co.box->lo[threadIdx.x] = s_box[threadIdx.x];
+    co.box->hi[threadIdx.x] = s_box[3 + threadIdx.x];
+  }
 }
 
 __global__ __launch_bounds__(256) void k_scatter(int n, const int* __restrict__ ptile, const int* __restrict__ pslot,
@@ -674,19 +694,6 @@ __global__ __launch_bounds__(256) void k_scatter(int n, const int* __restrict__ 
   list[cstart[ptile[p]] + pslot[p]] = p;
 }
 
-__global__ void k_box_reset(Box* b) {
-  if (threadIdx.x < 3) {
-    b->lo[threadIdx.x] = INT_MAX;
-    b->hi[threadIdx.x] = INT_MIN;
-  }
-}
-
-__global__ void k_box_full(Box* b, int ng) {
-  if (threadIdx.x < 3) {
-    b->lo[threadIdx.x] = 0;
-    b->hi[threadIdx.x] = ng - 1;
-  }
-}
 
 // ------------------------------------------------------------ postprocess --
 // compute_cov_from_F (utils.py:401-433) + compute_R_from_F (utils.py:376-398)
@@ -943,13 +950,13 @@ struct gsmpm_mpm {
   int* count[2] = {nullptr, nullptr};   // [ntiles + 1]
   int* cstart[2] = {nullptr, nullptr};  // [ntiles + 1]
   int* cbase[2] = {nullptr, nullptr};   // [ntiles + 1]
-  int* ctile[2] = {nullptr, nullptr};   // [max_chunks]
-  int* cfirst[2] = {nullptr, nullptr};  // [max_chunks]
-  int* nchunk[2] = {nullptr, nullptr};  // [1]
+  int4* chunk[2] = {nullptr, nullptr};  // [max_chunks] chunk records
+  int* nchunk[2] = {nullptr, nullptr};  // [2] {chunks, touched tiles}
+  int* touched[2] = {nullptr, nullptr}; // [ntiles] tiles the grid update owns
   int* list[2] = {nullptr, nullptr};    // [np]
   int* ptile = nullptr;                 // [np]
   int* pslot = nullptr;                 // [np]
-  Box* boxes = nullptr;  // [0],[1] ping-pong live-node boxes, [2] whole grid
+  Box* boxes = nullptr;  // [2] node box of the touched tiles, per parity (diagnostics)
   int cur_box = 0;       // parity of the boxes / buckets the next substep reads
   BcTable host_bc{};
   BcTable* dev_bc = nullptr;
@@ -976,15 +983,16 @@ void set_error(const std::string& m) { g_err = m; }
 static Particles particles_of(gsmpm_mpm* h) { return Particles{h->planes, h->n, h->np}; }
 
 static ChunkIn chunk_in(gsmpm_mpm* h, int c) {
-  return ChunkIn{h->count[c], h->cbase[c], h->ctile[c], h->cfirst[c], h->nchunk[c], h->list[c]};
+  return ChunkIn{h->count[c], h->cbase[c], h->chunk[c], h->nchunk[c], h->list[c], h->touched[c]};
 }
 static ChunkOut chunk_out(gsmpm_mpm* h, int c) {
-  return ChunkOut{h->cstart[c], h->cbase[c], h->ctile[c], h->cfirst[c], h->nchunk[c]};
+  return ChunkOut{h->cstart[c], h->cbase[c], h->chunk[c], h->nchunk[c], h->touched[c], h->boxes + c};
 }
 static BinOut bin_out(gsmpm_mpm* h, int c) { return BinOut{h->count[c], h->ptile, h->pslot}; }
 
 static int p2g_grid(gsmpm_mpm* h) { return std::min(h->tl.max_chunks, 1024); }
-static int g2p_grid(gsmpm_mpm* h) { return std::min(h->tl.max_chunks, 512); }
+static int g2p_grid(gsmpm_mpm* h) { return std::min(h->tl.max_chunks, 1024); }
+static int grid_grid(gsmpm_mpm* h) { return std::min(h->tl.ntiles, 2048); }
 
 template <int MAT>
 static void launch_p2g(gsmpm_mpm* h, int c, uint32_t mask, float dt, hipStream_t st) {
@@ -994,20 +1002,20 @@ static void launch_p2g(gsmpm_mpm* h, int c, uint32_t mask, float dt, hipStream_t
 
 // counts of parity c -> list offsets + chunk list, then the per-tile lists
 static int finish_binning(gsmpm_mpm* h, int c, hipStream_t st) {
-  hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, st, h->tl, h->count[c], chunk_out(h, c));
+  const int all = (h->prm.flags & GSMPM_FLAG_KEEP_GRID) ? 1 : 0;
+  hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, st, h->tl, h->g, h->count[c], chunk_out(h, c), all);
   hipLaunchKernelGGL(k_scatter, dim3(div_up(h->n, 256)), dim3(256), 0, st, h->n, h->ptile, h->pslot, h->cstart[c],
                      h->list[c]);
   GSMPM_LAUNCH_CHECK();
   return GSMPM_OK;
 }
 
-// (Re)build the chunk lists and the live box of parity `cur_box` from the current x.
+// (Re)build the chunk lists of parity `cur_box` from the current x.
 static int rebin(gsmpm_mpm* h, hipStream_t st) {
   const int c = h->cur_box;
   GSMPM_HIP(hipMemsetAsync(h->count[c], 0, sizeof(int) * (h->tl.ntiles + 1), st));
-  hipLaunchKernelGGL(k_box_reset, dim3(1), dim3(64), 0, st, h->boxes + c);
   hipLaunchKernelGGL(k_bin_all, dim3(div_up(h->n, 256)), dim3(256), 0, st, particles_of(h), h->g, h->tl,
-                     bin_out(h, c), h->boxes + c);
+                     bin_out(h, c));
   GSMPM_LAUNCH_CHECK();
   return finish_binning(h, c, st);
 }
@@ -1016,8 +1024,6 @@ static int launch_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc,
                            hipEvent_t* ev = nullptr, float* kernel_ms = nullptr) {
   const size_t nn = (size_t)h->g.ng * h->g.ng * h->g.ng;
   const bool keep = (h->prm.flags & GSMPM_FLAG_KEEP_GRID) != 0;
-  // the live node box is far smaller than n^3 in practice; cap the grid-stride launch
-  const int gblocks = (int)std::min<long>(div_up((long)nn, 256), 2048);
   GridStep gs;
   gs.dt = dt;
   gs.gx = (float)h->prm.gravity[0];
@@ -1039,12 +1045,12 @@ static int launch_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc,
     }
     GSMPM_LAUNCH_CHECK();
     if (ev) GSMPM_HIP(hipEventRecord(ev[1], st));
-    hipLaunchKernelGGL(k_grid, dim3(gblocks), dim3(256), 0, st, h->g, h->tl, chunk_in(h, c), h->slots, h->gacc, h->gvel,
-                       h->dev_bc, gs, keep ? h->boxes + 2 : h->boxes + c, h->boxes + nx, h->count[nx]);
+    hipLaunchKernelGGL(k_grid, dim3(grid_grid(h)), dim3(256), 0, st, h->g, h->tl, chunk_in(h, c), h->slots, h->gacc,
+                       h->gvel, h->dev_bc, gs, h->count[nx]);
     GSMPM_LAUNCH_CHECK();
     if (ev) GSMPM_HIP(hipEventRecord(ev[2], st));
     hipLaunchKernelGGL(k_g2p, dim3(g2p_grid(h)), dim3(kChunk), 0, st, particles_of(h), h->g, h->tl, chunk_in(h, c),
-                       bin_out(h, nx), h->gvel, dt, h->boxes + nx);
+                       bin_out(h, nx), h->gvel, dt);
     GSMPM_LAUNCH_CHECK();
     {
       int rc = finish_binning(h, nx, st);
@@ -1065,7 +1071,7 @@ static int launch_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc,
 }
 
 static void drop_graphs(gsmpm_mpm* h) {
-  for (auto& kv : h->graphs) hipGraphExecDestroy(kv.second);
+  for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
   h->graphs.clear();
   h->graph_box_parity.clear();
 }
@@ -1185,7 +1191,8 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
   if ((e = hipMalloc(&h->orig, sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc orig");
   if ((e = hipMalloc(&h->gacc, sizeof(float4) * nn)) != hipSuccess) return fail(e, "hipMalloc grid acc");
   if ((e = hipMalloc(&h->gvel, sizeof(float4) * nn)) != hipSuccess) return fail(e, "hipMalloc grid vel");
-  if ((e = hipMalloc(&h->boxes, sizeof(Box) * 3)) != hipSuccess) return fail(e, "hipMalloc boxes");
+  if ((e = hipMalloc(&h->boxes, sizeof(Box) * 2)) != hipSuccess) return fail(e, "hipMalloc boxes");
+  if ((e = hipMemset(h->boxes, 0, sizeof(Box) * 2)) != hipSuccess) return fail(e, "hipMemset");
   h->tl.td = (h->g.ng + kTile - 1) / kTile;
   h->tl.ntiles = h->tl.td * h->tl.td * h->tl.td;
   // every chunk but the last of each tile is full: <= n/256 + occupied tiles
@@ -1197,12 +1204,12 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
     if ((e = hipMalloc(&h->count[c], sizeof(int) * E)) != hipSuccess) return fail(e, "hipMalloc count");
     if ((e = hipMalloc(&h->cstart[c], sizeof(int) * E)) != hipSuccess) return fail(e, "hipMalloc cstart");
     if ((e = hipMalloc(&h->cbase[c], sizeof(int) * E)) != hipSuccess) return fail(e, "hipMalloc cbase");
-    if ((e = hipMalloc(&h->ctile[c], sizeof(int) * (size_t)h->tl.max_chunks)) != hipSuccess) return fail(e, "hipMalloc ctile");
-    if ((e = hipMalloc(&h->cfirst[c], sizeof(int) * (size_t)h->tl.max_chunks)) != hipSuccess) return fail(e, "hipMalloc cfirst");
-    if ((e = hipMalloc(&h->nchunk[c], sizeof(int))) != hipSuccess) return fail(e, "hipMalloc nchunk");
+    if ((e = hipMalloc(&h->chunk[c], sizeof(int4) * (size_t)h->tl.max_chunks)) != hipSuccess) return fail(e, "hipMalloc chunk");
+    if ((e = hipMalloc(&h->touched[c], sizeof(int) * (size_t)h->tl.ntiles)) != hipSuccess) return fail(e, "hipMalloc touched");
+    if ((e = hipMalloc(&h->nchunk[c], sizeof(int) * 2)) != hipSuccess) return fail(e, "hipMalloc nchunk");
     if ((e = hipMalloc(&h->list[c], sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc list");
     if ((e = hipMemset(h->count[c], 0, sizeof(int) * E)) != hipSuccess) return fail(e, "hipMemset");
-    if ((e = hipMemset(h->nchunk[c], 0, sizeof(int))) != hipSuccess) return fail(e, "hipMemset");
+    if ((e = hipMemset(h->nchunk[c], 0, sizeof(int) * 2)) != hipSuccess) return fail(e, "hipMemset");
   }
   if ((e = hipMalloc(&h->ptile, sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc ptile");
   if ((e = hipMalloc(&h->pslot, sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc pslot");
@@ -1214,10 +1221,6 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
   h->host_bc = BcTable{};
   if ((e = hipMemcpy(h->dev_bc, &h->host_bc, sizeof(BcTable), hipMemcpyHostToDevice)) != hipSuccess)
     return fail(e, "hipMemcpy bc");
-  // the live-node box starts as the whole grid
-  hipLaunchKernelGGL(k_box_full, dim3(1), dim3(64), 0, 0, h->boxes, h->g.ng);
-  hipLaunchKernelGGL(k_box_full, dim3(1), dim3(64), 0, 0, h->boxes + 1, h->g.ng);
-  hipLaunchKernelGGL(k_box_full, dim3(1), dim3(64), 0, 0, h->boxes + 2, h->g.ng);
   if ((e = hipDeviceSynchronize()) != hipSuccess) return fail(e, "init");
   *out = h;
   return GSMPM_OK;
@@ -1226,30 +1229,30 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
 int gsmpm_mpm_destroy(gsmpm_mpm* h) {
   if (!h) return GSMPM_OK;
   drop_graphs(h);
-  if (h->cap) hipStreamDestroy(h->cap);
-  hipFree(h->planes);
-  hipFree(h->orig);
-  hipFree(h->gacc);
-  hipFree(h->gvel);
-  hipFree(h->boxes);
-  hipFree(h->dev_bc);
-  hipFree(h->slots);
+  if (h->cap) (void)hipStreamDestroy(h->cap);
+  (void)hipFree(h->planes);
+  (void)hipFree(h->orig);
+  (void)hipFree(h->gacc);
+  (void)hipFree(h->gvel);
+  (void)hipFree(h->boxes);
+  (void)hipFree(h->dev_bc);
+  (void)hipFree(h->slots);
   for (int c = 0; c < 2; ++c) {
-    hipFree(h->count[c]);
-    hipFree(h->cstart[c]);
-    hipFree(h->cbase[c]);
-    hipFree(h->ctile[c]);
-    hipFree(h->cfirst[c]);
-    hipFree(h->nchunk[c]);
-    hipFree(h->list[c]);
+    (void)hipFree(h->count[c]);
+    (void)hipFree(h->cstart[c]);
+    (void)hipFree(h->cbase[c]);
+    (void)hipFree(h->chunk[c]);
+    (void)hipFree(h->touched[c]);
+    (void)hipFree(h->nchunk[c]);
+    (void)hipFree(h->list[c]);
   }
-  hipFree(h->ptile);
-  hipFree(h->pslot);
-  hipFree(h->planes_tmp);
-  hipFree(h->orig_tmp);
-  hipFree(h->sort_keys);
-  hipFree(h->sort_idx);
-  hipFree(h->sort_tmp);
+  (void)hipFree(h->ptile);
+  (void)hipFree(h->pslot);
+  (void)hipFree(h->planes_tmp);
+  (void)hipFree(h->orig_tmp);
+  (void)hipFree(h->sort_keys);
+  (void)hipFree(h->sort_idx);
+  (void)hipFree(h->sort_tmp);
   delete h;
   return GSMPM_OK;
 }
@@ -1404,7 +1407,7 @@ int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t nsub, const uint32_t* bc, voi
     }
     hipGraphExec_t exec;
     e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-    hipGraphDestroy(graph);
+    (void)hipGraphDestroy(graph);
     if (e != hipSuccess) {
       set_error(std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
       return GSMPM_EHIP;
@@ -1499,7 +1502,7 @@ int gsmpm_mpm_profile_substeps(gsmpm_mpm* h, float dt, int32_t nsub, const uint3
   int parity = h->cur_box;
   int rc = launch_substeps(h, dt, nsub, bc, st, parity, ev, kernel_ms);
   h->cur_box = parity;
-  for (int k = 0; k < 4; ++k) hipEventDestroy(ev[k]);
+  for (int k = 0; k < 4; ++k) (void)hipEventDestroy(ev[k]);
   return rc;
 }
 
@@ -1507,9 +1510,9 @@ int gsmpm_mpm_debug_stats(gsmpm_mpm* h, int32_t* out8, void* stream) {
   GSMPM_REQUIRE(h && out8, "gsmpm_mpm_debug_stats: null argument");
   hipStream_t st = (hipStream_t)stream;
   std::vector<int> hc(h->tl.ntiles + 1);
-  int nch = 0;
+  int nch[2] = {0, 0};
   GSMPM_HIP(hipMemcpyAsync(hc.data(), h->count[h->cur_box], sizeof(int) * hc.size(), hipMemcpyDeviceToHost, st));
-  GSMPM_HIP(hipMemcpyAsync(&nch, h->nchunk[h->cur_box], sizeof(int), hipMemcpyDeviceToHost, st));
+  GSMPM_HIP(hipMemcpyAsync(nch, h->nchunk[h->cur_box], sizeof(int) * 2, hipMemcpyDeviceToHost, st));
   GSMPM_HIP(hipStreamSynchronize(st));
   int active = 0, mx = 0;
   long tot = 0;
@@ -1521,8 +1524,8 @@ int gsmpm_mpm_debug_stats(gsmpm_mpm* h, int32_t* out8, void* stream) {
   out8[0] = active;
   out8[1] = mx;
   out8[2] = hc[h->tl.ntiles];  // particles outside the grid
-  out8[3] = nch;
-  out8[4] = h->tl.ntiles;
+  out8[3] = nch[0];
+  out8[4] = nch[1];  // tiles owned by the next grid update
   out8[5] = (int)tot;
   out8[6] = h->cur_box;
   out8[7] = (int)h->since_sort;

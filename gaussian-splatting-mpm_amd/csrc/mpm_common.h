@@ -30,7 +30,7 @@ constexpr int kMaxBC = 32;
 // Tiles: the grid is cut into kTile^3-cell tiles; a particle belongs to the
 // tile of its base cell, so its 3x3x3 stencil lies in the tile's
 // (kTile+2)^3-node window.
-constexpr int kTile = 8;
+constexpr int kTile = 8;  // k_grid decodes node offsets with 3-bit shifts
 constexpr int kTW = kTile + 2;          // window edge
 constexpr int kWin = kTW * kTW * kTW;   // window nodes (1000)
 

@@ -343,7 +343,7 @@ struct gsmpm_raster {
 };
 
 static int grow(void** p, size_t bytes) {
-  if (*p) hipFree(*p);
+  if (*p) (void)hipFree(*p);
   *p = nullptr;
   GSMPM_HIP(hipMalloc(p, bytes ? bytes : 16));
   return GSMPM_OK;
@@ -369,8 +369,8 @@ int gsmpm_raster_destroy(gsmpm_raster* r) {
   for (void* p : {(void*)r->radii_tmp, (void*)r->depth, (void*)r->xy, (void*)r->conic, (void*)r->rgb, (void*)r->tiles,
                   (void*)r->offsets, r->scan_tmp, (void*)r->keys, (void*)r->keys_sorted, (void*)r->vals,
                   (void*)r->vals_sorted, r->sort_tmp, (void*)r->ranges})
-    if (p) hipFree(p);
-  if (r->h_count) hipHostFree(r->h_count);
+    if (p) (void)hipFree(p);
+  if (r->h_count) (void)hipHostFree(r->h_count);
   delete r;
   return GSMPM_OK;
 }

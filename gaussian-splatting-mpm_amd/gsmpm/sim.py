@@ -103,7 +103,7 @@ class Simulator:
     def debug_stats(self):
         b = (ctypes.c_int32 * 8)()
         check(LIB.gsmpm_mpm_debug_stats(self._h, b, stream_of(self.device)), "gsmpm_mpm_debug_stats")
-        keys = ("active_tiles", "max_per_tile", "outside", "chunks", "tiles", "binned", "parity", "since_sort")
+        keys = ("active_tiles", "max_per_tile", "outside", "chunks", "touched_tiles", "binned", "parity", "since_sort")
         return dict(zip(keys, list(b)))
 
     def live_box(self):

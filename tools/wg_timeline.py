@@ -21,6 +21,8 @@ for k, name in enumerate(('p2g', 'g2p')):
     st = buf[k, :, 0].astype(np.int64); en = buf[k, :, 1].astype(np.int64)
     valid = st > 0
     n = int(valid.sum())
+    if n == 0:
+        print(name, ': no stamps'); continue
     st, en = st[:n], en[:n]
     t0 = st.min()
     dur = (en - st) / 100.0  # us
@@ -38,3 +40,15 @@ ok = st[:, 2] > 0
 print('g2p first-chunk segments (us): start->staged', np.median(seg(0, 2)[ok]), ' staged->particles', np.median(seg(2, 3)[ok]),
       ' particles->reserved', np.median(seg(3, 4)[ok]), ' reserved->end', np.median(seg(4, 1)[ok]))
 print('  max:', seg(0, 2)[ok].max(), seg(2, 3)[ok].max(), seg(3, 4)[ok].max(), seg(4, 1)[ok].max())
+
+order = np.argsort(-(st[:, 1] - st[:, 0]))
+print("slowest WGs: dur, seg staged/part/resv/end, cnt, tile, hwreg")
+for i in order[:12]:
+    r = st[i]
+    print(((r[1]-r[0])/100), ((r[2]-r[0])/100, (r[3]-r[2])/100, (r[4]-r[3])/100, (r[1]-r[4])/100), r[5], r[6], hex(r[7]))
+print("fastest:")
+for i in order[-4:]:
+    r = st[i]
+    print(((r[1]-r[0])/100), r[5], r[6], hex(r[7]))
+d = (st[:, 1] - st[:, 0]) / 100
+print("dur percentiles 50/75/90/95/99:", np.percentile(d, [50, 75, 90, 95, 99]).round(1))
