@@ -46,7 +46,7 @@ constexpr int kChunk = 256;  // particles per work chunk (one per lane of a 256-
 
 // Workgroup timeline stamps (diagnostics): [kernel][wg][start, end] in
 // s_memrealtime ticks (100 MHz), written by lane 0 of the first 4096 workgroups.
-__device__ unsigned long long g_stamps[2][4096][8];
+__device__ unsigned long long g_stamps[3][4096][8];
 __device__ __forceinline__ void stamp(int kern, int slot) {
   if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[kern][blockIdx.x][slot] = __builtin_amdgcn_s_memrealtime();
 }
@@ -71,10 +71,30 @@ struct ChunkIn {
   const int* touched;  // [ntiles] tiles whose nodes the next grid update owns
 };
 struct BinOut {
-  int* count;  // [ntiles + 1], zeroed before G2P
-  int* ptile;  // [n] next tile of each particle (storage index)
-  int* pslot;  // [n] rank of the particle inside that tile
+  int* count;    // [ntiles + 1], zeroed before G2P
+  int* ptile;    // [n] next tile of each particle (storage index)
+  int* pslot;    // [n] rank of the particle inside that tile
+  int* tflag;    // [ntiles] tile owned by the next grid update (zeroed before G2P)
+  int td, ntiles;
 };
+
+// A tile's nodes must be updated by the grid step when the tile or one of its
+// 7 lower neighbours holds particles (the 10^3 P2G window of tile t covers the
+// owned nodes of t + {0,1}^3).  The first reservation in a tile flags them
+// (idempotent plain stores); the scan compacts the flags into a list.
+__device__ __noinline__ void mark_window(const BinOut& bo, int t) {
+  const int td = bo.td;
+  const int ti = t / (td * td), tj = (t / td) % td, tk = t % td;
+  for (int a = 0; a < 2; ++a)
+    for (int b = 0; b < 2; ++b)
+      for (int c = 0; c < 2; ++c)
+        if (ti + a < td && tj + b < td && tk + c < td) bo.tflag[t + (a * td + b) * td + c] = 1;
+}
+__device__ __forceinline__ int reserve(const BinOut& bo, int t, int c) {
+  const int old = atomicAdd(&bo.count[t], c);
+  if (old == 0 && t < bo.ntiles) mark_window(bo, t);
+  return old;
+}
 
 __device__ __forceinline__ int tile_of(const float (&x)[3], const GridDims& g, const Tiles& tl, int (&tc)[3]) {
   bool ok = true;
@@ -187,23 +207,93 @@ __device__ __forceinline__ void p2g_term(int i, int j, int k, const float (&fx)[
 // order-independent.  The window is converted back to f32 once and written to
 // the chunk's slot with plain coalesced stores (no global atomics); k_grid sums
 // the <= 8 windows covering each node.
-__device__ __forceinline__ long long to_fixed(float v, int S) {
-  const unsigned b = __float_as_uint(v);
-  const int e = (int)((b >> 23) & 0xffu);
-  const long long mant = (long long)((b & 0x7fffffu) | 0x800000u);
-  const int sh = e - 150 + S;  // |v| = mant * 2^(e-150)
-  long long r = sh >= 0 ? (mant << min(sh, 39)) : (sh > -25 ? (mant >> (-sh)) : 0LL);
-  r = (e == 0) ? 0LL : r;  // zero / denormal
-  return (b >> 31) ? -r : r;
+// v * scale rounded to an integer, as two's complement int64, for
+// |v * scale| < 2^51: adding 1.5 * 2^52 in f64 leaves the integer in the low
+// mantissa bits (scale is a power of two, so the product is exact).
+__device__ __forceinline__ unsigned long long to_fixed(float v, double scale) {
+  const double d = __builtin_fma((double)v, scale, 6755399441055744.0);
+  return (unsigned long long)__double_as_longlong(d) - 0x4338000000000000ull;
+}
+
+__device__ __forceinline__ void lds_add(unsigned long long* a, unsigned long long v) {
+  __hip_atomic_fetch_add(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// The 27 contributions of one particle (utils.py:110-134), evaluated in
+// separable form: with dd_c[o] = (o - fx_c) dx the APIC momentum
+// v + C dpos is accumulated axis by axis (one FMA per component per node) and
+// the stress term dt nvt . dweight, whose dweight factors are products of
+// per-axis weights, collapses to two FMAs per component per node.  Same
+// quantities as the reference's per-node expression, different rounding (a
+// few ulp).
+template <int MAT>
+__device__ __forceinline__ void p2g_scatter(unsigned long long* cell0, const float (&fx)[3], const float (&w)[3][3],
+                                            const float (&dw)[3][3], const float (&v)[3], const float (&C)[3][3],
+                                            float m, const float (&nvt)[3][3], const GridDims& g, float dt,
+                                            double scale) {
+  float dd[3][3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int o = 0; o < 3; ++o) dd[c][o] = ((float)o - fx[c]) * g.dx;
+  float G[3][3];  // dt * inv_dx * nvt
+  if constexpr (MAT != 0) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) G[r][c] = dt * g.inv_dx * nvt[r][c];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    float qi[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) qi[r] = __builtin_fmaf(C[r][0], dd[0][i], v[r]);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      float qij[3], sa[3], sc[3];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) qij[r] = __builtin_fmaf(C[r][1], dd[1][j], qi[r]);
+      const float wij = w[0][i] * w[1][j];
+      const float mij = wij * m;
+      if constexpr (MAT != 0) {
+        const float a0 = dw[0][i] * w[1][j], a1 = w[0][i] * dw[1][j];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          sa[r] = __builtin_fmaf(G[r][0], a0, G[r][1] * a1);
+          sc[r] = G[r][2] * wij;
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const float wm = mij * w[2][k];
+        float add[3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          const float q = __builtin_fmaf(C[r][2], dd[2][k], qij[r]);
+          add[r] = wm * q;
+          if constexpr (MAT != 0) add[r] = __builtin_fmaf(sa[r], w[2][k], __builtin_fmaf(sc[r], dw[2][k], add[r]));
+        }
+        unsigned long long* cell = cell0 + (i * kTW + j) * kTW + k;
+        lds_add(cell + 0 * kWin, to_fixed(add[0], scale));
+        lds_add(cell + 1 * kWin, to_fixed(add[1], scale));
+        lds_add(cell + 2 * kWin, to_fixed(add[2], scale));
+        lds_add(cell + 3 * kWin, to_fixed(wm, scale));
+      }
+    }
+  }
 }
 
 template <int MAT>
 __global__ __launch_bounds__(256) void k_p2g(Particles ps, GridDims g, Tiles tl, ChunkIn ck,
                                              const BcTable* __restrict__ bct, uint32_t mask, float dt, MatConsts mc,
                                              float4* __restrict__ slots, float4* __restrict__ gacc) {
-  __shared__ unsigned long long s_acc[kWin * 4];
+  // channel-planar window: a wave's 8-byte atomics to random nodes of one
+  // channel spread over all 64 banks (the node-interleaved float4 layout put
+  // every channel on 16 of them: 75 % of LDS cycles were bank conflicts)
+  __shared__ unsigned long long s_acc[4 * kWin];
   __shared__ float s_max[4];
   const int ng = g.ng;
+  stamp(0, 0);
   const int nch = ck.nchunk[0];
   for (int w = blockIdx.x; w < nch; w += gridDim.x) {
     const int4 cr = ck.chunk[w];
@@ -265,37 +355,25 @@ __global__ __launch_bounds__(256) void k_p2g(Particles ps, GridDims g, Tiles tl,
     for (int o = 32; o > 0; o >>= 1) bound = fmaxf(bound, __shfl_xor(bound, o));
     if ((k & 63) == 0) s_max[k >> 6] = bound;
     __syncthreads();  // also orders the window zeroing before the adds
+    if (w == (int)blockIdx.x) stamp(0, 2);
     const float bmax = fmaxf(fmaxf(s_max[0], s_max[1]), fmaxf(s_max[2], s_max[3]));
     int ebits;
     frexpf(bmax, &ebits);                     // bmax < 2^ebits
-    const int S = bmax > 0.f ? 53 - ebits : 0;  // 256 * bmax * 2^S < 2^62
+    // every contribution below 2^50 (to_fixed needs < 2^51); a node sums <= 256 of them
+    const int S = bmax > 0.f ? 50 - ebits : 0;
     if (k < cnt) {
       const int l0 = base[0] - tx * kTile, l1 = base[1] - ty * kTile, l2 = base[2] - tz * kTile;
-      unsigned long long* cell0 = s_acc + 4 * ((l0 * kTW + l1) * kTW + l2);
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-#pragma unroll
-          for (int kk = 0; kk < 3; ++kk) {
-            float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-            p2g_term<MAT>(i, j, kk, fx, v, C, m, nvt, g, dt, a);
-            unsigned long long* cell = cell0 + 4 * ((i * kTW + j) * kTW + kk);
-            __hip_atomic_fetch_add(cell + 0, (unsigned long long)to_fixed(a.x, S), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_fetch_add(cell + 1, (unsigned long long)to_fixed(a.y, S), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_fetch_add(cell + 2, (unsigned long long)to_fixed(a.z, S), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_fetch_add(cell + 3, (unsigned long long)to_fixed(a.w, S), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-          }
+      p2g_scatter<MAT>(s_acc + ((l0 * kTW + l1) * kTW + l2), fx, ww, dw, v, C, m, nvt, g, dt, ldexp(1.0, S));
     }
     __syncthreads();
+    if (w == (int)blockIdx.x) stamp(0, 3);
     float* dst = reinterpret_cast<float*>(slots + (size_t)w * kWin);
-    for (int q = k; q < kWin * 4; q += kChunk) dst[q] = (float)ldexp((double)(long long)s_acc[q], -S);
+    for (int q = k; q < kWin * 4; q += kChunk)
+      dst[q] = (float)ldexp((double)(long long)s_acc[(q & 3) * kWin + (q >> 2)], -S);
     __syncthreads();  // LDS reuse by the next chunk
+    if (w == (int)blockIdx.x) stamp(0, 4);
   }
+  stamp(0, 1);
 }
 
 // ------------------------------------------------------------------ grid --
@@ -313,46 +391,77 @@ struct GridStep {
 __global__ __launch_bounds__(256) void k_grid(GridDims g, Tiles tl, ChunkIn ck, const float4* __restrict__ slots,
                                               float4* __restrict__ gacc, float4* __restrict__ gvel,
                                               const BcTable* __restrict__ bct, GridStep gs,
-                                              int* __restrict__ count_next) {
+                                              BinOut nb) {
   // housekeeping for the G2P that follows (stream order makes this safe)
-  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t <= tl.ntiles; t += gridDim.x * blockDim.x) count_next[t] = 0;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t <= tl.ntiles; t += gridDim.x * blockDim.x) {
+    nb.count[t] = 0;
+    if (t < tl.ntiles) nb.tflag[t] = 0;
+  }
 
   const int ng = g.ng, td = tl.td;
   const bool outside = ck.count[tl.ntiles] > 0;
-  const int ntouch = ck.nchunk[1];
-  // one touched tile (8^3 owned nodes) per workgroup iteration, two nodes per lane
-  for (int wt = blockIdx.x; wt < ntouch; wt += gridDim.x)
+  // particles outside the grid scatter through gacc anywhere on the boundary,
+  // and KEEP_GRID wants the dense grid: then every tile is updated
+  const bool all = outside || gs.keep;
+  const int ntouch = all ? tl.ntiles : ck.nchunk[1];
+  // one touched tile (8^3 owned nodes) per workgroup iteration, two nodes per
+  // lane; the chunk ranges of the <= 8 tiles whose windows cover it go to LDS
+  __shared__ int s_c0[8], s_nc[8];
+  for (int wt = blockIdx.x; wt < ntouch; wt += gridDim.x) {
+  const int T = all ? wt : ck.touched[wt];
+  const int ti = T / (td * td), tj = (T / td) % td, tk = T % td;
+  __syncthreads();  // readers of the previous tile's ranges are done
+  if (threadIdx.x < 8) {
+    const int a = threadIdx.x >> 2, b = (threadIdx.x >> 1) & 1, c = threadIdx.x & 1;
+    int c0 = 0, nc = 0;
+    if (ti >= a && tj >= b && tk >= c) {
+      const int t = ((ti - a) * td + (tj - b)) * td + (tk - c);
+      nc = (ck.count[t] + kChunk - 1) / kChunk;
+      c0 = ck.cbase[t];
+    }
+    s_c0[threadIdx.x] = c0;
+    s_nc[threadIdx.x] = nc;
+  }
+  __syncthreads();
   for (int q = threadIdx.x; q < kTile * kTile * kTile; q += blockDim.x) {
-    const int T = ck.touched[wt];
-    const int ti = T / (td * td), tj = (T / td) % td, tk = T % td;
     const int li = q >> 6, lj = (q >> 3) & 7, lk = q & 7;
     const int i = ti * kTile + li, j = tj * kTile + lj, k = tk * kTile + lk;
     if (i >= ng || j >= ng || k >= ng) continue;
     const size_t idx = ((size_t)i * ng + j) * ng + k;
     float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    // first chunk of each covering tile: 8 unconditional loads in flight
+    // (inapplicable ones read the all-zero slot max_chunks), then the rare
+    // extra chunks of tiles holding > 256 particles
+    float4 s8[8];
+    int extra = 0;
 #pragma unroll
-    for (int ax = 0; ax < 2; ++ax) {
-      if (ax && !(li < 2 && ti > 0)) continue;
+    for (int e = 0; e < 8; ++e) {
+      const int ax = e >> 2, ay = (e >> 1) & 1, az = e & 1;
+      const int nc = s_nc[e];
+      const bool on = (!ax || li < 2) && (!ay || lj < 2) && (!az || lk < 2) && nc > 0;
+      const int loc = ((li + kTile * ax) * kTW + (lj + kTile * ay)) * kTW + (lk + kTile * az);
+      const size_t off = on ? (size_t)s_c0[e] * kWin + loc : (size_t)tl.max_chunks * kWin;
+      s8[e] = slots[off];
+      extra |= (on && nc > 1) ? (1 << e) : 0;
+    }
 #pragma unroll
-      for (int ay = 0; ay < 2; ++ay) {
-        if (ay && !(lj < 2 && tj > 0)) continue;
-#pragma unroll
-        for (int az = 0; az < 2; ++az) {
-          if (az && !(lk < 2 && tk > 0)) continue;
-          const int t = ((ti - ax) * td + (tj - ay)) * td + (tk - az);
-          const int c = ck.count[t];
-          if (c > 0) {
-            const int loc = ((li + kTile * ax) * kTW + (lj + kTile * ay)) * kTW + (lk + kTile * az);
-            const int c0 = ck.cbase[t], nc = (c + kChunk - 1) / kChunk;
-            for (int w = c0; w < c0 + nc; ++w) {
-              const float4 s = slots[(size_t)w * kWin + loc];
-              a.x += s.x;
-              a.y += s.y;
-              a.z += s.z;
-              a.w += s.w;
-            }
-          }
-        }
+    for (int e = 0; e < 8; ++e) {
+      a.x += s8[e].x;
+      a.y += s8[e].y;
+      a.z += s8[e].z;
+      a.w += s8[e].w;
+    }
+    while (extra) {
+      const int e = __builtin_ctz(extra);
+      extra &= extra - 1;
+      const int ax = e >> 2, ay = (e >> 1) & 1, az = e & 1;
+      const int loc = ((li + kTile * ax) * kTW + (lj + kTile * ay)) * kTW + (lk + kTile * az);
+      for (int w = s_c0[e] + 1; w < s_c0[e] + s_nc[e]; ++w) {
+        const float4 sv = slots[(size_t)w * kWin + loc];
+        a.x += sv.x;
+        a.y += sv.y;
+        a.z += sv.z;
+        a.w += sv.w;
       }
     }
     if (outside || gs.keep) {
@@ -401,6 +510,7 @@ __global__ __launch_bounds__(256) void k_grid(GridDims g, Tiles tl, ChunkIn ck, 
     }
     gvel[idx] = make_float4(v[0], v[1], v[2], 0.f);
   }
+  }
 }
 
 // ------------------------------------------------------------------- G2P --
@@ -415,46 +525,69 @@ __device__ __forceinline__ void g2p_particle(const Particles& ps, int p, const G
   int base[3];
   float fx[3], w[3][3], dw[3][3];
   bspline(x, g.inv_dx, base, fx, w, dw);
-  float nv[3] = {0.f, 0.f, 0.f}, nC[3][3], nF[3][3];
+  // Separable form of the reference's per-node sums: along k accumulate
+  // P = sum w2 g, K = sum (k - fx2) w2 g, R = sum dw2 g (9 FMAs per node), then
+  // fold each (i, j) row in with its w0/w1 factors.  With dpos = o - fx the
+  // sums are v = sum w g, C = 4 inv_dx sum w g dpos^T, grad v = sum g dweight^T
+  // -- the same quantities, accumulated in a different order (a few ulp).
+  // The i loop stays rolled (weights picked by select) so only one slab of
+  // gathers is live.
+  float nv[3] = {0.f, 0.f, 0.f}, M[3][3], nF[3][3];
 #pragma unroll
   for (int r = 0; r < 3; ++r)
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      nC[r][c] = 0.f;
+      M[r][c] = 0.f;
       nF[r][c] = 0.f;
     }
-  // The i-slab loop stays rolled (weights picked by select) so that only one
-  // 9-node slab of gathers is live: the fully unrolled 27-node form hoists all
-  // 27 loads and needs > 256 VGPRs (1 wave/SIMD).  Same operations and
-  // accumulation order (i, j, k) as the reference.
+  float dk[3], ej[3];
+#pragma unroll
+  for (int o = 0; o < 3; ++o) {
+    dk[o] = ((float)o - fx[2]) * w[2][o];
+    ej[o] = ((float)o - fx[1]) * w[1][o];
+  }
 #pragma unroll 1
   for (int i = 0; i < 3; ++i) {
-    const float w0 = i == 0 ? w[0][0] : (i == 1 ? w[0][1] : w[0][2]);
-    const float dw0 = i == 0 ? dw[0][0] : (i == 1 ? dw[0][1] : dw[0][2]);
-    const float dp0 = (float)i - fx[0];
+    const float a = i == 0 ? w[0][0] : (i == 1 ? w[0][1] : w[0][2]);
+    const float da = i == 0 ? dw[0][0] : (i == 1 ? dw[0][1] : dw[0][2]);
+    const float di = ((float)i - fx[0]) * a;
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
+      float P[3] = {0.f, 0.f, 0.f}, K[3] = {0.f, 0.f, 0.f}, R[3] = {0.f, 0.f, 0.f};
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
         const float4 gv = fetch(base, i, j, k);
-        const float gvv[3] = {gv.x, gv.y, gv.z};
-        const float dpos[3] = {dp0, (float)j - fx[1], (float)k - fx[2]};
-        const float weight = w0 * w[1][j] * w[2][k];
-        const float cw = weight * g.inv_dx * 4.0f;
-        const float dwt[3] = {dw0 * w[1][j] * w[2][k] * g.inv_dx, w0 * dw[1][j] * w[2][k] * g.inv_dx,
-                              w0 * w[1][j] * dw[2][k] * g.inv_dx};
+        const float gg[3] = {gv.x, gv.y, gv.z};
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
-          nv[r] += gvv[r] * weight;
-#pragma unroll
-          for (int c = 0; c < 3; ++c) {
-            nC[r][c] += gvv[r] * dpos[c] * cw;
-            nF[r][c] += gvv[r] * dwt[c];
-          }
+          P[r] = __builtin_fmaf(w[2][k], gg[r], P[r]);
+          K[r] = __builtin_fmaf(dk[k], gg[r], K[r]);
+          R[r] = __builtin_fmaf(dw[2][k], gg[r], R[r]);
         }
+      }
+      const float b = w[1][j], ab = a * b;
+      const float f0 = di * b, f1 = a * ej[j], g0 = da * b, g1 = a * dw[1][j];
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        nv[r] = __builtin_fmaf(ab, P[r], nv[r]);
+        M[r][0] = __builtin_fmaf(f0, P[r], M[r][0]);
+        M[r][1] = __builtin_fmaf(f1, P[r], M[r][1]);
+        M[r][2] = __builtin_fmaf(ab, K[r], M[r][2]);
+        nF[r][0] = __builtin_fmaf(g0, P[r], nF[r][0]);
+        nF[r][1] = __builtin_fmaf(g1, P[r], nF[r][1]);
+        nF[r][2] = __builtin_fmaf(ab, R[r], nF[r][2]);
       }
     }
   }
+  float nC[3][3];
+  const float c4 = 4.0f * g.inv_dx;
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      nC[r][c] = M[r][c] * c4;
+      nF[r][c] = nF[r][c] * g.inv_dx;
+    }
   float F[3][3];
 #pragma unroll
   for (int i = 0; i < 9; ++i) F[i / 3][i % 3] = ps.ld(PF + i, p);
@@ -509,18 +642,28 @@ __global__ __launch_bounds__(256) void k_g2p(Particles ps, GridDims g, Tiles tl,
         int tc[3];
         const int nt = tile_of(xn, g, tl, tc);
         bo.ptile[p] = nt;
-        bo.pslot[p] = atomicAdd(&bo.count[nt], 1);
+        bo.pslot[p] = reserve(bo, nt, 1);
       }
       continue;  // workgroup-uniform
     }
     const int tx = t / (tl.td * tl.td), ty = (t / tl.td) % tl.td, tz = t % tl.td;
     const int lo0 = tx * kTile, lo1 = ty * kTile, lo2 = tz * kTile;
-    for (int q = k; q < kWin; q += kChunk) {
-      const int a = q / (kTW * kTW), b = (q / kTW) % kTW, c = q % kTW;
-      const int ix = lo0 + a, iy = lo1 + b, iz = lo2 + c;
-      float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (ix < ng && iy < ng && iz < ng) gv = gvel[((size_t)ix * ng + iy) * ng + iz];
-      s_win[q] = gv;
+    {
+      // all four loads in flight before the first LDS store (a guarded load
+      // per iteration compiles to one round trip each)
+      float4 gv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int q = min(k + u * kChunk, kWin - 1);
+        const int a = q / (kTW * kTW), b = (q / kTW) % kTW, c = q % kTW;
+        const int ix = lo0 + a, iy = lo1 + b, iz = lo2 + c;
+        const bool in = ix < ng && iy < ng && iz < ng;
+        gv[u] = gvel[in ? ((size_t)ix * ng + iy) * ng + iz : 0];
+        if (!in) gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (k + u * kChunk < kWin) s_win[k + u * kChunk] = gv[u];
     }
     if (k < 27) s_cnt[k] = 0;
     __syncthreads();
@@ -558,14 +701,14 @@ __global__ __launch_bounds__(256) void k_g2p(Particles ps, GridDims g, Tiles tl,
       const int c = s_cnt[k];
       if (c > 0) {
         const int ntile = ((tx + k / 9 - 1) * tl.td + (ty + (k / 3) % 3 - 1)) * tl.td + (tz + k % 3 - 1);
-        s_base[k] = atomicAdd(&bo.count[ntile], c);
+        s_base[k] = reserve(bo, ntile, c);
       }
     }
     __syncthreads();
     if (w == (int)blockIdx.x) stamp(1, 4);
     if (p >= 0) {
       bo.ptile[p] = nt;
-      bo.pslot[p] = code >= 0 ? s_base[code] + lslot : atomicAdd(&bo.count[nt], 1);
+      bo.pslot[p] = code >= 0 ? s_base[code] + lslot : reserve(bo, nt, 1);
     }
     __syncthreads();  // LDS reuse by the next chunk
   }
@@ -583,107 +726,174 @@ __global__ __launch_bounds__(256) void k_bin_all(Particles ps, GridDims g, Tiles
     int tc[3];
     const int t = tile_of(x, g, tl, tc);
     bo.ptile[p] = t;
-    bo.pslot[p] = atomicAdd(&bo.count[t], 1);
+    bo.pslot[p] = reserve(bo, t, 1);
   }
 }
 
-// One workgroup (1024 lanes): per-tile counts -> list offsets (exclusive
-// scan), the chunk records (ceil(count/256) per tile, pseudo-tile last), the
-// list of tiles the next grid update owns and their node bounding box.  A tile
-// is touched when it or one of its 7 lower neighbours holds particles: those
-// are exactly the owners of the nodes inside the occupied tiles' 10^3 windows.
-// Particles outside the grid (or KEEP_GRID) make every tile touched.
+// Per-tile counts -> list offsets (exclusive scan) and chunk records
+// (ceil(count/256) per tile, pseudo-tile last).
 struct ChunkOut {
-  int* cstart;   // [ntiles + 1] first list entry of each tile
-  int* cbase;    // [ntiles + 1]
-  int4* chunk;   // [max_chunks]
-  int* nchunk;   // [2]
-  int* touched;  // [ntiles]
-  Box* box;      // node box of the touched tiles (diagnostics)
+  int* cstart;         // [ntiles + 1] first list entry of each tile
+  int* cbase;          // [ntiles + 1] first chunk of each tile
+  int4* chunk;         // [max_chunks]
+  int* nchunk;         // [2] {chunks, touched tiles}
+  const int* tflag;    // [ntiles] touched flags from the binning
+  int* touched;        // [ntiles] compacted touched tiles
 };
-__device__ __forceinline__ bool tile_touched(const int* __restrict__ count, int t, int td) {
-  const int ti = t / (td * td), tj = (t / td) % td, tk = t % td;
-  bool any = false;
+
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  const int lane = threadIdx.x & 63;
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int c = 0; c < 2; ++c)
-        if (ti >= a && tj >= b && tk >= c) any = any || count[((ti - a) * td + (tj - b)) * td + (tk - c)] > 0;
-  return any;
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(v, o);
+    if (lane >= o) v += y;
+  }
+  return v;
 }
 
-__global__ __launch_bounds__(1024) void k_scan_tiles(Tiles tl, GridDims g, const int* __restrict__ count, ChunkOut co,
-                                                     int all_touched) {
-  __shared__ int s_a[1024], s_b[1024], s_c[1024];
-  __shared__ int s_box[6];
-  const int E = tl.ntiles + 1, td = tl.td;
-  const bool all = all_touched || count[tl.ntiles] > 0;
-  const int per = (E + 1023) / 1024;
-  const int t0 = threadIdx.x * per, t1 = min(E, t0 + per);
-  if (threadIdx.x < 3) {
-    s_box[threadIdx.x] = INT_MAX;
-    s_box[3 + threadIdx.x] = INT_MIN;
-  }
-  int sa = 0, sb = 0, sc = 0;
-  for (int t = t0; t < t1; ++t) {
-    const int c = count[t];
-    sa += c;
-    sb += (c + kChunk - 1) / kChunk;
-    sc += (t < tl.ntiles && (all || tile_touched(count, t, td))) ? 1 : 0;
-  }
-  s_a[threadIdx.x] = sa;
-  s_b[threadIdx.x] = sb;
-  s_c[threadIdx.x] = sc;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
-    const int xa = threadIdx.x >= o ? s_a[threadIdx.x - o] : 0;
-    const int xb = threadIdx.x >= o ? s_b[threadIdx.x - o] : 0;
-    const int xc = threadIdx.x >= o ? s_c[threadIdx.x - o] : 0;
-    __syncthreads();
-    s_a[threadIdx.x] += xa;
-    s_b[threadIdx.x] += xb;
-    s_c[threadIdx.x] += xc;
-    __syncthreads();
-  }
-  int oa = s_a[threadIdx.x] - sa, ob = s_b[threadIdx.x] - sb, oc = s_c[threadIdx.x] - sc;
-  int blo[3] = {INT_MAX, INT_MAX, INT_MAX}, bhi[3] = {INT_MIN, INT_MIN, INT_MIN};
-  for (int t = t0; t < t1; ++t) {
-    const int c = count[t];
-    const int nc = (c + kChunk - 1) / kChunk;
-    co.cstart[t] = oa;
-    co.cbase[t] = ob;
-    for (int k = 0; k < nc; ++k) co.chunk[ob + k] = make_int4(t, oa + k * kChunk, min(kChunk, c - k * kChunk), 0);
-    oa += c;
-    ob += nc;
-    if (t < tl.ntiles && (all || tile_touched(count, t, td))) {
-      co.touched[oc++] = t;
-      const int tc[3] = {t / (td * td), (t / td) % td, t % td};
+// Exclusive scan of three values over a 256-lane workgroup -> per-lane offsets and totals.
+__device__ __forceinline__ void block_scan3(const int (&v)[3], int (&o)[3], int (&tot)[3]) {
+  __shared__ int s_ws[3][4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-      for (int d = 0; d < 3; ++d) {
-        blo[d] = min(blo[d], tc[d] * kTile);
-        bhi[d] = max(bhi[d], min(g.ng - 1, tc[d] * kTile + kTile - 1));
+  for (int r = 0; r < 3; ++r) {
+    const int inc = wave_incl_scan(v[r]);
+    if (lane == 63) s_ws[r][wave] = inc;
+    o[r] = inc - v[r];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    tot[r] = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      if (w < wave) o[r] += s_ws[r][w];
+      tot[r] += s_ws[r][w];
+    }
+  }
+  __syncthreads();  // s_ws reusable
+}
+
+// Fused scan + scatter for grids with <= kFuseTiles tiles: every workgroup
+// scans the (L2-resident) tile counts itself -- a 4097-entry scan is a few
+// microseconds on one CU, so doing it redundantly on all CUs beats a
+// one-workgroup scan kernel followed by a scatter launch.  Workgroup b writes
+// the chunk records of its slice of tiles, then each lane places one particle.
+constexpr int kFuseTiles = 8192;
+__global__ __launch_bounds__(256) void k_finish_bins(Tiles tl, const int* __restrict__ count, ChunkOut co, int n,
+                                                     const int* __restrict__ ptile, const int* __restrict__ pslot,
+                                                     int* __restrict__ list) {
+  __shared__ int s_off[kFuseTiles];  // count | touched << 31, then list offsets
+  const int E = tl.ntiles + 1;
+  stamp(2, 0);
+  // batches of 8 independent loads per lane: the counts were just written by
+  // other XCDs, so each load is a far-memory round trip
+  for (int q0 = 0; q0 < E; q0 += 256 * 8) {
+    int cv[8], fv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int q = q0 + u * 256 + threadIdx.x;
+      cv[u] = count[min(q, E - 1)];  // unguarded: keeps the 16 loads in flight
+      fv[u] = co.tflag[min(q, tl.ntiles - 1)];
+      fv[u] = q < tl.ntiles ? fv[u] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int q = q0 + u * 256 + threadIdx.x;
+      if (q < E) s_off[q] = cv[u] | (fv[u] ? INT_MIN : 0);
+    }
+  }
+  __syncthreads();
+  const int per = (E + 255) / 256;
+  const int t0 = min(E, threadIdx.x * per), t1 = min(E, t0 + per);
+  stamp(2, 2);
+  int v[3] = {0, 0, 0};
+  for (int t = t0; t < t1; ++t) {
+    const int e = s_off[t], c = e & INT_MAX;
+    v[0] += c;
+    v[1] += (c + kChunk - 1) / kChunk;
+    v[2] += e < 0;
+  }
+  int o[3], tot[3];
+  block_scan3(v, o, tot);
+  stamp(2, 3);
+  const int R = (E + gridDim.x - 1) / gridDim.x;
+  const int w0 = blockIdx.x * R, w1 = min(E, w0 + R);
+  for (int t = t0; t < t1; ++t) {
+    const int e = s_off[t], c = e & INT_MAX;
+    const int nc = (c + kChunk - 1) / kChunk;
+    if (t >= w0 && t < w1) {
+      co.cbase[t] = o[1];
+      for (int k = 0; k < nc; ++k)
+        co.chunk[o[1] + k] = make_int4(t, o[0] + k * kChunk, min(kChunk, c - k * kChunk), 0);
+      if (e < 0) co.touched[o[2]] = t;
+    }
+    s_off[t] = o[0];
+    o[0] += c;
+    o[1] += nc;
+    o[2] += e < 0;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    co.nchunk[0] = tot[1];
+    co.nchunk[1] = tot[2];
+  }
+  __syncthreads();
+  stamp(2, 4);
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p < n) list[s_off[ptile[p]] + pslot[p]] = p;
+  stamp(2, 1);
+}
+
+// General path (any number of tiles): one 1024-lane workgroup in passes of
+// 1024 tiles (lane-interleaved, so the stores coalesce), then k_scatter.
+__global__ __launch_bounds__(1024) void k_scan_tiles(Tiles tl, const int* __restrict__ count, ChunkOut co) {
+  __shared__ int s_wsum[3][16];
+  __shared__ int s_carry[3];
+  const int E = tl.ntiles + 1;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (threadIdx.x < 3) s_carry[threadIdx.x] = 0;
+  for (int base = 0; base < E; base += 1024) {
+    const int t = base + threadIdx.x;
+    int v[3];
+    v[0] = t < E ? count[t] : 0;
+    v[1] = (v[0] + kChunk - 1) / kChunk;
+    v[2] = (t < tl.ntiles && co.tflag[t]) ? 1 : 0;
+    int inc[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      inc[r] = wave_incl_scan(v[r]);
+      if (lane == 63) s_wsum[r][wave] = inc[r];
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const int x = lane < 16 ? s_wsum[r][lane] : 0;
+        const int xi = wave_incl_scan(x);
+        if (lane < 16) s_wsum[r][lane] = xi - x;
       }
     }
-  }
-  __syncthreads();
+    __syncthreads();
+    int o[3];
 #pragma unroll
-  for (int d = 0; d < 3; ++d) {
-    const int lo = wave_min(blo[d]), hi = wave_max(bhi[d]);
-    if ((threadIdx.x & 63) == 0) {
-      atomicMin(&s_box[d], lo);
-      atomicMax(&s_box[3 + d], hi);
+    for (int r = 0; r < 3; ++r) o[r] = s_carry[r] + s_wsum[r][wave] + inc[r] - v[r];
+    __syncthreads();  // everyone has read the carry
+    if (threadIdx.x == 1023) {
+#pragma unroll
+      for (int r = 0; r < 3; ++r) s_carry[r] = o[r] + v[r];
     }
+    if (t < E) {
+      co.cstart[t] = o[0];
+      co.cbase[t] = o[1];
+      for (int k = 0; k < v[1]; ++k)
+        co.chunk[o[1] + k] = make_int4(t, o[0] + k * kChunk, min(kChunk, v[0] - k * kChunk), 0);
+      if (v[2]) co.touched[o[2]] = t;
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  if (threadIdx.x == 1023) {
-    co.nchunk[0] = s_b[1023];
-    co.nchunk[1] = s_c[1023];
-  }
-  if (threadIdx.x < 3) {
-    co.box->lo[threadIdx.x] = s_box[threadIdx.x];
-    co.box->hi[threadIdx.x] = s_box[3 + threadIdx.x];
+  if (threadIdx.x == 0) {
+    co.nchunk[0] = s_carry[1];
+    co.nchunk[1] = s_carry[2];
   }
 }
 
@@ -953,10 +1163,10 @@ struct gsmpm_mpm {
   int4* chunk[2] = {nullptr, nullptr};  // [max_chunks] chunk records
   int* nchunk[2] = {nullptr, nullptr};  // [2] {chunks, touched tiles}
   int* touched[2] = {nullptr, nullptr}; // [ntiles] tiles the grid update owns
+  int* tflag[2] = {nullptr, nullptr};   // [ntiles] membership flags of `touched`
   int* list[2] = {nullptr, nullptr};    // [np]
   int* ptile = nullptr;                 // [np]
   int* pslot = nullptr;                 // [np]
-  Box* boxes = nullptr;  // [2] node box of the touched tiles, per parity (diagnostics)
   int cur_box = 0;       // parity of the boxes / buckets the next substep reads
   BcTable host_bc{};
   BcTable* dev_bc = nullptr;
@@ -986,13 +1196,15 @@ static ChunkIn chunk_in(gsmpm_mpm* h, int c) {
   return ChunkIn{h->count[c], h->cbase[c], h->chunk[c], h->nchunk[c], h->list[c], h->touched[c]};
 }
 static ChunkOut chunk_out(gsmpm_mpm* h, int c) {
-  return ChunkOut{h->cstart[c], h->cbase[c], h->chunk[c], h->nchunk[c], h->touched[c], h->boxes + c};
+  return ChunkOut{h->cstart[c], h->cbase[c], h->chunk[c], h->nchunk[c], h->tflag[c], h->touched[c]};
 }
-static BinOut bin_out(gsmpm_mpm* h, int c) { return BinOut{h->count[c], h->ptile, h->pslot}; }
+static BinOut bin_out(gsmpm_mpm* h, int c) {
+  return BinOut{h->count[c], h->ptile, h->pslot, h->tflag[c], h->tl.td, h->tl.ntiles};
+}
 
 static int p2g_grid(gsmpm_mpm* h) { return std::min(h->tl.max_chunks, 1024); }
 static int g2p_grid(gsmpm_mpm* h) { return std::min(h->tl.max_chunks, 1024); }
-static int grid_grid(gsmpm_mpm* h) { return std::min(h->tl.ntiles, 2048); }
+static int grid_grid(gsmpm_mpm* h) { return std::min(h->tl.ntiles, 1024); }
 
 template <int MAT>
 static void launch_p2g(gsmpm_mpm* h, int c, uint32_t mask, float dt, hipStream_t st) {
@@ -1002,10 +1214,14 @@ static void launch_p2g(gsmpm_mpm* h, int c, uint32_t mask, float dt, hipStream_t
 
 // counts of parity c -> list offsets + chunk list, then the per-tile lists
 static int finish_binning(gsmpm_mpm* h, int c, hipStream_t st) {
-  const int all = (h->prm.flags & GSMPM_FLAG_KEEP_GRID) ? 1 : 0;
-  hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, st, h->tl, h->g, h->count[c], chunk_out(h, c), all);
-  hipLaunchKernelGGL(k_scatter, dim3(div_up(h->n, 256)), dim3(256), 0, st, h->n, h->ptile, h->pslot, h->cstart[c],
-                     h->list[c]);
+  if (h->tl.ntiles + 1 <= kFuseTiles) {
+    hipLaunchKernelGGL(k_finish_bins, dim3(div_up(h->n, 256)), dim3(256), 0, st, h->tl, h->count[c], chunk_out(h, c),
+                       h->n, h->ptile, h->pslot, h->list[c]);
+  } else {
+    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, st, h->tl, h->count[c], chunk_out(h, c));
+    hipLaunchKernelGGL(k_scatter, dim3(div_up(h->n, 256)), dim3(256), 0, st, h->n, h->ptile, h->pslot, h->cstart[c],
+                       h->list[c]);
+  }
   GSMPM_LAUNCH_CHECK();
   return GSMPM_OK;
 }
@@ -1014,6 +1230,8 @@ static int finish_binning(gsmpm_mpm* h, int c, hipStream_t st) {
 static int rebin(gsmpm_mpm* h, hipStream_t st) {
   const int c = h->cur_box;
   GSMPM_HIP(hipMemsetAsync(h->count[c], 0, sizeof(int) * (h->tl.ntiles + 1), st));
+  GSMPM_HIP(hipMemsetAsync(h->tflag[c], 0, sizeof(int) * h->tl.ntiles, st));
+  GSMPM_HIP(hipMemsetAsync(h->nchunk[c], 0, sizeof(int) * 2, st));
   hipLaunchKernelGGL(k_bin_all, dim3(div_up(h->n, 256)), dim3(256), 0, st, particles_of(h), h->g, h->tl,
                      bin_out(h, c));
   GSMPM_LAUNCH_CHECK();
@@ -1046,7 +1264,7 @@ static int launch_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc,
     GSMPM_LAUNCH_CHECK();
     if (ev) GSMPM_HIP(hipEventRecord(ev[1], st));
     hipLaunchKernelGGL(k_grid, dim3(grid_grid(h)), dim3(256), 0, st, h->g, h->tl, chunk_in(h, c), h->slots, h->gacc,
-                       h->gvel, h->dev_bc, gs, h->count[nx]);
+                       h->gvel, h->dev_bc, gs, bin_out(h, nx));
     GSMPM_LAUNCH_CHECK();
     if (ev) GSMPM_HIP(hipEventRecord(ev[2], st));
     hipLaunchKernelGGL(k_g2p, dim3(g2p_grid(h)), dim3(kChunk), 0, st, particles_of(h), h->g, h->tl, chunk_in(h, c),
@@ -1191,14 +1409,15 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
   if ((e = hipMalloc(&h->orig, sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc orig");
   if ((e = hipMalloc(&h->gacc, sizeof(float4) * nn)) != hipSuccess) return fail(e, "hipMalloc grid acc");
   if ((e = hipMalloc(&h->gvel, sizeof(float4) * nn)) != hipSuccess) return fail(e, "hipMalloc grid vel");
-  if ((e = hipMalloc(&h->boxes, sizeof(Box) * 2)) != hipSuccess) return fail(e, "hipMalloc boxes");
-  if ((e = hipMemset(h->boxes, 0, sizeof(Box) * 2)) != hipSuccess) return fail(e, "hipMemset");
   h->tl.td = (h->g.ng + kTile - 1) / kTile;
   h->tl.ntiles = h->tl.td * h->tl.td * h->tl.td;
   // every chunk but the last of each tile is full: <= n/256 + occupied tiles
   h->tl.max_chunks = h->n / kChunk + std::min(h->tl.ntiles + 1, h->n) + 1;
-  if ((e = hipMalloc(&h->slots, sizeof(float4) * (size_t)h->tl.max_chunks * kWin)) != hipSuccess)
+  // + one all-zero slot (index max_chunks) that k_grid reads for absent tiles
+  if ((e = hipMalloc(&h->slots, sizeof(float4) * (size_t)(h->tl.max_chunks + 1) * kWin)) != hipSuccess)
     return fail(e, "hipMalloc chunk slots");
+  if ((e = hipMemset(h->slots + (size_t)h->tl.max_chunks * kWin, 0, sizeof(float4) * kWin)) != hipSuccess)
+    return fail(e, "hipMemset");
   for (int c = 0; c < 2; ++c) {
     const size_t E = (size_t)h->tl.ntiles + 1;
     if ((e = hipMalloc(&h->count[c], sizeof(int) * E)) != hipSuccess) return fail(e, "hipMalloc count");
@@ -1206,6 +1425,8 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
     if ((e = hipMalloc(&h->cbase[c], sizeof(int) * E)) != hipSuccess) return fail(e, "hipMalloc cbase");
     if ((e = hipMalloc(&h->chunk[c], sizeof(int4) * (size_t)h->tl.max_chunks)) != hipSuccess) return fail(e, "hipMalloc chunk");
     if ((e = hipMalloc(&h->touched[c], sizeof(int) * (size_t)h->tl.ntiles)) != hipSuccess) return fail(e, "hipMalloc touched");
+    if ((e = hipMalloc(&h->tflag[c], sizeof(int) * (size_t)h->tl.ntiles)) != hipSuccess) return fail(e, "hipMalloc tflag");
+    if ((e = hipMemset(h->tflag[c], 0, sizeof(int) * (size_t)h->tl.ntiles)) != hipSuccess) return fail(e, "hipMemset");
     if ((e = hipMalloc(&h->nchunk[c], sizeof(int) * 2)) != hipSuccess) return fail(e, "hipMalloc nchunk");
     if ((e = hipMalloc(&h->list[c], sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc list");
     if ((e = hipMemset(h->count[c], 0, sizeof(int) * E)) != hipSuccess) return fail(e, "hipMemset");
@@ -1234,7 +1455,6 @@ int gsmpm_mpm_destroy(gsmpm_mpm* h) {
   (void)hipFree(h->orig);
   (void)hipFree(h->gacc);
   (void)hipFree(h->gvel);
-  (void)hipFree(h->boxes);
   (void)hipFree(h->dev_bc);
   (void)hipFree(h->slots);
   for (int c = 0; c < 2; ++c) {
@@ -1243,6 +1463,7 @@ int gsmpm_mpm_destroy(gsmpm_mpm* h) {
     (void)hipFree(h->cbase[c]);
     (void)hipFree(h->chunk[c]);
     (void)hipFree(h->touched[c]);
+    (void)hipFree(h->tflag[c]);
     (void)hipFree(h->nchunk[c]);
     (void)hipFree(h->list[c]);
   }
@@ -1535,18 +1756,33 @@ int gsmpm_mpm_debug_stats(gsmpm_mpm* h, int32_t* out8, void* stream) {
 int gsmpm_debug_stamps(uint64_t* out, void* stream) {
   GSMPM_REQUIRE(out, "gsmpm_debug_stamps: null argument");
   GSMPM_HIP(hipStreamSynchronize((hipStream_t)stream));
-  GSMPM_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 2 * 4096 * 8));
+  GSMPM_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 3 * 4096 * 8));
   return GSMPM_OK;
 }
 
 int gsmpm_mpm_live_box(gsmpm_mpm* h, int32_t* box6, void* stream) {
   GSMPM_REQUIRE(h && box6, "gsmpm_mpm_live_box: null argument");
-  Box b;
-  GSMPM_HIP(hipMemcpyAsync(&b, h->boxes + h->cur_box, sizeof(Box), hipMemcpyDeviceToHost, (hipStream_t)stream));
-  GSMPM_HIP(hipStreamSynchronize((hipStream_t)stream));
+  // node box of the tiles the next grid update owns
+  hipStream_t st = (hipStream_t)stream;
+  const int c = h->cur_box, td = h->tl.td;
+  int nch[2] = {0, 0};
+  GSMPM_HIP(hipMemcpyAsync(nch, h->nchunk[c], sizeof(int) * 2, hipMemcpyDeviceToHost, st));
+  GSMPM_HIP(hipStreamSynchronize(st));
+  std::vector<int> tl(nch[1]);
+  if (nch[1] > 0) {
+    GSMPM_HIP(hipMemcpyAsync(tl.data(), h->touched[c], sizeof(int) * nch[1], hipMemcpyDeviceToHost, st));
+    GSMPM_HIP(hipStreamSynchronize(st));
+  }
   for (int d = 0; d < 3; ++d) {
-    box6[d] = b.lo[d];
-    box6[3 + d] = b.hi[d];
+    box6[d] = INT_MAX;
+    box6[3 + d] = INT_MIN;
+  }
+  for (int t : tl) {
+    const int tc[3] = {t / (td * td), (t / td) % td, t % td};
+    for (int d = 0; d < 3; ++d) {
+      box6[d] = std::min(box6[d], tc[d] * kTile);
+      box6[3 + d] = std::max(box6[3 + d], std::min(h->g.ng - 1, tc[d] * kTile + kTile - 1));
+    }
   }
   return GSMPM_OK;
 }

@@ -14,7 +14,7 @@ sa = scene['sargs']
 masks, t = substep_masks(specs, 0.0, sa.substep_dt, 20)
 sim.profile(sa.substep_dt, masks)
 ms = sim.profile(sa.substep_dt, masks[:1])
-buf = np.zeros((2, 4096, 8), np.uint64)
+buf = np.zeros((3, 4096, 8), np.uint64)
 LIB.gsmpm_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), stream_of(dev))
 print('event ms p2g/grid/g2p', ms)
 for k, name in enumerate(('p2g', 'g2p')):
@@ -41,6 +41,10 @@ print('g2p first-chunk segments (us): start->staged', np.median(seg(0, 2)[ok]), 
       ' particles->reserved', np.median(seg(3, 4)[ok]), ' reserved->end', np.median(seg(4, 1)[ok]))
 print('  max:', seg(0, 2)[ok].max(), seg(2, 3)[ok].max(), seg(3, 4)[ok].max(), seg(4, 1)[ok].max())
 
+p = buf[0].astype(np.int64); p = p[p[:, 0] > 0]
+ok = p[:, 2] > 0
+sg = lambda a, b: np.median((p[ok, b] - p[ok, a]) / 100.0)
+print('p2g first-chunk median segments (us): start->front', sg(0, 2), ' front->scattered', sg(2, 3), ' scattered->written', sg(3, 4), ' ->end', sg(4, 1))
 order = np.argsort(-(st[:, 1] - st[:, 0]))
 print("slowest WGs: dur, seg staged/part/resv/end, cnt, tile, hwreg")
 for i in order[:12]:
@@ -52,3 +56,8 @@ for i in order[-4:]:
     print(((r[1]-r[0])/100), r[5], r[6], hex(r[7]))
 d = (st[:, 1] - st[:, 0]) / 100
 print("dur percentiles 50/75/90/95/99:", np.percentile(d, [50, 75, 90, 95, 99]).round(1))
+f = buf[2].astype(np.int64); f = f[f[:, 0] > 0]
+if len(f):
+    t0 = f[:, 0].min()
+    sg = lambda a, b: np.median((f[:, b] - f[:, a]) / 100.0)
+    print(f'finish_bins: {len(f)} WGs; start spread {(f[:,0].max()-t0)/100:.1f} us, end {(f[:,1].max()-t0)/100:.1f} us; median staged {sg(0,2)} counted+scanned {sg(2,3)} written {sg(3,4)} scattered {sg(4,1)}')
