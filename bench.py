@@ -102,27 +102,49 @@ def make_sim(scene, dev, use_graph=True):
     return sim, specs
 
 
-def algorithmic_bytes(n, live_nodes, material):
-    """Per-launch algorithmic bytes of the three fused kernels."""
-    stress = material != "jelly"
-    p2g = n * (64 + (48 + 40 if stress else 0)) + 16 * live_nodes
-    grid = 48 * live_nodes
-    g2p = n * 144 + 16 * live_nodes
-    return {"k_p2g": p2g, "k_grid": grid, "k_g2p": g2p}
+def algorithmic_bytes(n, n_grid, material):
+    """Per-launch algorithmic bytes: SURVEY.md §8(d)'s per-substep figure
+    B_sub = 208 N + 56 n^3 (+ 8 N for plastic materials), split over the kernel
+    that does each part of the work (Roofline):
+      k_p2g  reads x v C F m vol mu lam (112 B/particle) and writes m + mv
+             of every node (16 B/node, dense n^3 as the reference sweeps it);
+      k_grid reads m + mv (16) and writes v (12) per node;
+      k_g2p  reads v per node (12) and writes x v C F (96 B/particle).
+    The three sum to B_sub exactly."""
+    nodes = n_grid ** 3
+    plastic = 8 * n if material in ("metal",) else 0
+    return {"k_p2g": 112 * n + 16 * nodes + plastic, "k_grid": 28 * nodes, "k_g2p": 96 * n + 12 * nodes}
+
+
+def measured_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (profiles/traffic.json, written by tools/traffic.py from separate
+    FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950 note in
+    MI355X_MICROARCH.md), or None."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        return t["kernels"][kernel]["bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def cpu_baseline(scene, args, budget_s):
-    """The CPU oracle (scalar C restatement, 1 thread) on a bounded sample of
-    the same workload: as many lego substeps at N particles / 128^3 as fit in
-    ~budget_s, timed on this host."""
+    """The CPU restatement (oracle/mpm_oracle.c built with OpenMP:
+    liboracle_omp.so) on a bounded sample of the same workload -- as many lego
+    substeps at N particles / n^3 as fit in ~budget_s -- timed on this host's
+    cores (OMP_NUM_THREADS, else all cores in the affinity mask)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle as O  # cpu_baseline leg only
     sa = scene["sargs"]
     x = scene["xg"].cpu().numpy()
+    os.environ.setdefault("OMP_NUM_THREADS", str(len(os.sched_getaffinity(0))))
     sim = O.OracleMPM(x, scene["covs"].cpu().numpy(), scene["vols"].cpu().numpy(), n_grid=sa.n_grid,
                       grid_extent=sa.grid_extent, material=sa.material, E=sa.E, nu=sa.nu, density=sa.density,
-                      gravity=sa.gravity, jelly_quirk=not sa.jelly_fcr)
+                      gravity=sa.gravity, jelly_quirk=not sa.jelly_fcr, threaded=True)
+    threads = int(O.lib(True).om_threads())
     ops = []
     for d in sa.boundary_conditions:
         if d["type"] == "fixed_cube":
@@ -140,9 +162,9 @@ def cpu_baseline(scene, args, budget_s):
         el = time.perf_counter() - t0
         if el > budget_s or n_done >= 2000:
             break
-    return {"value": n_done * x.shape[0] / el, "unit": "particle-substeps/s", "cores": 1, "kind": "port",
-            "sample": f"{n_done} lego substeps of the same workload ({x.shape[0]} particles, {sa.n_grid}^3), "
-                      f"scalar C oracle (oracle/mpm_oracle.c), {el:.1f}s",
+    return {"value": n_done * x.shape[0] / el, "unit": "particle-substeps/s", "cores": threads, "kind": "port",
+            "sample": f"first {n_done} lego substeps of the same workload ({x.shape[0]} particles, {sa.n_grid}^3, "
+                      f"same BCs), C restatement oracle/mpm_oracle.c with OpenMP ({threads} threads), {el:.1f}s",
             "substeps_per_s": n_done / el}
 
 
@@ -241,11 +263,11 @@ def main():
     kern = None
     if world == 1:
         masks, state["t"] = substep_masks(specs, state["t"], dt, spf)
-        # nodes owned by the grid update: 8^3 per touched tile (Roofline)
+        # nodes owned by the grid update: 8^3 per touched tile
         live = sim.debug_stats()["touched_tiles"] * 512
         kms = sim.profile(dt, masks)
-        kern = {k: kms[i] / spf for i, k in enumerate(("k_p2g", "k_grid", "k_g2p"))}
-        abytes = algorithmic_bytes(n_local, live, sa.material)
+        kern = {k: kms[i] / spf for i, k in enumerate(("k_p2g", "k_grid", "k_g2p", "binning"))}
+        abytes = algorithmic_bytes(n_local, sa.n_grid, sa.material)
 
     out = {
         "metric": METRIC,
@@ -272,12 +294,15 @@ def main():
         "num_rendered": state["K"],
     }
     if kern is not None:
-        dom = max(kern, key=kern.get)
+        # dominant kernel among the three that carry the reference's work
+        dom = max(abytes, key=lambda k: kern[k])
         ach = abytes[dom] / (kern[dom] * 1e-3) / 1e9
         out["kernels_ms_per_launch"] = {k: round(v, 5) for k, v in kern.items()}
         out["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                           "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                           "algorithmic_bytes_per_launch": abytes[dom], "live_nodes": live}
+                           "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": measured_traffic(dom),
+                           "algorithmic_bytes_per_launch": abytes[dom],
+                           "basis": "SURVEY.md 8(d) B_sub = 208 N + 56 n^3 split per kernel (dense grid)",
+                           "live_nodes": live}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(scene, args, args.cpu_seconds)
     if rank == 0:

@@ -905,6 +905,14 @@ __global__ __launch_bounds__(256) void k_scatter(int n, const int* __restrict__ 
 }
 
 
+// Bounded wait (s_memrealtime ticks at 100 MHz) used by the profiling entry point.
+__global__ void k_spin(unsigned long long ticks) {
+  if (threadIdx.x == 0) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(64);
+  }
+}
+
 // ------------------------------------------------------------ postprocess --
 // compute_cov_from_F (utils.py:401-433) + compute_R_from_F (utils.py:376-398)
 __global__ __launch_bounds__(256) void k_postprocess(Particles ps) {
@@ -1253,7 +1261,8 @@ static int launch_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc,
     gs.mask = mask;
     const int c = parity, nx = parity ^ 1;
     if (keep) GSMPM_HIP(hipMemsetAsync(h->gacc, 0, nn * sizeof(float4), st));
-    if (ev) GSMPM_HIP(hipEventRecord(ev[0], st));
+    hipEvent_t* e5 = ev ? ev + 5 * s : nullptr;
+    if (ev) GSMPM_HIP(hipEventRecord(e5[0], st));
     switch (h->mat_kernel) {
       case 0: launch_p2g<0>(h, c, mask, dt, st); break;
       case 1: launch_p2g<1>(h, c, mask, dt, st); break;
@@ -1262,28 +1271,30 @@ static int launch_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc,
       default: launch_p2g<4>(h, c, mask, dt, st); break;
     }
     GSMPM_LAUNCH_CHECK();
-    if (ev) GSMPM_HIP(hipEventRecord(ev[1], st));
+    if (ev) GSMPM_HIP(hipEventRecord(e5[1], st));
     hipLaunchKernelGGL(k_grid, dim3(grid_grid(h)), dim3(256), 0, st, h->g, h->tl, chunk_in(h, c), h->slots, h->gacc,
                        h->gvel, h->dev_bc, gs, bin_out(h, nx));
     GSMPM_LAUNCH_CHECK();
-    if (ev) GSMPM_HIP(hipEventRecord(ev[2], st));
+    if (ev) GSMPM_HIP(hipEventRecord(e5[2], st));
     hipLaunchKernelGGL(k_g2p, dim3(g2p_grid(h)), dim3(kChunk), 0, st, particles_of(h), h->g, h->tl, chunk_in(h, c),
                        bin_out(h, nx), h->gvel, dt);
     GSMPM_LAUNCH_CHECK();
+    if (ev) GSMPM_HIP(hipEventRecord(e5[3], st));
     {
       int rc = finish_binning(h, nx, st);
       if (rc) return rc;
     }
-    if (ev) {
-      GSMPM_HIP(hipEventRecord(ev[3], st));
-      GSMPM_HIP(hipEventSynchronize(ev[3]));
-      for (int k = 0; k < 3; ++k) {
+    if (ev) GSMPM_HIP(hipEventRecord(e5[4], st));
+    parity = nx;
+  }
+  if (ev) {
+    GSMPM_HIP(hipEventSynchronize(ev[5 * nsub - 1]));
+    for (int s = 0; s < nsub; ++s)
+      for (int k = 0; k < 4; ++k) {
         float ms = 0.f;
-        GSMPM_HIP(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
+        GSMPM_HIP(hipEventElapsedTime(&ms, ev[5 * s + k], ev[5 * s + k + 1]));
         kernel_ms[k] += ms;
       }
-    }
-    parity = nx;
   }
   return GSMPM_OK;
 }
@@ -1717,13 +1728,20 @@ int gsmpm_mpm_profile_substeps(gsmpm_mpm* h, float dt, int32_t nsub, const uint3
     return GSMPM_ESTATE;
   }
   hipStream_t st = (hipStream_t)stream;
-  hipEvent_t ev[4];
-  for (int k = 0; k < 4; ++k) GSMPM_HIP(hipEventCreate(&ev[k]));
-  kernel_ms[0] = kernel_ms[1] = kernel_ms[2] = 0.f;
+  for (int k = 0; k < 4; ++k) kernel_ms[k] = 0.f;
+  if (nsub == 0) return GSMPM_OK;
+  std::vector<hipEvent_t> ev(5 * (size_t)nsub);
+  for (auto& e : ev) GSMPM_HIP(hipEventCreate(&e));
+  // Hold the stream with a bounded spin while the host enqueues every launch
+  // and event, so the kernels then run back to back and each event pair
+  // brackets one kernel (not host enqueue gaps).
+  const unsigned long long ticks = 100000ull + 30000ull * (unsigned long long)nsub;  // 1 ms + 0.3 ms/substep
+  hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, st, ticks);
+  GSMPM_LAUNCH_CHECK();
   int parity = h->cur_box;
-  int rc = launch_substeps(h, dt, nsub, bc, st, parity, ev, kernel_ms);
+  int rc = launch_substeps(h, dt, nsub, bc, st, parity, ev.data(), kernel_ms);
   h->cur_box = parity;
-  for (int k = 0; k < 4; ++k) (void)hipEventDestroy(ev[k]);
+  for (auto& e : ev) (void)hipEventDestroy(e);
   return rc;
 }
 

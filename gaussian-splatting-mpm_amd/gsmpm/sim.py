@@ -92,10 +92,11 @@ class Simulator:
         check(LIB.gsmpm_mpm_step(self._h, ctypes.c_float(dt), n, arr, stream_of(self.device)), "gsmpm_mpm_step")
 
     def profile(self, dt: float, masks):
-        """Eager substeps with hipEvents between kernels -> (p2g_ms, grid_ms, g2p_ms) summed."""
+        """Eager substeps with a hipEvent pair per kernel -> summed ms of
+        (k_p2g, k_grid, k_g2p, binning)."""
         n = len(masks)
         arr = (ctypes.c_uint32 * max(1, n))(*[int(m) & 0xFFFFFFFF for m in masks])
-        out = (ctypes.c_float * 3)()
+        out = (ctypes.c_float * 4)()
         check(LIB.gsmpm_mpm_profile_substeps(self._h, ctypes.c_float(dt), n, arr, out, stream_of(self.device)),
               "gsmpm_mpm_profile_substeps")
         return tuple(float(v) for v in out)

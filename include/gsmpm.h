@@ -129,19 +129,22 @@ int gsmpm_mpm_get_grid(gsmpm_mpm* h, int32_t which, float* out, void* stream);
 int gsmpm_mpm_world_outputs(gsmpm_mpm* h, float scale, const float center[3], int32_t render_space,
                             float* means_out, float* cov_out, void* stream);
 
-/* Measurement: run n substeps eagerly with hipEvents between the three fused
- * kernels on `stream`; kernel_ms[0..2] = summed time of k_p2g, k_grid, k_g2p.
+/* Measurement: run n substeps eagerly on `stream` with a hipEvent pair around
+ * every kernel (the stream is held by a bounded spin while the host enqueues,
+ * so the kernels run back to back); kernel_ms[0..3] = summed time of k_p2g,
+ * k_grid, k_g2p and the binning (k_finish_bins or k_scan_tiles + k_scatter).
  * Synchronises `stream`. */
 int gsmpm_mpm_profile_substeps(gsmpm_mpm* h, float dt, int32_t n_substeps, const uint32_t* bc_active,
                                float* kernel_ms, void* stream);
 /* Diagnostics of the tile buckets the next substep reads: {active tiles, max
- * particles in a tile, particles outside the grid, chunks, tiles, binned total,
- * parity, substeps since the last re-sort}.  Synchronises `stream`. */
+ * particles in a tile, particles outside the grid, chunks, touched tiles (owned
+ * by the next grid update), binned total, parity, substeps since the last
+ * re-sort}.  Synchronises `stream`. */
 int gsmpm_mpm_debug_stats(gsmpm_mpm* h, int32_t* out8, void* stream);
-/* Workgroup timeline of the last k_p2g / k_g2p launches: out[2][4096][2]
- * (start, end) in s_memrealtime ticks (100 MHz).  Diagnostics. */
-int gsmpm_debug_stamps(uint64_t* out, void* stream);  /* out[2][4096][8] */
-/* Current live-node box (lo[3], hi[3]) that k_grid sweeps; synchronises `stream`. */
+/* Workgroup timelines of the last k_p2g / k_g2p / k_finish_bins launches:
+ * out[3][4096][8] phase stamps in s_memrealtime ticks (100 MHz).  Diagnostics. */
+int gsmpm_debug_stamps(uint64_t* out, void* stream);
+/* Node box (lo[3], hi[3]) of the tiles the next grid update owns; synchronises `stream`. */
 int gsmpm_mpm_live_box(gsmpm_mpm* h, int32_t* box6, void* stream);
 
 /* Device 3x3 SVD (the ti.svd restatement used by the constitutive kernels) on

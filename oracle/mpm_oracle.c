@@ -10,6 +10,9 @@
 #include "oracle.h"
 #include <math.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include <stdlib.h>
 
 static inline float fmaxf_(float a, float b) { return a > b ? a : b; }
@@ -313,6 +316,7 @@ static void stress_fcr(const float F[9], const float U[9], const float V[9], flo
 /* compute_stress_from_F_trial, utils.py:13-54 */
 void om_stress(om_state* s, float dt) {
   const int mat = s->material;
+#pragma omp parallel for schedule(static)
   for (int p = 0; p < s->n; ++p) {
     float* Ft = s->F_trial + p * 9;
     float* F = s->F + p * 9;
@@ -359,11 +363,11 @@ static void bspline(const float xp[3], float inv_dx, int base[3], float fx[3], f
   }
 }
 
-/* p2g, utils.py:89-134 */
-void om_p2g(om_state* s, float dt) {
+/* p2g, utils.py:89-134: the scatter of one particle */
+static void p2g_particle(om_state* s, int p, float dt) {
   const int ng = s->ng;
   const float dx = s->dx, inv_dx = s->inv_dx;
-  for (int p = 0; p < s->n; ++p) {
+  {
     const float* st = s->stress + p * 9;
     int base[3]; float fx[3], w[3][3], dw[3][3];
     bspline(s->x + p * 3, inv_dx, base, fx, w, dw);
@@ -399,10 +403,46 @@ void om_p2g(om_state* s, float dt) {
   }
 }
 
+void om_p2g(om_state* s, float dt) {
+#ifndef _OPENMP
+  /* the checker: particles in index order, exactly the reference's serial sum */
+  for (int p = 0; p < s->n; ++p) p2g_particle(s, p, dt);
+#else
+  /* CPU-baseline build only (liboracle_omp.so): particles bucketed by x-slabs
+   * of 4 cells (stable, index order inside a slab); even slabs then odd slabs
+   * run in parallel -- a particle writes nodes base..base+2, so slabs two
+   * apart never touch the same node.  Same math, different summation order. */
+  const int W = 4, ng = s->ng, ns = (ng + W - 1) / W;
+  int* cnt = (int*)calloc((size_t)ns + 1, sizeof(int));
+  int* order = (int*)malloc(sizeof(int) * (size_t)(s->n > 0 ? s->n : 1));
+  int* slab = (int*)malloc(sizeof(int) * (size_t)(s->n > 0 ? s->n : 1));
+  for (int p = 0; p < s->n; ++p) {
+    int b = (int)(s->x[p * 3] * s->inv_dx - 0.5f);
+    b = b < 0 ? 0 : (b >= ng ? ng - 1 : b);
+    slab[p] = b / W;
+    cnt[slab[p] + 1]++;
+  }
+  for (int i = 0; i < ns; ++i) cnt[i + 1] += cnt[i];
+  int* pos = (int*)malloc(sizeof(int) * (size_t)ns);
+  memcpy(pos, cnt, sizeof(int) * (size_t)ns);
+  for (int p = 0; p < s->n; ++p) order[pos[slab[p]]++] = p;
+  for (int parity = 0; parity < 2; ++parity) {
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int sl = parity; sl < ns; sl += 2)
+      for (int q = cnt[sl]; q < cnt[sl + 1]; ++q) p2g_particle(s, order[q], dt);
+  }
+  free(pos);
+  free(slab);
+  free(order);
+  free(cnt);
+#endif
+}
+
 /* grid_normalization_and_gravity, utils.py:177-183 */
 void om_grid_normalize(om_state* s, float dt) {
-  size_t nn = (size_t)s->ng * s->ng * s->ng;
-  for (size_t g = 0; g < nn; ++g) {
+  const long nn = (long)s->ng * s->ng * s->ng;
+#pragma omp parallel for schedule(static)
+  for (long g = 0; g < nn; ++g) {
     if (s->gm[g] > 1e-15f) {
       for (int d = 0; d < 3; ++d) s->gv_out[g * 3 + d] = s->gv_in[g * 3 + d] / s->gm[g] + dt * s->gravity[d];
     }
@@ -417,6 +457,7 @@ void om_grid_ops(om_state* s, int n_ops, const om_gridop* ops, const int32_t* ac
   for (int o = 0; o < n_ops; ++o) {
     const om_gridop* op = &ops[o];
     if (op->kind == 0 && !active[o]) continue;
+#pragma omp parallel for schedule(static)
     for (int i = 0; i < ng; ++i)
       for (int j = 0; j < ng; ++j)
         for (int k = 0; k < ng; ++k) {
@@ -453,6 +494,7 @@ void om_grid_ops(om_state* s, int n_ops, const om_gridop* ops, const int32_t* ac
 void om_g2p(om_state* s, float dt) {
   const int ng = s->ng;
   const float inv_dx = s->inv_dx;
+#pragma omp parallel for schedule(static)
   for (int p = 0; p < s->n; ++p) {
     int base[3]; float fx[3], w[3][3], dw[3][3];
     bspline(s->x + p * 3, inv_dx, base, fx, w, dw);
@@ -495,6 +537,7 @@ void om_impulses(om_state* s, int n_imp, const om_impulse* imp, const int32_t* a
   for (int b = 0; b < n_imp; ++b) {
     if (!active[b]) continue;
     const om_impulse* im = &imp[b];
+#pragma omp parallel for schedule(static)
     for (int p = 0; p < s->n; ++p) {
       int in = 1;
       for (int d = 0; d < 3; ++d) in &= fabsf(s->x[p * 3 + d] - im->center[d]) < im->size[d];
@@ -502,6 +545,15 @@ void om_impulses(om_state* s, int n_imp, const om_impulse* imp, const int32_t* a
         for (int d = 0; d < 3; ++d) s->v[p * 3 + d] = s->v[p * 3 + d] + im->force[d] / s->mass[p] * im->substep_dt;
     }
   }
+}
+
+/* threads the substep uses (1 in the serial checker build) */
+int om_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
 }
 
 /* MPM_Simulator.p2g2p, solver.py:27-52 */

@@ -69,6 +69,7 @@ void om_impulses(om_state* s, int n_imp, const om_impulse* imp, const int32_t* a
 void om_substep(om_state* s, float dt, int n_imp, const om_impulse* imp, const int32_t* imp_active,
                 int n_ops, const om_gridop* ops, const int32_t* op_active);
 void om_postprocess(om_state* s);
+int om_threads(void);
 
 /* -------------------------------------------------------- rasterizer --- */
 typedef struct {

@@ -28,7 +28,7 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB = None
+_LIBS = {}
 
 F32P = ctypes.POINTER(ctypes.c_float)
 I32P = ctypes.POINTER(ctypes.c_int32)
@@ -68,17 +68,18 @@ class _RArgs(ctypes.Structure):
                 ("tanfovx", ctypes.c_float), ("tanfovy", ctypes.c_float)]
 
 
-def lib():
-    """Load (building if needed) liboracle.so."""
-    global _LIB
-    if _LIB is None:
-        path = os.path.join(_HERE, "liboracle.so")
+def lib(threaded: bool = False):
+    """Load (building if needed) liboracle.so, or with threaded=True the OpenMP
+    build liboracle_omp.so (bench.py's CPU-baseline leg only)."""
+    name = "liboracle_omp.so" if threaded else "liboracle.so"
+    if name not in _LIBS:
+        path = os.path.join(_HERE, name)
         if not os.path.exists(path):
-            subprocess.check_call(["make", "-s", "-C", _HERE])
+            subprocess.check_call(["make", "-s", "-C", _HERE, name])
         L = ctypes.CDLL(path)
         L.or_forward.restype = ctypes.c_int
-        _LIB = L
-    return _LIB
+        _LIBS[name] = L
+    return _LIBS[name]
 
 
 def _p(a):
@@ -126,7 +127,7 @@ class OracleMPM:
     """Mirror of ``MPM_Simulator`` (solver.py:9-177) on the CPU oracle."""
 
     def __init__(self, x, cov6, vol, *, n_grid, grid_extent=2.0, material="jelly", E=2e6, nu=0.4,
-                 density=1000.0, gravity=(0.0, -9.81, 0.0), jelly_quirk=True, v=None):
+                 density=1000.0, gravity=(0.0, -9.81, 0.0), jelly_quirk=True, v=None, threaded=False):
         x = np.ascontiguousarray(x, np.float32).reshape(-1, 3)
         n = x.shape[0]
         self.n, self.ng = n, n_grid
@@ -159,6 +160,7 @@ class OracleMPM:
                      "yield_stress", "gm", "gv_in", "gv_out"):
             setattr(st, name, _p(getattr(self, name)))
         self._st = st
+        self._L = lib(threaded)
         self.ops = []       # grid postprocess list (fixed_cube / collider) in order
         self.impulses = []
 
@@ -188,11 +190,11 @@ class OracleMPM:
             ia[:len(imp_active)] = imp_active
         if op_active is not None:
             oa[:len(op_active)] = op_active
-        lib().om_substep(ctypes.byref(self._st), ctypes.c_float(dt), ctypes.c_int(len(self.impulses)), imps, _p(ia),
+        self._L.om_substep(ctypes.byref(self._st), ctypes.c_float(dt), ctypes.c_int(len(self.impulses)), imps, _p(ia),
                          ctypes.c_int(len(self.ops)), ops, _p(oa))
 
     def postprocess(self):
-        lib().om_postprocess(ctypes.byref(self._st))
+        self._L.om_postprocess(ctypes.byref(self._st))
 
 
 def raster_forward(means3D, opacities, viewmatrix, projmatrix, campos, bg, W, H, tanfovx, tanfovy,
