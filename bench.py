@@ -12,9 +12,13 @@ n_grid 128 (--n_grid override), jelly as written.
 
     python bench.py [--gpus N --steps K --warmup W]
 
-Multi-GPU (torch.distributed.run, one rank per GPU): spatial-slab weak
-scaling through gsmpm.dist (each rank owns one lego-sized slab of a grid
-stacked along x; halo planes exchanged over RCCL every substep).
+Multi-GPU (torch.distributed.run, one rank per GPU), two modes:
+* default -- weak scaling: every rank simulates and renders its own lego scene
+  (synthetic seed = rank), independent objects, so no collective in the data
+  path (Multi-GPU); timing is barrier + max over ranks.
+* --slab  -- strong scaling of ONE lego scene cut into x-slabs (gsmpm.dist),
+  halo windows of the shared boundary planes exchanged over RCCL every
+  substep; lego's ~64 occupied planes hold at most 4 slabs.
 
 Prints ONE JSON line (rank 0).  value = particle-substeps/s over all ranks.
 """
@@ -47,6 +51,7 @@ def parse():
     ap.add_argument("--no-render", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--slab", action="store_true", help="strong scaling: one scene in x-slabs with halo exchange")
     return ap.parse_args()
 
 
@@ -176,27 +181,42 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # GSMPM_DIST_BACKEND=gloo (+ GSMPM_SHARE_GPU=1: every rank on cuda:0) is for
+    # rehearsing the multi-rank path on a one-GPU box; the driver uses RCCL.
+    backend = os.environ.get("GSMPM_DIST_BACKEND", "nccl")
+    if os.environ.get("GSMPM_SHARE_GPU") == "1":
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    red_dev = dev if backend == "nccl" else torch.device("cpu")
 
     from gsmpm import raster
     from gsmpm.bc import substep_masks
 
-    scene = build_scene(args, dev, rank=0)
+    slab = args.slab and world > 1
+    scene = build_scene(args, dev, rank=0 if slab else rank)
     sa = scene["sargs"]
     dt, spf = sa.substep_dt, sa.steps_per_frame
-    if world > 1:
-        from gsmpm.dist import SlabSimulator
-        sim = SlabSimulator.from_scene(scene, dev, rank, world)
-        specs = sim.specs
-    else:
-        sim, specs = make_sim(scene, dev)
-    n_local = sim.n
     g, mask, cam = scene["g"], scene["mask"], scene["cam"]
     feats = g.get_features[mask].contiguous()
     opac = g.get_opacity[mask].reshape(-1).contiguous()
+    if slab:
+        from gsmpm.dist import SlabSimulator, slab_partition
+        owner, bounds = slab_partition(scene["xg"].cpu().numpy(), sa.n_grid, sa.grid_extent, world)
+        mine = torch.from_numpy((owner == rank).nonzero()[0]).to(dev)
+        for k in ("xg", "covs", "vols"):
+            scene[k] = scene[k][mine].contiguous()
+        feats, opac = feats[mine].contiguous(), opac[mine].contiguous()
+        eng, specs = make_sim(scene, dev)
+        sim = SlabSimulator(eng, rank, world, bounds)
+    else:
+        sim, specs = make_sim(scene, dev)
+    n_local = sim.n
     bg = torch.zeros(3, device=dev)
     tanx, tany = math.tan(cam.FovX * 0.5), math.tan(cam.FovY * 0.5)
     state = {"t": 0.0, "K": 0}
@@ -206,16 +226,11 @@ def main():
         sim.step(dt, masks)
         sim.postprocess()
         if render and not args.no_render:
+            # every rank renders its own particles (its scene, or its slab's share)
             means_r, covs_r = sim.world_outputs(scene["s"], scene["c"].tolist(), render_space=True)
-            if world > 1:
-                means_r, covs_r, fe, op = sim.gather_for_render(means_r, covs_r, feats, opac)
-            else:
-                fe, op = feats, opac
-            if rank == 0:
-                K, _, _ = raster.forward(means_r, op, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg,
-                                         cam.height, cam.width, tanx, tany, sh_degree=3, shs=fe,
-                                         cov3D_precomp=covs_r)
-                state["K"] = K
+            K, _, _ = raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg,
+                                     cam.height, cam.width, tanx, tany, sh_degree=3, shs=feats, cov3D_precomp=covs_r)
+            state["K"] = K
 
     def barrier():
         if world > 1:
@@ -231,10 +246,10 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        tt = torch.tensor([elapsed], device=red_dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-        nt = torch.tensor([n_local], device=dev, dtype=torch.float64)
+        nt = torch.tensor([n_local], device=red_dev, dtype=torch.float64)
         dist.all_reduce(nt)
         n_total = int(nt.item())
     else:
@@ -262,11 +277,12 @@ def main():
         render_ms = (time.perf_counter() - r0) / 5 * 1e3
     kern = None
     if world == 1:
-        masks, state["t"] = substep_masks(specs, state["t"], dt, spf)
         # nodes owned by the grid update: 8^3 per touched tile
         live = sim.debug_stats()["touched_tiles"] * 512
-        kms = sim.profile(dt, masks)
-        kern = {k: kms[i] / spf for i, k in enumerate(("k_p2g", "k_grid", "k_g2p", "binning"))}
+        # per-launch kernel time: hipEvents on the simulator's stream around 20
+        # back-to-back launches of each kernel on the current frame's inputs
+        kms = sim.time_kernels(dt, substep_masks(specs, state["t"], dt, 1)[0][0], reps=20)
+        kern = {k: kms[i] for i, k in enumerate(("k_p2g", "k_grid", "k_g2p", "binning"))}
         abytes = algorithmic_bytes(n_local, sa.n_grid, sa.material)
 
     out = {
@@ -278,14 +294,16 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if slab else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (lego-like Gaussians, seed 0; lego PLY is an LFS pointer in the reference)",
         "config": {"workload": f"{args.config} frame: {spf} substeps + postprocess + render "
                                f"{cam.width}x{cam.height} SH3", "particles_per_gpu": n_local,
                    "particles_total": n_total, "n_grid": sa.n_grid, "material": sa.material,
-                   "substep_dt": dt, "parallelism": f"slab{world}" if world > 1 else "single"},
+                   "substep_dt": dt,
+                   "parallelism": (f"slab{world}" if slab else f"dp{world} independent scenes") if world > 1
+                   else "single"},
         "substeps_per_s": spf * args.steps / elapsed,
         "frames_per_s": args.steps / elapsed,
         "sim_ms_per_frame": sim_ms,

@@ -37,6 +37,8 @@
 
 #include "common.h"
 #include "constitutive.h"
+#include <hip/hip_ext.h>
+
 #include "mpm_common.h"
 #include "svd3.h"
 
@@ -388,10 +390,109 @@ struct GridStep {
   int keep;
 };
 
+// Chunk ranges of the <= 8 tiles whose 10^3 windows cover the owned nodes of
+// tile (ti, tj, tk) -> LDS (lanes 0..7; caller syncs).
+__device__ __forceinline__ void load_cover(const ChunkIn& ck, int td, int ti, int tj, int tk, int* s_c0, int* s_nc) {
+  if (threadIdx.x < 8) {
+    const int a = threadIdx.x >> 2, b = (threadIdx.x >> 1) & 1, c = threadIdx.x & 1;
+    int c0 = 0, nc = 0;
+    if (ti >= a && tj >= b && tk >= c) {
+      const int t = ((ti - a) * td + (tj - b)) * td + (tk - c);
+      nc = (ck.count[t] + kChunk - 1) / kChunk;
+      c0 = ck.cbase[t];
+    }
+    s_c0[threadIdx.x] = c0;
+    s_nc[threadIdx.x] = nc;
+  }
+}
+
+// Sum of the chunk windows covering owned node (li, lj, lk) of a tile: the
+// first chunk of each covering tile as 8 unconditional loads in flight
+// (inapplicable ones read the all-zero slot max_chunks), then the rare extra
+// chunks of tiles holding > 256 particles.
+__device__ __forceinline__ float4 node_sum(const float4* __restrict__ slots, int max_chunks, const int* s_c0,
+                                           const int* s_nc, int li, int lj, int lk) {
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 s8[8];
+  int extra = 0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int ax = e >> 2, ay = (e >> 1) & 1, az = e & 1;
+    const int nc = s_nc[e];
+    const bool on = (!ax || li < 2) && (!ay || lj < 2) && (!az || lk < 2) && nc > 0;
+    const int loc = ((li + kTile * ax) * kTW + (lj + kTile * ay)) * kTW + (lk + kTile * az);
+    const size_t off = on ? (size_t)s_c0[e] * kWin + loc : (size_t)max_chunks * kWin;
+    s8[e] = slots[off];
+    extra |= (on && nc > 1) ? (1 << e) : 0;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    a.x += s8[e].x;
+    a.y += s8[e].y;
+    a.z += s8[e].z;
+    a.w += s8[e].w;
+  }
+  while (extra) {
+    const int e = __builtin_ctz(extra);
+    extra &= extra - 1;
+    const int ax = e >> 2, ay = (e >> 1) & 1, az = e & 1;
+    const int loc = ((li + kTile * ax) * kTW + (lj + kTile * ay)) * kTW + (lk + kTile * az);
+    for (int w = s_c0[e] + 1; w < s_c0[e] + s_nc[e]; ++w) {
+      const float4 sv = slots[(size_t)w * kWin + loc];
+      a.x += sv.x;
+      a.y += sv.y;
+      a.z += sv.z;
+      a.w += sv.w;
+    }
+  }
+  return a;
+}
+
+// Slab halo windows (multi-GPU, gsmpm/dist.py): planes [x0[w], x0[w] + nx) of
+// the dense grid whose (m, m v) partial sums are exchanged with the rank that
+// shares them; the grid update then uses the reduced sums there.
+struct Halo {
+  int n;               // windows (0, 1 or 2)
+  int x0[2];           // first plane of each window (multiple of kTile)
+  int nx;              // planes per window (multiple of kTile)
+  float4* part;        // [n][nx][ng][ng] this rank's partial sums (k_halo_pack)
+  const float4* sum;   // [n][nx][ng][ng] reduced sums (read by k_grid)
+};
+
+// Partial (m, m v) of every node of the halo windows (zeros where this rank
+// has no particles), plus the gacc contributions of out-of-grid particles.
+__global__ __launch_bounds__(256) void k_halo_pack(GridDims g, Tiles tl, ChunkIn ck, const float4* __restrict__ slots,
+                                                   const float4* __restrict__ gacc, Halo halo, int use_gacc) {
+  __shared__ int s_c0[8], s_nc[8];
+  const int ng = g.ng, td = tl.td;
+  const int tpw = (halo.nx / kTile) * td * td;  // tiles per window
+  for (int wt = blockIdx.x; wt < halo.n * tpw; wt += gridDim.x) {
+    const int w = wt / tpw, r = wt % tpw;
+    const int ti = halo.x0[w] / kTile + r / (td * td), tj = (r / td) % td, tk = r % td;
+    __syncthreads();
+    load_cover(ck, td, ti, tj, tk, s_c0, s_nc);
+    __syncthreads();
+    for (int q = threadIdx.x; q < kTile * kTile * kTile; q += blockDim.x) {
+      const int li = q >> 6, lj = (q >> 3) & 7, lk = q & 7;
+      const int i = ti * kTile + li, j = tj * kTile + lj, k = tk * kTile + lk;
+      if (i >= ng || j >= ng || k >= ng) continue;
+      float4 a = node_sum(slots, tl.max_chunks, s_c0, s_nc, li, lj, lk);
+      if (use_gacc) {
+        const float4 o = gacc[((size_t)i * ng + j) * ng + k];
+        a.x += o.x;
+        a.y += o.y;
+        a.z += o.z;
+        a.w += o.w;
+      }
+      halo.part[(((size_t)w * halo.nx + (i - halo.x0[w])) * ng + j) * ng + k] = a;
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void k_grid(GridDims g, Tiles tl, ChunkIn ck, const float4* __restrict__ slots,
                                               float4* __restrict__ gacc, float4* __restrict__ gvel,
                                               const BcTable* __restrict__ bct, GridStep gs,
-                                              BinOut nb) {
+                                              BinOut nb, Halo halo) {
   // housekeeping for the G2P that follows (stream order makes this safe)
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t <= tl.ntiles; t += gridDim.x * blockDim.x) {
     nb.count[t] = 0;
@@ -404,112 +505,75 @@ __global__ __launch_bounds__(256) void k_grid(GridDims g, Tiles tl, ChunkIn ck, 
   // and KEEP_GRID wants the dense grid: then every tile is updated
   const bool all = outside || gs.keep;
   const int ntouch = all ? tl.ntiles : ck.nchunk[1];
-  // one touched tile (8^3 owned nodes) per workgroup iteration, two nodes per
-  // lane; the chunk ranges of the <= 8 tiles whose windows cover it go to LDS
+  // one touched tile (8^3 owned nodes) per workgroup iteration, two nodes per lane
   __shared__ int s_c0[8], s_nc[8];
   for (int wt = blockIdx.x; wt < ntouch; wt += gridDim.x) {
-  const int T = all ? wt : ck.touched[wt];
-  const int ti = T / (td * td), tj = (T / td) % td, tk = T % td;
-  __syncthreads();  // readers of the previous tile's ranges are done
-  if (threadIdx.x < 8) {
-    const int a = threadIdx.x >> 2, b = (threadIdx.x >> 1) & 1, c = threadIdx.x & 1;
-    int c0 = 0, nc = 0;
-    if (ti >= a && tj >= b && tk >= c) {
-      const int t = ((ti - a) * td + (tj - b)) * td + (tk - c);
-      nc = (ck.count[t] + kChunk - 1) / kChunk;
-      c0 = ck.cbase[t];
-    }
-    s_c0[threadIdx.x] = c0;
-    s_nc[threadIdx.x] = nc;
-  }
-  __syncthreads();
-  for (int q = threadIdx.x; q < kTile * kTile * kTile; q += blockDim.x) {
-    const int li = q >> 6, lj = (q >> 3) & 7, lk = q & 7;
-    const int i = ti * kTile + li, j = tj * kTile + lj, k = tk * kTile + lk;
-    if (i >= ng || j >= ng || k >= ng) continue;
-    const size_t idx = ((size_t)i * ng + j) * ng + k;
-    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-    // first chunk of each covering tile: 8 unconditional loads in flight
-    // (inapplicable ones read the all-zero slot max_chunks), then the rare
-    // extra chunks of tiles holding > 256 particles
-    float4 s8[8];
-    int extra = 0;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int ax = e >> 2, ay = (e >> 1) & 1, az = e & 1;
-      const int nc = s_nc[e];
-      const bool on = (!ax || li < 2) && (!ay || lj < 2) && (!az || lk < 2) && nc > 0;
-      const int loc = ((li + kTile * ax) * kTW + (lj + kTile * ay)) * kTW + (lk + kTile * az);
-      const size_t off = on ? (size_t)s_c0[e] * kWin + loc : (size_t)tl.max_chunks * kWin;
-      s8[e] = slots[off];
-      extra |= (on && nc > 1) ? (1 << e) : 0;
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      a.x += s8[e].x;
-      a.y += s8[e].y;
-      a.z += s8[e].z;
-      a.w += s8[e].w;
-    }
-    while (extra) {
-      const int e = __builtin_ctz(extra);
-      extra &= extra - 1;
-      const int ax = e >> 2, ay = (e >> 1) & 1, az = e & 1;
-      const int loc = ((li + kTile * ax) * kTW + (lj + kTile * ay)) * kTW + (lk + kTile * az);
-      for (int w = s_c0[e] + 1; w < s_c0[e] + s_nc[e]; ++w) {
-        const float4 sv = slots[(size_t)w * kWin + loc];
-        a.x += sv.x;
-        a.y += sv.y;
-        a.z += sv.z;
-        a.w += sv.w;
+    const int T = all ? wt : ck.touched[wt];
+    const int ti = T / (td * td), tj = (T / td) % td, tk = T % td;
+    __syncthreads();  // readers of the previous tile's ranges are done
+    load_cover(ck, td, ti, tj, tk, s_c0, s_nc);
+    __syncthreads();
+    int hw = -1;  // halo window holding this tile's planes (windows are tile-aligned)
+    for (int w = 0; w < halo.n; ++w)
+      if (ti * kTile >= halo.x0[w] && ti * kTile < halo.x0[w] + halo.nx) hw = w;
+    for (int q = threadIdx.x; q < kTile * kTile * kTile; q += blockDim.x) {
+      const int li = q >> 6, lj = (q >> 3) & 7, lk = q & 7;
+      const int i = ti * kTile + li, j = tj * kTile + lj, k = tk * kTile + lk;
+      if (i >= ng || j >= ng || k >= ng) continue;
+      const size_t idx = ((size_t)i * ng + j) * ng + k;
+      float4 a;
+      if (hw >= 0) {
+        a = halo.sum[(((size_t)hw * halo.nx + (i - halo.x0[hw])) * ng + j) * ng + k];  // includes gacc
+        if (outside || gs.keep) gacc[idx] = gs.keep ? a : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        a = node_sum(slots, tl.max_chunks, s_c0, s_nc, li, lj, lk);
+        if (outside || gs.keep) {
+          const float4 o = gacc[idx];
+          a.x += o.x;
+          a.y += o.y;
+          a.z += o.z;
+          a.w += o.w;
+          gacc[idx] = gs.keep ? a : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
       }
-    }
-    if (outside || gs.keep) {
-      const float4 o = gacc[idx];
-      a.x += o.x;
-      a.y += o.y;
-      a.z += o.z;
-      a.w += o.w;
-      gacc[idx] = gs.keep ? a : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    float v[3] = {0.f, 0.f, 0.f};
-    if (a.w > 1e-15f) {
-      v[0] = a.x / a.w + gs.dt * gs.gx;
-      v[1] = a.y / a.w + gs.dt * gs.gy;
-      v[2] = a.z / a.w + gs.dt * gs.gz;
-      const int nops = bct->n_ops;
-      for (int o = 0; o < nops; ++o) {
-        const GridOp& op = bct->op[o];
-        const float p0 = (float)i * g.dx, p1 = (float)j * g.dx, p2 = (float)k * g.dx;
-        if (op.kind == 0) {
-          if (!((gs.mask >> op.bit) & 1u)) continue;
-          if (fabsf(p0 - op.a[0]) < op.b[0] && fabsf(p1 - op.a[1]) < op.b[1] && fabsf(p2 - op.a[2]) < op.b[2]) {
-            v[0] = 0.f;
-            v[1] = 0.f;
-            v[2] = 0.f;
-          }
-        } else {
-          const float o0 = p0 - op.a[0], o1 = p1 - op.a[1], o2 = p2 - op.a[2];
-          const float dot = o0 * op.b[0] + o1 * op.b[1] + o2 * op.b[2];
-          if (dot < 0.0f) {
-            const float nc = v[0] * op.b[0] + v[1] * op.b[1] + v[2] * op.b[2];
-            const float mn = fminf(nc, 0.0f);
-#pragma unroll
-            for (int d = 0; d < 3; ++d) v[d] = v[d] - mn * op.b[d];
-            const float len = sqrtf(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
-            if (nc < 0.0f && len > 1e-20f) {
-              const float sc = fmaxf(0.0f, len + nc * op.friction);
-#pragma unroll
-              for (int d = 0; d < 3; ++d) v[d] = sc * (v[d] / len);
+      float v[3] = {0.f, 0.f, 0.f};
+      if (a.w > 1e-15f) {
+        v[0] = a.x / a.w + gs.dt * gs.gx;
+        v[1] = a.y / a.w + gs.dt * gs.gy;
+        v[2] = a.z / a.w + gs.dt * gs.gz;
+        const int nops = bct->n_ops;
+        for (int o = 0; o < nops; ++o) {
+          const GridOp& op = bct->op[o];
+          const float p0 = (float)i * g.dx, p1 = (float)j * g.dx, p2 = (float)k * g.dx;
+          if (op.kind == 0) {
+            if (!((gs.mask >> op.bit) & 1u)) continue;
+            if (fabsf(p0 - op.a[0]) < op.b[0] && fabsf(p1 - op.a[1]) < op.b[1] && fabsf(p2 - op.a[2]) < op.b[2]) {
+              v[0] = 0.f;
+              v[1] = 0.f;
+              v[2] = 0.f;
             }
+          } else {
+            const float o0 = p0 - op.a[0], o1 = p1 - op.a[1], o2 = p2 - op.a[2];
+            const float dot = o0 * op.b[0] + o1 * op.b[1] + o2 * op.b[2];
+            if (dot < 0.0f) {
+              const float nc = v[0] * op.b[0] + v[1] * op.b[1] + v[2] * op.b[2];
+              const float mn = fminf(nc, 0.0f);
 #pragma unroll
-            for (int d = 0; d < 3; ++d) v[d] = v[d] * 0.99f;
+              for (int d = 0; d < 3; ++d) v[d] = v[d] - mn * op.b[d];
+              const float len = sqrtf(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+              if (nc < 0.0f && len > 1e-20f) {
+                const float sc = fmaxf(0.0f, len + nc * op.friction);
+#pragma unroll
+                for (int d = 0; d < 3; ++d) v[d] = sc * (v[d] / len);
+              }
+#pragma unroll
+              for (int d = 0; d < 3; ++d) v[d] = v[d] * 0.99f;
+            }
           }
         }
       }
+      gvel[idx] = make_float4(v[0], v[1], v[2], 0.f);
     }
-    gvel[idx] = make_float4(v[0], v[1], v[2], 0.f);
-  }
   }
 }
 
@@ -739,6 +803,8 @@ struct ChunkOut {
   int* nchunk;         // [2] {chunks, touched tiles}
   const int* tflag;    // [ntiles] touched flags from the binning
   int* touched;        // [ntiles] compacted touched tiles
+  int* escape;         // [1] set when a touched tile lies outside tile planes [tx_lo, tx_hi]
+  int tx_lo, tx_hi;    // (slab ranks: the planes this rank may touch, own slab + halo windows)
 };
 
 __device__ __forceinline__ int wave_incl_scan(int v) {
@@ -826,7 +892,11 @@ __global__ __launch_bounds__(256) void k_finish_bins(Tiles tl, const int* __rest
       co.cbase[t] = o[1];
       for (int k = 0; k < nc; ++k)
         co.chunk[o[1] + k] = make_int4(t, o[0] + k * kChunk, min(kChunk, c - k * kChunk), 0);
-      if (e < 0) co.touched[o[2]] = t;
+      if (e < 0) {
+        co.touched[o[2]] = t;
+        const int tx = t / (tl.td * tl.td);
+        if (tx < co.tx_lo || tx > co.tx_hi) *co.escape = 1;
+      }
     }
     s_off[t] = o[0];
     o[0] += c;
@@ -887,7 +957,11 @@ __global__ __launch_bounds__(1024) void k_scan_tiles(Tiles tl, const int* __rest
       co.cbase[t] = o[1];
       for (int k = 0; k < v[1]; ++k)
         co.chunk[o[1] + k] = make_int4(t, o[0] + k * kChunk, min(kChunk, v[0] - k * kChunk), 0);
-      if (v[2]) co.touched[o[2]] = t;
+      if (v[2]) {
+        co.touched[o[2]] = t;
+        const int tx = t / (tl.td * tl.td);
+        if (tx < co.tx_lo || tx > co.tx_hi) *co.escape = 1;
+      }
     }
     __syncthreads();
   }
@@ -904,14 +978,6 @@ __global__ __launch_bounds__(256) void k_scatter(int n, const int* __restrict__ 
   list[cstart[ptile[p]] + pslot[p]] = p;
 }
 
-
-// Bounded wait (s_memrealtime ticks at 100 MHz) used by the profiling entry point.
-__global__ void k_spin(unsigned long long ticks) {
-  if (threadIdx.x == 0) {
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(64);
-  }
-}
 
 // ------------------------------------------------------------ postprocess --
 // compute_cov_from_F (utils.py:401-433) + compute_R_from_F (utils.py:376-398)
@@ -1173,6 +1239,9 @@ struct gsmpm_mpm {
   int* touched[2] = {nullptr, nullptr}; // [ntiles] tiles the grid update owns
   int* tflag[2] = {nullptr, nullptr};   // [ntiles] membership flags of `touched`
   int* list[2] = {nullptr, nullptr};    // [np]
+  Halo halo{};                          // slab halo windows (gsmpm_mpm_set_halo)
+  int tx_lo = 0, tx_hi = 1 << 30;       // tile planes this rank may touch
+  int* escape = nullptr;                // [1] device flag, see ChunkOut
   int* ptile = nullptr;                 // [np]
   int* pslot = nullptr;                 // [np]
   int cur_box = 0;       // parity of the boxes / buckets the next substep reads
@@ -1204,7 +1273,8 @@ static ChunkIn chunk_in(gsmpm_mpm* h, int c) {
   return ChunkIn{h->count[c], h->cbase[c], h->chunk[c], h->nchunk[c], h->list[c], h->touched[c]};
 }
 static ChunkOut chunk_out(gsmpm_mpm* h, int c) {
-  return ChunkOut{h->cstart[c], h->cbase[c], h->chunk[c], h->nchunk[c], h->tflag[c], h->touched[c]};
+  return ChunkOut{h->cstart[c], h->cbase[c], h->chunk[c], h->nchunk[c], h->tflag[c], h->touched[c],
+                  h->escape, h->tx_lo, h->tx_hi};
 }
 static BinOut bin_out(gsmpm_mpm* h, int c) {
   return BinOut{h->count[c], h->ptile, h->pslot, h->tflag[c], h->tl.td, h->tl.ntiles};
@@ -1214,21 +1284,33 @@ static int p2g_grid(gsmpm_mpm* h) { return std::min(h->tl.max_chunks, 1024); }
 static int g2p_grid(gsmpm_mpm* h) { return std::min(h->tl.max_chunks, 1024); }
 static int grid_grid(gsmpm_mpm* h) { return std::min(h->tl.ntiles, 1024); }
 
+// Kernel launch; with ev = {start, stop} the dispatch packet itself stamps the
+// two events (hipExtLaunchKernel), i.e. the kernel's own begin/end -- the same
+// interval rocprofv3's kernel trace reports.
+template <typename F, typename... Args>
+static void launch(const hipEvent_t* ev, F kernel, dim3 grid, dim3 block, hipStream_t st, Args... args) {
+  if (ev)
+    hipExtLaunchKernelGGL(kernel, grid, block, 0, st, ev[0], ev[1], 0, args...);
+  else
+    hipLaunchKernelGGL(kernel, grid, block, 0, st, args...);
+}
+
 template <int MAT>
-static void launch_p2g(gsmpm_mpm* h, int c, uint32_t mask, float dt, hipStream_t st) {
-  hipLaunchKernelGGL(k_p2g<MAT>, dim3(p2g_grid(h)), dim3(kChunk), 0, st, particles_of(h), h->g, h->tl, chunk_in(h, c),
-                     h->dev_bc, mask, dt, h->mc, h->slots, h->gacc);
+static void launch_p2g(gsmpm_mpm* h, int c, uint32_t mask, float dt, hipStream_t st, const hipEvent_t* ev) {
+  launch(ev, k_p2g<MAT>, dim3(p2g_grid(h)), dim3(kChunk), st, particles_of(h), h->g, h->tl, chunk_in(h, c),
+         (const BcTable*)h->dev_bc, mask, dt, h->mc, h->slots, h->gacc);
 }
 
 // counts of parity c -> list offsets + chunk list, then the per-tile lists
-static int finish_binning(gsmpm_mpm* h, int c, hipStream_t st) {
+static int finish_binning(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t* ev = nullptr) {
   if (h->tl.ntiles + 1 <= kFuseTiles) {
-    hipLaunchKernelGGL(k_finish_bins, dim3(div_up(h->n, 256)), dim3(256), 0, st, h->tl, h->count[c], chunk_out(h, c),
-                       h->n, h->ptile, h->pslot, h->list[c]);
+    launch(ev, k_finish_bins, dim3(div_up(h->n, 256)), dim3(256), st, h->tl, (const int*)h->count[c], chunk_out(h, c),
+           h->n, (const int*)h->ptile, (const int*)h->pslot, h->list[c]);
   } else {
-    hipLaunchKernelGGL(k_scan_tiles, dim3(1), dim3(1024), 0, st, h->tl, h->count[c], chunk_out(h, c));
-    hipLaunchKernelGGL(k_scatter, dim3(div_up(h->n, 256)), dim3(256), 0, st, h->n, h->ptile, h->pslot, h->cstart[c],
-                       h->list[c]);
+    const hipEvent_t e0[2] = {ev ? ev[0] : nullptr, nullptr}, e1[2] = {nullptr, ev ? ev[1] : nullptr};
+    launch(ev ? e0 : nullptr, k_scan_tiles, dim3(1), dim3(1024), st, h->tl, (const int*)h->count[c], chunk_out(h, c));
+    launch(ev ? e1 : nullptr, k_scatter, dim3(div_up(h->n, 256)), dim3(256), st, h->n, (const int*)h->ptile,
+           (const int*)h->pslot, (const int*)h->cstart[c], h->list[c]);
   }
   GSMPM_LAUNCH_CHECK();
   return GSMPM_OK;
@@ -1246,53 +1328,71 @@ static int rebin(gsmpm_mpm* h, hipStream_t st) {
   return finish_binning(h, c, st);
 }
 
-static int launch_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc, hipStream_t st, int& parity,
-                           hipEvent_t* ev = nullptr, float* kernel_ms = nullptr) {
-  const size_t nn = (size_t)h->g.ng * h->g.ng * h->g.ng;
-  const bool keep = (h->prm.flags & GSMPM_FLAG_KEEP_GRID) != 0;
+static GridStep grid_step(gsmpm_mpm* h, float dt, uint32_t mask) {
   GridStep gs;
   gs.dt = dt;
   gs.gx = (float)h->prm.gravity[0];
   gs.gy = (float)h->prm.gravity[1];
   gs.gz = (float)h->prm.gravity[2];
-  gs.keep = keep ? 1 : 0;
+  gs.keep = (h->prm.flags & GSMPM_FLAG_KEEP_GRID) ? 1 : 0;
+  gs.mask = mask;
+  return gs;
+}
+
+// First half of a substep (parity c): P2G, and the halo partial sums when the
+// simulator is one slab of a multi-GPU domain.
+static int substep_begin(gsmpm_mpm* h, float dt, uint32_t mask, int c, hipStream_t st, const hipEvent_t* e8) {
+  const bool keep = (h->prm.flags & GSMPM_FLAG_KEEP_GRID) != 0;
+  if (keep) {
+    const size_t nn = (size_t)h->g.ng * h->g.ng * h->g.ng;
+    GSMPM_HIP(hipMemsetAsync(h->gacc, 0, nn * sizeof(float4), st));
+  }
+  switch (h->mat_kernel) {
+    case 0: launch_p2g<0>(h, c, mask, dt, st, e8); break;
+    case 1: launch_p2g<1>(h, c, mask, dt, st, e8); break;
+    case 2: launch_p2g<2>(h, c, mask, dt, st, e8); break;
+    case 3: launch_p2g<3>(h, c, mask, dt, st, e8); break;
+    default: launch_p2g<4>(h, c, mask, dt, st, e8); break;
+  }
+  GSMPM_LAUNCH_CHECK();
+  if (h->halo.n > 0) {
+    // gacc holds out-of-grid contributions only when particles left the grid; include it always (cheap)
+    hipLaunchKernelGGL(k_halo_pack, dim3(1024), dim3(256), 0, st, h->g, h->tl, chunk_in(h, c),
+                       (const float4*)h->slots, (const float4*)h->gacc, h->halo, 1);
+    GSMPM_LAUNCH_CHECK();
+  }
+  return GSMPM_OK;
+}
+
+// Second half: grid update (reduced halo sums in the windows), G2P, binning of parity nx.
+static int substep_end(gsmpm_mpm* h, float dt, uint32_t mask, int c, hipStream_t st, const hipEvent_t* e8) {
+  const int nx = c ^ 1;
+  launch(e8 ? e8 + 2 : nullptr, k_grid, dim3(grid_grid(h)), dim3(256), st, h->g, h->tl, chunk_in(h, c),
+         (const float4*)h->slots, h->gacc, h->gvel, (const BcTable*)h->dev_bc, grid_step(h, dt, mask), bin_out(h, nx),
+         h->halo);
+  GSMPM_LAUNCH_CHECK();
+  launch(e8 ? e8 + 4 : nullptr, k_g2p, dim3(g2p_grid(h)), dim3(kChunk), st, particles_of(h), h->g, h->tl,
+         chunk_in(h, c), bin_out(h, nx), (const float4*)h->gvel, dt);
+  GSMPM_LAUNCH_CHECK();
+  return finish_binning(h, nx, st, e8 ? e8 + 6 : nullptr);
+}
+
+static int launch_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc, hipStream_t st, int& parity,
+                           hipEvent_t* ev = nullptr, float* kernel_ms = nullptr) {
   for (int s = 0; s < nsub; ++s) {
     const uint32_t mask = bc ? bc[s] : 0xffffffffu;
-    gs.mask = mask;
-    const int c = parity, nx = parity ^ 1;
-    if (keep) GSMPM_HIP(hipMemsetAsync(h->gacc, 0, nn * sizeof(float4), st));
-    hipEvent_t* e5 = ev ? ev + 5 * s : nullptr;
-    if (ev) GSMPM_HIP(hipEventRecord(e5[0], st));
-    switch (h->mat_kernel) {
-      case 0: launch_p2g<0>(h, c, mask, dt, st); break;
-      case 1: launch_p2g<1>(h, c, mask, dt, st); break;
-      case 2: launch_p2g<2>(h, c, mask, dt, st); break;
-      case 3: launch_p2g<3>(h, c, mask, dt, st); break;
-      default: launch_p2g<4>(h, c, mask, dt, st); break;
-    }
-    GSMPM_LAUNCH_CHECK();
-    if (ev) GSMPM_HIP(hipEventRecord(e5[1], st));
-    hipLaunchKernelGGL(k_grid, dim3(grid_grid(h)), dim3(256), 0, st, h->g, h->tl, chunk_in(h, c), h->slots, h->gacc,
-                       h->gvel, h->dev_bc, gs, bin_out(h, nx));
-    GSMPM_LAUNCH_CHECK();
-    if (ev) GSMPM_HIP(hipEventRecord(e5[2], st));
-    hipLaunchKernelGGL(k_g2p, dim3(g2p_grid(h)), dim3(kChunk), 0, st, particles_of(h), h->g, h->tl, chunk_in(h, c),
-                       bin_out(h, nx), h->gvel, dt);
-    GSMPM_LAUNCH_CHECK();
-    if (ev) GSMPM_HIP(hipEventRecord(e5[3], st));
-    {
-      int rc = finish_binning(h, nx, st);
-      if (rc) return rc;
-    }
-    if (ev) GSMPM_HIP(hipEventRecord(e5[4], st));
-    parity = nx;
+    const hipEvent_t* e8 = ev ? ev + 8 * s : nullptr;
+    int rc = substep_begin(h, dt, mask, parity, st, e8);
+    if (!rc) rc = substep_end(h, dt, mask, parity, st, e8);
+    if (rc) return rc;
+    parity ^= 1;
   }
   if (ev) {
-    GSMPM_HIP(hipEventSynchronize(ev[5 * nsub - 1]));
+    GSMPM_HIP(hipStreamSynchronize(st));
     for (int s = 0; s < nsub; ++s)
       for (int k = 0; k < 4; ++k) {
         float ms = 0.f;
-        GSMPM_HIP(hipEventElapsedTime(&ms, ev[5 * s + k], ev[5 * s + k + 1]));
+        GSMPM_HIP(hipEventElapsedTime(&ms, ev[8 * s + 2 * k], ev[8 * s + 2 * k + 1]));
         kernel_ms[k] += ms;
       }
   }
@@ -1443,6 +1543,8 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
     if ((e = hipMemset(h->count[c], 0, sizeof(int) * E)) != hipSuccess) return fail(e, "hipMemset");
     if ((e = hipMemset(h->nchunk[c], 0, sizeof(int) * 2)) != hipSuccess) return fail(e, "hipMemset");
   }
+  if ((e = hipMalloc(&h->escape, sizeof(int))) != hipSuccess) return fail(e, "hipMalloc escape");
+  if ((e = hipMemset(h->escape, 0, sizeof(int))) != hipSuccess) return fail(e, "hipMemset");
   if ((e = hipMalloc(&h->ptile, sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc ptile");
   if ((e = hipMalloc(&h->pslot, sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc pslot");
   if ((e = hipMalloc(&h->dev_bc, sizeof(BcTable))) != hipSuccess) return fail(e, "hipMalloc bc table");
@@ -1479,6 +1581,7 @@ int gsmpm_mpm_destroy(gsmpm_mpm* h) {
     (void)hipFree(h->list[c]);
   }
   (void)hipFree(h->ptile);
+  (void)hipFree(h->escape);
   (void)hipFree(h->pslot);
   (void)hipFree(h->planes_tmp);
   (void)hipFree(h->orig_tmp);
@@ -1602,6 +1705,11 @@ int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t nsub, const uint32_t* bc, voi
     return GSMPM_ESTATE;
   }
   GSMPM_REQUIRE(nsub >= 0, "gsmpm_mpm_step: n_substeps < 0");
+  if (h->halo.n > 0) {
+    set_error("gsmpm_mpm_step: this simulator is a slab with halo windows; step it with "
+              "gsmpm_mpm_substep_begin / exchange / gsmpm_mpm_substep_end");
+    return GSMPM_ESTATE;
+  }
   if (nsub == 0) return GSMPM_OK;
   hipStream_t st = (hipStream_t)stream;
   if (!(h->prm.flags & GSMPM_FLAG_NO_SORT) && h->resort_interval > 0 && h->since_sort >= h->resort_interval) {
@@ -1649,6 +1757,67 @@ int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t nsub, const uint32_t* bc, voi
   }
   GSMPM_HIP(hipGraphLaunch(it->second, st));
   h->cur_box = h->graph_box_parity[key];
+  return GSMPM_OK;
+}
+
+int gsmpm_mpm_set_halo(gsmpm_mpm* h, int32_t n_windows, const int32_t* x0, int32_t nx, float* part, const float* sum,
+                       int32_t allow_lo, int32_t allow_hi) {
+  GSMPM_REQUIRE(h, "gsmpm_mpm_set_halo: null handle");
+  GSMPM_REQUIRE(n_windows >= 0 && n_windows <= 2, "gsmpm_mpm_set_halo: 0..2 windows");
+  GSMPM_REQUIRE(allow_lo < allow_hi, "gsmpm_mpm_set_halo: empty allowed plane range");
+  Halo hl{};
+  hl.n = n_windows;
+  if (n_windows > 0) {
+    GSMPM_REQUIRE(x0 && part && sum, "gsmpm_mpm_set_halo: null window argument");
+    GSMPM_REQUIRE(nx > 0 && nx % kTile == 0, "gsmpm_mpm_set_halo: nx must be a positive multiple of 8");
+    for (int w = 0; w < n_windows; ++w) {
+      GSMPM_REQUIRE(x0[w] >= 0 && x0[w] % kTile == 0 && x0[w] + nx <= h->tl.td * kTile,
+                    "gsmpm_mpm_set_halo: window must be tile-aligned and inside the grid");
+      hl.x0[w] = x0[w];
+    }
+    if (n_windows == 2) GSMPM_REQUIRE(x0[0] + nx <= x0[1], "gsmpm_mpm_set_halo: windows overlap / out of order");
+    hl.nx = nx;
+    hl.part = reinterpret_cast<float4*>(part);
+    hl.sum = reinterpret_cast<const float4*>(sum);
+  }
+  h->halo = hl;
+  h->tx_lo = std::max(0, allow_lo) / kTile;
+  h->tx_hi = std::max(0, allow_hi - 1) / kTile;
+  drop_graphs(h);  // kernel arguments changed
+  return GSMPM_OK;
+}
+
+int gsmpm_mpm_substep_begin(gsmpm_mpm* h, float dt, uint32_t bc_active, void* stream) {
+  GSMPM_REQUIRE(h, "gsmpm_mpm_substep_begin: null handle");
+  if (!h->has_particles) {
+    set_error("gsmpm_mpm_substep_begin: particles not set");
+    return GSMPM_ESTATE;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  if (!(h->prm.flags & GSMPM_FLAG_NO_SORT) && h->resort_interval > 0 && h->since_sort >= h->resort_interval) {
+    int rc = resort(h, st);
+    if (rc) return rc;
+  }
+  return substep_begin(h, dt, bc_active, h->cur_box, st, nullptr);
+}
+
+int gsmpm_mpm_substep_end(gsmpm_mpm* h, float dt, uint32_t bc_active, void* stream) {
+  GSMPM_REQUIRE(h, "gsmpm_mpm_substep_end: null handle");
+  int rc = substep_end(h, dt, bc_active, h->cur_box, (hipStream_t)stream, nullptr);
+  if (rc) return rc;
+  h->cur_box ^= 1;
+  h->since_sort += 1;
+  return GSMPM_OK;
+}
+
+int gsmpm_mpm_halo_status(gsmpm_mpm* h, int32_t* escaped, void* stream) {
+  GSMPM_REQUIRE(h && escaped, "gsmpm_mpm_halo_status: null argument");
+  hipStream_t st = (hipStream_t)stream;
+  int v = 0;
+  GSMPM_HIP(hipMemcpyAsync(&v, h->escape, sizeof(int), hipMemcpyDeviceToHost, st));
+  GSMPM_HIP(hipStreamSynchronize(st));
+  GSMPM_HIP(hipMemsetAsync(h->escape, 0, sizeof(int), st));
+  *escaped = v;
   return GSMPM_OK;
 }
 
@@ -1730,19 +1899,70 @@ int gsmpm_mpm_profile_substeps(gsmpm_mpm* h, float dt, int32_t nsub, const uint3
   hipStream_t st = (hipStream_t)stream;
   for (int k = 0; k < 4; ++k) kernel_ms[k] = 0.f;
   if (nsub == 0) return GSMPM_OK;
-  std::vector<hipEvent_t> ev(5 * (size_t)nsub);
+  std::vector<hipEvent_t> ev(8 * (size_t)nsub);
   for (auto& e : ev) GSMPM_HIP(hipEventCreate(&e));
-  // Hold the stream with a bounded spin while the host enqueues every launch
-  // and event, so the kernels then run back to back and each event pair
-  // brackets one kernel (not host enqueue gaps).
-  const unsigned long long ticks = 100000ull + 30000ull * (unsigned long long)nsub;  // 1 ms + 0.3 ms/substep
-  hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, st, ticks);
-  GSMPM_LAUNCH_CHECK();
   int parity = h->cur_box;
   int rc = launch_substeps(h, dt, nsub, bc, st, parity, ev.data(), kernel_ms);
   h->cur_box = parity;
   for (auto& e : ev) (void)hipEventDestroy(e);
   return rc;
+}
+
+int gsmpm_mpm_time_kernels(gsmpm_mpm* h, float dt, uint32_t bc_active, int32_t reps, float* ms4, void* stream) {
+  GSMPM_REQUIRE(h && ms4 && reps > 0, "gsmpm_mpm_time_kernels: bad argument");
+  if (!h->has_particles) {
+    set_error("gsmpm_mpm_time_kernels: particles not set");
+    return GSMPM_ESTATE;
+  }
+  hipStream_t st = (hipStream_t)stream;
+  const size_t pbytes = sizeof(float) * (size_t)NPLANES * h->np;
+  if (!h->planes_tmp) GSMPM_HIP(hipMalloc(&h->planes_tmp, pbytes));
+  GSMPM_HIP(hipMemcpyAsync(h->planes_tmp, h->planes, pbytes, hipMemcpyDeviceToDevice, st));
+  const int c = h->cur_box, nx = c ^ 1;
+  const GridStep gs = grid_step(h, dt, bc_active);
+  hipEvent_t e[2];
+  GSMPM_HIP(hipEventCreate(&e[0]));
+  GSMPM_HIP(hipEventCreate(&e[1]));
+  auto grid = [&]() {
+    launch(nullptr, k_grid, dim3(grid_grid(h)), dim3(256), st, h->g, h->tl, chunk_in(h, c), (const float4*)h->slots,
+           h->gacc, h->gvel, (const BcTable*)h->dev_bc, gs, bin_out(h, nx), h->halo);
+  };
+  auto g2p = [&]() {
+    launch(nullptr, k_g2p, dim3(g2p_grid(h)), dim3(kChunk), st, particles_of(h), h->g, h->tl, chunk_in(h, c),
+           bin_out(h, nx), (const float4*)h->gvel, dt);
+  };
+  auto timed = [&](int k, auto&& body) -> int {
+    GSMPM_HIP(hipEventRecord(e[0], st));
+    for (int r = 0; r < reps; ++r) body();
+    GSMPM_HIP(hipEventRecord(e[1], st));
+    GSMPM_HIP(hipEventSynchronize(e[1]));
+    float ms = 0.f;
+    GSMPM_HIP(hipEventElapsedTime(&ms, e[0], e[1]));
+    ms4[k] = ms / reps;
+    return GSMPM_OK;
+  };
+  int rc = timed(0, [&]() {
+    switch (h->mat_kernel) {
+      case 0: launch_p2g<0>(h, c, bc_active, dt, st, nullptr); break;
+      case 1: launch_p2g<1>(h, c, bc_active, dt, st, nullptr); break;
+      case 2: launch_p2g<2>(h, c, bc_active, dt, st, nullptr); break;
+      case 3: launch_p2g<3>(h, c, bc_active, dt, st, nullptr); break;
+      default: launch_p2g<4>(h, c, bc_active, dt, st, nullptr); break;
+    }
+  });
+  if (!rc) rc = timed(1, grid);
+  if (!rc) rc = timed(2, g2p);
+  if (!rc) {
+    grid();  // fresh bins of parity nx from one G2P, then time the binning on them
+    g2p();
+    rc = timed(3, [&]() { finish_binning(h, nx, st); });
+  }
+  (void)hipEventDestroy(e[0]);
+  (void)hipEventDestroy(e[1]);
+  if (rc) return rc;
+  // restore the state: the repeated G2P launches advanced the particles
+  GSMPM_HIP(hipMemcpyAsync(h->planes, h->planes_tmp, pbytes, hipMemcpyDeviceToDevice, st));
+  return rebin(h, st);
 }
 
 int gsmpm_mpm_debug_stats(gsmpm_mpm* h, int32_t* out8, void* stream) {

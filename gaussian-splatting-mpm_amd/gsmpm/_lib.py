@@ -66,6 +66,11 @@ _SIGS = {
                                                     ctypes.c_double]),
     "gsmpm_mpm_step": (ctypes.c_int, [c_void_p, ctypes.c_float, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint32),
                                       c_void_p]),
+    "gsmpm_mpm_set_halo": (ctypes.c_int, [c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32,
+                                          c_void_p, c_void_p, ctypes.c_int32, ctypes.c_int32]),
+    "gsmpm_mpm_substep_begin": (ctypes.c_int, [c_void_p, ctypes.c_float, ctypes.c_uint32, c_void_p]),
+    "gsmpm_mpm_substep_end": (ctypes.c_int, [c_void_p, ctypes.c_float, ctypes.c_uint32, c_void_p]),
+    "gsmpm_mpm_halo_status": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int32), c_void_p]),
     "gsmpm_mpm_resort": (ctypes.c_int, [c_void_p, ctypes.c_int32, c_void_p]),
     "gsmpm_mpm_postprocess": (ctypes.c_int, [c_void_p, c_void_p]),
     "gsmpm_mpm_field_width": (ctypes.c_int, [ctypes.c_int32]),
@@ -77,6 +82,8 @@ _SIGS = {
     "gsmpm_mpm_profile_substeps": (ctypes.c_int, [c_void_p, ctypes.c_float, ctypes.c_int32,
                                                    ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_float),
                                                    c_void_p]),
+    "gsmpm_mpm_time_kernels": (ctypes.c_int, [c_void_p, ctypes.c_float, ctypes.c_uint32, ctypes.c_int32,
+                                              ctypes.POINTER(ctypes.c_float), c_void_p]),
     "gsmpm_mpm_debug_stats": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int32), c_void_p]),
     "gsmpm_debug_stamps": (ctypes.c_int, [c_void_p, c_void_p]),
     "gsmpm_mpm_live_box": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int32), c_void_p]),

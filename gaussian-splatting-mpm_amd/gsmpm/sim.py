@@ -91,6 +91,37 @@ class Simulator:
         arr = (ctypes.c_uint32 * n)(*[int(m) & 0xFFFFFFFF for m in masks])
         check(LIB.gsmpm_mpm_step(self._h, ctypes.c_float(dt), n, arr, stream_of(self.device)), "gsmpm_mpm_step")
 
+    # ---------------------------------------------------------- slab mode --
+    def set_halo(self, x0s, nx: int, part=None, total=None, allow=(0, 1 << 30)):
+        """Halo windows of a multi-GPU slab (gsmpm/dist.py): planes
+        [x0, x0 + nx) for x0 in x0s.  Returns (part, total) device buffers
+        [len(x0s), nx, n, n, 4]: the library writes this rank's partial sums to
+        `part` and reads the reduced sums from `total`."""
+        nw, ng = len(x0s), self.n_grid
+        shape = (nw, nx, ng, ng, 4)
+        if nw and part is None:
+            part = torch.zeros(shape, dtype=torch.float32, device=self.device)
+        if nw and total is None:
+            total = torch.zeros(shape, dtype=torch.float32, device=self.device)
+        arr = (ctypes.c_int32 * max(1, nw))(*[int(v) for v in x0s])
+        check(LIB.gsmpm_mpm_set_halo(self._h, nw, arr, int(nx), ptr(part) if nw else None,
+                                     ptr(total) if nw else None, int(allow[0]), int(allow[1])), "gsmpm_mpm_set_halo")
+        self._halo = (part, total)  # keep the buffers alive
+        return part, total
+
+    def substep_begin(self, dt: float, mask: int):
+        check(LIB.gsmpm_mpm_substep_begin(self._h, ctypes.c_float(dt), int(mask) & 0xFFFFFFFF,
+                                          stream_of(self.device)), "gsmpm_mpm_substep_begin")
+
+    def substep_end(self, dt: float, mask: int):
+        check(LIB.gsmpm_mpm_substep_end(self._h, ctypes.c_float(dt), int(mask) & 0xFFFFFFFF,
+                                        stream_of(self.device)), "gsmpm_mpm_substep_end")
+
+    def halo_escaped(self) -> bool:
+        v = ctypes.c_int32(0)
+        check(LIB.gsmpm_mpm_halo_status(self._h, ctypes.byref(v), stream_of(self.device)), "gsmpm_mpm_halo_status")
+        return bool(v.value)
+
     def profile(self, dt: float, masks):
         """Eager substeps with a hipEvent pair per kernel -> summed ms of
         (k_p2g, k_grid, k_g2p, binning)."""
@@ -99,6 +130,14 @@ class Simulator:
         out = (ctypes.c_float * 4)()
         check(LIB.gsmpm_mpm_profile_substeps(self._h, ctypes.c_float(dt), n, arr, out, stream_of(self.device)),
               "gsmpm_mpm_profile_substeps")
+        return tuple(float(v) for v in out)
+
+    def time_kernels(self, dt: float, mask: int, reps: int = 20):
+        """Per-launch ms of (k_p2g, k_grid, k_g2p, binning): hipEvents around
+        `reps` back-to-back launches of each on this stream; state restored."""
+        out = (ctypes.c_float * 4)()
+        check(LIB.gsmpm_mpm_time_kernels(self._h, ctypes.c_float(dt), int(mask) & 0xFFFFFFFF, int(reps), out,
+                                         stream_of(self.device)), "gsmpm_mpm_time_kernels")
         return tuple(float(v) for v in out)
 
     def debug_stats(self):

@@ -85,6 +85,22 @@ int gsmpm_mpm_add_plane_collider(gsmpm_mpm* h, const double point[3], const doub
  * all active.  Asynchronous on `stream`. */
 int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t n_substeps, const uint32_t* bc_active, void* stream);
 
+/* Multi-GPU slab (driver gsmpm/dist.py, no reference counterpart:
+ * the reference is single-GPU).  Up to two halo windows of nx planes starting
+ * at planes x0[w] (tile-aligned): after P2G, gsmpm_mpm_substep_begin writes
+ * this rank's partial (m, m v) of every window node to part[n][nx][n_grid^2][4];
+ * the caller sums the partials of the ranks sharing the window into
+ * sum[n][nx][n_grid^2][4] (RCCL/gloo send-recv), then gsmpm_mpm_substep_end
+ * runs the grid update with those sums, G2P and the binning.  Particles must
+ * stay within planes [allow_lo, allow_hi) (own slab + windows): a touched tile
+ * outside sets the flag read by gsmpm_mpm_halo_status.  n_windows = 0 turns
+ * the slab mode off.  part / sum are caller-owned device buffers. */
+int gsmpm_mpm_set_halo(gsmpm_mpm* h, int32_t n_windows, const int32_t* x0, int32_t nx, float* part, const float* sum,
+                       int32_t allow_lo, int32_t allow_hi);
+int gsmpm_mpm_substep_begin(gsmpm_mpm* h, float dt, uint32_t bc_active, void* stream);
+int gsmpm_mpm_substep_end(gsmpm_mpm* h, float dt, uint32_t bc_active, void* stream);
+int gsmpm_mpm_halo_status(gsmpm_mpm* h, int32_t* escaped, void* stream);
+
 /* Re-sort particle storage into Morton order of the current cells now (only
  * summation order changes; rows stay in caller order).  interval >= 0 also sets
  * how many substeps gsmpm_mpm_step lets pass between automatic re-sorts
@@ -129,13 +145,19 @@ int gsmpm_mpm_get_grid(gsmpm_mpm* h, int32_t which, float* out, void* stream);
 int gsmpm_mpm_world_outputs(gsmpm_mpm* h, float scale, const float center[3], int32_t render_space,
                             float* means_out, float* cov_out, void* stream);
 
-/* Measurement: run n substeps eagerly on `stream` with a hipEvent pair around
- * every kernel (the stream is held by a bounded spin while the host enqueues,
- * so the kernels run back to back); kernel_ms[0..3] = summed time of k_p2g,
- * k_grid, k_g2p and the binning (k_finish_bins or k_scan_tiles + k_scatter).
+/* Measurement: run n substeps eagerly on `stream`, each kernel launched with
+ * hipExtLaunchKernel start/stop events (stamped by its own dispatch, the
+ * interval rocprofv3 reports); kernel_ms[0..3] = summed time of k_p2g,
+ * k_grid, k_g2p and the binning (k_finish_bins, or k_scan_tiles..k_scatter).
  * Synchronises `stream`. */
 int gsmpm_mpm_profile_substeps(gsmpm_mpm* h, float dt, int32_t n_substeps, const uint32_t* bc_active,
                                float* kernel_ms, void* stream);
+/* Measurement: average duration (ms) of one launch of k_p2g, k_grid, k_g2p
+ * and the binning, each launched `reps` times back to back between two
+ * hipEvents on `stream` (so event overhead is amortised); the launches use the
+ * current substep's inputs (BC mask `bc_active`).  Particle state and bins are
+ * restored afterwards.  Synchronises `stream`. */
+int gsmpm_mpm_time_kernels(gsmpm_mpm* h, float dt, uint32_t bc_active, int32_t reps, float* ms4, void* stream);
 /* Diagnostics of the tile buckets the next substep reads: {active tiles, max
  * particles in a tile, particles outside the grid, chunks, touched tiles (owned
  * by the next grid update), binned total, parity, substeps since the last

@@ -193,6 +193,58 @@ class OracleMPM:
         self._L.om_substep(ctypes.byref(self._st), ctypes.c_float(dt), ctypes.c_int(len(self.impulses)), imps, _p(ia),
                          ctypes.c_int(len(self.ops)), ops, _p(oa))
 
+    # ---- split substep (multi-GPU slab tests: the halo exchange sits between the halves) ----
+    def _tables(self, imp_active, op_active):
+        ops = (_GridOp * max(1, len(self.ops)))()
+        for i, (k, a, b, fr) in enumerate(self.ops):
+            ops[i].kind = k; ops[i].a[:] = list(a); ops[i].b[:] = list(b); ops[i].friction = fr
+        imps = (_Impulse * max(1, len(self.impulses)))()
+        for i, (c, s, fo, sdt) in enumerate(self.impulses):
+            imps[i].center[:] = list(c); imps[i].size[:] = list(s); imps[i].force[:] = list(fo); imps[i].substep_dt = sdt
+        ia = np.zeros(max(1, len(self.impulses)), np.int32)
+        oa = np.zeros(max(1, len(self.ops)), np.int32)
+        if imp_active is not None:
+            ia[:len(imp_active)] = imp_active
+        if op_active is not None:
+            oa[:len(op_active)] = op_active
+        return imps, ia, ops, oa
+
+    def substep_begin(self, dt, imp_active=None):
+        """solver.py:27-40: grid reset, impulses, stress, P2G (om_substep's first half)."""
+        imps, ia, _, _ = self._tables(imp_active, None)
+        self.gm[:] = 0; self.gv_in[:] = 0; self.gv_out[:] = 0
+        L, st = self._L, ctypes.byref(self._st)
+        L.om_impulses(st, ctypes.c_int(len(self.impulses)), imps, _p(ia))
+        L.om_stress(st, ctypes.c_float(dt))
+        L.om_p2g(st, ctypes.c_float(dt))
+
+    def window_sums(self, x0, nx):
+        """(m v, m) of planes [x0, x0 + nx) as [nx, n, n, 4] (planes outside the grid: 0)."""
+        ng = self.ng
+        out = np.zeros((nx, ng, ng, 4), np.float32)
+        lo, hi = max(0, x0), min(ng, x0 + nx)
+        if lo < hi:
+            gv = self.gv_in.reshape(ng, ng, ng, 3)
+            gm = self.gm.reshape(ng, ng, ng)
+            out[lo - x0:hi - x0, :, :, :3] = gv[lo:hi]
+            out[lo - x0:hi - x0, :, :, 3] = gm[lo:hi]
+        return out
+
+    def set_window_sums(self, x0, arr):
+        ng, nx = self.ng, arr.shape[0]
+        lo, hi = max(0, x0), min(ng, x0 + nx)
+        if lo < hi:
+            self.gv_in.reshape(ng, ng, ng, 3)[lo:hi] = arr[lo - x0:hi - x0, :, :, :3]
+            self.gm.reshape(ng, ng, ng)[lo:hi] = arr[lo - x0:hi - x0, :, :, 3]
+
+    def substep_end(self, dt, op_active=None):
+        """solver.py:41-52: grid normalisation, grid postprocess list, G2P."""
+        _, _, ops, oa = self._tables(None, op_active)
+        L, st = self._L, ctypes.byref(self._st)
+        L.om_grid_normalize(st, ctypes.c_float(dt))
+        L.om_grid_ops(st, ctypes.c_int(len(self.ops)), ops, _p(oa))
+        L.om_g2p(st, ctypes.c_float(dt))
+
     def postprocess(self):
         self._L.om_postprocess(ctypes.byref(self._st))
 
