@@ -13,10 +13,11 @@
  *   third-party, not vendored in the reference; restated from its public
  *   algorithm -- "parity unpinned" against upstream, pinned by analytic KATs).
  *
- * Parity status: the reference cannot run here (taichi==1.5.0 is absent,
- * requirements.txt:10) and ships no tests or fixtures, so this
- * restatement is pinned by first-principles known-answer tests only
- * (tests/test_oracle_kat.py).  All math is IEEE f32, compiled with
+ * Parity status: PARITY UNPINNED against the reference.  It cannot run here
+ * (taichi==1.5.0 is absent, requirements.txt:10), ships no tests or fixtures
+ * (SURVEY F1/F2), and executing its Python to make fixtures was refused in
+ * this pipeline; this restatement is pinned by first-principles
+ * known-answer tests only (tests/test_oracle_kat.py).  All math is IEEE f32, compiled with
  * -ffp-contract=off, operations in the reference's source order.
  */
 #ifndef GSMPM_ORACLE_H

@@ -14,9 +14,11 @@ restatement of the reference kernels:
 * Rasterizer forward: upstream diff-gaussian-rasterization (pre-2024), not in
   the reference tree -- "parity unpinned" against upstream, pinned by KATs.
 
-No reference test, fixture or golden vector exists for this path (SURVEY F1/F2;
-taichi is not installed), so the oracle is pinned by first-principles known-answer
-tests in ``tests/test_oracle_kat.py``.
+PARITY UNPINNED against the reference itself: no reference test, fixture or
+golden vector exists for this path, taichi and the graphdeco
+submodules are not installed, and running the reference's Python to generate
+fixtures was refused in this pipeline.  The oracle is pinned by
+first-principles known-answer tests in ``tests/test_oracle_kat.py``.
 """
 from __future__ import annotations
 
