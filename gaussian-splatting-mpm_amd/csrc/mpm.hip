@@ -357,7 +357,13 @@ __global__ __launch_bounds__(256) void k_p2g(Particles ps, GridDims g, Tiles tl,
     for (int o = 32; o > 0; o >>= 1) bound = fmaxf(bound, __shfl_xor(bound, o));
     if ((k & 63) == 0) s_max[k >> 6] = bound;
     __syncthreads();  // also orders the window zeroing before the adds
-    if (w == (int)blockIdx.x) stamp(0, 2);
+    if (w == (int)blockIdx.x) {
+      stamp(0, 2);
+      if (threadIdx.x == 0 && blockIdx.x < 4096) {
+        g_stamps[0][blockIdx.x][5] = cnt;
+        g_stamps[0][blockIdx.x][6] = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));  // HW_ID
+      }
+    }
     const float bmax = fmaxf(fmaxf(s_max[0], s_max[1]), fmaxf(s_max[2], s_max[3]));
     int ebits;
     frexpf(bmax, &ebits);                     // bmax < 2^ebits

@@ -61,3 +61,19 @@ if len(f):
     t0 = f[:, 0].min()
     sg = lambda a, b: np.median((f[:, b] - f[:, a]) / 100.0)
     print(f'finish_bins: {len(f)} WGs; start spread {(f[:,0].max()-t0)/100:.1f} us, end {(f[:,1].max()-t0)/100:.1f} us; median staged {sg(0,2)} counted+scanned {sg(2,3)} written {sg(3,4)} scattered {sg(4,1)}')
+# P2G: duration vs co-residency on the same CU (HW_ID: CU_ID bits 8-11, SH bit 12, SE bits 13-15 on gfx9)
+p = buf[0].astype(np.int64); p = p[p[:, 0] > 0]
+if len(p):
+    hw = p[:, 6]
+    cu = (hw >> 8) & 0xF; sh = (hw >> 12) & 1; se = (hw >> 13) & 0x7
+    key = se * 32 + sh * 16 + cu
+    xcc = None
+    dur = (p[:, 1] - p[:, 0]) / 100.0
+    from collections import Counter
+    occ = Counter(key.tolist())
+    per = np.array([occ[k] for k in key.tolist()])
+    for n in sorted(set(per.tolist())):
+        sel = per == n
+        print(f"p2g WGs on CUs hosting {n} WGs: {sel.sum()} WGs, median dur {np.median(dur[sel]):.1f} us, max {dur[sel].max():.1f}, mean cnt {p[sel,5].mean():.0f}")
+    big = p[:, 5] >= 200
+    print(f"p2g dur by chunk size: >=200: median {np.median(dur[big]):.1f}; <200: median {np.median(dur[~big]):.1f}; distinct CU keys {len(occ)}")
