@@ -71,7 +71,10 @@ def build_scene(args, dev, rank=0):
     cli = ["--n_grid", str(args.n_grid)] + (["--material", args.material] if args.material else [])
     a = parser.parse_args(cli)
     margs, sargs, rargs = mp.extract(a), sp.extract(a), rp.extract(a)
-    g = GaussianModel(3, device=dev).init_synthetic(args.particles, seed=rank)
+    # lego-like box for lego*; config D (bicycle) fills its sim_area [0,1]^3 as U([0.05, 0.95]^3)
+    box = ((0.05,) * 3, (0.95,) * 3) if args.config.startswith("bicycle") else \
+        ((-0.65, -0.65, -0.55), (0.65, 0.65, 0.55))
+    g = GaussianModel(3, device=dev).init_synthetic(args.particles, seed=rank, box=box)
     bound = torch.tensor(sargs.sim_area, device=dev)
     xyz = g.get_xyz
     mask = torch.logical_and((xyz <= bound[1]).all(1), (xyz >= bound[0]).all(1))
@@ -121,15 +124,17 @@ def algorithmic_bytes(n, n_grid, material):
     return {"k_p2g": 112 * n + 16 * nodes + plastic, "k_grid": 28 * nodes, "k_g2p": 96 * n + 12 * nodes}
 
 
-def measured_traffic(kernel):
+def measured_traffic(kernel, workload):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (profiles/traffic.json, written by tools/traffic.py from separate
     FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950 note in
-    MI355X_MICROARCH.md), or None."""
+    MI355X_MICROARCH.md) when it was measured on this same workload, else None."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
     try:
         with open(path) as f:
             t = json.load(f)
+        if t.get("workload") != workload:
+            return None
         return t["kernels"][kernel]["bytes_per_launch"]
     except (OSError, KeyError, ValueError):
         return None
@@ -317,7 +322,8 @@ def main():
         ach = abytes[dom] / (kern[dom] * 1e-3) / 1e9
         out["kernels_ms_per_launch"] = {k: round(v, 5) for k, v in kern.items()}
         out["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                           "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": measured_traffic(dom),
+                           "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": measured_traffic(dom, {"config": args.config, "particles": args.particles,
+                                                                   "n_grid": sa.n_grid, "material": sa.material}),
                            "algorithmic_bytes_per_launch": abytes[dom],
                            "basis": "SURVEY.md 8(d) B_sub = 208 N + 56 n^3 split per kernel (dense grid)",
                            "live_nodes": live}

@@ -920,60 +920,97 @@ __global__ __launch_bounds__(256) void k_finish_bins(Tiles tl, const int* __rest
   stamp(2, 1);
 }
 
-// General path (any number of tiles): one 1024-lane workgroup in passes of
-// 1024 tiles (lane-interleaved, so the stores coalesce), then k_scatter.
-__global__ __launch_bounds__(1024) void k_scan_tiles(Tiles tl, const int* __restrict__ count, ChunkOut co) {
+// General path (any number of tiles), three launches: per-1024-tile block
+// sums, then one workgroup per block adds the sums of the blocks before it and
+// scans its own tiles (stores lane-contiguous), then k_scatter.
+__device__ __forceinline__ void tile_values(const Tiles& tl, const int* __restrict__ count, const int* __restrict__ tflag,
+                                            int t, int (&v)[3]) {
+  const int E = tl.ntiles + 1;
+  v[0] = t < E ? count[min(t, E - 1)] : 0;
+  v[1] = (v[0] + kChunk - 1) / kChunk;
+  v[2] = (t < tl.ntiles && tflag[min(t, tl.ntiles - 1)]) ? 1 : 0;
+}
+
+// sum of three values over a 1024-lane workgroup (all lanes get the totals)
+__device__ __forceinline__ void block_sum3_1024(int (&v)[3]) {
+  __shared__ int s_w[3][16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    int x = v[r];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+    if (lane == 0) s_w[r][wave] = x;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    int x = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) x += s_w[r][w];
+    v[r] = x;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(1024) void k_scan_partials(Tiles tl, const int* __restrict__ count,
+                                                        const int* __restrict__ tflag, int4* __restrict__ part) {
+  int v[3];
+  tile_values(tl, count, tflag, blockIdx.x * 1024 + threadIdx.x, v);
+  block_sum3_1024(v);
+  if (threadIdx.x == 0) part[blockIdx.x] = make_int4(v[0], v[1], v[2], 0);
+}
+
+__global__ __launch_bounds__(1024) void k_scan_tiles(Tiles tl, const int* __restrict__ count, ChunkOut co,
+                                                     const int4* __restrict__ part) {
   __shared__ int s_wsum[3][16];
-  __shared__ int s_carry[3];
   const int E = tl.ntiles + 1;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (threadIdx.x < 3) s_carry[threadIdx.x] = 0;
-  for (int base = 0; base < E; base += 1024) {
-    const int t = base + threadIdx.x;
-    int v[3];
-    v[0] = t < E ? count[t] : 0;
-    v[1] = (v[0] + kChunk - 1) / kChunk;
-    v[2] = (t < tl.ntiles && co.tflag[t]) ? 1 : 0;
-    int inc[3];
+  // offsets of this block = sums of the blocks before it
+  int carry[3] = {0, 0, 0};
+  for (int q = threadIdx.x; q < (int)blockIdx.x; q += 1024) {
+    const int4 pq = part[q];
+    carry[0] += pq.x;
+    carry[1] += pq.y;
+    carry[2] += pq.z;
+  }
+  block_sum3_1024(carry);
+  const int t = blockIdx.x * 1024 + threadIdx.x;
+  int v[3];
+  tile_values(tl, count, co.tflag, t, v);
+  int inc[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    inc[r] = wave_incl_scan(v[r]);
+    if (lane == 63) s_wsum[r][wave] = inc[r];
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
-      inc[r] = wave_incl_scan(v[r]);
-      if (lane == 63) s_wsum[r][wave] = inc[r];
+      const int x = lane < 16 ? s_wsum[r][lane] : 0;
+      const int xi = wave_incl_scan(x);
+      if (lane < 16) s_wsum[r][lane] = xi - x;
     }
-    __syncthreads();
-    if (threadIdx.x < 64) {
-#pragma unroll
-      for (int r = 0; r < 3; ++r) {
-        const int x = lane < 16 ? s_wsum[r][lane] : 0;
-        const int xi = wave_incl_scan(x);
-        if (lane < 16) s_wsum[r][lane] = xi - x;
-      }
-    }
-    __syncthreads();
-    int o[3];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) o[r] = s_carry[r] + s_wsum[r][wave] + inc[r] - v[r];
-    __syncthreads();  // everyone has read the carry
-    if (threadIdx.x == 1023) {
-#pragma unroll
-      for (int r = 0; r < 3; ++r) s_carry[r] = o[r] + v[r];
-    }
-    if (t < E) {
-      co.cstart[t] = o[0];
-      co.cbase[t] = o[1];
-      for (int k = 0; k < v[1]; ++k)
-        co.chunk[o[1] + k] = make_int4(t, o[0] + k * kChunk, min(kChunk, v[0] - k * kChunk), 0);
-      if (v[2]) {
-        co.touched[o[2]] = t;
-        const int tx = t / (tl.td * tl.td);
-        if (tx < co.tx_lo || tx > co.tx_hi) *co.escape = 1;
-      }
-    }
-    __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    co.nchunk[0] = s_carry[1];
-    co.nchunk[1] = s_carry[2];
+  __syncthreads();
+  int o[3];
+#pragma unroll
+  for (int r = 0; r < 3; ++r) o[r] = carry[r] + s_wsum[r][wave] + inc[r] - v[r];
+  if (t < E) {
+    co.cstart[t] = o[0];
+    co.cbase[t] = o[1];
+    for (int k = 0; k < v[1]; ++k)
+      co.chunk[o[1] + k] = make_int4(t, o[0] + k * kChunk, min(kChunk, v[0] - k * kChunk), 0);
+    if (v[2]) {
+      co.touched[o[2]] = t;
+      const int tx = t / (tl.td * tl.td);
+      if (tx < co.tx_lo || tx > co.tx_hi) *co.escape = 1;
+    }
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 1023) {
+    co.nchunk[0] = o[1] + v[1];
+    co.nchunk[1] = o[2] + v[2];
   }
 }
 
@@ -1248,6 +1285,7 @@ struct gsmpm_mpm {
   Halo halo{};                          // slab halo windows (gsmpm_mpm_set_halo)
   int tx_lo = 0, tx_hi = 1 << 30;       // tile planes this rank may touch
   int* escape = nullptr;                // [1] device flag, see ChunkOut
+  int4* scan_part = nullptr;            // [ceil((ntiles + 1) / 1024)] block sums (large-grid binning)
   int* ptile = nullptr;                 // [np]
   int* pslot = nullptr;                 // [np]
   int cur_box = 0;       // parity of the boxes / buckets the next substep reads
@@ -1314,7 +1352,11 @@ static int finish_binning(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t*
            h->n, (const int*)h->ptile, (const int*)h->pslot, h->list[c]);
   } else {
     const hipEvent_t e0[2] = {ev ? ev[0] : nullptr, nullptr}, e1[2] = {nullptr, ev ? ev[1] : nullptr};
-    launch(ev ? e0 : nullptr, k_scan_tiles, dim3(1), dim3(1024), st, h->tl, (const int*)h->count[c], chunk_out(h, c));
+    const int nblk = div_up(h->tl.ntiles + 1, 1024);
+    launch(ev ? e0 : nullptr, k_scan_partials, dim3(nblk), dim3(1024), st, h->tl, (const int*)h->count[c],
+           (const int*)h->tflag[c], h->scan_part);
+    launch(nullptr, k_scan_tiles, dim3(nblk), dim3(1024), st, h->tl, (const int*)h->count[c], chunk_out(h, c),
+           (const int4*)h->scan_part);
     launch(ev ? e1 : nullptr, k_scatter, dim3(div_up(h->n, 256)), dim3(256), st, h->n, (const int*)h->ptile,
            (const int*)h->pslot, (const int*)h->cstart[c], h->list[c]);
   }
@@ -1550,6 +1592,8 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
     if ((e = hipMemset(h->nchunk[c], 0, sizeof(int) * 2)) != hipSuccess) return fail(e, "hipMemset");
   }
   if ((e = hipMalloc(&h->escape, sizeof(int))) != hipSuccess) return fail(e, "hipMalloc escape");
+  if ((e = hipMalloc(&h->scan_part, sizeof(int4) * (size_t)div_up(h->tl.ntiles + 1, 1024))) != hipSuccess)
+    return fail(e, "hipMalloc scan partials");
   if ((e = hipMemset(h->escape, 0, sizeof(int))) != hipSuccess) return fail(e, "hipMemset");
   if ((e = hipMalloc(&h->ptile, sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc ptile");
   if ((e = hipMalloc(&h->pslot, sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc pslot");
@@ -1588,6 +1632,7 @@ int gsmpm_mpm_destroy(gsmpm_mpm* h) {
   }
   (void)hipFree(h->ptile);
   (void)hipFree(h->escape);
+  (void)hipFree(h->scan_part);
   (void)hipFree(h->pslot);
   (void)hipFree(h->planes_tmp);
   (void)hipFree(h->orig_tmp);

@@ -138,3 +138,17 @@ def test_resort_keeps_caller_order(dev):
     ref.postprocess()
     cov = s.mpm_state.particle_cov.to_torch().cpu().numpy().reshape(-1, 6)
     assert rel_err(cov, ref.cov) < TOL
+
+
+def test_large_grid_binning_path(dev):
+    """> 8192 tiles (176^3 -> 10,648 tiles) takes the multi-workgroup scan +
+    scatter binning instead of the fused one; same parity bar."""
+    from gpu_helpers import dropin_sim
+    prob = lego_problem(3000, 176)
+    ref, imps, ops = build_oracle_sim(prob)
+    dt = prob["cfg"]["substep_dt"]
+    s, _ = dropin_sim(prob, dev)
+    oracle_run(ref, imps, ops, dt, 12)
+    for _ in range(12):
+        s.p2g2p(dt)
+    _compare(s, ref)

@@ -37,7 +37,11 @@ def main():
         res[k] = {"fetch_bytes": fb, "write_bytes": wb, "bytes_per_launch": fb + wb,
                   "fetch_size_kib_raw": f.get(k), "write_size_kib_raw": w.get(k)}
     doc = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes (tools/pmc.sh)",
-           "correction": "FETCH_SIZE x2 (gfx950), KiB -> bytes", "kernels": res}
+           "correction": "FETCH_SIZE x2 (gfx950), KiB -> bytes",
+           # tools/pmc_probe.py's workload (bench.py only uses these numbers for the same one)
+           "workload": {"config": os.environ.get("CONFIG", "lego.json"), "particles": int(os.environ.get("N", 100000)),
+                        "n_grid": int(os.environ.get("NG", 128)), "material": os.environ.get("MAT") or "jelly"},
+           "kernels": res}
     with open(out, "w") as fh:
         json.dump(doc, fh, indent=1)
     print(json.dumps(doc, indent=1))
