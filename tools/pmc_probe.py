@@ -5,7 +5,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'
 import torch
 import bench
 from gsmpm.bc import substep_masks
-class A: particles = 100000; n_grid = 128; config = 'lego.json'; material = os.environ.get('MAT')
+class A: particles = int(os.environ.get('N', 100000)); n_grid = int(os.environ.get('NG', 128)); config = os.environ.get('CONFIG', 'lego.json'); material = os.environ.get('MAT')
 dev = torch.device('cuda:0')
 scene = bench.build_scene(A, dev)
 sim, specs = bench.make_sim(scene, dev)
