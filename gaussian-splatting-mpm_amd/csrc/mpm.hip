@@ -586,12 +586,16 @@ __global__ __launch_bounds__(256) void k_grid(GridDims g, Tiles tl, ChunkIn ck, 
 // ------------------------------------------------------------------- G2P --
 // g2p (utils.py:218-282) without the dead update_cov; the gather
 // reads through `fetch(base, i, j, k)` (LDS window or global v_out).
-template <typename Fetch>
-__device__ __forceinline__ void g2p_particle(const Particles& ps, int p, const GridDims& g, float dt, Fetch fetch,
-                                             float (&xn)[3]) {
-  float x[3];
+// x of a particle (loaded early by the callers, so its latency overlaps the
+// grid window staging)
+__device__ __forceinline__ void load_x(const Particles& ps, int p, float (&x)[3]) {
 #pragma unroll
   for (int d = 0; d < 3; ++d) x[d] = ps.ld(PX + d, p);
+}
+
+template <typename Fetch>
+__device__ __forceinline__ void g2p_particle(const Particles& ps, int p, const float (&x)[3], const GridDims& g,
+                                             float dt, Fetch fetch, float (&xn)[3]) {
   int base[3];
   float fx[3], w[3][3], dw[3][3];
   bspline(x, g.inv_dx, base, fx, w, dw);
@@ -699,8 +703,9 @@ __global__ __launch_bounds__(256) void k_g2p(Particles ps, GridDims g, Tiles tl,
     if (t == tl.ntiles) {
       if (k < cnt) {
         const int p = ck.list[first + k];
-        float xn[3];
-        g2p_particle(ps, p, g, dt,
+        float x0[3], xn[3];
+        load_x(ps, p, x0);
+        g2p_particle(ps, p, x0, g, dt,
                      [&](const int (&base)[3], int i, int j, int kk) {
                        const int ix = base[0] + i, iy = base[1] + j, iz = base[2] + kk;
                        float4 gv = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -718,6 +723,14 @@ __global__ __launch_bounds__(256) void k_g2p(Particles ps, GridDims g, Tiles tl,
     }
     const int tx = t / (tl.td * tl.td), ty = (t / tl.td) % tl.td, tz = t % tl.td;
     const int lo0 = tx * kTile, lo1 = ty * kTile, lo2 = tz * kTile;
+    // the particle's list entry and x are requested first so their round
+    // trips overlap the window staging below
+    int p = -1;
+    float x0[3] = {0.f, 0.f, 0.f};
+    if (k < cnt) {
+      p = ck.list[first + k];
+      load_x(ps, p, x0);
+    }
     {
       // all four loads in flight before the first LDS store (a guarded load
       // per iteration compiles to one round trip each)
@@ -745,11 +758,10 @@ __global__ __launch_bounds__(256) void k_g2p(Particles ps, GridDims g, Tiles tl,
         g_stamps[1][blockIdx.x][7] = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));  // HW_ID
       }
     }
-    int p = -1, code = -1, lslot = 0, nt = -1;
+    int code = -1, lslot = 0, nt = -1;
     if (k < cnt) {
-      p = ck.list[first + k];
       float xn[3];
-      g2p_particle(ps, p, g, dt,
+      g2p_particle(ps, p, x0, g, dt,
                    [&](const int (&base)[3], int i, int j, int kk) {
                      const float4* wb = s_win + ((base[0] - lo0) * kTW + (base[1] - lo1)) * kTW + (base[2] - lo2);
                      return wb[(i * kTW + j) * kTW + kk];
@@ -856,23 +868,26 @@ __global__ __launch_bounds__(256) void k_finish_bins(Tiles tl, const int* __rest
                                                      const int* __restrict__ ptile, const int* __restrict__ pslot,
                                                      int* __restrict__ list) {
   __shared__ int s_off[kFuseTiles];  // count | touched << 31, then list offsets
+  __shared__ int s_aux[kFuseTiles];  // first chunk (low 16 bits) | touched-list rank (high 16 bits)
   const int E = tl.ntiles + 1;
   stamp(2, 0);
-  // batches of 8 independent loads per lane: the counts were just written by
-  // other XCDs, so each load is a far-memory round trip
-  for (int q0 = 0; q0 < E; q0 += 256 * 8) {
-    int cv[8], fv[8];
+  // this lane's particle bin, requested first (independent of the scan)
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  const int pt = ptile[min(p, n - 1)], psl = pslot[min(p, n - 1)];
+  // tile counts / flags: 16 + 16 unguarded loads in flight per lane per batch
+  // (written by other XCDs just before, so each batch is one far round trip)
+  for (int q0 = 0; q0 < E; q0 += 256 * 16) {
+    int cv[16], fv[16];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 16; ++u) {
       const int q = q0 + u * 256 + threadIdx.x;
-      cv[u] = count[min(q, E - 1)];  // unguarded: keeps the 16 loads in flight
+      cv[u] = count[min(q, E - 1)];
       fv[u] = co.tflag[min(q, tl.ntiles - 1)];
-      fv[u] = q < tl.ntiles ? fv[u] : 0;
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < 16; ++u) {
       const int q = q0 + u * 256 + threadIdx.x;
-      if (q < E) s_off[q] = cv[u] | (fv[u] ? INT_MIN : 0);
+      if (q < E) s_off[q] = cv[u] | ((q < tl.ntiles && fv[u]) ? INT_MIN : 0);
     }
   }
   __syncthreads();
@@ -889,24 +904,13 @@ __global__ __launch_bounds__(256) void k_finish_bins(Tiles tl, const int* __rest
   int o[3], tot[3];
   block_scan3(v, o, tot);
   stamp(2, 3);
-  const int R = (E + gridDim.x - 1) / gridDim.x;
-  const int w0 = blockIdx.x * R, w1 = min(E, w0 + R);
+  // exclusive offsets per tile back into LDS (each lane its own contiguous tiles)
   for (int t = t0; t < t1; ++t) {
     const int e = s_off[t], c = e & INT_MAX;
-    const int nc = (c + kChunk - 1) / kChunk;
-    if (t >= w0 && t < w1) {
-      co.cbase[t] = o[1];
-      for (int k = 0; k < nc; ++k)
-        co.chunk[o[1] + k] = make_int4(t, o[0] + k * kChunk, min(kChunk, c - k * kChunk), 0);
-      if (e < 0) {
-        co.touched[o[2]] = t;
-        const int tx = t / (tl.td * tl.td);
-        if (tx < co.tx_lo || tx > co.tx_hi) *co.escape = 1;
-      }
-    }
     s_off[t] = o[0];
+    s_aux[t] = o[1] | (o[2] << 16);
     o[0] += c;
-    o[1] += nc;
+    o[1] += (c + kChunk - 1) / kChunk;
     o[2] += e < 0;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -915,8 +919,23 @@ __global__ __launch_bounds__(256) void k_finish_bins(Tiles tl, const int* __rest
   }
   __syncthreads();
   stamp(2, 4);
-  const int p = blockIdx.x * 256 + threadIdx.x;
-  if (p < n) list[s_off[ptile[p]] + pslot[p]] = p;
+  // this workgroup's slice of tiles: one lane per tile writes its chunk
+  // records, first chunk and touched-list entry
+  const int R = (E + gridDim.x - 1) / gridDim.x;
+  for (int t = blockIdx.x * R + threadIdx.x; t < min(E, (int)(blockIdx.x + 1) * R); t += 256) {
+    const int off = s_off[t], aux = s_aux[t];
+    const int c = (t + 1 < E ? s_off[t + 1] : tot[0]) - off;
+    const int cb = aux & 0xffff, rk = aux >> 16;
+    const bool touched = (t + 1 < E ? (s_aux[t + 1] >> 16) : tot[2]) > rk;
+    co.cbase[t] = cb;
+    for (int k = 0; k * kChunk < c; ++k) co.chunk[cb + k] = make_int4(t, off + k * kChunk, min(kChunk, c - k * kChunk), 0);
+    if (touched) {
+      co.touched[rk] = t;
+      const int tx = t / (tl.td * tl.td);
+      if (tx < co.tx_lo || tx > co.tx_hi) *co.escape = 1;
+    }
+  }
+  if (p < n) list[s_off[pt] + psl] = p;
   stamp(2, 1);
 }
 
@@ -1347,7 +1366,8 @@ static void launch_p2g(gsmpm_mpm* h, int c, uint32_t mask, float dt, hipStream_t
 
 // counts of parity c -> list offsets + chunk list, then the per-tile lists
 static int finish_binning(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t* ev = nullptr) {
-  if (h->tl.ntiles + 1 <= kFuseTiles) {
+  // fused path: tile table fits LDS, first-chunk indices fit 16 bits (s_aux)
+  if (h->tl.ntiles + 1 <= kFuseTiles && h->tl.max_chunks < 65536) {
     launch(ev, k_finish_bins, dim3(div_up(h->n, 256)), dim3(256), st, h->tl, (const int*)h->count[c], chunk_out(h, c),
            h->n, (const int*)h->ptile, (const int*)h->pslot, h->list[c]);
   } else {
