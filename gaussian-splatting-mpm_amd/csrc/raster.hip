@@ -272,9 +272,11 @@ __global__ __launch_bounds__(kBlock) void k_render(const uint2* __restrict__ ran
       const float2 g = s_xy[j];
       const float dx = g.x - pfx, dy = g.y - pfy;
       const float4 co = s_co[j];
-      const float power = -0.5f * (co.x * dx * dx + co.z * dy * dy) - co.y * dx * dy;
+      // the blend loop is the renderer's hot loop: FMAs and the hardware
+      // exp2 (v_exp_f32, ~1 ulp) -- pixel parity is 1e-3, not bitwise
+      const float power = __builtin_fmaf(-0.5f, __builtin_fmaf(co.x * dx, dx, co.z * dy * dy), -co.y * dx * dy);
       if (power > 0.0f) continue;
-      const float alpha = fminf(0.99f, co.w * expf(power));
+      const float alpha = fminf(0.99f, co.w * __builtin_amdgcn_exp2f(power * 1.4426950408889634f));
       if (alpha < 1.0f / 255.0f) continue;
       const float test_T = T * (1 - alpha);
       if (test_T < 0.0001f) {
@@ -282,9 +284,10 @@ __global__ __launch_bounds__(kBlock) void k_render(const uint2* __restrict__ ran
         continue;
       }
       const float4 c = s_rgb[j];
-      C0 += c.x * alpha * T;
-      C1 += c.y * alpha * T;
-      C2 += c.z * alpha * T;
+      const float aT = alpha * T;
+      C0 = __builtin_fmaf(c.x, aT, C0);
+      C1 = __builtin_fmaf(c.y, aT, C1);
+      C2 = __builtin_fmaf(c.z, aT, C2);
       T = test_T;
     }
   }
