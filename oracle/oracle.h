@@ -72,6 +72,35 @@ void om_substep(om_state* s, float dt, int n_imp, const om_impulse* imp, const i
 void om_postprocess(om_state* s);
 int om_threads(void);
 
+
+/* ------------------------------------------- differentiable path (diff_oracle.c) --- */
+typedef struct {
+  int n, ng, L;                          /* particles, grid, state levels (31) */
+  float dx, inv_dx, gravity[3];
+  float *x, *v, *F, *C, *stress;         /* [L][n][3|9] */
+  float *gx, *gv, *gF, *gC, *gstress;    /* adjoints, same shapes */
+  float *vol, *mass;                     /* [n] */
+  float *logE, *y, *mu, *lam;            /* [n] */
+  float *glogE, *gy, *gmu, *glam;        /* [n] */
+  float *init_cov, *cov, *gcov;          /* [6n] */
+  float *gm, *gv_in, *gv_out;            /* dense grid [ng^3] / [ng^3][3] */
+  float *g_gv_in, *g_gv_out;             /* grid adjoints (persist across substeps) */
+  int n_box;                             /* grid_postprocess[0] is a fixed cube */
+  float box_c[3], box_s[3];
+  float* g_gm;  /* [ng^3] or NULL.  Test-only: when set, the mass adjoint the
+                   reference lacks (grid_mass has no needs_grad, model.py:167)
+                   is added so a finite-difference check can see every path. */
+} od_state;
+
+void od_mu_lam(od_state* s);
+void od_substep_forward(od_state* s, float dt, int level);
+void od_substep_backward(od_state* s, float dt, int level);
+void od_cov_forward(od_state* s);
+void od_cov_backward(od_state* s);
+void od_learn(od_state* s);
+void od_cycle_init(od_state* s);
+void od_clear_grads(od_state* s);
+
 /* -------------------------------------------------------- rasterizer --- */
 typedef struct {
   int P, D, M, W, H;

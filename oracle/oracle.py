@@ -278,3 +278,95 @@ def raster_forward(means3D, opacities, viewmatrix, projmatrix, campos, bg, W, H,
     tt = np.zeros(P, np.int32)
     K = lib().or_forward(ctypes.byref(a), _p(color), _p(radii), _p(depth), _p(tt))
     return color, radii, K, depth, tt
+
+
+# ------------------------------------------------------------------ differentiable path --
+class _DState(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("ng", ctypes.c_int), ("L", ctypes.c_int),
+                ("dx", ctypes.c_float), ("inv_dx", ctypes.c_float), ("gravity", ctypes.c_float * 3)] + \
+               [(nm, F32P) for nm in ("x", "v", "F", "C", "stress", "gx", "gv", "gF", "gC", "gstress", "vol", "mass",
+                                      "logE", "y", "mu", "lam", "glogE", "gy", "gmu", "glam", "init_cov", "cov", "gcov",
+                                      "gm", "gv_in", "gv_out", "g_gv_in", "g_gv_out")] + \
+               [("n_box", ctypes.c_int), ("box_c", ctypes.c_float * 3), ("box_s", ctypes.c_float * 3), ("g_gm", F32P)]
+
+
+class OracleDiff:
+    """Mirror of MPM_Simulator with args.fitting=True (MPM_state_opt,
+    p2g2p_forward/backward, postprocess_forward/backward, learn, clear_grads,
+    cycle_init) on the CPU restatement in diff_oracle.c."""
+
+    def __init__(self, x, cov6, vol, *, n_grid, grid_extent=2.0, E=2e6, nu=0.4, density=1000.0,
+                 gravity=(0.0, -9.81, 0.0), init_v=None, levels=31, ground_only=False, exact_mass_grad=False):
+        x = np.ascontiguousarray(x, np.float32).reshape(-1, 3)
+        n, L = x.shape[0], levels
+        self.n, self.ng, self.L = n, n_grid, L
+        f = lambda *shape: np.zeros(shape, np.float32)
+        self.x = f(L, n, 3); self.v = f(L, n, 3); self.F = f(L, n, 9); self.C = f(L, n, 9); self.stress = f(L, n, 9)
+        self.gx = f(L, n, 3); self.gv = f(L, n, 3); self.gF = f(L, n, 9); self.gC = f(L, n, 9)
+        self.gstress = f(L, n, 9)
+        self.x[0] = x
+        if init_v is not None:
+            self.v[0] = np.asarray(init_v, np.float32).reshape(n, 3)
+        self.F[0] = np.tile(np.eye(3, dtype=np.float32).reshape(1, 9), (n, 1))
+        self.vol = np.ascontiguousarray(vol, np.float32).reshape(n).copy()
+        self.mass = (np.float32(density) * self.vol).astype(np.float32)
+        self.logE = np.full(n, math.log10(E), np.float32)
+        self.y = np.full(n, -math.log(0.49 / nu - 1), np.float32)
+        self.mu = f(n); self.lam = f(n); self.glogE = f(n); self.gy = f(n); self.gmu = f(n); self.glam = f(n)
+        self.init_cov = np.ascontiguousarray(cov6, np.float32).reshape(n * 6).copy()
+        self.cov = self.init_cov.copy(); self.gcov = f(n * 6)
+        nn = n_grid ** 3
+        self.gm = f(nn); self.gv_in = f(nn, 3); self.gv_out = f(nn, 3); self.g_gv_in = f(nn, 3); self.g_gv_out = f(nn, 3)
+        st = _DState()
+        st.n, st.ng, st.L = n, n_grid, L
+        st.dx, st.inv_dx = grid_extent / n_grid, n_grid / grid_extent
+        st.gravity[:] = [float(g) for g in gravity]
+        for nm, _ in _DState._fields_:
+            if hasattr(self, nm) and isinstance(getattr(self, nm), np.ndarray):
+                setattr(st, nm, _p(getattr(self, nm)))
+        st.n_box = 0
+        if exact_mass_grad:  # test-only, see oracle.h
+            self.g_gm = f(nn)
+            st.g_gm = _p(self.g_gm)
+        self._st = st
+        self._L = lib()
+        if ground_only:
+            self.set_bc_ground_only()
+        self._L.od_mu_lam(ctypes.byref(st))
+
+    def set_bc_ground_only(self):
+        """StickyGroundBC (boundary_conditions.py:88-95) as grid_postprocess[0]."""
+        self.set_fixed_box([1.0, 0.6, 1.0], [1.0, 0.1, 1.0])
+
+    def set_fixed_box(self, center, size):
+        self._st.n_box = 1
+        self._st.box_c[:] = list(center)
+        self._st.box_s[:] = list(size)
+
+    def mu_lam(self):
+        self._L.od_mu_lam(ctypes.byref(self._st))
+
+    def p2g2p_forward(self, dt, s):
+        self._L.od_substep_forward(ctypes.byref(self._st), ctypes.c_float(dt), ctypes.c_int(s))
+
+    def p2g2p_backward(self, dt, s):
+        self._L.od_substep_backward(ctypes.byref(self._st), ctypes.c_float(dt), ctypes.c_int(s))
+
+    def postprocess_forward(self):
+        self._L.od_cov_forward(ctypes.byref(self._st))
+
+    def postprocess_backward(self):
+        self._L.od_cov_backward(ctypes.byref(self._st))
+
+    def set_grads(self, xyz_grad, cov_grad):
+        self.gx[self.L - 1] = np.asarray(xyz_grad, np.float32).reshape(self.n, 3)
+        self.gcov[:] = np.asarray(cov_grad, np.float32).reshape(-1)
+
+    def learn(self):
+        self._L.od_learn(ctypes.byref(self._st))
+
+    def cycle_init(self):
+        self._L.od_cycle_init(ctypes.byref(self._st))
+
+    def clear_grads(self):
+        self._L.od_clear_grads(ctypes.byref(self._st))
