@@ -52,6 +52,19 @@ class RasterArgs(ctypes.Structure):
     ]
 
 
+class FitParams(ctypes.Structure):
+    _fields_ = [
+        ("n_particles", ctypes.c_int32),
+        ("n_grid", ctypes.c_int32),
+        ("grid_extent", ctypes.c_double),
+        ("levels", ctypes.c_int32),
+        ("E", ctypes.c_double),
+        ("nu", ctypes.c_double),
+        ("density", ctypes.c_double),
+        ("gravity", ctypes.c_double * 3),
+    ]
+
+
 # entry point -> (restype, argtypes); mirrors include/gsmpm.h
 _SIGS = {
     "gsmpm_last_error": (ctypes.c_char_p, []),
@@ -92,6 +105,23 @@ _SIGS = {
                                           ctypes.c_float, c_void_p, c_void_p, c_void_p]),
     "gsmpm_particle_volume": (ctypes.c_int, [c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_double, c_void_p,
                                              c_void_p, c_void_p]),
+    "gsmpm_fit_create": (ctypes.c_int, [ctypes.POINTER(FitParams), ctypes.POINTER(c_void_p)]),
+    "gsmpm_fit_destroy": (ctypes.c_int, [c_void_p]),
+    "gsmpm_fit_set_particles": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gsmpm_fit_set_fixed_cube": (ctypes.c_int, [c_void_p, ctypes.c_double * 3, ctypes.c_double * 3]),
+    "gsmpm_fit_forward": (ctypes.c_int, [c_void_p, ctypes.c_float, ctypes.c_int32, c_void_p]),
+    "gsmpm_fit_backward": (ctypes.c_int, [c_void_p, ctypes.c_float, ctypes.c_int32, c_void_p]),
+    "gsmpm_fit_postprocess_forward": (ctypes.c_int, [c_void_p, c_void_p]),
+    "gsmpm_fit_postprocess_backward": (ctypes.c_int, [c_void_p, c_void_p]),
+    "gsmpm_fit_set_grads": (ctypes.c_int, [c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gsmpm_fit_learn": (ctypes.c_int, [c_void_p, c_void_p]),
+    "gsmpm_fit_cycle_init": (ctypes.c_int, [c_void_p, c_void_p]),
+    "gsmpm_fit_clear_grads": (ctypes.c_int, [c_void_p, c_void_p]),
+    "gsmpm_fit_mu_lam": (ctypes.c_int, [c_void_p, c_void_p]),
+    "gsmpm_fit_field_width": (ctypes.c_int, [ctypes.c_int32]),
+    "gsmpm_fit_get": (ctypes.c_int, [c_void_p, ctypes.c_int32, ctypes.c_int32, c_void_p, c_void_p]),
+    "gsmpm_fit_set": (ctypes.c_int, [c_void_p, ctypes.c_int32, ctypes.c_int32, c_void_p, c_void_p]),
+    "gsmpm_fit_get_grid": (ctypes.c_int, [c_void_p, ctypes.c_int32, c_void_p, c_void_p]),
     "gsmpm_raster_create": (ctypes.c_int, [ctypes.POINTER(c_void_p)]),
     "gsmpm_raster_destroy": (ctypes.c_int, [c_void_p]),
     "gsmpm_raster_forward": (ctypes.c_int, [c_void_p, ctypes.POINTER(RasterArgs), c_void_p, c_void_p,
@@ -102,6 +132,9 @@ _SIGS = {
 # field ids (include/gsmpm.h)
 FIELD = {"x": 0, "v": 1, "C": 2, "F_trial": 3, "cov": 4, "init_cov": 5, "R": 6, "mass": 7, "vol": 8, "mu": 9,
          "lam": 10, "yield_stress": 11}
+FIT_FIELD = {k: i for i, k in enumerate(
+    ("x", "v", "F", "C", "stress", "gx", "gv", "gF", "gC", "gstress", "logE", "y", "mu", "lam", "glogE", "gy", "gmu",
+     "glam", "cov", "gcov", "init_cov", "vol", "mass"))}
 FLAG_JELLY_FCR, FLAG_KEEP_GRID, FLAG_NO_GRAPH, FLAG_NO_SORT = 1, 2, 4, 8
 
 

@@ -16,13 +16,14 @@ from mpm_solver.utils import material_types
 
 
 class FieldView:
-    """Stand-in for a Taichi field: to_torch / from_torch / to_numpy / fill / shape."""
+    """Stand-in for a Taichi field: to_torch / from_torch / to_numpy / fill / shape (+ .grad)."""
 
-    def __init__(self, owner, getter, setter=None, shape=None):
+    def __init__(self, owner, getter, setter=None, shape=None, grad=None):
         self._owner = owner
         self._get = getter
         self._set = setter
         self.shape = shape
+        self.grad = grad
 
     def to_torch(self, device=None):
         self._owner.flush()
@@ -84,6 +85,89 @@ class MPM_model:
         self.lam = FieldView(owner, lambda: sim.get("lam"), lambda t: sim.set("lam", t), shape=(n,))
         self.yield_stress = FieldView(owner, lambda: sim.get("yield_stress"), lambda t: sim.set("yield_stress", t),
                                       shape=(n,))
+
+
+    def _bind_fit(self, owner):
+        """logE / y / mu / lam and their .grad on the fitting path (model.py:35-44)."""
+        self._owner = owner
+        fit = owner._fit
+        n = self.n_particles
+
+        def fv(name):
+            g = FieldView(owner, lambda: fit.get("g" + name), lambda t: fit.set("g" + name, t), (n,))
+            return FieldView(owner, lambda: fit.get(name), lambda t: fit.set(name, t), (n,), grad=g)
+        self.logE, self.y, self.mu, self.lam = fv("logE"), fv("y"), fv("mu"), fv("lam")
+        self.material = FieldView(owner, lambda: torch.full((n,), float(self.material_code), device=fit.device),
+                                  shape=(n,))
+
+    def clear_grad(self):
+        if self._owner is not None and getattr(self._owner, "fitting", False):
+            for k in ("glogE", "gy", "gmu", "glam"):
+                self._owner._fit.set(k, torch.zeros(self.n_particles))
+
+
+class MPM_state_opt:
+    """Differentiable particle + grid state (model.py:135-223): fields with 31
+    levels; ``to_torch()`` returns the reference's (31, N, ...) shapes."""
+
+    def __init__(self, owner, args):
+        fit = owner._fit
+        n, L, ng = owner.n_particles, fit.levels, args.n_grid
+        self.n_particles = n
+        self._fit = fit
+
+        def leveled(name, tail):
+            def get(nm=name):
+                return torch.stack([fit.get(nm, s).view(n, *tail) for s in range(L)])
+
+            def put(t, nm=name):
+                t = t.reshape(L, n, -1)
+                for s in range(L):
+                    fit.set(nm, t[s], s)
+            return get, put
+
+        def view(name, tail):
+            g, p = leveled(name, tail)
+            gg, gp = leveled("g" + name, tail)
+            return FieldView(owner, g, p, (L, n, *tail), grad=FieldView(owner, gg, gp, (L, n, *tail)))
+        self.particle_xyz = view("x", (3,))
+        self.particle_vel = view("v", (3,))
+        self.particle_F = view("F", (3, 3))
+        self.particle_stress = view("stress", (3, 3))
+        self.particle_C = view("C", (3, 3))
+        self.particle_cov = FieldView(owner, lambda: fit.get("cov").view(-1), lambda t: fit.set("cov", t), (6 * n,),
+                                      grad=FieldView(owner, lambda: fit.get("gcov").view(-1),
+                                                     lambda t: fit.set("gcov", t), (6 * n,)))
+        self.particle_init_cov = FieldView(owner, lambda: fit.get("init_cov").view(-1), None, (6 * n,))
+        self.particle_vol = FieldView(owner, lambda: fit.get("vol"), None, (n,))
+        self.particle_mass = FieldView(owner, lambda: fit.get("mass"), None, (n,))
+        density = float(args.density)
+        self.particle_density = FieldView(owner, lambda: torch.full((n,), density, device=fit.device), None, (n,))
+        self.grid_mass = FieldView(owner, lambda: fit.get_grid("mass"), None, (ng, ng, ng))
+        self.grid_v_in = FieldView(owner, lambda: fit.get_grid("v_in"), None, (ng, ng, ng, 3),
+                                   grad=FieldView(owner, lambda: fit.get_grid("v_in_grad"), None, (ng, ng, ng, 3)))
+        self.grid_v_out = FieldView(owner, lambda: fit.get_grid("v_out"), None, (ng, ng, ng, 3),
+                                    grad=FieldView(owner, lambda: fit.get_grid("v_out_grad"), None, (ng, ng, ng, 3)))
+
+    def set_grads(self, xyz_grad, cov_grad):
+        """model.py:192-202: x.grad[30] = xyz_grad, cov.grad = cov_grad."""
+        self._fit.set_grads(xyz_grad, cov_grad)
+
+    def cycle_init(self):
+        """model.py:216-223: level 30 -> level 0 for x, v, F, stress, C."""
+        self._fit.cycle_init()
+
+    def clear_grad(self):
+        """model.py:204-214 (the state half of clear_grads; the reference's own
+        MPM_model.clear_grad is the other half): the library clears both, so the
+        model's adjoints are put back."""
+        keep = {k: self._fit.get(k) for k in ("glogE", "gy", "gmu", "glam")}
+        self._fit.clear_grads()
+        for k, t in keep.items():
+            self._fit.set(k, t)
+
+    def reset_grid_state(self):
+        pass  # done inside every gsmpm_fit_forward / _backward
 
 
 class MPM_state:

@@ -185,6 +185,81 @@ int gsmpm_constitutive(int32_t material, const float* F_trial, int32_t n, const 
 int gsmpm_particle_volume(const float* x, int32_t n, int32_t n_grid, double grid_extent, int32_t* scratch,
                           float* vol_out, void* stream);
 
+/* ------------------------------------------------ differentiable MPM ---
+ * Replaces MPM_Simulator with args.fitting=True (solver.py:54-108,131-133,
+ * 167-177) over MPM_model's logE/y/mu/lam (model.py:35-44) and
+ * MPM_state_opt (model.py:135-223): L state levels of x, v, F, stress, C
+ * (level s+1 = substep s of level s), adjoints of all of them, the dense grid
+ * and its adjoints.  Same numerics and the same accumulation behaviour as
+ * Taichi's reverse mode on those kernels.
+ */
+typedef struct gsmpm_fit gsmpm_fit;
+
+typedef struct {
+  int32_t n_particles;
+  int32_t n_grid;               /* MPMParams.n_grid */
+  double grid_extent;
+  int32_t levels;               /* 31 in the reference (model.py:145-149) */
+  double E, nu, density;        /* logE = log10 E, y = -log(0.49/nu - 1) (model.py:41-43) */
+  double gravity[3];
+} gsmpm_fit_params;
+
+int gsmpm_fit_create(const gsmpm_fit_params* p, gsmpm_fit** out);
+int gsmpm_fit_destroy(gsmpm_fit* h);
+/* MPM_state_opt.__init__ + init2 (model.py:150-187): xyz [N,3], cov6 [N,6],
+ * vol [N], init_v [N,3] (NULL = 0) as level 0; F[0] = I, C[0] = stress[0] = 0;
+ * mass = density * vol; mu/lam from logE/y (model.py:44). */
+int gsmpm_fit_set_particles(gsmpm_fit* h, const float* xyz, const float* cov6, const float* vol,
+                            const float* init_v, void* stream);
+/* grid_postprocess[0] as a fixed cube (set_bc_ground_only, solver.py:131-133,
+ * StickyGroundBC boundary_conditions.py:88-95 = center (1,0.6,1), size (1,0.1,1)). */
+int gsmpm_fit_set_fixed_cube(gsmpm_fit* h, const double center[3], const double size[3]);
+/* p2g2p_forward(dt, s), solver.py:54-69: level s -> level s+1. */
+int gsmpm_fit_forward(gsmpm_fit* h, float dt, int32_t s, void* stream);
+/* p2g2p_backward(dt, s), solver.py:71-90. */
+int gsmpm_fit_backward(gsmpm_fit* h, float dt, int32_t s, void* stream);
+/* postprocess_forward / _backward, solver.py:167-171 (compute_cov_from_F_opt, utils.py:435-467) */
+int gsmpm_fit_postprocess_forward(gsmpm_fit* h, void* stream);
+int gsmpm_fit_postprocess_backward(gsmpm_fit* h, void* stream);
+/* MPM_state_opt.set_grads (model.py:192-202): xyz_grad [N,3] -> x.grad[L-1], cov_grad [6N] -> cov.grad */
+int gsmpm_fit_set_grads(gsmpm_fit* h, const float* xyz_grad, const float* cov_grad, void* stream);
+int gsmpm_fit_learn(gsmpm_fit* h, void* stream);        /* solver.py:92-108 */
+int gsmpm_fit_cycle_init(gsmpm_fit* h, void* stream);   /* model.py:216-223 */
+int gsmpm_fit_clear_grads(gsmpm_fit* h, void* stream);  /* solver.py:173-175 */
+int gsmpm_fit_mu_lam(gsmpm_fit* h, void* stream);       /* compute_mu_lam_from_E_nu, utils.py:349-362 */
+
+/* Fields, external particle order; leveled ones take `level`, the rest ignore it. */
+#define GSMPM_FIT_X 0          /* particle_xyz[level]    [N,3] */
+#define GSMPM_FIT_V 1          /* particle_vel[level]    [N,3] */
+#define GSMPM_FIT_F 2          /* particle_F[level]      [N,9] */
+#define GSMPM_FIT_C 3          /* particle_C[level]      [N,9] */
+#define GSMPM_FIT_STRESS 4     /* particle_stress[level] [N,9] */
+#define GSMPM_FIT_GX 5         /* .grad of the above, same shapes */
+#define GSMPM_FIT_GV 6
+#define GSMPM_FIT_GF 7
+#define GSMPM_FIT_GC 8
+#define GSMPM_FIT_GSTRESS 9
+#define GSMPM_FIT_LOGE 10      /* [N] */
+#define GSMPM_FIT_Y 11
+#define GSMPM_FIT_MU 12
+#define GSMPM_FIT_LAM 13
+#define GSMPM_FIT_GLOGE 14
+#define GSMPM_FIT_GY 15
+#define GSMPM_FIT_GMU 16
+#define GSMPM_FIT_GLAM 17
+#define GSMPM_FIT_COV 18       /* particle_cov [N,6] */
+#define GSMPM_FIT_GCOV 19
+#define GSMPM_FIT_INIT_COV 20
+#define GSMPM_FIT_VOL 21
+#define GSMPM_FIT_MASS 22
+#define GSMPM_FIT_FIELD_COUNT 23
+int gsmpm_fit_field_width(int32_t field);
+int gsmpm_fit_get(gsmpm_fit* h, int32_t field, int32_t level, float* out, void* stream);
+int gsmpm_fit_set(gsmpm_fit* h, int32_t field, int32_t level, const float* in, void* stream);
+/* Dense grid of the last substep: GSMPM_GRID_MASS [n^3], _V_IN / _V_OUT [n^3,3],
+ * and 3 / 4 for grid_v_in.grad / grid_v_out.grad [n^3,3]. */
+int gsmpm_fit_get_grid(gsmpm_fit* h, int32_t which, float* out, void* stream);
+
 /* -------------------------------------------------------- rasterizer ---
  * Replaces diff_gaussian_rasterization._C.rasterize_gaussians (forward;
  * called via GaussianRasterizer.forward at main.py:148-156).  Upstream
