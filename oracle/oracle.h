@@ -113,6 +113,12 @@ typedef struct {
 /* Returns num_rendered; out_color is (3,H,W), out_radii (P). */
 int or_forward(const or_args* a, float* out_color, int32_t* out_radii,
                float* out_depth /*P, may be null*/, int32_t* out_tiles_touched /*P, may be null*/);
+/* Backward of the same forward for dL/d(out_color) [3,H,W].  Outputs (P rows):
+ * dL_dmeans2D [P,3] (NDC, z = 0), dL_dcolors [P,3], dL_dopacity [P],
+ * dL_dmeans3D [P,3], dL_dcov3D [P,6], dL_dsh [P,M,3] (if shs), dL_dscales [P,3]
+ * and dL_drot [P,4] (if scales/rotations; may be null otherwise). */
+void or_backward(const or_args* a, const float* dL_dpix, float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity,
+                 float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drot);
 
 #ifdef __cplusplus
 }

@@ -280,6 +280,39 @@ def raster_forward(means3D, opacities, viewmatrix, projmatrix, campos, bg, W, H,
     return color, radii, K, depth, tt
 
 
+def raster_backward(dL_dcolor, means3D, opacities, viewmatrix, projmatrix, campos, bg, W, H, tanfovx, tanfovy,
+                    shs=None, sh_degree=3, colors_precomp=None, cov3D_precomp=None, scales=None, rotations=None,
+                    scale_modifier=1.0):
+    """Backward of raster_forward for dL/dcolor (3,H,W).  Returns a dict:
+    means2D (P,3), colors (P,3), opacity (P,), means3D (P,3), cov3D (P,6),
+    sh (P,M,3) or None, scales (P,3) or None, rotations (P,4) or None."""
+    c = lambda a: None if a is None else np.ascontiguousarray(np.asarray(a, np.float32))
+    means3D = c(means3D).reshape(-1, 3)
+    P = means3D.shape[0]
+    a = _RArgs()
+    a.P, a.W, a.H = P, W, H
+    a.D = sh_degree
+    keep = []
+    shs_c = c(shs)
+    a.M = 0 if shs_c is None else int(shs_c.reshape(P, -1, 3).shape[1])
+    for name, arr in (("means3D", means3D), ("shs", shs_c), ("colors_precomp", c(colors_precomp)),
+                      ("opacities", c(opacities)), ("scales", c(scales)), ("rotations", c(rotations)),
+                      ("cov3D_precomp", c(cov3D_precomp)), ("viewmatrix", c(viewmatrix)),
+                      ("projmatrix", c(projmatrix)), ("campos", c(campos)), ("bg", c(bg))):
+        keep.append(arr)
+        setattr(a, name, _p(arr))
+    a.scale_modifier = scale_modifier
+    a.tanfovx, a.tanfovy = tanfovx, tanfovy
+    g = c(dL_dcolor).reshape(3, H, W)
+    z = lambda *shape: np.zeros(shape, np.float32)
+    out = {"means2D": z(P, 3), "colors": z(P, 3), "opacity": z(P), "means3D": z(P, 3), "cov3D": z(P, 6),
+           "sh": z(P, max(a.M, 1), 3) if shs_c is not None else None,
+           "scales": z(P, 3) if scales is not None else None, "rotations": z(P, 4) if rotations is not None else None}
+    lib().or_backward(ctypes.byref(a), _p(g), _p(out["means2D"]), _p(out["colors"]), _p(out["opacity"]),
+                      _p(out["means3D"]), _p(out["cov3D"]), _p(out["sh"]), _p(out["scales"]), _p(out["rotations"]))
+    return out
+
+
 # ------------------------------------------------------------------ differentiable path --
 class _DState(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int), ("ng", ctypes.c_int), ("L", ctypes.c_int),
