@@ -15,11 +15,24 @@
 //                  256 Gaussians staged in LDS (xy, conic/opacity, rgb) and
 //                  front-to-back alpha blending with the upstream cut-offs
 //                  (alpha < 1/255 skip, alpha <= 0.99, T < 1e-4 stop), block
-//                  early exit via __syncthreads_count.
+//                  early exit via __syncthreads_count; records each pixel's
+//                  final T and last contributor for the backward pass.
+//
+// Backward (upstream's BACKWARD::render + preprocess, for extra.py's
+// training loop):
+//   k_render_bwd     one workgroup per tile, back to front from each pixel's
+//                    last contributor; the 256 pixels' contributions to each
+//                    (Gaussian, tile) pair are summed on chip (wave shuffles +
+//                    LDS) and stored once per pair at the pair's emission
+//                    index -- the sort carries emission indices, so a
+//                    Gaussian's pairs are contiguous (no global atomics);
+//   k_preprocess_bwd one lane per Gaussian: sums its pair records, then the
+//                    2D-covariance / projection / SH / 3D-covariance adjoints.
 #include <hip/hip_runtime.h>
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 
 #include <cstring>
 #include <string>
@@ -120,7 +133,7 @@ __device__ __forceinline__ void cov2d(const float* mean, const RasterDev& a, con
   out[2] = cc + 0.3f;
 }
 
-__device__ __forceinline__ void sh_rgb(const RasterDev& a, int idx, const float* pos, float rgb[3]) {
+__device__ __forceinline__ void sh_rgb(const RasterDev& a, int idx, const float* pos, float rgb[3], unsigned& clamp) {
   float dir[3] = {pos[0] - a.campos[0], pos[1] - a.campos[1], pos[2] - a.campos[2]};
   const float len = sqrtf(dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2]);
   dir[0] /= len;
@@ -148,6 +161,7 @@ __device__ __forceinline__ void sh_rgb(const RasterDev& a, int idx, const float*
       }
     }
     r += 0.5f;
+    clamp |= (r < 0.0f ? 1u : 0u) << ch;
     rgb[ch] = fmaxf(r, 0.0f);
   }
 }
@@ -191,18 +205,19 @@ __global__ __launch_bounds__(256) void k_preprocess(RasterDev a, int* __restrict
   get_rect(px, py, rad, a.grid_x, a.grid_y, rmin, rmax);
   if ((rmax[0] - rmin[0]) * (rmax[1] - rmin[1]) == 0) return;
   float rgb[3];
+  unsigned clamp = 0;
   if (a.colors_precomp) {
     rgb[0] = a.colors_precomp[(size_t)idx * 3 + 0];
     rgb[1] = a.colors_precomp[(size_t)idx * 3 + 1];
     rgb[2] = a.colors_precomp[(size_t)idx * 3 + 2];
   } else {
-    sh_rgb(a, idx, p, rgb);
+    sh_rgb(a, idx, p, rgb, clamp);
   }
   depth[idx] = pv[2];
   radii[idx] = rad;
   xy[idx] = make_float2(px, py);
   conic_o[idx] = make_float4(cv[2] * di, -cv[1] * di, cv[0] * di, a.opacities[idx]);
-  rgbo[idx] = make_float4(rgb[0], rgb[1], rgb[2], 0.f);
+  rgbo[idx] = make_float4(rgb[0], rgb[1], rgb[2], __uint_as_float(clamp));  // .w: SH clamp bits
   tiles[idx] = (unsigned)((rmax[1] - rmin[1]) * (rmax[0] - rmin[0]));
 }
 
@@ -244,7 +259,8 @@ __global__ __launch_bounds__(256) void k_ranges(int L, const unsigned long long*
 __global__ __launch_bounds__(kBlock) void k_render(const uint2* __restrict__ ranges, const unsigned* __restrict__ list,
                                                    int W, int H, int gx, const float2* __restrict__ xy,
                                                    const float4* __restrict__ conic_o, const float4* __restrict__ rgbo,
-                                                   const float* __restrict__ bg, float* __restrict__ out) {
+                                                   const float* __restrict__ bg, float* __restrict__ out,
+                                                   float* __restrict__ final_T, int* __restrict__ n_contrib) {
   __shared__ float2 s_xy[kBlock];
   __shared__ float4 s_co[kBlock];
   __shared__ float4 s_rgb[kBlock];
@@ -257,6 +273,7 @@ __global__ __launch_bounds__(kBlock) void k_render(const uint2* __restrict__ ran
   int todo = (int)(range.y - range.x);
   const float pfx = (float)px, pfy = (float)py;
   float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f;
+  int contributor = 0, last = 0;
   for (int i = 0; i < rounds; ++i, todo -= kBlock) {
     if (__syncthreads_count(done) == kBlock) break;
     const int prog = i * kBlock + threadIdx.x;
@@ -269,6 +286,7 @@ __global__ __launch_bounds__(kBlock) void k_render(const uint2* __restrict__ ran
     __syncthreads();
     const int nb = min(kBlock, todo);
     for (int j = 0; !done && j < nb; ++j) {
+      ++contributor;
       const float2 g = s_xy[j];
       const float dx = g.x - pfx, dy = g.y - pfy;
       const float4 co = s_co[j];
@@ -289,6 +307,7 @@ __global__ __launch_bounds__(kBlock) void k_render(const uint2* __restrict__ ran
       C1 = __builtin_fmaf(c.y, aT, C1);
       C2 = __builtin_fmaf(c.z, aT, C2);
       T = test_T;
+      last = contributor;
     }
   }
   if (inside) {
@@ -296,7 +315,376 @@ __global__ __launch_bounds__(kBlock) void k_render(const uint2* __restrict__ ran
     out[pix] = C0 + T * bg[0];
     out[HW + pix] = C1 + T * bg[1];
     out[2 * HW + pix] = C2 + T * bg[2];
+    final_T[pix] = T;
+    n_contrib[pix] = last;
   }
+}
+
+// sorted emission index -> Gaussian id (the sort carries emission indices)
+__global__ __launch_bounds__(256) void k_ids(int K, const unsigned* __restrict__ pos, const unsigned* __restrict__ vals,
+                                             unsigned* __restrict__ ids) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < K) ids[k] = vals[pos[k]];
+}
+
+// ------------------------------------------------------------- backward --
+// Per-pixel adjoint of the blend (upstream BACKWARD::renderCUDA), back to
+// front.  Pair record (3 x float4 at the pair's emission index):
+//   (dmean2D.x, dmean2D.y, dconic.a, dconic.b) (dconic.c, dopacity, dR, dG) (dB, 0, 0, 0)
+// with upstream's conventions: dmean2D w.r.t. NDC (x W/2, H/2), the conic's
+// off-diagonal term halved, alpha's 0.99 clamp not differentiated.
+constexpr int kRec = 9;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_render_bwd(const uint2* __restrict__ ranges,
+                                                       const unsigned* __restrict__ pos_sorted,
+                                                       const unsigned* __restrict__ ids, int W, int H, int gx,
+                                                       const float2* __restrict__ xy, const float4* __restrict__ conic_o,
+                                                       const float4* __restrict__ rgbo, const float* __restrict__ bg,
+                                                       const float* __restrict__ final_T,
+                                                       const int* __restrict__ n_contrib,
+                                                       const float* __restrict__ dL_dpix, float4* __restrict__ rec) {
+  __shared__ float2 s_xy[kBlock];
+  __shared__ float4 s_co[kBlock];
+  __shared__ float4 s_rgb[kBlock];
+  __shared__ float s_part[kBlock / 64][kRec][kBlock];
+  __shared__ int s_maxlast;
+  const int tx = threadIdx.x % kBX, ty = threadIdx.x / kBX;
+  const int px = blockIdx.x * kBX + tx, py = blockIdx.y * kBY + ty;
+  const bool inside = px < W && py < H;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint2 range = ranges[blockIdx.y * gx + blockIdx.x];
+  const int todo0 = (int)(range.y - range.x);
+  const size_t pix = (size_t)py * W + px, HW = (size_t)H * W;
+  const float T_final = inside ? final_T[pix] : 0.f;
+  const int last = inside ? n_contrib[pix] : 0;
+  float dpx[3] = {0.f, 0.f, 0.f};
+  if (inside)
+    for (int ch = 0; ch < 3; ++ch) dpx[ch] = dL_dpix[ch * HW + pix];
+  const float bg_dot = bg[0] * dpx[0] + bg[1] * dpx[1] + bg[2] * dpx[2];
+  if (threadIdx.x == 0) s_maxlast = 0;
+  __syncthreads();
+  atomicMax(&s_maxlast, last);
+  __syncthreads();
+  const int maxlast = s_maxlast;  // list positions >= maxlast contribute to no pixel of the tile
+  float T = T_final, accum[3] = {0.f, 0.f, 0.f}, last_color[3] = {0.f, 0.f, 0.f}, last_alpha = 0.f;
+  const float pfx = (float)px, pfy = (float)py;
+  const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
+  const int rounds = (todo0 + kBlock - 1) / kBlock;
+  for (int i = 0; i < rounds; ++i) {
+    const int hi = todo0 - i * kBlock;          // this batch covers positions [hi - nb, hi)
+    const int nb = min(kBlock, hi);
+    const int myp = hi - 1 - (int)threadIdx.x;  // list position of this thread's element
+    if (hi - nb >= maxlast) {                   // nothing in this batch contributes: zero records
+      if ((int)threadIdx.x < nb) {
+        float4* r = rec + (size_t)pos_sorted[range.x + myp] * 3;
+        r[0] = r[1] = r[2] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      continue;
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < nb) {
+      const unsigned id = ids[range.x + myp];
+      s_xy[threadIdx.x] = xy[id];
+      s_co[threadIdx.x] = conic_o[id];
+      s_rgb[threadIdx.x] = rgbo[id];
+    }
+    __syncthreads();
+    for (int j = 0; j < nb; ++j) {
+      const int contributor = hi - 1 - j;
+      float g[kRec] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      bool act = false;
+      if (contributor < last) {
+        const float2 gp = s_xy[j];
+        const float dx = gp.x - pfx, dy = gp.y - pfy;
+        const float4 co = s_co[j];
+        const float power = __builtin_fmaf(-0.5f, __builtin_fmaf(co.x * dx, dx, co.z * dy * dy), -co.y * dx * dy);
+        if (power <= 0.0f) {
+          const float G = __builtin_amdgcn_exp2f(power * 1.4426950408889634f);
+          const float alpha = fminf(0.99f, co.w * G);
+          if (alpha >= 1.0f / 255.0f) {
+            act = true;
+            T = T / (1.f - alpha);
+            const float dchannel_dcolor = alpha * T;
+            const float4 c = s_rgb[j];
+            const float cc[3] = {c.x, c.y, c.z};
+            float dL_dalpha = 0.f;
+            for (int ch = 0; ch < 3; ++ch) {
+              accum[ch] = last_alpha * last_color[ch] + (1.f - last_alpha) * accum[ch];
+              last_color[ch] = cc[ch];
+              dL_dalpha += (cc[ch] - accum[ch]) * dpx[ch];
+              g[6 + ch] = dchannel_dcolor * dpx[ch];
+            }
+            dL_dalpha *= T;
+            last_alpha = alpha;
+            dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
+            const float dL_dG = co.w * dL_dalpha;
+            const float gdx = G * dx, gdy = G * dy;
+            const float dG_ddelx = -gdx * co.x - gdy * co.y;
+            const float dG_ddely = -gdy * co.z - gdx * co.y;
+            g[0] = dL_dG * dG_ddelx * ddelx_dx;
+            g[1] = dL_dG * dG_ddely * ddely_dy;
+            g[2] = -0.5f * gdx * dx * dL_dG;
+            g[3] = -0.5f * gdx * dy * dL_dG;
+            g[4] = -0.5f * gdy * dy * dL_dG;
+            g[5] = G * dL_dalpha;
+          }
+        }
+      }
+      if (__ballot(act)) {
+#pragma unroll
+        for (int q = 0; q < kRec; ++q) g[q] = wave_sum(g[q]);
+      }
+      if (lane == 0)
+#pragma unroll
+        for (int q = 0; q < kRec; ++q) s_part[wave][q][j] = g[q];
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < nb) {
+      const int j = threadIdx.x;
+      float o[kRec];
+#pragma unroll
+      for (int q = 0; q < kRec; ++q) o[q] = s_part[0][q][j] + s_part[1][q][j] + s_part[2][q][j] + s_part[3][q][j];
+      float4* r = rec + (size_t)pos_sorted[range.x + myp] * 3;
+      r[0] = make_float4(o[0], o[1], o[2], o[3]);
+      r[1] = make_float4(o[4], o[5], o[6], o[7]);
+      r[2] = make_float4(o[8], 0.f, 0.f, 0.f);
+    }
+  }
+}
+
+__device__ __forceinline__ void dnormvdv(const float v[3], const float dv[3], float out[3]) {
+  const float sum2 = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+  const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+  out[0] = ((sum2 - v[0] * v[0]) * dv[0] - v[1] * v[0] * dv[1] - v[2] * v[0] * dv[2]) * invsum32;
+  out[1] = (-v[0] * v[1] * dv[0] + (sum2 - v[1] * v[1]) * dv[1] - v[2] * v[1] * dv[2]) * invsum32;
+  out[2] = (-v[0] * v[2] * dv[0] - v[1] * v[2] * dv[1] + (sum2 - v[2] * v[2]) * dv[2]) * invsum32;
+}
+
+struct RasterGrads {
+  float *dmeans2D, *dcolors, *dopacity, *dmeans3D, *dcov3D, *dsh, *dscales, *drot;
+};
+
+// computeColorFromSH backward (upstream): dL/dsh and the view-direction term of dL/dmean
+__device__ void sh_backward(const RasterDev& a, int idx, const float* pos, unsigned clamp, const float dcol[3],
+                            float* dsh, float dmean[3]) {
+  const float dir_orig[3] = {pos[0] - a.campos[0], pos[1] - a.campos[1], pos[2] - a.campos[2]};
+  const float len = sqrtf(dir_orig[0] * dir_orig[0] + dir_orig[1] * dir_orig[1] + dir_orig[2] * dir_orig[2]);
+  const float x = dir_orig[0] / len, y = dir_orig[1] / len, z = dir_orig[2] / len;
+  const float* sh = a.shs + (size_t)idx * a.M * 3;
+  float g[3];
+  for (int ch = 0; ch < 3; ++ch) g[ch] = ((clamp >> ch) & 1u) ? 0.f : dcol[ch];
+  float dRdx[3] = {0.f, 0.f, 0.f}, dRdy[3] = {0.f, 0.f, 0.f}, dRdz[3] = {0.f, 0.f, 0.f};
+  const int used = a.D > 2 ? 16 : a.D > 1 ? 9 : a.D > 0 ? 4 : 1;
+  float coef[16];
+  coef[0] = kSH_C0;
+  if (a.D > 0) {
+    coef[1] = -kSH_C1 * y;
+    coef[2] = kSH_C1 * z;
+    coef[3] = -kSH_C1 * x;
+    for (int ch = 0; ch < 3; ++ch) {
+      dRdx[ch] = -kSH_C1 * sh[3 * 3 + ch];
+      dRdy[ch] = -kSH_C1 * sh[1 * 3 + ch];
+      dRdz[ch] = kSH_C1 * sh[2 * 3 + ch];
+    }
+    if (a.D > 1) {
+      const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+      coef[4] = kSH_C2[0] * xy;
+      coef[5] = kSH_C2[1] * yz;
+      coef[6] = kSH_C2[2] * (2.f * zz - xx - yy);
+      coef[7] = kSH_C2[3] * xz;
+      coef[8] = kSH_C2[4] * (xx - yy);
+      for (int ch = 0; ch < 3; ++ch) {
+        const float* S = sh + ch;
+        dRdx[ch] += kSH_C2[0] * y * S[4 * 3] + kSH_C2[2] * 2.f * -x * S[6 * 3] + kSH_C2[3] * z * S[7 * 3] +
+                    kSH_C2[4] * 2.f * x * S[8 * 3];
+        dRdy[ch] += kSH_C2[0] * x * S[4 * 3] + kSH_C2[1] * z * S[5 * 3] + kSH_C2[2] * 2.f * -y * S[6 * 3] +
+                    kSH_C2[4] * 2.f * -y * S[8 * 3];
+        dRdz[ch] += kSH_C2[1] * y * S[5 * 3] + kSH_C2[2] * 2.f * 2.f * z * S[6 * 3] + kSH_C2[3] * x * S[7 * 3];
+      }
+      if (a.D > 2) {
+        coef[9] = kSH_C3[0] * y * (3.f * xx - yy);
+        coef[10] = kSH_C3[1] * xy * z;
+        coef[11] = kSH_C3[2] * y * (4.f * zz - xx - yy);
+        coef[12] = kSH_C3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy);
+        coef[13] = kSH_C3[4] * x * (4.f * zz - xx - yy);
+        coef[14] = kSH_C3[5] * z * (xx - yy);
+        coef[15] = kSH_C3[6] * x * (xx - 3.f * yy);
+        for (int ch = 0; ch < 3; ++ch) {
+          const float* S = sh + ch;
+          dRdx[ch] += kSH_C3[0] * S[9 * 3] * 3.f * 2.f * xy + kSH_C3[1] * S[10 * 3] * yz +
+                      kSH_C3[2] * S[11 * 3] * -2.f * xy + kSH_C3[3] * S[12 * 3] * -3.f * 2.f * xz +
+                      kSH_C3[4] * S[13 * 3] * (-3.f * xx + 4.f * zz - yy) + kSH_C3[5] * S[14 * 3] * 2.f * xz +
+                      kSH_C3[6] * S[15 * 3] * 3.f * (xx - yy);
+          dRdy[ch] += kSH_C3[0] * S[9 * 3] * 3.f * (xx - yy) + kSH_C3[1] * S[10 * 3] * xz +
+                      kSH_C3[2] * S[11 * 3] * (-3.f * yy + 4.f * zz - xx) + kSH_C3[3] * S[12 * 3] * -3.f * 2.f * yz +
+                      kSH_C3[4] * S[13 * 3] * -2.f * xy + kSH_C3[5] * S[14 * 3] * -2.f * yz +
+                      kSH_C3[6] * S[15 * 3] * -3.f * 2.f * xy;
+          dRdz[ch] += kSH_C3[1] * S[10 * 3] * xy + kSH_C3[2] * S[11 * 3] * 4.f * 2.f * yz +
+                      kSH_C3[3] * S[12 * 3] * 3.f * (2.f * zz - xx - yy) + kSH_C3[4] * S[13 * 3] * 4.f * 2.f * xz +
+                      kSH_C3[5] * S[14 * 3] * (xx - yy);
+        }
+      }
+    }
+  }
+  float* d = dsh + (size_t)idx * a.M * 3;
+  for (int k = 0; k < a.M; ++k)
+    for (int ch = 0; ch < 3; ++ch) d[k * 3 + ch] = k < used ? coef[k] * g[ch] : 0.f;
+  const float dL_ddir[3] = {dRdx[0] * g[0] + dRdx[1] * g[1] + dRdx[2] * g[2],
+                            dRdy[0] * g[0] + dRdy[1] * g[1] + dRdy[2] * g[2],
+                            dRdz[0] * g[0] + dRdz[1] * g[1] + dRdz[2] * g[2]};
+  float dm[3];
+  dnormvdv(dir_orig, dL_ddir, dm);
+  for (int q = 0; q < 3; ++q) dmean[q] += dm[q];
+}
+
+// computeCov3D backward: dL/d(mod * scale) and dL/d(unnormalised quaternion)
+__device__ void cov3d_backward(const float* s, float mod, const float* rot, const float* dc, float* ds, float* dq) {
+  const float S[3] = {mod * s[0], mod * s[1], mod * s[2]};
+  const float r = rot[0], x = rot[1], y = rot[2], z = rot[3];
+  const float R[9] = {1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+                      2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+                      2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y)};
+  const float G[9] = {dc[0], 0.5f * dc[1], 0.5f * dc[2], 0.5f * dc[1], dc[3], 0.5f * dc[4], 0.5f * dc[2], 0.5f * dc[4], dc[5]};
+  float M[9], dM[9], dR[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) M[i * 3 + j] = R[i * 3 + j] * S[j];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) dM[i * 3 + j] = 2.f * (G[i * 3 + 0] * M[0 * 3 + j] + G[i * 3 + 1] * M[1 * 3 + j] + G[i * 3 + 2] * M[2 * 3 + j]);
+  for (int j = 0; j < 3; ++j) {
+    ds[j] = dM[0 * 3 + j] * R[0 * 3 + j] + dM[1 * 3 + j] * R[1 * 3 + j] + dM[2 * 3 + j] * R[2 * 3 + j];
+    for (int i = 0; i < 3; ++i) dR[i * 3 + j] = dM[i * 3 + j] * S[j];
+  }
+  dq[0] = 2.f * (-z * dR[1] + y * dR[2] + z * dR[3] - x * dR[5] - y * dR[6] + x * dR[7]);
+  dq[1] = 2.f * (y * dR[1] + z * dR[2] + y * dR[3] - 2.f * x * dR[4] - r * dR[5] + z * dR[6] + r * dR[7] - 2.f * x * dR[8]);
+  dq[2] = 2.f * (-2.f * y * dR[0] + x * dR[1] + r * dR[2] + x * dR[3] + z * dR[5] - r * dR[6] + z * dR[7] - 2.f * y * dR[8]);
+  dq[3] = 2.f * (-2.f * z * dR[0] - r * dR[1] + x * dR[2] + r * dR[3] - 2.f * z * dR[4] + y * dR[5] + x * dR[6] + y * dR[7]);
+}
+
+// computeCov2DCUDA + preprocessCUDA backward, one lane per Gaussian.
+__global__ __launch_bounds__(256) void k_preprocess_bwd(RasterDev a, const int* __restrict__ radii,
+                                                        const unsigned* __restrict__ offsets,
+                                                        const float4* __restrict__ rgbo, const float4* __restrict__ rec,
+                                                        RasterGrads o) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= a.P) return;
+  float g[kRec] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float dm[3] = {0.f, 0.f, 0.f}, dcov[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bool on = radii[idx] > 0;
+  const float* m = a.means3D + (size_t)idx * 3;
+  float c6[6];
+  const float* c3 = nullptr;
+  if (on) {
+    const unsigned b = idx ? offsets[idx - 1] : 0u, e = offsets[idx];
+    for (unsigned k = b; k < e; ++k) {
+      const float4 r0 = rec[(size_t)k * 3], r1 = rec[(size_t)k * 3 + 1], r2 = rec[(size_t)k * 3 + 2];
+      g[0] += r0.x; g[1] += r0.y; g[2] += r0.z; g[3] += r0.w;
+      g[4] += r1.x; g[5] += r1.y; g[6] += r1.z; g[7] += r1.w;
+      g[8] += r2.x;
+    }
+    if (a.cov3D_precomp) {
+      c3 = a.cov3D_precomp + (size_t)idx * 6;
+    } else {
+      cov3d_from_sr(a.scales + (size_t)idx * 3, a.scale_modifier, a.rotations + (size_t)idx * 4, c6);
+      c3 = c6;
+    }
+    const float* vm = a.viewmatrix;
+    float t[3];
+    xform4x3(m, vm, t);
+    const float limx = 1.3f * a.tanfovx, limy = 1.3f * a.tanfovy;
+    const float txtz = t[0] / t[2], tytz = t[1] / t[2];
+    t[0] = fminf(limx, fmaxf(-limx, txtz)) * t[2];
+    t[1] = fminf(limy, fmaxf(-limy, tytz)) * t[2];
+    const float x_mul = (txtz < -limx || txtz > limx) ? 0.f : 1.f;
+    const float y_mul = (tytz < -limy || tytz > limy) ? 0.f : 1.f;
+    const float hx = a.focal_x, hy = a.focal_y;
+    const float J00 = hx / t[2], J02 = -(hx * t[0]) / (t[2] * t[2]);
+    const float J11 = hy / t[2], J12 = -(hy * t[1]) / (t[2] * t[2]);
+    const float Wm[9] = {vm[0], vm[4], vm[8], vm[1], vm[5], vm[9], vm[2], vm[6], vm[10]};
+    float T0[3], T1[3];
+    for (int c = 0; c < 3; ++c) {
+      T0[c] = J00 * Wm[0 * 3 + c] + J02 * Wm[2 * 3 + c];
+      T1[c] = J11 * Wm[1 * 3 + c] + J12 * Wm[2 * 3 + c];
+    }
+    const float V[9] = {c3[0], c3[1], c3[2], c3[1], c3[3], c3[4], c3[2], c3[4], c3[5]};
+    float VT0[3], VT1[3];
+    for (int r = 0; r < 3; ++r) {
+      VT0[r] = V[r * 3 + 0] * T0[0] + V[r * 3 + 1] * T0[1] + V[r * 3 + 2] * T0[2];
+      VT1[r] = V[r * 3 + 0] * T1[0] + V[r * 3 + 1] * T1[1] + V[r * 3 + 2] * T1[2];
+    }
+    const float ca = T0[0] * VT0[0] + T0[1] * VT0[1] + T0[2] * VT0[2] + 0.3f;
+    const float cb = T0[0] * VT1[0] + T0[1] * VT1[1] + T0[2] * VT1[2];
+    const float cc = T1[0] * VT1[0] + T1[1] * VT1[1] + T1[2] * VT1[2] + 0.3f;
+    const float denom = ca * cc - cb * cb;
+    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+    const float dco[3] = {g[2], g[3], g[4]};
+    float dL_da = 0.f, dL_db = 0.f, dL_dc = 0.f;
+    if (denom2inv != 0.f) {
+      dL_da = denom2inv * (-cc * cc * dco[0] + 2.f * cb * cc * dco[1] + (denom - ca * cc) * dco[2]);
+      dL_dc = denom2inv * (-ca * ca * dco[2] + 2.f * ca * cb * dco[1] + (denom - ca * cc) * dco[0]);
+      dL_db = denom2inv * 2.f * (cb * cc * dco[0] - (denom + 2.f * cb * cb) * dco[1] + ca * cb * dco[2]);
+      const int di[6] = {0, 0, 0, 1, 1, 2}, dj[6] = {0, 1, 2, 1, 2, 2};
+#pragma unroll
+      for (int e2 = 0; e2 < 6; ++e2) {
+        const int p = di[e2], q = dj[e2];
+        dcov[e2] = p == q ? T0[p] * T0[p] * dL_da + T0[p] * T1[p] * dL_db + T1[p] * T1[p] * dL_dc
+                          : 2.f * T0[p] * T0[q] * dL_da + (T0[p] * T1[q] + T0[q] * T1[p]) * dL_db +
+                                2.f * T1[p] * T1[q] * dL_dc;
+      }
+    }
+    float dT0[3], dT1[3];
+    for (int c = 0; c < 3; ++c) {
+      dT0[c] = 2.f * VT0[c] * dL_da + VT1[c] * dL_db;
+      dT1[c] = VT0[c] * dL_db + 2.f * VT1[c] * dL_dc;
+    }
+    const float dJ00 = Wm[0] * dT0[0] + Wm[1] * dT0[1] + Wm[2] * dT0[2];
+    const float dJ02 = Wm[6] * dT0[0] + Wm[7] * dT0[1] + Wm[8] * dT0[2];
+    const float dJ11 = Wm[3] * dT1[0] + Wm[4] * dT1[1] + Wm[5] * dT1[2];
+    const float dJ12 = Wm[6] * dT1[0] + Wm[7] * dT1[1] + Wm[8] * dT1[2];
+    const float tz = 1.f / t[2], tz2 = tz * tz, tz3 = tz2 * tz;
+    const float dtx = x_mul * -hx * tz2 * dJ02;
+    const float dty = y_mul * -hy * tz2 * dJ12;
+    const float dtz = -hx * tz2 * dJ00 - hy * tz2 * dJ11 + (2.f * hx * t[0]) * tz3 * dJ02 + (2.f * hy * t[1]) * tz3 * dJ12;
+    dm[0] = vm[0] * dtx + vm[1] * dty + vm[2] * dtz;
+    dm[1] = vm[4] * dtx + vm[5] * dty + vm[6] * dtz;
+    dm[2] = vm[8] * dtx + vm[9] * dty + vm[10] * dtz;
+    const float* pm = a.projmatrix;
+    const float hw = pm[3] * m[0] + pm[7] * m[1] + pm[11] * m[2] + pm[15];
+    const float mw = 1.0f / (hw + 0.0000001f);
+    const float mul1 = (pm[0] * m[0] + pm[4] * m[1] + pm[8] * m[2] + pm[12]) * mw * mw;
+    const float mul2 = (pm[1] * m[0] + pm[5] * m[1] + pm[9] * m[2] + pm[13]) * mw * mw;
+    dm[0] += (pm[0] * mw - pm[3] * mul1) * g[0] + (pm[1] * mw - pm[3] * mul2) * g[1];
+    dm[1] += (pm[4] * mw - pm[7] * mul1) * g[0] + (pm[5] * mw - pm[7] * mul2) * g[1];
+    dm[2] += (pm[8] * mw - pm[11] * mul1) * g[0] + (pm[9] * mw - pm[11] * mul2) * g[1];
+  }
+  if (a.shs) {
+    if (on) {
+      sh_backward(a, idx, m, __float_as_uint(rgbo[idx].w), g + 6, o.dsh, dm);
+    } else {
+      float* d = o.dsh + (size_t)idx * a.M * 3;
+      for (int k = 0; k < a.M * 3; ++k) d[k] = 0.f;
+    }
+  }
+  if (a.scales) {
+    float ds[3] = {0.f, 0.f, 0.f}, dq[4] = {0.f, 0.f, 0.f, 0.f};
+    if (on) cov3d_backward(a.scales + (size_t)idx * 3, a.scale_modifier, a.rotations + (size_t)idx * 4, dcov, ds, dq);
+    for (int q = 0; q < 3; ++q) o.dscales[(size_t)idx * 3 + q] = ds[q];
+    for (int q = 0; q < 4; ++q) o.drot[(size_t)idx * 4 + q] = dq[q];
+  }
+  o.dmeans2D[(size_t)idx * 3 + 0] = g[0];
+  o.dmeans2D[(size_t)idx * 3 + 1] = g[1];
+  o.dmeans2D[(size_t)idx * 3 + 2] = 0.f;
+  for (int q = 0; q < 3; ++q) {
+    o.dcolors[(size_t)idx * 3 + q] = g[6 + q];
+    o.dmeans3D[(size_t)idx * 3 + q] = dm[q];
+  }
+  o.dopacity[idx] = g[5];
+  for (int q = 0; q < 6; ++q) o.dcov3D[(size_t)idx * 6 + q] = dcov[q];
 }
 
 __global__ __launch_bounds__(256) void k_mark_visible(const float* __restrict__ m, int P, const float* __restrict__ vm,
@@ -339,10 +727,20 @@ struct gsmpm_raster {
   unsigned *vals = nullptr, *vals_sorted = nullptr;
   void* sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
+  unsigned* ids_sorted = nullptr;  // Gaussian id per sorted pair (vals_sorted holds emission indices)
+  float4* rec = nullptr;           // backward pair records, 3 x float4 per pair
+  size_t capRec = 0;
   // tile ranges
   size_t capT = 0;
   uint2* ranges = nullptr;
   unsigned* h_count = nullptr;  // pinned
+  // per pixel (backward)
+  size_t capPix = 0;
+  float* final_T = nullptr;
+  int* n_contrib = nullptr;
+  // the forward the state belongs to
+  int P = -1, W = 0, H = 0, gx = 0, gy = 0;
+  unsigned K = 0;
 };
 
 static int grow(void** p, size_t bytes) {
@@ -371,7 +769,8 @@ int gsmpm_raster_destroy(gsmpm_raster* r) {
   if (!r) return GSMPM_OK;
   for (void* p : {(void*)r->radii_tmp, (void*)r->depth, (void*)r->xy, (void*)r->conic, (void*)r->rgb, (void*)r->tiles,
                   (void*)r->offsets, r->scan_tmp, (void*)r->keys, (void*)r->keys_sorted, (void*)r->vals,
-                  (void*)r->vals_sorted, r->sort_tmp, (void*)r->ranges})
+                  (void*)r->vals_sorted, r->sort_tmp, (void*)r->ranges, (void*)r->ids_sorted, (void*)r->rec,
+                  (void*)r->final_T, (void*)r->n_contrib})
     if (p) (void)hipFree(p);
   if (r->h_count) (void)hipHostFree(r->h_count);
   delete r;
@@ -440,6 +839,13 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     r->capT = ntiles;
   }
   GSMPM_HIP(hipMemsetAsync(r->ranges, 0, ntiles * sizeof(uint2), st));
+  const size_t npix = (size_t)in->W * in->H;
+  if (npix > r->capPix) {
+    int rc;
+    if ((rc = grow((void**)&r->final_T, npix * sizeof(float)))) return rc;
+    if ((rc = grow((void**)&r->n_contrib, npix * sizeof(int)))) return rc;
+    r->capPix = npix;
+  }
   unsigned K = 0;
   if (P > 0) {
     hipLaunchKernelGGL(k_preprocess, dim3(div_up(P, 256)), dim3(256), 0, st, a, out_radii, r->depth, r->xy, r->conic,
@@ -459,9 +865,10 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       if ((rc = grow((void**)&r->keys_sorted, cap * 8))) return rc;
       if ((rc = grow((void**)&r->vals, cap * 4))) return rc;
       if ((rc = grow((void**)&r->vals_sorted, cap * 4))) return rc;
+      if ((rc = grow((void**)&r->ids_sorted, cap * 4))) return rc;
       size_t bytes = 0;
-      GSMPM_HIP(rocprim::radix_sort_pairs(nullptr, bytes, r->keys, r->keys_sorted, r->vals, r->vals_sorted, cap, 0,
-                                          64, st));
+      GSMPM_HIP(rocprim::radix_sort_pairs(nullptr, bytes, r->keys, r->keys_sorted, rocprim::counting_iterator<unsigned>(0u),
+                                          r->vals_sorted, cap, 0, 64, st));
       if ((rc = grow(&r->sort_tmp, bytes))) return rc;
       r->sort_tmp_bytes = bytes;
       r->capK = cap;
@@ -471,15 +878,62 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     GSMPM_LAUNCH_CHECK();
     const int bits = msb_bits((unsigned)ntiles);
     size_t bytes = r->sort_tmp_bytes;
-    GSMPM_HIP(rocprim::radix_sort_pairs(r->sort_tmp, bytes, r->keys, r->keys_sorted, r->vals, r->vals_sorted,
-                                        (size_t)K, 0, 32 + bits, st));
+    // values = emission indices (a Gaussian's pairs are contiguous in emission order: the
+    // backward sums them without atomics); ids_sorted maps them back to Gaussians
+    GSMPM_HIP(rocprim::radix_sort_pairs(r->sort_tmp, bytes, r->keys, r->keys_sorted,
+                                        rocprim::counting_iterator<unsigned>(0u), r->vals_sorted, (size_t)K, 0,
+                                        32 + bits, st));
+    hipLaunchKernelGGL(k_ids, dim3(div_up(K, 256)), dim3(256), 0, st, (int)K, r->vals_sorted, r->vals, r->ids_sorted);
     hipLaunchKernelGGL(k_ranges, dim3(div_up(K, 256)), dim3(256), 0, st, (int)K, r->keys_sorted, r->ranges);
     GSMPM_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(k_render, dim3(a.grid_x, a.grid_y), dim3(kBlock), 0, st, r->ranges, r->vals_sorted, a.W, a.H,
-                     a.grid_x, r->xy, r->conic, r->rgb, in->bg, out_color);
+  hipLaunchKernelGGL(k_render, dim3(a.grid_x, a.grid_y), dim3(kBlock), 0, st, r->ranges, r->ids_sorted, a.W, a.H,
+                     a.grid_x, r->xy, r->conic, r->rgb, in->bg, out_color, r->final_T, r->n_contrib);
   GSMPM_LAUNCH_CHECK();
   if (num_rendered) *num_rendered = (int32_t)K;
+  r->P = P;
+  r->W = a.W;
+  r->H = a.H;
+  r->gx = a.grid_x;
+  r->gy = a.grid_y;
+  r->K = K;
+  return GSMPM_OK;
+}
+
+int gsmpm_raster_backward(gsmpm_raster* r, const gsmpm_raster_args* in, const int32_t* radii, const float* dL_dcolor,
+                          float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D,
+                          float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations, void* stream) {
+  GSMPM_REQUIRE(r && in && radii && dL_dcolor && dL_dmeans2D && dL_dcolors && dL_dopacity && dL_dmeans3D && dL_dcov3D,
+                "gsmpm_raster_backward: null argument");
+  GSMPM_REQUIRE(r->P == in->P && r->W == in->W && r->H == in->H,
+                "gsmpm_raster_backward: the context holds no forward of these sizes (one context per differentiable forward)");
+  GSMPM_REQUIRE(!in->shs || dL_dsh, "gsmpm_raster_backward: shs given but no dL_dsh output");
+  GSMPM_REQUIRE(!in->scales || (dL_dscales && dL_drotations), "gsmpm_raster_backward: scales given but no outputs");
+  hipStream_t st = (hipStream_t)stream;
+  if (in->P == 0) return GSMPM_OK;
+  RasterDev a;
+  a.P = in->P; a.D = in->D; a.M = in->M; a.W = in->W; a.H = in->H;
+  a.means3D = in->means3D; a.shs = in->shs; a.colors_precomp = in->colors_precomp; a.opacities = in->opacities;
+  a.scales = in->scales; a.rotations = in->rotations; a.cov3D_precomp = in->cov3D_precomp;
+  a.scale_modifier = in->scale_modifier; a.viewmatrix = in->viewmatrix; a.projmatrix = in->projmatrix;
+  a.campos = in->campos; a.bg = in->bg; a.tanfovx = in->tanfovx; a.tanfovy = in->tanfovy;
+  a.focal_x = in->W / (2.0f * in->tanfovx);
+  a.focal_y = in->H / (2.0f * in->tanfovy);
+  a.grid_x = r->gx; a.grid_y = r->gy;
+  const size_t K = r->K;
+  if (K > r->capRec) {
+    int rc;
+    if ((rc = grow((void**)&r->rec, (K + K / 4 + 1024) * 3 * sizeof(float4)))) return rc;
+    r->capRec = K + K / 4 + 1024;
+  }
+  if (K > 0)
+    hipLaunchKernelGGL(k_render_bwd, dim3(r->gx, r->gy), dim3(kBlock), 0, st, r->ranges, r->vals_sorted,
+                       r->ids_sorted, a.W, a.H, r->gx, r->xy, r->conic, r->rgb, in->bg, r->final_T, r->n_contrib,
+                       dL_dcolor, r->rec);
+  RasterGrads o{dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations};
+  hipLaunchKernelGGL(k_preprocess_bwd, dim3(div_up(a.P, 256)), dim3(256), 0, st, a, radii, r->offsets, r->rgb,
+                     r->rec, o);
+  GSMPM_LAUNCH_CHECK();
   return GSMPM_OK;
 }
 

@@ -3,8 +3,11 @@
 Same Python surface as the graphdeco-inria extension the reference imports at
 main.py:16 / extra.py:16 (pre-2024 API: the forward returns ``(color, radii)``,
 consumed as ``rendered_image, _ = rasterizer(...)`` at main.py:148), backed by
-the HIP forward in libgsmpm.so.  The backward pass (needed only by extra.py's
-system identification) is not implemented yet and raises.
+the HIP kernels in libgsmpm.so.  The backward (upstream's
+_RasterizeGaussians.backward, used by extra.py's loss.backward()) returns the
+gradients of means3D, means2D (w.r.t. NDC, as upstream), shs / colors_precomp,
+opacities, scales / rotations or cov3D_precomp; a forward that needs them runs
+on a context of its own that keeps its binning and per-pixel state.
 """
 from __future__ import annotations
 
@@ -46,18 +49,39 @@ class _RasterizeGaussians(torch.autograd.Function):
     def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp,
                 raster_settings):
         s = raster_settings
-        num_rendered, color, radii = _raster.forward(
-            means3D, opacities.reshape(-1), s.viewmatrix, s.projmatrix, s.campos, s.bg, s.image_height,
-            s.image_width, s.tanfovx, s.tanfovy, sh_degree=s.sh_degree, shs=_opt(sh),
-            colors_precomp=_opt(colors_precomp), scales=_opt(scales), rotations=_opt(rotations),
-            cov3D_precomp=_opt(cov3Ds_precomp), scale_modifier=s.scale_modifier, prefiltered=s.prefiltered)
+        kw = dict(sh_degree=s.sh_degree, shs=_opt(sh), colors_precomp=_opt(colors_precomp), scales=_opt(scales),
+                  rotations=_opt(rotations), cov3D_precomp=_opt(cov3Ds_precomp), scale_modifier=s.scale_modifier,
+                  prefiltered=s.prefiltered)
+        args = (means3D, opacities.reshape(-1), s.viewmatrix, s.projmatrix, s.campos, s.bg, s.image_height,
+                s.image_width, s.tanfovx, s.tanfovy)
+        if any(ctx.needs_input_grad[:8]):
+            context = _raster.RasterContext()
+            num_rendered, color, radii, a, keep = _raster.forward(*args, **kw, context=context, return_args=True)
+            ctx.state = (context, a, keep, radii)
+            ctx.shapes = [None if t is None else (t.shape, t.dtype) for t in
+                          (means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp)]
+        else:
+            num_rendered, color, radii = _raster.forward(*args, **kw)
         ctx.num_rendered = num_rendered
         ctx.mark_non_differentiable(radii)
         return color, radii
 
     @staticmethod
     def backward(ctx, grad_out_color, _):
-        raise NotImplementedError("rasterizer backward is not implemented yet (SURVEY §8(f) item 1)")
+        context, a, keep, radii = ctx.state
+        shp = ctx.shapes
+        P = a.P
+
+        def cast(t, i):
+            if t is None or shp[i] is None or shp[i][0].numel() == 0 or not ctx.needs_input_grad[i]:
+                return None
+            return t.reshape(shp[i][0]).to(shp[i][1])
+        if P == 0:
+            return (None,) * 9
+        g = _raster.backward(context, keep, a, radii, grad_out_color)
+        ctx.state = None  # frees the context's buffers once the graph is released
+        return (cast(g["means3D"], 0), cast(g["means2D"], 1), cast(g["sh"], 2), cast(g["colors"], 3),
+                cast(g["opacity"], 4), cast(g["scales"], 5), cast(g["rotations"], 6), cast(g["cov3D"], 7), None)
 
 
 class GaussianRasterizer(nn.Module):

@@ -20,6 +20,21 @@ def _context(device_index: int):
     return h
 
 
+class RasterContext:
+    """A dedicated gsmpm_raster context: holds one forward's binning and
+    per-pixel state until its backward (upstream keeps geom/binning/image
+    buffers in the autograd context for the same reason)."""
+
+    def __init__(self):
+        self.h = ctypes.c_void_p()
+        check(LIB.gsmpm_raster_create(ctypes.byref(self.h)), "gsmpm_raster_create")
+
+    def __del__(self):
+        if getattr(self, "h", None) is not None and self.h.value:
+            LIB.gsmpm_raster_destroy(self.h)
+            self.h = None
+
+
 def _f32(t):
     if t is None:
         return None
@@ -28,19 +43,15 @@ def _f32(t):
     return t.detach().to(torch.float32).contiguous()
 
 
-def forward(means3D, opacities, viewmatrix, projmatrix, campos, bg, image_height, image_width, tanfovx, tanfovy,
-            sh_degree=0, shs=None, colors_precomp=None, scales=None, rotations=None, cov3D_precomp=None,
-            scale_modifier=1.0, prefiltered=False):
-    """Returns (num_rendered, color [3,H,W], radii [P] int32)."""
-    dev = means3D.device
+def _args(means3D, opacities, viewmatrix, projmatrix, campos, bg, image_height, image_width, tanfovx, tanfovy,
+          sh_degree, shs, colors_precomp, scales, rotations, cov3D_precomp, scale_modifier, prefiltered):
+    """(RasterArgs, the f32 tensors it points into)."""
     means3D = _f32(means3D)
     P = means3D.shape[0] if means3D is not None else 0
     shs, colors_precomp = _f32(shs), _f32(colors_precomp)
     scales, rotations, cov3D_precomp = _f32(scales), _f32(rotations), _f32(cov3D_precomp)
     opacities = _f32(opacities)
     vm, pm, cp, bgc = _f32(viewmatrix), _f32(projmatrix), _f32(campos), _f32(bg)
-    color = torch.empty((3, image_height, image_width), dtype=torch.float32, device=dev)
-    radii = torch.zeros(P, dtype=torch.int32, device=dev)
     a = _lib.RasterArgs()
     a.P, a.D = P, int(sh_degree)
     a.M = 0 if shs is None else int(shs.reshape(P, -1, 3).shape[1]) if P > 0 else 0
@@ -54,14 +65,55 @@ def forward(means3D, opacities, viewmatrix, projmatrix, campos, bg, image_height
     a.viewmatrix, a.projmatrix, a.campos, a.bg = ptr(vm), ptr(pm), ptr(cp), ptr(bgc)
     a.tanfovx, a.tanfovy = float(tanfovx), float(tanfovy)
     a.prefiltered = int(bool(prefiltered))
+    keep = dict(means3D=means3D, shs=shs, colors_precomp=colors_precomp, scales=scales, rotations=rotations,
+                cov3D_precomp=cov3D_precomp, opacities=opacities, vm=vm, pm=pm, cp=cp, bg=bgc)
+    return a, keep
+
+
+def backward(context, keep, a, radii, grad_color):
+    """gsmpm_raster_backward on the state of `context`'s forward.  Returns a dict of
+    means2D [P,3], colors [P,3], opacity [P], means3D [P,3], cov3D [P,6],
+    sh [P,M,3] | None, scales [P,3] | None, rotations [P,4] | None."""
+    dev = keep["means3D"].device
+    P = a.P
+    z = lambda *shape: torch.empty(shape, dtype=torch.float32, device=dev)
+    g = {"means2D": z(P, 3), "colors": z(P, 3), "opacity": z(P), "means3D": z(P, 3), "cov3D": z(P, 6),
+         "sh": z(P, a.M, 3) if keep["shs"] is not None else None,
+         "scales": z(P, 3) if keep["scales"] is not None else None,
+         "rotations": z(P, 4) if keep["rotations"] is not None else None}
+    grad_color = grad_color.detach().to(torch.float32).contiguous()
+    with torch.cuda.device(dev):
+        check(LIB.gsmpm_raster_backward(context.h, ctypes.byref(a), ptr(radii), ptr(grad_color), ptr(g["means2D"]),
+                                        ptr(g["colors"]), ptr(g["opacity"]), ptr(g["means3D"]), ptr(g["cov3D"]),
+                                        ptr(g["sh"]), ptr(g["scales"]), ptr(g["rotations"]), stream_of(dev)),
+              "rasterize_gaussians_backward")
+    return g
+
+
+def forward(means3D, opacities, viewmatrix, projmatrix, campos, bg, image_height, image_width, tanfovx, tanfovy,
+            sh_degree=0, shs=None, colors_precomp=None, scales=None, rotations=None, cov3D_precomp=None,
+            scale_modifier=1.0, prefiltered=False, context=None, return_args=False):
+    """Returns (num_rendered, color [3,H,W], radii [P] int32) [+ (args, kept tensors)
+    when return_args].  `context` (a RasterContext) keeps this forward's state
+    for `backward`; by default a shared per-device context is used."""
+    dev = means3D.device
+    a, keep = _args(means3D, opacities, viewmatrix, projmatrix, campos, bg, image_height, image_width, tanfovx,
+                    tanfovy, sh_degree, shs, colors_precomp, scales, rotations, cov3D_precomp, scale_modifier,
+                    prefiltered)
+    P = a.P
+    color = torch.empty((3, image_height, image_width), dtype=torch.float32, device=dev)
+    radii = torch.zeros(P, dtype=torch.int32, device=dev)
+    nr = ctypes.c_int32(0)
     if P == 0:
         # nothing to splat: the image is the background (upstream behaviour)
-        color[:] = bgc.view(3, 1, 1)
-        return 0, color, radii
-    nr = ctypes.c_int32(0)
-    with torch.cuda.device(dev):
-        check(LIB.gsmpm_raster_forward(_context(dev.index or 0), ctypes.byref(a), ptr(color), ptr(radii),
-                                       ctypes.byref(nr), stream_of(dev)), "rasterize_gaussians")
+        color[:] = keep["bg"].view(3, 1, 1)
+    else:
+        with torch.cuda.device(dev):
+            check(LIB.gsmpm_raster_forward(context.h if context is not None else _context(dev.index or 0),
+                                           ctypes.byref(a), ptr(color), ptr(radii), ctypes.byref(nr),
+                                           stream_of(dev)), "rasterize_gaussians")
+    if return_args:
+        return int(nr.value), color, radii, a, keep
     return int(nr.value), color, radii
 
 

@@ -295,6 +295,16 @@ int gsmpm_raster_destroy(gsmpm_raster* r);
  * upstream forward also syncs on num_rendered). */
 int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* a, float* out_color, int32_t* out_radii,
                          int32_t* num_rendered, void* stream);
+/* Replaces _C.rasterize_gaussians_backward (upstream's _RasterizeGaussians.backward,
+ * used by extra.py's loss.backward(), extra.py:198-200,218).  Uses the state of
+ * the last gsmpm_raster_forward on this context (same args; keep one context
+ * per differentiable forward).  dL_dcolor [3,H,W]; outputs, all [P,...] and
+ * fully written: dL_dmeans2D [P,3] (w.r.t. NDC, z = 0), dL_dcolors [P,3],
+ * dL_dopacity [P], dL_dmeans3D [P,3], dL_dcov3D [P,6], dL_dsh [P,M,3] (if
+ * shs), dL_dscales [P,3] and dL_drotations [P,4] (if scales/rotations). */
+int gsmpm_raster_backward(gsmpm_raster* r, const gsmpm_raster_args* a, const int32_t* radii, const float* dL_dcolor,
+                          float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D,
+                          float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations, void* stream);
 /* GaussianRasterizer.markVisible -> _C.mark_visible: visible[P] (u8) = view z > 0.2 */
 int gsmpm_raster_mark_visible(const float* means3D, int32_t P, const float* viewmatrix, const float* projmatrix,
                               uint8_t* visible, void* stream);
