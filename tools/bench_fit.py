@@ -4,8 +4,9 @@
 One step = one extra.py training iteration of the differentiable MPM
 (extra.py:205-241 without the renderer): 30 x p2g2p_forward(0.03/30, s),
 postprocess_forward, set_grads, postprocess_backward, 30 x p2g2p_backward,
-learn, cycle_init -- on n_grid 50 (extra.py:57), synthetic torus Gaussians
-(models_extra/torus is not in the reference), sticky ground.
+learn, cycle_init -- on n_grid 50 (extra.py:57), sticky ground, SURVEY §8(d)
+config E: 20,000 torus Gaussians (R = 0.3, r = 0.1; models_extra/torus is not
+in the reference, so the torus and its initial velocity are synthetic).
 
 Prints one JSON line like bench.py: value = particle-substeps/s counting the
 forward and backward substeps (2 x 30 per particle per iteration); a
@@ -32,7 +33,7 @@ GRAV = (0.0, -9.8, 0.0)
 def torus(n, seed=0):
     rng = np.random.default_rng(seed)
     th, ph = rng.uniform(0, 2 * np.pi, n), rng.uniform(0, 2 * np.pi, n)
-    r, R = 0.12 * np.sqrt(rng.uniform(0, 1, n)), 0.4
+    r, R = 0.1 * np.sqrt(rng.uniform(0, 1, n)), 0.3
     x = np.stack([1.0 + (R + r * np.cos(ph)) * np.cos(th), 0.85 + r * np.sin(ph),
                   1.0 + (R + r * np.cos(ph)) * np.sin(th)], 1).astype(np.float32)
     cov = np.tile(np.array([4e-6, 1e-6, 0, 4e-6, 5e-7, 4e-6], np.float32), (n, 1))
@@ -50,7 +51,7 @@ def volumes(x):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--particles", type=int, default=100_000)
+    ap.add_argument("--particles", type=int, default=20_000)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--cpu-particles", type=int, default=4000)
