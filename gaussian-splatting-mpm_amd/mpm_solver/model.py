@@ -150,8 +150,9 @@ class MPM_state_opt:
                                     grad=FieldView(owner, lambda: fit.get_grid("v_out_grad"), None, (ng, ng, ng, 3)))
 
     def set_grads(self, xyz_grad, cov_grad):
-        """model.py:192-202: x.grad[30] = xyz_grad, cov.grad = cov_grad."""
-        self._fit.set_grads(xyz_grad, cov_grad)
+        """model.py:192-202: x.grad[30] = xyz_grad, cov.grad = cov_grad (numpy, as
+        extra.py:226-228 passes them, or tensors)."""
+        self._fit.set_grads(torch.as_tensor(xyz_grad), torch.as_tensor(cov_grad))
 
     def cycle_init(self):
         """model.py:216-223: level 30 -> level 0 for x, v, F, stress, C."""
