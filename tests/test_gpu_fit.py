@@ -46,13 +46,25 @@ def _scene(n=4000, seed=0):
     return x, cov, v
 
 
-def _adjoint_close(a, b, what):
+def _adjoint_close(a, b, what, later_iteration=False):
+    """Per-element rule above.  later_iteration: the second training iteration
+    starts from a state in ground contact where a few particles sit on a
+    branch (m > 1e-15, |J| clamp) that summation order can flip;
+    tools/fit_probe3.py (12 GPU runs) measured there, GPU-vs-GPU exactly as
+    GPU-vs-oracle: 3.4 % of entries beyond 5e-3, 1.7 % beyond 2e-2, 0.4 %
+    beyond 5e-2, median 2e-6.  The rule then is: <= 1 % beyond 5e-2, median
+    < 1e-4, max 5e-2 of the largest entry."""
     a = np.asarray(a, np.float64).reshape(-1)
     b = np.asarray(b, np.float64).reshape(-1)
     r = np.abs(a - b) / (np.abs(b) + 1e-3 * np.abs(b).max() + 1e-30)
-    frac = float((r > 5e-3).mean())
     e = rel_err(a, b)
-    assert frac <= 1e-3 and e < 5e-2, (what, frac, e, float(np.median(r)))
+    med = float(np.median(r))
+    if later_iteration:
+        frac = float((r > 5e-2).mean())
+        assert frac <= 1e-2 and med < 1e-4 and e < 5e-2, (what, frac, e, med)
+        return
+    frac = float((r > 5e-3).mean())
+    assert frac <= 1e-3 and e < 5e-2, (what, frac, e, med)
 
 
 def _pair(dev, n=4000, seed=0):
@@ -186,14 +198,18 @@ def test_fit_dropin_extra_py_loop(dev):
         for s in reversed(range(NSUB)):
             sim.p2g2p_backward(DT, s)
             o.p2g2p_backward(DT, s)
-        _adjoint_close(sim.mpm_model.logE.grad.to_torch().cpu().numpy(), o.glogE, ("glogE", it))
-        _adjoint_close(sim.mpm_model.y.grad.to_torch().cpu().numpy(), o.gy, ("gy", it))
+        _adjoint_close(sim.mpm_model.logE.grad.to_torch().cpu().numpy(), o.glogE, ("glogE", it), it > 0)
+        _adjoint_close(sim.mpm_model.y.grad.to_torch().cpu().numpy(), o.gy, ("gy", it), it > 0)
         sim.learn()
         o.learn()
         sim.mpm_state.cycle_init()
         o.cycle_init()
+    # learn() clips each adjoint to +-1: a particle whose (ill-conditioned, see
+    # _adjoint_close) adjoint changes sign moves by 2 x 0.8; allow 1 % of them
+    logE = sim.mpm_model.logE.to_torch().cpu().numpy()
+    assert (np.abs(logE - o.logE) > 1e-4).mean() <= 1e-2
     E_opt = 10 ** sim.mpm_model.logE.to_torch().mean().item()
-    assert abs(np.log10(E_opt) - o.logE.astype(np.float64).mean()) < 1e-4
+    assert abs(np.log10(E_opt) - o.logE.astype(np.float64).mean()) < 1.6 * 1e-2
     with pytest.raises(TypeError):
         sim.postprocess()
 

@@ -54,6 +54,15 @@ for r in range(12):
         g.learn(); g.cycle_init()
     runs.append(per)
     del g
+def pct(a, b):
+    a = np.asarray(a, np.float64); b = np.asarray(b, np.float64)
+    r = np.abs(a - b) / (np.abs(b) + 1e-3 * np.abs(b).max() + 1e-30)
+    return [float((r > t).mean()) for t in (5e-3, 2e-2, 5e-2)], float(np.percentile(r, 99))
+for it in range(2):
+    fo = [pct(runs[r][it][0], ref[it][0]) for r in range(12)]
+    fg = [pct(runs[r][it][0], runs[0][it][0]) for r in range(1, 12)]
+    print(it, "frac>(5e-3,2e-2,5e-2) gpu-vs-oracle worst", [max(f[0][k] for f in fo) for k in range(3)], "p99", max(f[1] for f in fo),
+          "| gpu-vs-gpu worst", [max(f[0][k] for f in fg) for k in range(3)], "p99", max(f[1] for f in fg))
 for it in range(2):
     vo = [rel_err(runs[r][it][0], ref[it][0]) for r in range(12)]
     vg = [rel_err(runs[r][it][0], runs[0][it][0]) for r in range(1, 12)]
