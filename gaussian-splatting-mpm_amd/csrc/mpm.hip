@@ -595,7 +595,7 @@ __device__ __forceinline__ void load_x(const Particles& ps, int p, float (&x)[3]
 
 template <typename Fetch>
 __device__ __forceinline__ void g2p_particle(const Particles& ps, int p, const float (&x)[3], const GridDims& g,
-                                             float dt, Fetch fetch, float (&xn)[3]) {
+                                             float dt, Fetch fetch, float (&xn)[3], const float* Fpre = nullptr) {
   int base[3];
   float fx[3], w[3][3], dw[3][3];
   bspline(x, g.inv_dx, base, fx, w, dw);
@@ -664,7 +664,7 @@ __device__ __forceinline__ void g2p_particle(const Particles& ps, int p, const f
     }
   float F[3][3];
 #pragma unroll
-  for (int i = 0; i < 9; ++i) F[i / 3][i % 3] = ps.ld(PF + i, p);
+  for (int i = 0; i < 9; ++i) F[i / 3][i % 3] = Fpre ? Fpre[i] : ps.ld(PF + i, p);
 #pragma unroll
   for (int d = 0; d < 3; ++d) {
     ps.st(PV + d, p, nv[d]);
@@ -726,10 +726,12 @@ __global__ __launch_bounds__(256) void k_g2p(Particles ps, GridDims g, Tiles tl,
     // the particle's list entry and x are requested first so their round
     // trips overlap the window staging below
     int p = -1;
-    float x0[3] = {0.f, 0.f, 0.f};
+    float x0[3] = {0.f, 0.f, 0.f}, F0[9];
     if (k < cnt) {
       p = ck.list[first + k];
       load_x(ps, p, x0);
+#pragma unroll
+      for (int i = 0; i < 9; ++i) F0[i] = ps.ld(PF + i, p);  // F in flight with x (latency-bound phase)
     }
     {
       // all four loads in flight before the first LDS store (a guarded load
@@ -766,7 +768,7 @@ __global__ __launch_bounds__(256) void k_g2p(Particles ps, GridDims g, Tiles tl,
                      const float4* wb = s_win + ((base[0] - lo0) * kTW + (base[1] - lo1)) * kTW + (base[2] - lo2);
                      return wb[(i * kTW + j) * kTW + kk];
                    },
-                   xn);
+                   xn, F0);
       int tc[3];
       nt = tile_of(xn, g, tl, tc);
       if (nt < tl.ntiles) {
