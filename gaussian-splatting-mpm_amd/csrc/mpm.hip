@@ -495,7 +495,7 @@ __global__ __launch_bounds__(256) void k_halo_pack(GridDims g, Tiles tl, ChunkIn
   }
 }
 
-__global__ __launch_bounds__(256) void k_grid(GridDims g, Tiles tl, ChunkIn ck, const float4* __restrict__ slots,
+__global__ __launch_bounds__(512) void k_grid(GridDims g, Tiles tl, ChunkIn ck, const float4* __restrict__ slots,
                                               float4* __restrict__ gacc, float4* __restrict__ gvel,
                                               const BcTable* __restrict__ bct, GridStep gs,
                                               BinOut nb, Halo halo) {
@@ -511,7 +511,7 @@ __global__ __launch_bounds__(256) void k_grid(GridDims g, Tiles tl, ChunkIn ck, 
   // and KEEP_GRID wants the dense grid: then every tile is updated
   const bool all = outside || gs.keep;
   const int ntouch = all ? tl.ntiles : ck.nchunk[1];
-  // one touched tile (8^3 owned nodes) per workgroup iteration, two nodes per lane
+  // one touched tile (8^3 owned nodes) per workgroup iteration, one node per lane (512 lanes: one round of window loads)
   __shared__ int s_c0[8], s_nc[8];
   for (int wt = blockIdx.x; wt < ntouch; wt += gridDim.x) {
     const int T = all ? wt : ck.touched[wt];
@@ -1437,7 +1437,7 @@ static int substep_begin(gsmpm_mpm* h, float dt, uint32_t mask, int c, hipStream
 // Second half: grid update (reduced halo sums in the windows), G2P, binning of parity nx.
 static int substep_end(gsmpm_mpm* h, float dt, uint32_t mask, int c, hipStream_t st, const hipEvent_t* e8) {
   const int nx = c ^ 1;
-  launch(e8 ? e8 + 2 : nullptr, k_grid, dim3(grid_grid(h)), dim3(256), st, h->g, h->tl, chunk_in(h, c),
+  launch(e8 ? e8 + 2 : nullptr, k_grid, dim3(grid_grid(h)), dim3(512), st, h->g, h->tl, chunk_in(h, c),
          (const float4*)h->slots, h->gacc, h->gvel, (const BcTable*)h->dev_bc, grid_step(h, dt, mask), bin_out(h, nx),
          h->halo);
   GSMPM_LAUNCH_CHECK();
@@ -1997,7 +1997,7 @@ int gsmpm_mpm_time_kernels(gsmpm_mpm* h, float dt, uint32_t bc_active, int32_t r
   GSMPM_HIP(hipEventCreate(&e[0]));
   GSMPM_HIP(hipEventCreate(&e[1]));
   auto grid = [&]() {
-    launch(nullptr, k_grid, dim3(grid_grid(h)), dim3(256), st, h->g, h->tl, chunk_in(h, c), (const float4*)h->slots,
+    launch(nullptr, k_grid, dim3(grid_grid(h)), dim3(512), st, h->g, h->tl, chunk_in(h, c), (const float4*)h->slots,
            h->gacc, h->gvel, (const BcTable*)h->dev_bc, gs, bin_out(h, nx), h->halo);
   };
   auto g2p = [&]() {
