@@ -121,7 +121,9 @@ def algorithmic_bytes(n, n_grid, material):
     The three sum to B_sub exactly."""
     nodes = n_grid ** 3
     plastic = 8 * n if material in ("metal",) else 0
-    return {"k_p2g": 112 * n + 16 * nodes + plastic, "k_grid": 28 * nodes, "k_g2p": 96 * n + 12 * nodes}
+    return {"k_p2g": 112 * n + 16 * nodes + plastic, "k_grid": 28 * nodes, "k_g2p": 96 * n + 12 * nodes,
+            # fused pipeline: one launch does G2P of substep s and P2G of s + 1
+            "k_fused": 208 * n + 28 * nodes + plastic, "k_grid_f": 28 * nodes}
 
 
 def measured_traffic(kernel, workload):
@@ -282,13 +284,15 @@ def main():
         render_ms = (time.perf_counter() - r0) / 5 * 1e3
     kern = None
     if world == 1:
-        # nodes owned by the grid update: 8^3 per touched tile
-        live = sim.debug_stats()["touched_tiles"] * 512
+        fused = sim.pipeline == "fused"
+        # nodes owned by the grid update: 8x8x7 (fused) / 8^3 cells per touched tile
+        live = sim.debug_stats()["touched_tiles"] * (448 if fused else 512)
         # per-launch kernel time: hipEvents on the simulator's stream around 20
         # back-to-back launches of each kernel on the current frame's inputs
         kms = sim.time_kernels(dt, substep_masks(specs, state["t"], dt, 1)[0][0], reps=20)
-        kern = {k: kms[i] for i, k in enumerate(("k_p2g", "k_grid", "k_g2p", "binning"))}
-        abytes = algorithmic_bytes(n_local, sa.n_grid, sa.material)
+        names = ("k_fused", "k_grid_f", "binning") if fused else ("k_p2g", "k_grid", "k_g2p", "binning")
+        kern = {k: kms[i] for i, k in enumerate(names)}
+        abytes = {k: v for k, v in algorithmic_bytes(n_local, sa.n_grid, sa.material).items() if k in kern}
 
     out = {
         "metric": METRIC,
@@ -326,6 +330,7 @@ def main():
                                                                    "n_grid": sa.n_grid, "material": sa.material}),
                            "algorithmic_bytes_per_launch": abytes[dom],
                            "basis": "SURVEY.md 8(d) B_sub = 208 N + 56 n^3 split per kernel (dense grid)",
+                           "pipeline": sim.pipeline,
                            "live_nodes": live}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(scene, args, args.cpu_seconds)

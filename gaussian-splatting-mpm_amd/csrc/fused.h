@@ -1,0 +1,473 @@
+// fused.h -- the default substep pipeline of libgsmpm (included by mpm.hip
+// inside namespace gsmpm, after the per-phase kernels it shares helpers with).
+//
+// The reference runs every substep as stress -> p2g -> grid -> g2p
+// (mpm_solver/solver.py:27-52).  Here G2P of substep s and P2G of substep
+// s + 1 run in ONE kernel, `k_fused`, so a substep is two launches
+// (k_fused, k_grid_f) instead of four:
+//
+//   k_fused   one workgroup per <= 256-particle chunk of a tile: stage the
+//             tile's v_out window in LDS, gather (g2p, utils.py:218-282),
+//             then -- with x, v, C, F_trial still in registers -- impulse,
+//             return map + stress (utils.py:13-54) and the APIC scatter
+//             (p2g, utils.py:89-134) into the chunk's 64-bit fixed-point LDS
+//             window, stored to the chunk's slot
+//   k_grid_f  one workgroup per touched tile: sum the covering chunk windows
+//             (fixed order), normalise + gravity + BC list -> v_out
+//
+// Particles keep the chunk (tile) they were binned into for `rebin_interval`
+// substeps, so a chunk's window must hold the stencils of particles that
+// moved since the binning: the window is the tile plus a ONE-cell margin on
+// every side (base cell in [o - 1, o + T], nodes [o - 1, o + T + 3)).  With
+// tiles of 8 x 8 x 7 cells that is 12 x 12 x 11 = 1584 nodes, 50.7 KB of u64
+// accumulators -- three workgroups per CU.  A particle that moved further
+// gathers from the dense v_out and scatters with global float atomics into
+// the dense accumulator, and raises the escape flag that makes the next grid
+// update sweep every tile (correct for any motion, fast for CFL-bounded
+// motion; the lego scene moves < 0.06 cells per substep).
+//
+// Binning is done by the G2P half of k_fused every `rebin_interval` substeps
+// (counts + touched flags), `k_finish_bins` turns the counts into chunk
+// records, exactly as in the per-phase pipeline.
+
+constexpr int kFT0 = 8, kFT1 = 8, kFT2 = 7;                  // tile cells per axis
+constexpr int kFW0 = kFT0 + 4, kFW1 = kFT1 + 4, kFW2 = kFT2 + 4;  // window nodes per axis
+constexpr int kFWin = kFW0 * kFW1 * kFW2;                      // 1584
+constexpr int kFTN = kFT0 * kFT1 * kFT2;                       // owned nodes per tile (448)
+
+struct FTiles {
+  int td0, td1, td2;  // tiles per axis
+  int ntiles;         // td0 * td1 * td2 (the pseudo-tile "outside" is index ntiles)
+  int max_chunks;
+};
+
+struct BinOutF {
+  int* count;  // [ntiles + 1] (zeroed before a binning launch)
+  int* ptile;  // [n]
+  int* pslot;  // [n]
+  int* tflag;  // [ntiles] (zeroed with count)
+  FTiles tl;
+};
+
+__device__ __forceinline__ void ftile_decode(const FTiles& tl, int t, int& tx, int& ty, int& tz) {
+  tz = t % tl.td2;
+  ty = (t / tl.td2) % tl.td1;
+  tx = t / (tl.td1 * tl.td2);
+}
+
+// tile of a particle's base cell (utils.py:95 truncation), `ntiles` outside the grid
+__device__ __forceinline__ int ftile_of(const float (&x)[3], const GridDims& g, const FTiles& tl, int (&tc)[3]) {
+  bool ok = true;
+  int b[3];
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    const float gp = x[d] * g.inv_dx - 0.5f;
+    ok = ok && (gp >= 0.0f) && (gp < (float)g.ng);  // false for NaN
+    b[d] = ok ? (int)gp : 0;
+  }
+  tc[0] = b[0] / kFT0;
+  tc[1] = b[1] / kFT1;
+  tc[2] = b[2] / kFT2;
+  return ok ? (tc[0] * tl.td1 + tc[1]) * tl.td2 + tc[2] : tl.ntiles;
+}
+
+// The window of tile t (nodes [o - 1, o + T + 3) per axis) reaches into the
+// 27 tiles t + {-1, 0, 1}^3: the first reservation in t flags them for the
+// grid update (idempotent plain stores).
+__device__ __noinline__ void mark27(int* __restrict__ tflag, int t, int td0, int td1, int td2) {
+  const int tz = t % td2, ty = (t / td2) % td1, tx = t / (td1 * td2);
+  for (int a = -1; a <= 1; ++a)
+    for (int b = -1; b <= 1; ++b)
+      for (int c = -1; c <= 1; ++c) {
+        const int x = tx + a, y = ty + b, z = tz + c;
+        if ((unsigned)x < (unsigned)td0 && (unsigned)y < (unsigned)td1 && (unsigned)z < (unsigned)td2)
+          tflag[(x * td1 + y) * td2 + z] = 1;
+      }
+}
+__device__ __forceinline__ int reserve_f(const BinOutF& bo, int t, int c) {
+  const int old = atomicAdd(&bo.count[t], c);
+  if (old == 0 && t < bo.tl.ntiles) mark27(bo.tflag, t, bo.tl.td0, bo.tl.td1, bo.tl.td2);
+  return old;
+}
+
+// base cell of a particle as bspline() computes it
+__device__ __forceinline__ void base_of(const float (&x)[3], float inv_dx, int (&b)[3]) {
+#pragma unroll
+  for (int d = 0; d < 3; ++d) b[d] = (int)(x[d] * inv_dx - 0.5f);
+}
+// stencil inside the chunk window whose first node is o
+__device__ __forceinline__ bool in_window(const int (&b)[3], int o0, int o1, int o2) {
+  return (unsigned)(b[0] - o0) <= (unsigned)(kFW0 - 3) && (unsigned)(b[1] - o1) <= (unsigned)(kFW1 - 3) &&
+         (unsigned)(b[2] - o2) <= (unsigned)(kFW2 - 3);
+}
+// the per-phase pipeline's in-grid test (tile_of): base cell inside [0, ng)^3
+__device__ __forceinline__ bool in_grid(const float (&x)[3], const GridDims& g) {
+  bool ok = true;
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    const float gp = x[d] * g.inv_dx - 0.5f;
+    ok = ok && (gp >= 0.0f) && (gp < (float)g.ng);
+  }
+  return ok;
+}
+
+// MODE bit 1: G2P of the previous grid update; bit 2: P2G of this substep.
+// `bin` (uniform): re-bin the particles by their new x into `bo`.
+template <int MAT, int MODE>
+__global__ __launch_bounds__(256) void k_fused(Particles ps, GridDims g, FTiles tl, ChunkIn ck, BinOutF bo, int bin,
+                                               const float4* __restrict__ gvel, const BcTable* __restrict__ bct,
+                                               uint32_t mask, float dt, MatConsts mc, float4* __restrict__ slots,
+                                               float4* __restrict__ gacc, int* __restrict__ esc) {
+  constexpr bool G2P = (MODE & 1) != 0, P2G = (MODE & 2) != 0;
+  // channel-planar u64 accumulators; the G2P v window aliases them (it is
+  // consumed before the accumulators are zeroed)
+  __shared__ unsigned long long s_acc[4 * kFWin];
+  __shared__ float s_max[4];
+  __shared__ int s_cnt[27], s_base[27];
+  float4* s_win = reinterpret_cast<float4*>(s_acc);
+  const int ng = g.ng;
+  constexpr int SK = MODE == 3 ? 0 : 1;  // diagnostics slot (k_p2g's / k_g2p's in the per-phase pipeline)
+  stamp(SK, 0);
+  const int nch = ck.nchunk[0];
+  for (int w = blockIdx.x; w < nch; w += gridDim.x) {
+    const int4 cr = ck.chunk[w];
+    const int t = cr.x, first = cr.y, cnt = cr.z;
+    const int k = threadIdx.x;
+    const bool outside = t == tl.ntiles;  // workgroup-uniform
+    int tx = 0, ty = 0, tz = 0;
+    if (!outside) ftile_decode(tl, t, tx, ty, tz);
+    const int o0 = tx * kFT0 - 1, o1 = ty * kFT1 - 1, o2 = tz * kFT2 - 1;  // first window node
+    int p = -1;
+    float x[3] = {0.f, 0.f, 0.f}, v[3] = {0.f, 0.f, 0.f}, C[3][3], F[3][3], m = 0.f;
+    // particle loads first: their round trips overlap the window staging
+    if (k < cnt) {
+      p = ck.list[first + k];
+#pragma unroll
+      for (int d = 0; d < 3; ++d) x[d] = ps.ld(PX + d, p);
+      if (G2P || MAT != 0) {
+#pragma unroll
+        for (int i = 0; i < 9; ++i) F[i / 3][i % 3] = ps.ld(PF + i, p);
+      }
+      if (P2G) m = ps.ld(PMASS, p);
+      if (!G2P) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) v[d] = ps.ld(PV + d, p);
+#pragma unroll
+        for (int i = 0; i < 9; ++i) C[i / 3][i % 3] = ps.ld(PC + i, p);
+      }
+    }
+    if constexpr (G2P) {
+      if (!outside) {
+        float4 gv[7];
+#pragma unroll
+        for (int u = 0; u < 7; ++u) {
+          const int q = min(k + u * 256, kFWin - 1);
+          const int a = q / (kFW1 * kFW2), b = (q / kFW2) % kFW1, c = q % kFW2;
+          const int ix = o0 + a, iy = o1 + b, iz = o2 + c;
+          const bool in = (unsigned)ix < (unsigned)ng && (unsigned)iy < (unsigned)ng && (unsigned)iz < (unsigned)ng;
+          gv[u] = gvel[in ? ((size_t)ix * ng + iy) * ng + iz : 0];
+          if (!in) gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 7; ++u)
+          if (k + u * 256 < kFWin) s_win[k + u * 256] = gv[u];
+      }
+      if (k < 27) s_cnt[k] = 0;
+      __syncthreads();
+      if (w == (int)blockIdx.x) {
+        stamp(SK, 2);
+        if (threadIdx.x == 0 && blockIdx.x < 4096) {
+          g_stamps[SK][blockIdx.x][5] = cnt;
+          g_stamps[SK][blockIdx.x][6] = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));  // HW_ID
+          g_stamps[SK][blockIdx.x][7] = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (31 << 11));  // XCC_ID
+        }
+      }
+      int code = -1, lslot = 0, nt = -1;
+      if (k < cnt) {
+        int b[3];
+        base_of(x, g.inv_dx, b);
+        float gvd[3][3];
+        if (!outside && in_window(b, o0, o1, o2)) {
+          g2p_gather(x, g,
+                     [&](const int (&base)[3], int i, int j, int kk) {
+                       const float4* wb = s_win + ((base[0] - o0) * kFW1 + (base[1] - o1)) * kFW2 + (base[2] - o2);
+                       return wb[(i * kFW1 + j) * kFW2 + kk];
+                     },
+                     v, C, gvd);
+        } else {
+          g2p_gather(x, g,
+                     [&](const int (&base)[3], int i, int j, int kk) {
+                       const int ix = base[0] + i, iy = base[1] + j, iz = base[2] + kk;
+                       float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+                       if ((unsigned)ix < (unsigned)ng && (unsigned)iy < (unsigned)ng && (unsigned)iz < (unsigned)ng)
+                         r = gvel[((size_t)ix * ng + iy) * ng + iz];
+                       return r;
+                     },
+                     v, C, gvd);
+        }
+        float Fn[3][3];
+        f_trial(gvd, F, dt, Fn);
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+          ps.st(PV + d, p, v[d]);
+          x[d] = x[d] + dt * v[d];
+          ps.st(PX + d, p, x[d]);
+        }
+#pragma unroll
+        for (int i = 0; i < 9; ++i) {
+          ps.st(PC + i, p, C[i / 3][i % 3]);
+          F[i / 3][i % 3] = Fn[i / 3][i % 3];
+        }
+        // F_trial is stored here unless the return map below replaces it
+        if (!P2G || MAT == 0 || MAT == 4) {
+#pragma unroll
+          for (int i = 0; i < 9; ++i) ps.st(PF + i, p, F[i / 3][i % 3]);
+        }
+        if (bin) {
+          int tc[3];
+          nt = ftile_of(x, g, tl, tc);
+          if (!outside && nt < tl.ntiles) {
+            const int d0 = tc[0] - tx, d1 = tc[1] - ty, d2 = tc[2] - tz;
+            if (abs(d0) <= 1 && abs(d1) <= 1 && abs(d2) <= 1) {
+              code = (d0 + 1) * 9 + (d1 + 1) * 3 + (d2 + 1);
+              lslot = atomicAdd(&s_cnt[code], 1);
+            }
+          }
+        }
+      }
+      if (bin) {
+        __syncthreads();
+        if (k < 27) {
+          const int c = s_cnt[k];
+          if (c > 0) {
+            const int ntile = ((tx + k / 9 - 1) * tl.td1 + (ty + (k / 3) % 3 - 1)) * tl.td2 + (tz + k % 3 - 1);
+            s_base[k] = reserve_f(bo, ntile, c);
+          }
+        }
+        __syncthreads();
+        if (p >= 0) {
+          bo.ptile[p] = nt;
+          bo.pslot[p] = code >= 0 ? s_base[code] + lslot : reserve_f(bo, nt, 1);
+        }
+      }
+      __syncthreads();  // the window is consumed (and s_cnt / s_base read) before LDS is reused
+      if (w == (int)blockIdx.x) stamp(SK, 3);
+    }
+    if constexpr (P2G) {
+      if (!outside)
+        for (int q = k; q < kFWin * 4; q += 256) s_acc[q] = 0ull;
+      float nvt[3][3];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) nvt[i / 3][i % 3] = 0.f;
+      float bound = 0.f;
+      if (k < cnt) {
+        // ImpulseBC.apply (boundary_conditions.py:41-45); the kicked v lives in registers only
+        if (mask) {
+          const int ni = bct->n_imp;
+          for (int b = 0; b < ni; ++b) {
+            const Impulse& im = bct->imp[b];
+            if (!((mask >> im.bit) & 1u)) continue;
+            const bool in = fabsf(x[0] - im.c[0]) < im.s[0] && fabsf(x[1] - im.c[1]) < im.s[1] &&
+                            fabsf(x[2] - im.c[2]) < im.s[2];
+            if (in) {
+#pragma unroll
+              for (int d = 0; d < 3; ++d) v[d] = v[d] + im.f[d] / m * im.sdt;
+            }
+          }
+        }
+        // compute_stress_from_F_trial (utils.py:13-54)
+        if constexpr (MAT != 0) {
+          float tau[3][3];
+          float yld = ps.ld(PYLD, p);
+          const float mu = ps.ld(PMU, p), lam = ps.ld(PLAM, p);
+          return_map_and_stress<MAT>(F, mu, lam, yld, dt, mc, tau);
+          if constexpr (MAT == 1 || MAT == 2 || MAT == 3) {
+#pragma unroll
+            for (int i = 0; i < 9; ++i) ps.st(PF + i, p, F[i / 3][i % 3]);
+          }
+          if constexpr (MAT == 1) ps.st(PYLD, p, yld);
+          const float nvol = -ps.ld(PVOL, p);
+#pragma unroll
+          for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) nvt[i][j] = nvol * tau[i][j];
+        }
+        float vm = 0.f, cm = 0.f, sm = 0.f;
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+          vm = fmaxf(vm, fabsf(v[r]));
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            cm = fmaxf(cm, fabsf(C[r][c]));
+            sm = fmaxf(sm, fabsf(nvt[r][c]));
+          }
+        }
+        bound = fmaxf(m, m * (vm + 4.5f * g.dx * cm) + dt * 4.5f * g.inv_dx * sm) * 1.01f;
+      }
+      if (outside) {
+        // chunk of particles binned outside the grid: bounds-checked global path
+        if (k < cnt) p2g_global<MAT>(x, v, C, m, nvt, g, dt, gacc);
+        if (k == 0 && cnt > 0) *esc = 1;
+        __syncthreads();
+        continue;  // workgroup-uniform
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) bound = fmaxf(bound, __shfl_xor(bound, o));
+      if ((k & 63) == 0) s_max[k >> 6] = bound;
+      __syncthreads();  // also orders the zeroing before the adds
+      const float bmax = fmaxf(fmaxf(s_max[0], s_max[1]), fmaxf(s_max[2], s_max[3]));
+      int ebits;
+      frexpf(bmax, &ebits);
+      const int S = bmax > 0.f ? 50 - ebits : 0;  // see k_p2g
+      if (k < cnt) {
+        int b[3];
+        base_of(x, g.inv_dx, b);
+        if (in_grid(x, g) && in_window(b, o0, o1, o2)) {
+          int bb[3];
+          float fx[3], ww[3][3], dw[3][3];
+          bspline(x, g.inv_dx, bb, fx, ww, dw);
+          p2g_scatter<MAT, kFW1, kFW2, kFWin>(s_acc + ((b[0] - o0) * kFW1 + (b[1] - o1)) * kFW2 + (b[2] - o2), fx, ww,
+                                              dw, v, C, m, nvt, g, dt, ldexp(1.0, S));
+        } else {
+          p2g_global<MAT>(x, v, C, m, nvt, g, dt, gacc);
+          *esc = 1;
+        }
+      }
+      __syncthreads();
+      if (w == (int)blockIdx.x) stamp(SK, 4);
+      float* dst = reinterpret_cast<float*>(slots + (size_t)w * kFWin);
+      for (int q = k; q < kFWin * 4; q += 256)
+        dst[q] = (float)ldexp((double)(long long)s_acc[(q & 3) * kFWin + (q >> 2)], -S);
+      __syncthreads();  // LDS reuse by the next chunk
+    }
+  }
+  stamp(SK, 1);
+}
+
+// Chunk ranges of the 27 tiles whose windows reach tile (ti, tj, tk) -> LDS
+// (lanes 0..26; caller syncs).
+__device__ __forceinline__ void load_cover27(const ChunkIn& ck, const FTiles& tl, int ti, int tj, int tk, int* s_c0,
+                                             int* s_nc) {
+  const int e = threadIdx.x;
+  if (e < 27) {
+    const int x = ti + e / 9 - 1, y = tj + (e / 3) % 3 - 1, z = tk + e % 3 - 1;
+    int c0 = 0, nc = 0;
+    if ((unsigned)x < (unsigned)tl.td0 && (unsigned)y < (unsigned)tl.td1 && (unsigned)z < (unsigned)tl.td2) {
+      const int t = (x * tl.td1 + y) * tl.td2 + z;
+      nc = (ck.count[t] + kChunk - 1) / kChunk;
+      c0 = ck.cbase[t];
+    }
+    s_c0[e] = c0;
+    s_nc[e] = nc;
+  }
+}
+
+// Sum of the chunk windows covering owned node (l0, l1, l2) of a tile.  Per
+// axis a node lies in its own tile's window and, when l < 3, in the lower
+// neighbour's (l + T + 1 < T + 4), when l = T - 1 in the upper one's: <= 8
+// windows, read as 8 unconditional loads (absent ones from the zero slot).
+__device__ __forceinline__ float4 node_sum_f(const float4* __restrict__ slots, int max_chunks, const int* s_c0,
+                                             const int* s_nc, int l0, int l1, int l2) {
+  const int sec0 = l0 < 3 ? -1 : (l0 == kFT0 - 1 ? 1 : 0);
+  const int sec1 = l1 < 3 ? -1 : (l1 == kFT1 - 1 ? 1 : 0);
+  const int sec2 = l2 < 3 ? -1 : (l2 == kFT2 - 1 ? 1 : 0);
+  float4 s8[8];
+  int extra = 0;
+  int loc8[8], ci8[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int ax = e >> 2, ay = (e >> 1) & 1, az = e & 1;
+    const int a = ax ? sec0 : 0, b = ay ? sec1 : 0, c = az ? sec2 : 0;
+    bool on = (!ax || sec0) && (!ay || sec1) && (!az || sec2);
+    const int ci = (a + 1) * 9 + (b + 1) * 3 + (c + 1);
+    const int nc = s_nc[ci];
+    on = on && nc > 0;
+    const int loc = ((l0 - a * kFT0 + 1) * kFW1 + (l1 - b * kFT1 + 1)) * kFW2 + (l2 - c * kFT2 + 1);
+    loc8[e] = loc;
+    ci8[e] = ci;
+    const size_t off = on ? (size_t)s_c0[ci] * kFWin + loc : (size_t)max_chunks * kFWin;
+    s8[e] = slots[off];
+    extra |= (on && nc > 1) ? (1 << e) : 0;
+  }
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    acc.x += s8[e].x;
+    acc.y += s8[e].y;
+    acc.z += s8[e].z;
+    acc.w += s8[e].w;
+  }
+  while (extra) {
+    const int e = __builtin_ctz(extra);
+    extra &= extra - 1;
+    const int ci = ci8[e], loc = loc8[e];
+    for (int w = s_c0[ci] + 1; w < s_c0[ci] + s_nc[ci]; ++w) {
+      const float4 sv = slots[(size_t)w * kFWin + loc];
+      acc.x += sv.x;
+      acc.y += sv.y;
+      acc.z += sv.z;
+      acc.w += sv.w;
+    }
+  }
+  return acc;
+}
+
+// Grid update of the fused pipeline.  esc_in: some particle scattered through
+// gacc in the P2G this update consumes -> every tile, plus gacc (re-zeroed).
+// esc_clear: the flag the next P2G raises.  zc / zf (optional): the counts /
+// touched flags the next binning launch accumulates into.
+__global__ __launch_bounds__(512) void k_grid_f(GridDims g, FTiles tl, ChunkIn ck, const float4* __restrict__ slots,
+                                                float4* __restrict__ gacc, float4* __restrict__ gvel,
+                                                const BcTable* __restrict__ bct, GridStep gs,
+                                                const int* __restrict__ esc_in, int* __restrict__ esc_clear,
+                                                int* __restrict__ zc, int* __restrict__ zf) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *esc_clear = 0;
+  if (zc) {
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t <= tl.ntiles; t += gridDim.x * blockDim.x) {
+      zc[t] = 0;
+      if (t < tl.ntiles) zf[t] = 0;
+    }
+  }
+  const int ng = g.ng;
+  const bool all = *esc_in != 0;
+  const int ntouch = all ? tl.ntiles : ck.nchunk[1];
+  __shared__ int s_c0[27], s_nc[27];
+  for (int wt = blockIdx.x; wt < ntouch; wt += gridDim.x) {
+    const int T = all ? wt : ck.touched[wt];
+    int ti, tj, tk;
+    ftile_decode(tl, T, ti, tj, tk);
+    __syncthreads();  // readers of the previous tile's ranges are done
+    load_cover27(ck, tl, ti, tj, tk, s_c0, s_nc);
+    __syncthreads();
+    for (int q = threadIdx.x; q < kFTN; q += blockDim.x) {
+      const int l0 = q / (kFT1 * kFT2), l1 = (q / kFT2) % kFT1, l2 = q % kFT2;
+      const int i = ti * kFT0 + l0, j = tj * kFT1 + l1, k = tk * kFT2 + l2;
+      if (i >= ng || j >= ng || k >= ng) continue;
+      const size_t idx = ((size_t)i * ng + j) * ng + k;
+      float4 a = node_sum_f(slots, tl.max_chunks, s_c0, s_nc, l0, l1, l2);
+      if (all) {
+        const float4 o = gacc[idx];
+        a.x += o.x;
+        a.y += o.y;
+        a.z += o.z;
+        a.w += o.w;
+        gacc[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      gvel[idx] = node_update(a, i, j, k, g, gs, bct);
+    }
+  }
+}
+
+// bin every particle by its current x (set_particles / resort / set x)
+__global__ __launch_bounds__(256) void k_bin_all_f(Particles ps, GridDims g, BinOutF bo) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < ps.n) {
+    float x[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) x[d] = ps.ld(PX + d, p);
+    int tc[3];
+    const int t = ftile_of(x, g, bo.tl, tc);
+    bo.ptile[p] = t;
+    bo.pslot[p] = reserve_f(bo, t, 1);
+  }
+}

@@ -198,6 +198,37 @@ __device__ __forceinline__ void p2g_term(int i, int j, int k, const float (&fx)[
   acc.w += wm;
 }
 
+// Bounds-checked scatter of one particle into the dense accumulator with f32
+// global atomics: the path of particles outside the grid (the reference's
+// out-of-range writes are undefined; here they are dropped) and of
+// particles that left their chunk's window.
+template <int MAT>
+__device__ __forceinline__ void p2g_global(const float (&x)[3], const float (&v)[3], const float (&C)[3][3], float m,
+                                           const float (&nvt)[3][3], const GridDims& g, float dt,
+                                           float4* __restrict__ gacc) {
+  const int ng = g.ng;
+  int base[3];
+  float fx[3], ww[3][3], dw[3][3];
+  bspline(x, g.inv_dx, base, fx, ww, dw);
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 3; ++kk) {
+        const int ix = base[0] + i, iy = base[1] + j, iz = base[2] + kk;
+        if ((unsigned)ix < (unsigned)ng && (unsigned)iy < (unsigned)ng && (unsigned)iz < (unsigned)ng) {
+          float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+          p2g_term<MAT>(i, j, kk, fx, v, C, m, nvt, g, dt, a);
+          float* cell = reinterpret_cast<float*>(gacc + (((size_t)ix * ng + iy) * ng + iz));
+          unsafeAtomicAdd(cell + 0, a.x);
+          unsafeAtomicAdd(cell + 1, a.y);
+          unsafeAtomicAdd(cell + 2, a.z);
+          unsafeAtomicAdd(cell + 3, a.w);
+        }
+      }
+}
+
 // ------------------------------------------------------------------- P2G --
 // One workgroup per <= 256-particle chunk of one tile, one particle per lane.
 // Contributions are accumulated into the tile's 10^3-node window in LDS as
@@ -228,7 +259,7 @@ __device__ __forceinline__ void lds_add(unsigned long long* a, unsigned long lon
 // per-axis weights, collapses to two FMAs per component per node.  Same
 // quantities as the reference's per-node expression, different rounding (a
 // few ulp).
-template <int MAT>
+template <int MAT, int WY = kTW, int WZ = kTW, int WN = kWin>
 __device__ __forceinline__ void p2g_scatter(unsigned long long* cell0, const float (&fx)[3], const float (&w)[3][3],
                                             const float (&dw)[3][3], const float (&v)[3], const float (&C)[3][3],
                                             float m, const float (&nvt)[3][3], const GridDims& g, float dt,
@@ -275,11 +306,11 @@ __device__ __forceinline__ void p2g_scatter(unsigned long long* cell0, const flo
           add[r] = wm * q;
           if constexpr (MAT != 0) add[r] = __builtin_fmaf(sa[r], w[2][k], __builtin_fmaf(sc[r], dw[2][k], add[r]));
         }
-        unsigned long long* cell = cell0 + (i * kTW + j) * kTW + k;
-        lds_add(cell + 0 * kWin, to_fixed(add[0], scale));
-        lds_add(cell + 1 * kWin, to_fixed(add[1], scale));
-        lds_add(cell + 2 * kWin, to_fixed(add[2], scale));
-        lds_add(cell + 3 * kWin, to_fixed(wm, scale));
+        unsigned long long* cell = cell0 + (i * WY + j) * WZ + k;
+        lds_add(cell + 0 * WN, to_fixed(add[0], scale));
+        lds_add(cell + 1 * WN, to_fixed(add[1], scale));
+        lds_add(cell + 2 * WN, to_fixed(add[2], scale));
+        lds_add(cell + 3 * WN, to_fixed(wm, scale));
       }
     }
   }
@@ -307,26 +338,7 @@ __global__ __launch_bounds__(256) void k_p2g(Particles ps, GridDims g, Tiles tl,
         const int p = ck.list[first + k];
         float x[3], v[3], C[3][3], m, nvt[3][3];
         particle_front<MAT>(ps, p, bct, mask, dt, mc, x, v, C, m, nvt);
-        int base[3];
-        float fx[3], ww[3][3], dw[3][3];
-        bspline(x, g.inv_dx, base, fx, ww, dw);
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-#pragma unroll
-          for (int j = 0; j < 3; ++j)
-#pragma unroll
-            for (int kk = 0; kk < 3; ++kk) {
-              const int ix = base[0] + i, iy = base[1] + j, iz = base[2] + kk;
-              if ((unsigned)ix < (unsigned)ng && (unsigned)iy < (unsigned)ng && (unsigned)iz < (unsigned)ng) {
-                float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-                p2g_term<MAT>(i, j, kk, fx, v, C, m, nvt, g, dt, a);
-                float* cell = reinterpret_cast<float*>(gacc + (((size_t)ix * ng + iy) * ng + iz));
-                unsafeAtomicAdd(cell + 0, a.x);
-                unsafeAtomicAdd(cell + 1, a.y);
-                unsafeAtomicAdd(cell + 2, a.z);
-                unsafeAtomicAdd(cell + 3, a.w);
-              }
-            }
+        p2g_global<MAT>(x, v, C, m, nvt, g, dt, gacc);
       }
       continue;  // workgroup-uniform
     }
@@ -395,6 +407,50 @@ struct GridStep {
   uint32_t mask;
   int keep;
 };
+
+// grid_normalization_and_gravity (utils.py:177-183) and the grid_postprocess
+// list (solver.py:41-46) of one node: BasicBC.apply (boundary_conditions.py:
+// 23-27) / MPM_Collider.collide (collider.py:13-44), pointwise, in list order.
+__device__ __forceinline__ float4 node_update(const float4& a, int i, int j, int k, const GridDims& g,
+                                              const GridStep& gs, const BcTable* __restrict__ bct) {
+  float v[3] = {0.f, 0.f, 0.f};
+  if (a.w > 1e-15f) {
+    v[0] = a.x / a.w + gs.dt * gs.gx;
+    v[1] = a.y / a.w + gs.dt * gs.gy;
+    v[2] = a.z / a.w + gs.dt * gs.gz;
+    const int nops = bct->n_ops;
+    for (int o = 0; o < nops; ++o) {
+      const GridOp& op = bct->op[o];
+      const float p0 = (float)i * g.dx, p1 = (float)j * g.dx, p2 = (float)k * g.dx;
+      if (op.kind == 0) {
+        if (!((gs.mask >> op.bit) & 1u)) continue;
+        if (fabsf(p0 - op.a[0]) < op.b[0] && fabsf(p1 - op.a[1]) < op.b[1] && fabsf(p2 - op.a[2]) < op.b[2]) {
+          v[0] = 0.f;
+          v[1] = 0.f;
+          v[2] = 0.f;
+        }
+      } else {
+        const float o0 = p0 - op.a[0], o1 = p1 - op.a[1], o2 = p2 - op.a[2];
+        const float dot = o0 * op.b[0] + o1 * op.b[1] + o2 * op.b[2];
+        if (dot < 0.0f) {
+          const float nc = v[0] * op.b[0] + v[1] * op.b[1] + v[2] * op.b[2];
+          const float mn = fminf(nc, 0.0f);
+#pragma unroll
+          for (int d = 0; d < 3; ++d) v[d] = v[d] - mn * op.b[d];
+          const float len = sqrtf(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+          if (nc < 0.0f && len > 1e-20f) {
+            const float sc = fmaxf(0.0f, len + nc * op.friction);
+#pragma unroll
+            for (int d = 0; d < 3; ++d) v[d] = sc * (v[d] / len);
+          }
+#pragma unroll
+          for (int d = 0; d < 3; ++d) v[d] = v[d] * 0.99f;
+        }
+      }
+    }
+  }
+  return make_float4(v[0], v[1], v[2], 0.f);
+}
 
 // Chunk ranges of the <= 8 tiles whose 10^3 windows cover the owned nodes of
 // tile (ti, tj, tk) -> LDS (lanes 0..7; caller syncs).
@@ -542,43 +598,7 @@ __global__ __launch_bounds__(512) void k_grid(GridDims g, Tiles tl, ChunkIn ck, 
           gacc[idx] = gs.keep ? a : make_float4(0.f, 0.f, 0.f, 0.f);
         }
       }
-      float v[3] = {0.f, 0.f, 0.f};
-      if (a.w > 1e-15f) {
-        v[0] = a.x / a.w + gs.dt * gs.gx;
-        v[1] = a.y / a.w + gs.dt * gs.gy;
-        v[2] = a.z / a.w + gs.dt * gs.gz;
-        const int nops = bct->n_ops;
-        for (int o = 0; o < nops; ++o) {
-          const GridOp& op = bct->op[o];
-          const float p0 = (float)i * g.dx, p1 = (float)j * g.dx, p2 = (float)k * g.dx;
-          if (op.kind == 0) {
-            if (!((gs.mask >> op.bit) & 1u)) continue;
-            if (fabsf(p0 - op.a[0]) < op.b[0] && fabsf(p1 - op.a[1]) < op.b[1] && fabsf(p2 - op.a[2]) < op.b[2]) {
-              v[0] = 0.f;
-              v[1] = 0.f;
-              v[2] = 0.f;
-            }
-          } else {
-            const float o0 = p0 - op.a[0], o1 = p1 - op.a[1], o2 = p2 - op.a[2];
-            const float dot = o0 * op.b[0] + o1 * op.b[1] + o2 * op.b[2];
-            if (dot < 0.0f) {
-              const float nc = v[0] * op.b[0] + v[1] * op.b[1] + v[2] * op.b[2];
-              const float mn = fminf(nc, 0.0f);
-#pragma unroll
-              for (int d = 0; d < 3; ++d) v[d] = v[d] - mn * op.b[d];
-              const float len = sqrtf(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
-              if (nc < 0.0f && len > 1e-20f) {
-                const float sc = fmaxf(0.0f, len + nc * op.friction);
-#pragma unroll
-                for (int d = 0; d < 3; ++d) v[d] = sc * (v[d] / len);
-              }
-#pragma unroll
-              for (int d = 0; d < 3; ++d) v[d] = v[d] * 0.99f;
-            }
-          }
-        }
-      }
-      gvel[idx] = make_float4(v[0], v[1], v[2], 0.f);
+      gvel[idx] = node_update(a, i, j, k, g, gs, bct);
     }
   }
 }
@@ -594,8 +614,8 @@ __device__ __forceinline__ void load_x(const Particles& ps, int p, float (&x)[3]
 }
 
 template <typename Fetch>
-__device__ __forceinline__ void g2p_particle(const Particles& ps, int p, const float (&x)[3], const GridDims& g,
-                                             float dt, Fetch fetch, float (&xn)[3], const float* Fpre = nullptr) {
+__device__ __forceinline__ void g2p_gather(const float (&x)[3], const GridDims& g, Fetch fetch, float (&nv)[3],
+                                           float (&nC)[3][3], float (&nF)[3][3]) {
   int base[3];
   float fx[3], w[3][3], dw[3][3];
   bspline(x, g.inv_dx, base, fx, w, dw);
@@ -606,14 +626,16 @@ __device__ __forceinline__ void g2p_particle(const Particles& ps, int p, const f
   // -- the same quantities, accumulated in a different order (a few ulp).
   // The i loop stays rolled (weights picked by select) so only one slab of
   // gathers is live.
-  float nv[3] = {0.f, 0.f, 0.f}, M[3][3], nF[3][3];
+  float M[3][3];
 #pragma unroll
-  for (int r = 0; r < 3; ++r)
+  for (int r = 0; r < 3; ++r) {
+    nv[r] = 0.f;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       M[r][c] = 0.f;
       nF[r][c] = 0.f;
     }
+  }
   float dk[3], ej[3];
 #pragma unroll
   for (int o = 0; o < 3; ++o) {
@@ -653,7 +675,6 @@ __device__ __forceinline__ void g2p_particle(const Particles& ps, int p, const f
       }
     }
   }
-  float nC[3][3];
   const float c4 = 4.0f * g.inv_dx;
 #pragma unroll
   for (int r = 0; r < 3; ++r)
@@ -662,6 +683,26 @@ __device__ __forceinline__ void g2p_particle(const Particles& ps, int p, const f
       nC[r][c] = M[r][c] * c4;
       nF[r][c] = nF[r][c] * g.inv_dx;
     }
+}
+
+// F_trial = (I + dt grad v) F (utils.py:275-282), the reference's operation order
+__device__ __forceinline__ void f_trial(const float (&gv)[3][3], const float (&F)[3][3], float dt, float (&Fn)[3][3]) {
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const float a0 = (r == 0 ? 1.0f : 0.0f) + gv[r][0] * dt;
+      const float a1 = (r == 1 ? 1.0f : 0.0f) + gv[r][1] * dt;
+      const float a2 = (r == 2 ? 1.0f : 0.0f) + gv[r][2] * dt;
+      Fn[r][c] = a0 * F[0][c] + a1 * F[1][c] + a2 * F[2][c];
+    }
+}
+
+template <typename Fetch>
+__device__ __forceinline__ void g2p_particle(const Particles& ps, int p, const float (&x)[3], const GridDims& g,
+                                             float dt, Fetch fetch, float (&xn)[3], const float* Fpre = nullptr) {
+  float nv[3], nC[3][3], nF[3][3];
+  g2p_gather(x, g, fetch, nv, nC, nF);
   float F[3][3];
 #pragma unroll
   for (int i = 0; i < 9; ++i) F[i / 3][i % 3] = Fpre ? Fpre[i] : ps.ld(PF + i, p);
@@ -673,15 +714,10 @@ __device__ __forceinline__ void g2p_particle(const Particles& ps, int p, const f
   }
 #pragma unroll
   for (int i = 0; i < 9; ++i) ps.st(PC + i, p, nC[i / 3][i % 3]);
+  float Fn[3][3];
+  f_trial(nF, F, dt, Fn);
 #pragma unroll
-  for (int r = 0; r < 3; ++r)
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const float a0 = (r == 0 ? 1.0f : 0.0f) + nF[r][0] * dt;
-      const float a1 = (r == 1 ? 1.0f : 0.0f) + nF[r][1] * dt;
-      const float a2 = (r == 2 ? 1.0f : 0.0f) + nF[r][2] * dt;
-      ps.st(PF + r * 3 + c, p, a0 * F[0][c] + a1 * F[1][c] + a2 * F[2][c]);
-    }
+  for (int i = 0; i < 9; ++i) ps.st(PF + i, p, Fn[i / 3][i % 3]);
 }
 
 // One workgroup per chunk: stage the tile's 10^3 window of v_out in LDS,
@@ -1043,6 +1079,8 @@ __global__ __launch_bounds__(256) void k_scatter(int n, const int* __restrict__ 
 }
 
 
+#include "fused.h"
+
 // ------------------------------------------------------------ postprocess --
 // compute_cov_from_F (utils.py:401-433) + compute_R_from_F (utils.py:376-398)
 __global__ __launch_bounds__(256) void k_postprocess(Particles ps) {
@@ -1324,8 +1362,25 @@ struct gsmpm_mpm {
   int* sort_idx = nullptr;        // [2][np]
   void* sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
+  // fused G2P2G pipeline (fused.h): its own tiling, chunk lists and slots
+  bool fused = true;                      // chosen at create (GSMPM_FLAG_PHASED / KEEP_GRID select the per-phase one)
+  FTiles ftl{};
+  float4* fslots = nullptr;               // [max_chunks + 1][kFWin]
+  int* fcount[2] = {nullptr, nullptr};
+  int* fcstart[2] = {nullptr, nullptr};
+  int* fcbase[2] = {nullptr, nullptr};
+  int4* fchunk[2] = {nullptr, nullptr};
+  int* fnchunk[2] = {nullptr, nullptr};
+  int* ftouched[2] = {nullptr, nullptr};
+  int* ftflag[2] = {nullptr, nullptr};
+  int* flist[2] = {nullptr, nullptr};
+  int* fesc = nullptr;                    // [2] escape flags (alternating per grid update)
+  int fbpar = 0;                          // parity of the bins the next k_fused reads
+  int fep = 0;                            // escape flag the next P2G raises
+  int rebin_interval = 10;                // substeps between re-binnings (fused pipeline)
   std::map<std::vector<uint32_t>, hipGraphExec_t> graphs;
   std::map<std::vector<uint32_t>, int> graph_box_parity;
+  std::map<std::vector<uint32_t>, std::pair<int, int>> graph_fstate;  // (fbpar, fep) after the graph
 };
 
 namespace gsmpm {
@@ -1344,6 +1399,19 @@ static ChunkOut chunk_out(gsmpm_mpm* h, int c) {
 static BinOut bin_out(gsmpm_mpm* h, int c) {
   return BinOut{h->count[c], h->ptile, h->pslot, h->tflag[c], h->tl.td, h->tl.ntiles};
 }
+
+static bool use_fused(const gsmpm_mpm* h) { return h->fused && h->halo.n == 0; }
+
+static ChunkIn chunk_in_f(gsmpm_mpm* h, int c) {
+  return ChunkIn{h->fcount[c], h->fcbase[c], h->fchunk[c], h->fnchunk[c], h->flist[c], h->ftouched[c]};
+}
+static ChunkOut chunk_out_f(gsmpm_mpm* h, int c) {
+  return ChunkOut{h->fcstart[c], h->fcbase[c], h->fchunk[c], h->fnchunk[c], h->ftflag[c], h->ftouched[c],
+                  h->escape, 0, INT_MAX};
+}
+static BinOutF bin_out_f(gsmpm_mpm* h, int c) { return BinOutF{h->fcount[c], h->ptile, h->pslot, h->ftflag[c], h->ftl}; }
+// k_finish_bins / the scan kernels only use ntiles and max_chunks of a Tiles
+static Tiles ftiles_flat(const gsmpm_mpm* h) { return Tiles{h->ftl.td0, h->ftl.ntiles, h->ftl.max_chunks}; }
 
 static int p2g_grid(gsmpm_mpm* h) { return std::min(h->tl.max_chunks, 1024); }
 static int g2p_grid(gsmpm_mpm* h) { return std::min(h->tl.max_chunks, 1024); }
@@ -1366,28 +1434,45 @@ static void launch_p2g(gsmpm_mpm* h, int c, uint32_t mask, float dt, hipStream_t
          (const BcTable*)h->dev_bc, mask, dt, h->mc, h->slots, h->gacc);
 }
 
-// counts of parity c -> list offsets + chunk list, then the per-tile lists
-static int finish_binning(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t* ev = nullptr) {
+// counts -> list offsets + chunk list, then the per-tile lists
+static int finish_bins_on(gsmpm_mpm* h, const Tiles& tl, const int* count, const ChunkOut& co, int* list,
+                          hipStream_t st, const hipEvent_t* ev) {
   // fused path: tile table fits LDS, first-chunk indices fit 16 bits (s_aux)
-  if (h->tl.ntiles + 1 <= kFuseTiles && h->tl.max_chunks < 65536) {
-    launch(ev, k_finish_bins, dim3(div_up(h->n, 256)), dim3(256), st, h->tl, (const int*)h->count[c], chunk_out(h, c),
-           h->n, (const int*)h->ptile, (const int*)h->pslot, h->list[c]);
+  if (tl.ntiles + 1 <= kFuseTiles && tl.max_chunks < 65536) {
+    launch(ev, k_finish_bins, dim3(div_up(h->n, 256)), dim3(256), st, tl, count, co, h->n, (const int*)h->ptile,
+           (const int*)h->pslot, list);
   } else {
     const hipEvent_t e0[2] = {ev ? ev[0] : nullptr, nullptr}, e1[2] = {nullptr, ev ? ev[1] : nullptr};
-    const int nblk = div_up(h->tl.ntiles + 1, 1024);
-    launch(ev ? e0 : nullptr, k_scan_partials, dim3(nblk), dim3(1024), st, h->tl, (const int*)h->count[c],
-           (const int*)h->tflag[c], h->scan_part);
-    launch(nullptr, k_scan_tiles, dim3(nblk), dim3(1024), st, h->tl, (const int*)h->count[c], chunk_out(h, c),
-           (const int4*)h->scan_part);
+    const int nblk = div_up(tl.ntiles + 1, 1024);
+    launch(ev ? e0 : nullptr, k_scan_partials, dim3(nblk), dim3(1024), st, tl, count, (const int*)co.tflag,
+           h->scan_part);
+    launch(nullptr, k_scan_tiles, dim3(nblk), dim3(1024), st, tl, count, co, (const int4*)h->scan_part);
     launch(ev ? e1 : nullptr, k_scatter, dim3(div_up(h->n, 256)), dim3(256), st, h->n, (const int*)h->ptile,
-           (const int*)h->pslot, (const int*)h->cstart[c], h->list[c]);
+           (const int*)h->pslot, (const int*)co.cstart, list);
   }
   GSMPM_LAUNCH_CHECK();
   return GSMPM_OK;
 }
+static int finish_binning(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t* ev = nullptr) {
+  return finish_bins_on(h, h->tl, h->count[c], chunk_out(h, c), h->list[c], st, ev);
+}
+static int finish_binning_f(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t* ev = nullptr) {
+  return finish_bins_on(h, ftiles_flat(h), h->fcount[c], chunk_out_f(h, c), h->flist[c], st, ev);
+}
 
-// (Re)build the chunk lists of parity `cur_box` from the current x.
-static int rebin(gsmpm_mpm* h, hipStream_t st) {
+// (Re)build the fused pipeline's chunk lists of parity `fbpar` from the current x.
+static int rebin_f(gsmpm_mpm* h, hipStream_t st) {
+  const int c = h->fbpar;
+  GSMPM_HIP(hipMemsetAsync(h->fcount[c], 0, sizeof(int) * (h->ftl.ntiles + 1), st));
+  GSMPM_HIP(hipMemsetAsync(h->ftflag[c], 0, sizeof(int) * h->ftl.ntiles, st));
+  GSMPM_HIP(hipMemsetAsync(h->fnchunk[c], 0, sizeof(int) * 2, st));
+  hipLaunchKernelGGL(k_bin_all_f, dim3(div_up(h->n, 256)), dim3(256), 0, st, particles_of(h), h->g, bin_out_f(h, c));
+  GSMPM_LAUNCH_CHECK();
+  return finish_binning_f(h, c, st);
+}
+
+// (Re)build the per-phase pipeline's chunk lists of parity `cur_box` from the current x.
+static int rebin_phased(gsmpm_mpm* h, hipStream_t st) {
   const int c = h->cur_box;
   GSMPM_HIP(hipMemsetAsync(h->count[c], 0, sizeof(int) * (h->tl.ntiles + 1), st));
   GSMPM_HIP(hipMemsetAsync(h->tflag[c], 0, sizeof(int) * h->tl.ntiles, st));
@@ -1397,6 +1482,8 @@ static int rebin(gsmpm_mpm* h, hipStream_t st) {
   GSMPM_LAUNCH_CHECK();
   return finish_binning(h, c, st);
 }
+
+static int rebin(gsmpm_mpm* h, hipStream_t st) { return use_fused(h) ? rebin_f(h, st) : rebin_phased(h, st); }
 
 static GridStep grid_step(gsmpm_mpm* h, float dt, uint32_t mask) {
   GridStep gs;
@@ -1469,10 +1556,110 @@ static int launch_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc,
   return GSMPM_OK;
 }
 
+// ------------------------------------------------------ fused pipeline --
+static int fused_grid(gsmpm_mpm* h) { return std::min(h->ftl.max_chunks, 1024); }
+
+template <int MAT, int MODE>
+static void launch_fused_t(gsmpm_mpm* h, int c, const BinOutF& bo, int bin, uint32_t mask, float dt, int* esc,
+                           hipStream_t st, const hipEvent_t* ev) {
+  launch(ev, k_fused<MAT, MODE>, dim3(fused_grid(h)), dim3(256), st, particles_of(h), h->g, h->ftl, chunk_in_f(h, c),
+         bo, bin, (const float4*)h->gvel, (const BcTable*)h->dev_bc, mask, dt, h->mc, h->fslots, h->gacc, esc);
+}
+template <int MODE>
+static void launch_fused_m(gsmpm_mpm* h, int c, const BinOutF& bo, int bin, uint32_t mask, float dt, int* esc,
+                           hipStream_t st, const hipEvent_t* ev) {
+  switch (h->mat_kernel) {
+    case 0: launch_fused_t<0, MODE>(h, c, bo, bin, mask, dt, esc, st, ev); break;
+    case 1: launch_fused_t<1, MODE>(h, c, bo, bin, mask, dt, esc, st, ev); break;
+    case 2: launch_fused_t<2, MODE>(h, c, bo, bin, mask, dt, esc, st, ev); break;
+    case 3: launch_fused_t<3, MODE>(h, c, bo, bin, mask, dt, esc, st, ev); break;
+    default: launch_fused_t<4, MODE>(h, c, bo, bin, mask, dt, esc, st, ev); break;
+  }
+}
+// mode 1: G2P only, 2: P2G only, 3: G2P of the last grid update + P2G
+static int launch_fused(gsmpm_mpm* h, int mode, int c, bool bin, uint32_t mask, float dt, int* esc, hipStream_t st,
+                        const hipEvent_t* ev) {
+  const BinOutF bo = bin_out_f(h, c ^ 1);
+  if (mode == 1)
+    launch_fused_t<0, 1>(h, c, bo, bin ? 1 : 0, mask, dt, esc, st, ev);  // G2P does not depend on the material
+  else if (mode == 2)
+    launch_fused_m<2>(h, c, bo, bin ? 1 : 0, mask, dt, esc, st, ev);
+  else
+    launch_fused_m<3>(h, c, bo, bin ? 1 : 0, mask, dt, esc, st, ev);
+  GSMPM_LAUNCH_CHECK();
+  return GSMPM_OK;
+}
+
+static int launch_grid_f(gsmpm_mpm* h, int wp, float dt, uint32_t mask, int ep, int* zc, int* zf, hipStream_t st,
+                         const hipEvent_t* ev) {
+  launch(ev, k_grid_f, dim3(std::min(h->ftl.ntiles, 1024)), dim3(512), st, h->g, h->ftl, chunk_in_f(h, wp),
+         (const float4*)h->fslots, h->gacc, h->gvel, (const BcTable*)h->dev_bc, grid_step(h, dt, mask),
+         (const int*)(h->fesc + ep), h->fesc + (ep ^ 1), zc, zf);
+  GSMPM_LAUNCH_CHECK();
+  return GSMPM_OK;
+}
+
+// nsub substeps = nsub + 1 k_fused launches (P2G, nsub - 1 x G2P+P2G, G2P)
+// and nsub grid updates; the particles are re-binned by the G2P half every
+// rebin_interval substeps and at the end, so the bins are fresh for the next
+// call.  bp / ep: bins parity / escape flag, updated.  ev: 8 events per
+// k_fused launch ({K, grid, binning} pairs), summed into kernel_ms[0..2].
+static int launch_substeps_f(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc, hipStream_t st, int& bp, int& ep,
+                             hipEvent_t* ev = nullptr, float* kernel_ms = nullptr) {
+  const int R = std::max(1, h->rebin_interval);
+  int wp = bp;
+  bool zeroed = false;  // counts / flags of parity bp ^ 1 zeroed by a grid launch since the last binning
+  for (int s = 0; s <= nsub; ++s) {
+    const int mode = s == 0 ? 2 : (s == nsub ? 1 : 3);
+    const bool bin = s == nsub || (s > 0 && s % R == 0);
+    const uint32_t mask = s < nsub ? (bc ? bc[s] : 0xffffffffu) : 0u;
+    hipEvent_t* e8 = ev ? ev + 8 * s : nullptr;
+    if (bin && !zeroed) {
+      GSMPM_HIP(hipMemsetAsync(h->fcount[bp ^ 1], 0, sizeof(int) * (h->ftl.ntiles + 1), st));
+      GSMPM_HIP(hipMemsetAsync(h->ftflag[bp ^ 1], 0, sizeof(int) * h->ftl.ntiles, st));
+    }
+    int rc = launch_fused(h, mode, bp, bin, mask, dt, h->fesc + ep, st, e8);
+    if (rc) return rc;
+    if (mode & 2) wp = bp;
+    if (bin) {
+      rc = finish_binning_f(h, bp ^ 1, st, e8 ? e8 + 4 : nullptr);
+      if (rc) return rc;
+      bp ^= 1;
+      zeroed = false;
+    }
+    if (s < nsub) {
+      const bool next_bin = s + 1 == nsub || (s + 1) % R == 0;
+      int *zc = nullptr, *zf = nullptr;
+      if (next_bin && wp == bp) {  // this grid launch does not read parity bp ^ 1
+        zc = h->fcount[bp ^ 1];
+        zf = h->ftflag[bp ^ 1];
+        zeroed = true;
+      }
+      rc = launch_grid_f(h, wp, dt, mask, ep, zc, zf, st, e8 ? e8 + 2 : nullptr);
+      if (rc) return rc;
+      ep ^= 1;
+    }
+  }
+  if (ev) {
+    GSMPM_HIP(hipStreamSynchronize(st));
+    for (int s = 0; s <= nsub; ++s) {
+      const bool bin = s == nsub || (s > 0 && s % R == 0);
+      for (int k = 0; k < 3; ++k) {
+        if ((k == 1 && s == nsub) || (k == 2 && !bin)) continue;
+        float ms = 0.f;
+        GSMPM_HIP(hipEventElapsedTime(&ms, ev[8 * s + 2 * k], ev[8 * s + 2 * k + 1]));
+        kernel_ms[k] += ms;
+      }
+    }
+  }
+  return GSMPM_OK;
+}
+
 static void drop_graphs(gsmpm_mpm* h) {
   for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
   h->graphs.clear();
   h->graph_box_parity.clear();
+  h->graph_fstate.clear();
 }
 
 static int upload_bc(gsmpm_mpm* h) {
@@ -1614,7 +1801,40 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
     if ((e = hipMemset(h->nchunk[c], 0, sizeof(int) * 2)) != hipSuccess) return fail(e, "hipMemset");
   }
   if ((e = hipMalloc(&h->escape, sizeof(int))) != hipSuccess) return fail(e, "hipMalloc escape");
-  if ((e = hipMalloc(&h->scan_part, sizeof(int4) * (size_t)div_up(h->tl.ntiles + 1, 1024))) != hipSuccess)
+  // fused pipeline: 8 x 8 x 7-cell tiles (fused.h)
+  h->fused = !(prm->flags & (GSMPM_FLAG_PHASED | GSMPM_FLAG_KEEP_GRID));
+  h->ftl.td0 = (h->g.ng + kFT0 - 1) / kFT0;
+  h->ftl.td1 = (h->g.ng + kFT1 - 1) / kFT1;
+  h->ftl.td2 = (h->g.ng + kFT2 - 1) / kFT2;
+  h->ftl.ntiles = h->ftl.td0 * h->ftl.td1 * h->ftl.td2;
+  h->ftl.max_chunks = h->n / kChunk + std::min(h->ftl.ntiles + 1, h->n) + 1;
+  if (h->fused) {
+    const size_t E = (size_t)h->ftl.ntiles + 1;
+    if ((e = hipMalloc(&h->fslots, sizeof(float4) * (size_t)(h->ftl.max_chunks + 1) * kFWin)) != hipSuccess)
+      return fail(e, "hipMalloc fused slots");
+    if ((e = hipMemset(h->fslots + (size_t)h->ftl.max_chunks * kFWin, 0, sizeof(float4) * kFWin)) != hipSuccess)
+      return fail(e, "hipMemset");
+    for (int c = 0; c < 2; ++c) {
+      if ((e = hipMalloc(&h->fcount[c], sizeof(int) * E)) != hipSuccess) return fail(e, "hipMalloc count");
+      if ((e = hipMalloc(&h->fcstart[c], sizeof(int) * E)) != hipSuccess) return fail(e, "hipMalloc cstart");
+      if ((e = hipMalloc(&h->fcbase[c], sizeof(int) * E)) != hipSuccess) return fail(e, "hipMalloc cbase");
+      if ((e = hipMalloc(&h->fchunk[c], sizeof(int4) * (size_t)h->ftl.max_chunks)) != hipSuccess)
+        return fail(e, "hipMalloc chunk");
+      if ((e = hipMalloc(&h->ftouched[c], sizeof(int) * (size_t)h->ftl.ntiles)) != hipSuccess)
+        return fail(e, "hipMalloc touched");
+      if ((e = hipMalloc(&h->ftflag[c], sizeof(int) * (size_t)h->ftl.ntiles)) != hipSuccess)
+        return fail(e, "hipMalloc tflag");
+      if ((e = hipMalloc(&h->fnchunk[c], sizeof(int) * 2)) != hipSuccess) return fail(e, "hipMalloc nchunk");
+      if ((e = hipMalloc(&h->flist[c], sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc list");
+      if ((e = hipMemset(h->fcount[c], 0, sizeof(int) * E)) != hipSuccess) return fail(e, "hipMemset");
+      if ((e = hipMemset(h->ftflag[c], 0, sizeof(int) * (size_t)h->ftl.ntiles)) != hipSuccess) return fail(e, "hipMemset");
+      if ((e = hipMemset(h->fnchunk[c], 0, sizeof(int) * 2)) != hipSuccess) return fail(e, "hipMemset");
+    }
+    if ((e = hipMalloc(&h->fesc, sizeof(int) * 2)) != hipSuccess) return fail(e, "hipMalloc escape flags");
+    if ((e = hipMemset(h->fesc, 0, sizeof(int) * 2)) != hipSuccess) return fail(e, "hipMemset");
+  }
+  const int scan_tiles = std::max(h->tl.ntiles, h->ftl.ntiles) + 1;
+  if ((e = hipMalloc(&h->scan_part, sizeof(int4) * (size_t)div_up(scan_tiles, 1024))) != hipSuccess)
     return fail(e, "hipMalloc scan partials");
   if ((e = hipMemset(h->escape, 0, sizeof(int))) != hipSuccess) return fail(e, "hipMemset");
   if ((e = hipMalloc(&h->ptile, sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc ptile");
@@ -1652,6 +1872,18 @@ int gsmpm_mpm_destroy(gsmpm_mpm* h) {
     (void)hipFree(h->nchunk[c]);
     (void)hipFree(h->list[c]);
   }
+  for (int c = 0; c < 2; ++c) {
+    (void)hipFree(h->fcount[c]);
+    (void)hipFree(h->fcstart[c]);
+    (void)hipFree(h->fcbase[c]);
+    (void)hipFree(h->fchunk[c]);
+    (void)hipFree(h->ftouched[c]);
+    (void)hipFree(h->ftflag[c]);
+    (void)hipFree(h->fnchunk[c]);
+    (void)hipFree(h->flist[c]);
+  }
+  (void)hipFree(h->fslots);
+  (void)hipFree(h->fesc);
   (void)hipFree(h->ptile);
   (void)hipFree(h->escape);
   (void)hipFree(h->scan_part);
@@ -1791,27 +2023,33 @@ int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t nsub, const uint32_t* bc, voi
   }
   h->since_sort += nsub;
   const bool use_graph = !(h->prm.flags & GSMPM_FLAG_NO_GRAPH) && nsub >= 2;
+  const bool fz = use_fused(h);
   if (!use_graph) {
     int parity = h->cur_box;
-    int rc = launch_substeps(h, dt, nsub, bc, st, parity);
+    int rc = fz ? launch_substeps_f(h, dt, nsub, bc, st, h->fbpar, h->fep)
+                : launch_substeps(h, dt, nsub, bc, st, parity);
     h->cur_box = parity;
     return rc;
   }
   std::vector<uint32_t> key;
-  key.reserve(nsub + 3);
+  key.reserve(nsub + 7);
   uint32_t dtb;
   std::memcpy(&dtb, &dt, 4);
   key.push_back(dtb);
   key.push_back((uint32_t)nsub);
   key.push_back((uint32_t)h->cur_box);
+  key.push_back(fz ? 1u : 0u);
+  key.push_back((uint32_t)h->fbpar);
+  key.push_back((uint32_t)h->fep);
+  key.push_back((uint32_t)h->rebin_interval);
   for (int s = 0; s < nsub; ++s) key.push_back(bc ? bc[s] : 0xffffffffu);
   auto it = h->graphs.find(key);
   if (it == h->graphs.end()) {
     if (h->graphs.size() >= 16) drop_graphs(h);
     hipGraph_t graph;
-    int parity = h->cur_box;
+    int parity = h->cur_box, bp = h->fbpar, ep = h->fep;
     GSMPM_HIP(hipStreamBeginCapture(h->cap, hipStreamCaptureModeRelaxed));
-    int rc = launch_substeps(h, dt, nsub, bc, h->cap, parity);
+    int rc = fz ? launch_substeps_f(h, dt, nsub, bc, h->cap, bp, ep) : launch_substeps(h, dt, nsub, bc, h->cap, parity);
     hipError_t e = hipStreamEndCapture(h->cap, &graph);
     if (rc) return rc;
     if (e != hipSuccess) {
@@ -1827,9 +2065,12 @@ int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t nsub, const uint32_t* bc, voi
     }
     it = h->graphs.emplace(key, exec).first;
     h->graph_box_parity[key] = parity;
+    h->graph_fstate[key] = std::make_pair(bp, ep);
   }
   GSMPM_HIP(hipGraphLaunch(it->second, st));
   h->cur_box = h->graph_box_parity[key];
+  h->fbpar = h->graph_fstate[key].first;
+  h->fep = h->graph_fstate[key].second;
   return GSMPM_OK;
 }
 
@@ -1857,6 +2098,13 @@ int gsmpm_mpm_set_halo(gsmpm_mpm* h, int32_t n_windows, const int32_t* x0, int32
   h->tx_lo = std::max(0, allow_lo) / kTile;
   h->tx_hi = std::max(0, allow_hi - 1) / kTile;
   drop_graphs(h);  // kernel arguments changed
+  // slabs run the per-phase pipeline (halo windows between P2G and the grid
+  // update); its bins must describe the current x
+  if (h->has_particles) {
+    int rc = rebin(h, nullptr);
+    if (rc) return rc;
+    GSMPM_HIP(hipStreamSynchronize(nullptr));
+  }
   return GSMPM_OK;
 }
 
@@ -1867,6 +2115,11 @@ int gsmpm_mpm_substep_begin(gsmpm_mpm* h, float dt, uint32_t bc_active, void* st
     return GSMPM_ESTATE;
   }
   hipStream_t st = (hipStream_t)stream;
+  if (use_fused(h)) {
+    set_error("gsmpm_mpm_substep_begin: the split substep is the slab path; set halo windows first "
+              "(gsmpm_mpm_set_halo) or create the simulator with GSMPM_FLAG_PHASED");
+    return GSMPM_ESTATE;
+  }
   if (!(h->prm.flags & GSMPM_FLAG_NO_SORT) && h->resort_interval > 0 && h->since_sort >= h->resort_interval) {
     int rc = resort(h, st);
     if (rc) return rc;
@@ -1876,6 +2129,10 @@ int gsmpm_mpm_substep_begin(gsmpm_mpm* h, float dt, uint32_t bc_active, void* st
 
 int gsmpm_mpm_substep_end(gsmpm_mpm* h, float dt, uint32_t bc_active, void* stream) {
   GSMPM_REQUIRE(h, "gsmpm_mpm_substep_end: null handle");
+  if (use_fused(h)) {
+    set_error("gsmpm_mpm_substep_end: the split substep is the slab path (see gsmpm_mpm_substep_begin)");
+    return GSMPM_ESTATE;
+  }
   int rc = substep_end(h, dt, bc_active, h->cur_box, (hipStream_t)stream, nullptr);
   if (rc) return rc;
   h->cur_box ^= 1;
@@ -1892,6 +2149,18 @@ int gsmpm_mpm_halo_status(gsmpm_mpm* h, int32_t* escaped, void* stream) {
   GSMPM_HIP(hipMemsetAsync(h->escape, 0, sizeof(int), st));
   *escaped = v;
   return GSMPM_OK;
+}
+
+int gsmpm_mpm_set_rebin_interval(gsmpm_mpm* h, int32_t substeps) {
+  GSMPM_REQUIRE(h, "gsmpm_mpm_set_rebin_interval: null handle");
+  GSMPM_REQUIRE(substeps >= 1, "gsmpm_mpm_set_rebin_interval: substeps must be >= 1");
+  h->rebin_interval = substeps;
+  return GSMPM_OK;
+}
+
+int gsmpm_mpm_pipeline(gsmpm_mpm* h) {
+  GSMPM_REQUIRE(h, "gsmpm_mpm_pipeline: null handle");
+  return use_fused(h) ? GSMPM_PIPE_FUSED : GSMPM_PIPE_PHASED;
 }
 
 int gsmpm_mpm_resort(gsmpm_mpm* h, int32_t interval, void* stream) {
@@ -1972,6 +2241,13 @@ int gsmpm_mpm_profile_substeps(gsmpm_mpm* h, float dt, int32_t nsub, const uint3
   hipStream_t st = (hipStream_t)stream;
   for (int k = 0; k < 4; ++k) kernel_ms[k] = 0.f;
   if (nsub == 0) return GSMPM_OK;
+  if (use_fused(h)) {
+    std::vector<hipEvent_t> ev(8 * (size_t)(nsub + 1));
+    for (auto& e : ev) GSMPM_HIP(hipEventCreate(&e));
+    int rc = launch_substeps_f(h, dt, nsub, bc, st, h->fbpar, h->fep, ev.data(), kernel_ms);
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    return rc;
+  }
   std::vector<hipEvent_t> ev(8 * (size_t)nsub);
   for (auto& e : ev) GSMPM_HIP(hipEventCreate(&e));
   int parity = h->cur_box;
@@ -1979,6 +2255,49 @@ int gsmpm_mpm_profile_substeps(gsmpm_mpm* h, float dt, int32_t nsub, const uint3
   h->cur_box = parity;
   for (auto& e : ev) (void)hipEventDestroy(e);
   return rc;
+}
+
+// fused pipeline: ms4 = {k_fused (G2P + P2G), k_grid_f, binning, 0}; state restored afterwards
+static int time_kernels_f(gsmpm_mpm* h, float dt, uint32_t mask, int reps, float* ms4, hipStream_t st, size_t pbytes) {
+  const int c = h->fbpar, ep = h->fep;
+  const size_t nn = (size_t)h->g.ng * h->g.ng * h->g.ng;
+  hipEvent_t e[2];
+  GSMPM_HIP(hipEventCreate(&e[0]));
+  GSMPM_HIP(hipEventCreate(&e[1]));
+  auto timed = [&](int k, auto&& body) -> int {
+    GSMPM_HIP(hipEventRecord(e[0], st));
+    for (int r = 0; r < reps; ++r) {
+      int rc = body();
+      if (rc) return rc;
+    }
+    GSMPM_HIP(hipEventRecord(e[1], st));
+    GSMPM_HIP(hipEventSynchronize(e[1]));
+    float ms = 0.f;
+    GSMPM_HIP(hipEventElapsedTime(&ms, e[0], e[1]));
+    ms4[k] = ms / reps;
+    return GSMPM_OK;
+  };
+  ms4[3] = 0.f;
+  int rc = launch_fused(h, 2, c, false, mask, dt, h->fesc + ep, st, nullptr);  // windows of the current x
+  if (!rc) rc = launch_grid_f(h, c, dt, mask, ep, nullptr, nullptr, st, nullptr);
+  if (!rc) rc = timed(0, [&]() { return launch_fused(h, 3, c, false, mask, dt, h->fesc + ep, st, nullptr); });
+  if (!rc) {
+    GSMPM_HIP(hipMemsetAsync(h->fesc, 0, 2 * sizeof(int), st));  // time the touched-tile update
+    rc = timed(1, [&]() { return launch_grid_f(h, c, dt, mask, ep, nullptr, nullptr, st, nullptr); });
+  }
+  if (!rc) {
+    GSMPM_HIP(hipMemsetAsync(h->fcount[c ^ 1], 0, sizeof(int) * (h->ftl.ntiles + 1), st));
+    GSMPM_HIP(hipMemsetAsync(h->ftflag[c ^ 1], 0, sizeof(int) * h->ftl.ntiles, st));
+    rc = launch_fused(h, 1, c, true, mask, dt, h->fesc + ep, st, nullptr);
+    if (!rc) rc = timed(2, [&]() { return finish_binning_f(h, c ^ 1, st); });
+  }
+  (void)hipEventDestroy(e[0]);
+  (void)hipEventDestroy(e[1]);
+  if (rc) return rc;
+  GSMPM_HIP(hipMemcpyAsync(h->planes, h->planes_tmp, pbytes, hipMemcpyDeviceToDevice, st));
+  GSMPM_HIP(hipMemsetAsync(h->fesc, 0, 2 * sizeof(int), st));
+  GSMPM_HIP(hipMemsetAsync(h->gacc, 0, nn * sizeof(float4), st));
+  return rebin(h, st);
 }
 
 int gsmpm_mpm_time_kernels(gsmpm_mpm* h, float dt, uint32_t bc_active, int32_t reps, float* ms4, void* stream) {
@@ -1991,6 +2310,7 @@ int gsmpm_mpm_time_kernels(gsmpm_mpm* h, float dt, uint32_t bc_active, int32_t r
   const size_t pbytes = sizeof(float) * (size_t)NPLANES * h->np;
   if (!h->planes_tmp) GSMPM_HIP(hipMalloc(&h->planes_tmp, pbytes));
   GSMPM_HIP(hipMemcpyAsync(h->planes_tmp, h->planes, pbytes, hipMemcpyDeviceToDevice, st));
+  if (use_fused(h)) return time_kernels_f(h, dt, bc_active, reps, ms4, st, pbytes);
   const int c = h->cur_box, nx = c ^ 1;
   const GridStep gs = grid_step(h, dt, bc_active);
   hipEvent_t e[2];
@@ -2041,25 +2361,28 @@ int gsmpm_mpm_time_kernels(gsmpm_mpm* h, float dt, uint32_t bc_active, int32_t r
 int gsmpm_mpm_debug_stats(gsmpm_mpm* h, int32_t* out8, void* stream) {
   GSMPM_REQUIRE(h && out8, "gsmpm_mpm_debug_stats: null argument");
   hipStream_t st = (hipStream_t)stream;
-  std::vector<int> hc(h->tl.ntiles + 1);
+  const bool fz = use_fused(h);
+  const int ntiles = fz ? h->ftl.ntiles : h->tl.ntiles, par = fz ? h->fbpar : h->cur_box;
+  std::vector<int> hc(ntiles + 1);
   int nch[2] = {0, 0};
-  GSMPM_HIP(hipMemcpyAsync(hc.data(), h->count[h->cur_box], sizeof(int) * hc.size(), hipMemcpyDeviceToHost, st));
-  GSMPM_HIP(hipMemcpyAsync(nch, h->nchunk[h->cur_box], sizeof(int) * 2, hipMemcpyDeviceToHost, st));
+  GSMPM_HIP(hipMemcpyAsync(hc.data(), fz ? h->fcount[par] : h->count[par], sizeof(int) * hc.size(),
+                           hipMemcpyDeviceToHost, st));
+  GSMPM_HIP(hipMemcpyAsync(nch, fz ? h->fnchunk[par] : h->nchunk[par], sizeof(int) * 2, hipMemcpyDeviceToHost, st));
   GSMPM_HIP(hipStreamSynchronize(st));
   int active = 0, mx = 0;
   long tot = 0;
-  for (int t = 0; t < h->tl.ntiles; ++t) {
+  for (int t = 0; t < ntiles; ++t) {
     active += hc[t] > 0;
     mx = std::max(mx, hc[t]);
     tot += hc[t];
   }
   out8[0] = active;
   out8[1] = mx;
-  out8[2] = hc[h->tl.ntiles];  // particles outside the grid
+  out8[2] = hc[ntiles];  // particles outside the grid
   out8[3] = nch[0];
   out8[4] = nch[1];  // tiles owned by the next grid update
   out8[5] = (int)tot;
-  out8[6] = h->cur_box;
+  out8[6] = par;
   out8[7] = (int)h->since_sort;
   return GSMPM_OK;
 }
@@ -2075,24 +2398,38 @@ int gsmpm_mpm_live_box(gsmpm_mpm* h, int32_t* box6, void* stream) {
   GSMPM_REQUIRE(h && box6, "gsmpm_mpm_live_box: null argument");
   // node box of the tiles the next grid update owns
   hipStream_t st = (hipStream_t)stream;
-  const int c = h->cur_box, td = h->tl.td;
+  const bool fz = use_fused(h);
+  const int c = fz ? h->fbpar : h->cur_box, td = h->tl.td;
   int nch[2] = {0, 0};
-  GSMPM_HIP(hipMemcpyAsync(nch, h->nchunk[c], sizeof(int) * 2, hipMemcpyDeviceToHost, st));
+  GSMPM_HIP(hipMemcpyAsync(nch, fz ? h->fnchunk[c] : h->nchunk[c], sizeof(int) * 2, hipMemcpyDeviceToHost, st));
   GSMPM_HIP(hipStreamSynchronize(st));
   std::vector<int> tl(nch[1]);
   if (nch[1] > 0) {
-    GSMPM_HIP(hipMemcpyAsync(tl.data(), h->touched[c], sizeof(int) * nch[1], hipMemcpyDeviceToHost, st));
+    GSMPM_HIP(hipMemcpyAsync(tl.data(), fz ? h->ftouched[c] : h->touched[c], sizeof(int) * nch[1],
+                             hipMemcpyDeviceToHost, st));
     GSMPM_HIP(hipStreamSynchronize(st));
   }
   for (int d = 0; d < 3; ++d) {
     box6[d] = INT_MAX;
     box6[3 + d] = INT_MIN;
   }
+  const int fT[3] = {kFT0, kFT1, kFT2};
   for (int t : tl) {
-    const int tc[3] = {t / (td * td), (t / td) % td, t % td};
+    int tc[3], T[3];
+    if (fz) {
+      tc[2] = t % h->ftl.td2;
+      tc[1] = (t / h->ftl.td2) % h->ftl.td1;
+      tc[0] = t / (h->ftl.td1 * h->ftl.td2);
+      for (int d = 0; d < 3; ++d) T[d] = fT[d];
+    } else {
+      tc[0] = t / (td * td);
+      tc[1] = (t / td) % td;
+      tc[2] = t % td;
+      for (int d = 0; d < 3; ++d) T[d] = kTile;
+    }
     for (int d = 0; d < 3; ++d) {
-      box6[d] = std::min(box6[d], tc[d] * kTile);
-      box6[3 + d] = std::max(box6[3 + d], std::min(h->g.ng - 1, tc[d] * kTile + kTile - 1));
+      box6[d] = std::min(box6[d], tc[d] * T[d]);
+      box6[3 + d] = std::max(box6[3 + d], std::min(h->g.ng - 1, tc[d] * T[d] + T[d] - 1));
     }
   }
   return GSMPM_OK;

@@ -85,6 +85,8 @@ _SIGS = {
     "gsmpm_mpm_substep_end": (ctypes.c_int, [c_void_p, ctypes.c_float, ctypes.c_uint32, c_void_p]),
     "gsmpm_mpm_halo_status": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int32), c_void_p]),
     "gsmpm_mpm_resort": (ctypes.c_int, [c_void_p, ctypes.c_int32, c_void_p]),
+    "gsmpm_mpm_set_rebin_interval": (ctypes.c_int, [c_void_p, ctypes.c_int32]),
+    "gsmpm_mpm_pipeline": (ctypes.c_int, [c_void_p]),
     "gsmpm_mpm_postprocess": (ctypes.c_int, [c_void_p, c_void_p]),
     "gsmpm_mpm_field_width": (ctypes.c_int, [ctypes.c_int32]),
     "gsmpm_mpm_get": (ctypes.c_int, [c_void_p, ctypes.c_int32, c_void_p, c_void_p]),
@@ -137,7 +139,8 @@ FIELD = {"x": 0, "v": 1, "C": 2, "F_trial": 3, "cov": 4, "init_cov": 5, "R": 6, 
 FIT_FIELD = {k: i for i, k in enumerate(
     ("x", "v", "F", "C", "stress", "gx", "gv", "gF", "gC", "gstress", "logE", "y", "mu", "lam", "glogE", "gy", "gmu",
      "glam", "cov", "gcov", "init_cov", "vol", "mass"))}
-FLAG_JELLY_FCR, FLAG_KEEP_GRID, FLAG_NO_GRAPH, FLAG_NO_SORT = 1, 2, 4, 8
+FLAG_JELLY_FCR, FLAG_KEEP_GRID, FLAG_NO_GRAPH, FLAG_NO_SORT, FLAG_PHASED = 1, 2, 4, 8, 16
+PIPE_PHASED, PIPE_FUSED = 0, 1
 
 
 class GsmpmError(RuntimeError):

@@ -30,7 +30,8 @@ class Simulator:
                  E: float = 2e6, nu: float = 0.4, density: float = 1000.0, gravity=(0.0, -9.81, 0.0),
                  yield_stress: float = 0.005, hardening: float = 1.0, xi: float = 1.0,
                  plastic_viscosity: float = 0.008, friction_angle: float = 25.0, jelly_fcr: bool = False,
-                 keep_grid: bool = False, use_graph: bool = True, sort: bool = True, device=None):
+                 keep_grid: bool = False, use_graph: bool = True, sort: bool = True, phased: bool = False,
+                 device=None):
         code = MATERIALS.get(material, -1) if isinstance(material, str) else int(material)
         if code not in (0, 1, 2, 3):
             raise TypeError("Material not supported yet")  # model.py:27-30
@@ -56,6 +57,8 @@ class Simulator:
             flags |= _lib.FLAG_NO_GRAPH
         if not sort:
             flags |= _lib.FLAG_NO_SORT
+        if phased:
+            flags |= _lib.FLAG_PHASED
         p.flags = flags
         self.params = p
         h = ctypes.c_void_p()
@@ -124,7 +127,7 @@ class Simulator:
 
     def profile(self, dt: float, masks):
         """Eager substeps with a hipEvent pair per kernel -> summed ms of
-        (k_p2g, k_grid, k_g2p, binning)."""
+        (k_p2g, k_grid, k_g2p, binning); fused pipeline: (k_fused, k_grid_f, binning, 0)."""
         n = len(masks)
         arr = (ctypes.c_uint32 * max(1, n))(*[int(m) & 0xFFFFFFFF for m in masks])
         out = (ctypes.c_float * 4)()
@@ -133,8 +136,9 @@ class Simulator:
         return tuple(float(v) for v in out)
 
     def time_kernels(self, dt: float, mask: int, reps: int = 20):
-        """Per-launch ms of (k_p2g, k_grid, k_g2p, binning): hipEvents around
-        `reps` back-to-back launches of each on this stream; state restored."""
+        """Per-launch ms of (k_p2g, k_grid, k_g2p, binning) -- fused pipeline:
+        (k_fused, k_grid_f, binning, 0) -- from hipEvents around `reps`
+        back-to-back launches of each on this stream; state restored."""
         out = (ctypes.c_float * 4)()
         check(LIB.gsmpm_mpm_time_kernels(self._h, ctypes.c_float(dt), int(mask) & 0xFFFFFFFF, int(reps), out,
                                          stream_of(self.device)), "gsmpm_mpm_time_kernels")
@@ -150,6 +154,16 @@ class Simulator:
         b = (ctypes.c_int32 * 6)()
         check(LIB.gsmpm_mpm_live_box(self._h, b, stream_of(self.device)), "gsmpm_mpm_live_box")
         return list(b[:3]), list(b[3:])
+
+    @property
+    def pipeline(self) -> str:
+        """'fused' (k_fused + k_grid_f per substep) or 'phased' (k_p2g, k_grid, k_g2p, binning)."""
+        code = check(LIB.gsmpm_mpm_pipeline(self._h), "gsmpm_mpm_pipeline")
+        return "fused" if code == _lib.PIPE_FUSED else "phased"
+
+    def set_rebin_interval(self, substeps: int):
+        """Fused pipeline: substeps between particle re-binnings (any value >= 1 is correct)."""
+        check(LIB.gsmpm_mpm_set_rebin_interval(self._h, int(substeps)), "gsmpm_mpm_set_rebin_interval")
 
     def resort(self, interval: int = -1):
         """Re-sort storage into Morton order now; interval >= 0 sets the automatic period."""

@@ -51,7 +51,8 @@ class MPM_Simulator:
         self._sim = Simulator(
             self.n_particles, n_grid=args.n_grid, grid_extent=args.grid_extent, material=args.material, E=args.E,
             nu=args.nu, density=args.density, gravity=args.gravity, jelly_fcr=bool(getattr(args, "jelly_fcr", False)),
-            keep_grid=bool(getattr(args, "keep_grid", False)), device=xyzs.device if xyzs.is_cuda else None)
+            keep_grid=bool(getattr(args, "keep_grid", False)), phased=bool(getattr(args, "phased", False)),
+            device=xyzs.device if xyzs.is_cuda else None)
         self._sim.set_particles(xyzs.reshape(-1, 3), covs.reshape(-1, 6), volumes.reshape(-1), init_v)
         self.mpm_model._bind(self)
         self.mpm_state = MPM_state(self, args)

@@ -43,6 +43,12 @@ typedef struct gsmpm_mpm gsmpm_mpm;
 #define GSMPM_FLAG_KEEP_GRID 2u   /* keep m / m*v of the last substep readable (debug, slower) */
 #define GSMPM_FLAG_NO_GRAPH 4u    /* launch substeps eagerly instead of through a cached hipGraph */
 #define GSMPM_FLAG_NO_SORT 8u     /* keep particles in input order (no spatial sort) */
+#define GSMPM_FLAG_PHASED 16u     /* per-phase substep (P2G, grid, G2P, binning: 4 launches) instead of the
+                                     fused G2P2G pipeline (2 launches); also implied by KEEP_GRID and slabs */
+
+/* substep pipelines (gsmpm_mpm_pipeline) */
+#define GSMPM_PIPE_PHASED 0
+#define GSMPM_PIPE_FUSED 1
 
 typedef struct {
   int32_t n_particles;
@@ -107,6 +113,14 @@ int gsmpm_mpm_halo_status(gsmpm_mpm* h, int32_t* escaped, void* stream);
  * (0 = never; default 100).  No counterpart in the reference. */
 int gsmpm_mpm_resort(gsmpm_mpm* h, int32_t interval, void* stream);
 
+/* Fused pipeline: substeps between re-binnings of the particles into tiles
+ * (default 10; any value is correct -- particles that moved more than one cell
+ * since their binning take a slower global path).  No counterpart in the
+ * reference (its p2g2p has no binning, solver.py:27-52). */
+int gsmpm_mpm_set_rebin_interval(gsmpm_mpm* h, int32_t substeps);
+/* GSMPM_PIPE_FUSED or GSMPM_PIPE_PHASED: the pipeline gsmpm_mpm_step runs now. */
+int gsmpm_mpm_pipeline(gsmpm_mpm* h);
+
 /* MPM_Simulator.postprocess (solver.py:135-137): compute_cov_from_F and
  * compute_R_from_F (utils.py:376-433). */
 int gsmpm_mpm_postprocess(gsmpm_mpm* h, void* stream);
@@ -148,14 +162,16 @@ int gsmpm_mpm_world_outputs(gsmpm_mpm* h, float scale, const float center[3], in
 /* Measurement: run n substeps eagerly on `stream`, each kernel launched with
  * hipExtLaunchKernel start/stop events (stamped by its own dispatch, the
  * interval rocprofv3 reports); kernel_ms[0..3] = summed time of k_p2g,
- * k_grid, k_g2p and the binning (k_finish_bins, or k_scan_tiles..k_scatter).
+ * k_grid, k_g2p and the binning (k_finish_bins, or k_scan_tiles..k_scatter)
+ * -- for the fused pipeline {k_fused, k_grid_f, binning, 0}.
  * Synchronises `stream`. */
 int gsmpm_mpm_profile_substeps(gsmpm_mpm* h, float dt, int32_t n_substeps, const uint32_t* bc_active,
                                float* kernel_ms, void* stream);
 /* Measurement: average duration (ms) of one launch of k_p2g, k_grid, k_g2p
  * and the binning, each launched `reps` times back to back between two
  * hipEvents on `stream` (so event overhead is amortised); the launches use the
- * current substep's inputs (BC mask `bc_active`).  Particle state and bins are
+ * current substep's inputs (BC mask `bc_active`).  Fused pipeline: {k_fused
+ * (G2P + P2G), k_grid_f, binning, 0}.  Particle state and bins are
  * restored afterwards.  Synchronises `stream`. */
 int gsmpm_mpm_time_kernels(gsmpm_mpm* h, float dt, uint32_t bc_active, int32_t reps, float* ms4, void* stream);
 /* Diagnostics of the tile buckets the next substep reads: {active tiles, max

@@ -13,6 +13,20 @@ from scenarios import build_oracle_sim, lego_problem, oracle_run
 
 pytestmark = pytest.mark.gpu
 
+# both substep pipelines: the fused G2P2G one (default) and the per-phase one
+# (slabs, KEEP_GRID); the fused one re-bins every 10 substeps by default, the
+# "fused_r1" case every substep, "fused_r50" almost never (margin escapes)
+PIPES = ["fused", "phased"]
+
+
+def _pipe_over(pipe):
+    return {"phased": pipe == "phased"}
+
+
+def _set_rebin(s, pipe):
+    if pipe.startswith("fused_r"):
+        s._sim.set_rebin_interval(int(pipe[len("fused_r"):]))
+
 TOL = 1e-4
 # v and C are grid-velocity gradients (C = sum v_i dpos^T w 4/dx^2): with a stiff
 # stress model they amplify the float-atomic summation order by ~1/dx, so they get
@@ -45,13 +59,16 @@ def _compare(s, ref, fields=("x", "v", "C", "F_trial"), tol=TOL, extra=None):
     return errs
 
 
-def test_lego_config_A_parity(dev):
+@pytest.mark.parametrize("pipe", PIPES + ["fused_r1", "fused_r50"])
+def test_lego_config_A_parity(dev, pipe):
     """configs[0]: lego.json jelly (as written), 5k Gaussians, 64^3, 50 substeps."""
     from gpu_helpers import dropin_sim
     prob = lego_problem(5000, 64)
     ref, imps, ops = build_oracle_sim(prob)
     dt = prob["cfg"]["substep_dt"]
-    s, args = dropin_sim(prob, dev)
+    s, args = dropin_sim(prob, dev, **_pipe_over(pipe))
+    _set_rebin(s, pipe)
+    assert s._sim.pipeline == ("phased" if pipe == "phased" else "fused")
     t = oracle_run(ref, imps, ops, dt, 50)
     for _ in range(50):
         s.p2g2p(dt)
@@ -65,14 +82,15 @@ def test_lego_config_A_parity(dev):
     assert rel_err(R, ref.R) < TOL
 
 
+@pytest.mark.parametrize("pipe", PIPES)
 @pytest.mark.parametrize("material,quirk", [("metal", True), ("sand", True), ("foam", True), ("jelly", False)])
-def test_materials_parity(dev, material, quirk):
+def test_materials_parity(dev, material, quirk, pipe):
     """Return maps + SVD stress (metal/sand/foam) and FCR jelly (F3 fixed), 30 substeps."""
     from gpu_helpers import dropin_sim
     prob = lego_problem(4000, 48)
     ref, imps, ops = build_oracle_sim(prob, material=material, jelly_quirk=quirk)
     dt = prob["cfg"]["substep_dt"]
-    s, _ = dropin_sim(prob, dev, material=material, jelly_fcr=not quirk)
+    s, _ = dropin_sim(prob, dev, material=material, jelly_fcr=not quirk, **_pipe_over(pipe))
     oracle_run(ref, imps, ops, dt, 30)
     for _ in range(30):
         s.p2g2p(dt)
@@ -83,7 +101,8 @@ def test_materials_parity(dev, material, quirk):
         assert rel_err(y, ref.yield_stress) < extra["yield"]
 
 
-def test_impulse_window(dev):
+@pytest.mark.parametrize("pipe", PIPES)
+def test_impulse_window(dev, pipe):
     """ImpulseBC active on a host-decided window mid-run (boundary_conditions.py:41-45)."""
     from gpu_helpers import dropin_sim
     prob = lego_problem(3000, 48)
@@ -93,14 +112,15 @@ def test_impulse_window(dev):
             d["force"] = [-80.0, 0.0, 30.0]
     ref, imps, ops = build_oracle_sim(prob)
     dt = prob["cfg"]["substep_dt"]
-    s, _ = dropin_sim(prob, dev)
+    s, _ = dropin_sim(prob, dev, **_pipe_over(pipe))
     oracle_run(ref, imps, ops, dt, 40)
     for _ in range(40):
         s.p2g2p(dt)
     _compare(s, ref)
 
 
-def test_eager_equals_graph(dev):
+@pytest.mark.parametrize("pipe", PIPES)
+def test_eager_equals_graph(dev, pipe):
     """Per-substep launches and the cached hipGraph replay give identical state."""
     import torch
     from gsmpm.sim import Simulator
@@ -109,7 +129,7 @@ def test_eager_equals_graph(dev):
     outs = []
     for graph in (False, True):
         sim = Simulator(len(prob["x"]), n_grid=48, material="metal", E=cfg["E"], nu=cfg["nu"],
-                        density=cfg["density"], gravity=cfg["gravity"], use_graph=graph)
+                        density=cfg["density"], gravity=cfg["gravity"], use_graph=graph, phased=pipe == "phased")
         t = lambda a: torch.from_numpy(a).to(dev)
         sim.set_particles(t(prob["x"]), t(prob["cov"]), t(prob["vol"]))
         b = sim.add_fixed_cube([1.0, 1.2, 0.5], [1.0, 0.8, 0.3])
@@ -119,14 +139,15 @@ def test_eager_equals_graph(dev):
     assert rel_err(outs[0], outs[1]) < 1e-6
 
 
-def test_resort_keeps_caller_order(dev):
+@pytest.mark.parametrize("pipe", PIPES)
+def test_resort_keeps_caller_order(dev, pipe):
     """Device Morton re-sorts between substeps only permute storage: fields read
     back in caller order and still match the oracle."""
     from gpu_helpers import dropin_sim
     prob = lego_problem(3000, 48)
     ref, imps, ops = build_oracle_sim(prob)
     dt = prob["cfg"]["substep_dt"]
-    s, _ = dropin_sim(prob, dev)
+    s, _ = dropin_sim(prob, dev, **_pipe_over(pipe))
     s._sim.resort(interval=7)
     oracle_run(ref, imps, ops, dt, 60)
     for k in range(60):
@@ -140,15 +161,55 @@ def test_resort_keeps_caller_order(dev):
     assert rel_err(cov, ref.cov) < TOL
 
 
-def test_large_grid_binning_path(dev):
-    """> 8192 tiles (176^3 -> 10,648 tiles) takes the multi-workgroup scan +
-    scatter binning instead of the fused one; same parity bar."""
+@pytest.mark.parametrize("pipe", PIPES)
+def test_large_grid_binning_path(dev, pipe):
+    """> 8192 tiles (176^3 -> 10,648 8^3 tiles, 10,672 8x8x7 tiles) takes the
+    multi-workgroup scan + scatter binning instead of the fused one; same parity bar."""
     from gpu_helpers import dropin_sim
     prob = lego_problem(3000, 176)
     ref, imps, ops = build_oracle_sim(prob)
     dt = prob["cfg"]["substep_dt"]
-    s, _ = dropin_sim(prob, dev)
+    s, _ = dropin_sim(prob, dev, **_pipe_over(pipe))
     oracle_run(ref, imps, ops, dt, 12)
     for _ in range(12):
         s.p2g2p(dt)
     _compare(s, ref)
+
+
+@pytest.mark.parametrize("material", ["jelly", "metal"])
+def test_fused_margin_escapes(dev, material):
+    """Fused pipeline with bins kept for 50 substeps while a swirl moves
+    particles ~0.3 cells per substep (9 cells over the run): most particles
+    leave their chunk's one-cell window margin and take the global gather /
+    float-atomic scatter path, and every grid update sweeps all tiles.  Same
+    parity bar as the binned path."""
+    import torch
+    import oracle as O
+    from gsmpm.sim import Simulator
+    prob = lego_problem(3000, 48)
+    cfg = prob["cfg"]
+    x = prob["x"].astype(np.float32)
+    c = x.mean(0)
+    r = x - c
+    v0 = (200.0 * np.stack([-r[:, 1], r[:, 0], 0.3 * r[:, 0]], 1)).astype(np.float32)
+    dt = 1e-4
+    dx = cfg["grid_extent"] / 48
+    assert np.abs(v0).max() * dt * 30 > 2 * dx  # beyond the margin within the run
+    kw = dict(n_grid=48, grid_extent=cfg["grid_extent"], material=material, E=cfg["E"], nu=cfg["nu"],
+              density=cfg["density"], gravity=cfg["gravity"])
+    ref = O.OracleMPM(x, prob["cov"], prob["vol"], v=v0, **kw)
+    ref.add_collider([0.0, 0.0, 0.4], [0.0, 0.0, 1.0], 0.0)
+    sim = Simulator(len(x), **kw)
+    sim.set_rebin_interval(50)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    sim.set_particles(t(x), t(prob["cov"]), t(prob["vol"]), t(v0))
+    sim.add_plane_collider([0.0, 0.0, 0.4], [0.0, 0.0, 1.0], 0.0)
+    assert sim.pipeline == "fused"
+    for _ in range(30):
+        ref.substep(dt, [], [1])
+    sim.step(dt, [0xFFFFFFFF] * 30)
+    got = {"x": sim.get("x"), "v": sim.get("v"), "C": sim.get("C"), "F_trial": sim.get("F_trial")}
+    exp = {"x": ref.x, "v": ref.v, "C": ref.C, "F_trial": ref.F_trial}
+    for k in got:
+        e = rel_err(got[k].cpu().numpy().reshape(exp[k].shape), exp[k])
+        assert e < TOL_DERIVED.get(k, TOL), (k, e)

@@ -1,0 +1,43 @@
+"""Workgroup timeline of one fused-pipeline k_fused launch (G2P + P2G) on the
+bench scene (GPU diagnostic).  Stamps: 0 start, 2 window staged, 3 G2P done,
+4 scatter done, 1 end (s_memrealtime, 100 MHz)."""
+import os, sys, ctypes
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..', 'gaussian-splatting-mpm_amd'))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
+import numpy as np, torch
+import bench
+from gsmpm.bc import substep_masks
+from gsmpm._lib import LIB, stream_of
+class A: particles = int(os.environ.get('N', 100000)); n_grid = int(os.environ.get('NG', 128)); config = 'lego.json'; material = os.environ.get('MAT')
+dev = torch.device('cuda:0')
+scene = bench.build_scene(A, dev)
+sim, specs = bench.make_sim(scene, dev)
+sa = scene['sargs']
+masks, t = substep_masks(specs, 0.0, sa.substep_dt, 300)
+sim.step(sa.substep_dt, masks[:100]); sim.step(sa.substep_dt, masks[100:200])
+print('stats', sim.debug_stats(), 'pipeline', sim.pipeline)
+ms = sim.profile(sa.substep_dt, masks[200:203])
+print('event ms K/grid/bins per 3 substeps', ms)
+buf = np.zeros((3, 4096, 8), np.uint64)
+LIB.gsmpm_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), stream_of(dev))
+b = buf[0].astype(np.int64)
+b = b[b[:, 0] > 0]
+t0 = b[:, 0].min()
+ok = b[:, 2] > 0
+dur = (b[:, 1] - b[:, 0]) / 100
+print(f"k_fused: {len(b)} WGs ({ok.sum()} with a chunk); start spread {(b[:,0].max()-t0)/100:.1f} us; end {(b[:,1].max()-t0)/100:.1f} us")
+print("  WG dur percentiles 50/90/99/max:", np.percentile(dur[ok], [50, 90, 99, 100]).round(2))
+seg = lambda a, c: (b[ok, c] - b[ok, a]) / 100
+for name, a, c in (("start->staged", 0, 2), ("staged->g2p", 2, 3), ("g2p->scattered", 3, 4), ("scattered->end", 4, 1)):
+    x = seg(a, c)
+    print(f"  {name}: median {np.median(x):.2f} p90 {np.percentile(x, 90):.2f} max {x.max():.2f}")
+st = (b[ok, 0] - t0) / 100
+print("  start histogram", np.histogram(st, bins=10)[0].tolist(), "edges", np.histogram(st, bins=10)[1].round(1).tolist())
+print("  WGs per XCC", np.bincount(b[ok, 7] & 0xf).tolist())
+cnt = b[ok, 5]
+print("  chunk sizes: mean", cnt.mean().round(1), "<=64:", (cnt <= 64).sum(), ">=200:", (cnt >= 200).sum())
+big = cnt >= 200
+print("  dur by size >=200 median", np.median(dur[ok][big]).round(2), "<64 median", np.median(dur[ok][cnt < 64]).round(2))
+# second-chunk WGs (grid-stride): count WGs whose end - start >> single chunk
+ms2 = sim.time_kernels(sa.substep_dt, masks[203], reps=20)
+print('time_kernels K/grid/bins', ms2)
