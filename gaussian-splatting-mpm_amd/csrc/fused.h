@@ -71,23 +71,64 @@ __device__ __forceinline__ int ftile_of(const float (&x)[3], const GridDims& g, 
   return ok ? (tc[0] * tl.td1 + tc[1]) * tl.td2 + tc[2] : tl.ntiles;
 }
 
-// The window of tile t (nodes [o - 1, o + T + 3) per axis) reaches into the
-// 27 tiles t + {-1, 0, 1}^3: the first reservation in t flags them for the
-// grid update (idempotent plain stores).
-__device__ __noinline__ void mark27(int* __restrict__ tflag, int t, int td0, int td1, int td2) {
+// Touched tiles.  At binning time a tile's particles have their base cell in
+// the tile, so their stencils reach the tiles t + {0, 1}^3: the first
+// reservation in t flags those (idempotent plain stores).  A particle that
+// later moves below its tile (base = tile origin - 1 on some axis) also
+// reaches the lower neighbours; k_fused adds those to the touched list when
+// it first sees such a particle in a chunk (add_lower_tiles).
+__device__ __noinline__ void mark8(int* __restrict__ tflag, int t, int td0, int td1, int td2) {
   const int tz = t % td2, ty = (t / td2) % td1, tx = t / (td1 * td2);
-  for (int a = -1; a <= 1; ++a)
-    for (int b = -1; b <= 1; ++b)
-      for (int c = -1; c <= 1; ++c) {
-        const int x = tx + a, y = ty + b, z = tz + c;
-        if ((unsigned)x < (unsigned)td0 && (unsigned)y < (unsigned)td1 && (unsigned)z < (unsigned)td2)
-          tflag[(x * td1 + y) * td2 + z] = 1;
-      }
+  for (int a = 0; a <= 1; ++a)
+    for (int b = 0; b <= 1; ++b)
+      for (int c = 0; c <= 1; ++c)
+        if (tx + a < td0 && ty + b < td1 && tz + c < td2) tflag[((tx + a) * td1 + ty + b) * td2 + tz + c] = 1;
 }
 __device__ __forceinline__ int reserve_f(const BinOutF& bo, int t, int c) {
   const int old = atomicAdd(&bo.count[t], c);
-  if (old == 0 && t < bo.tl.ntiles) mark27(bo.tflag, t, bo.tl.td0, bo.tl.td1, bo.tl.td2);
+  if (old == 0 && t < bo.tl.ntiles) mark8(bo.tflag, t, bo.tl.td0, bo.tl.td1, bo.tl.td2);
   return old;
+}
+
+// The touched list of the bins a k_fused launch reads (the grid update that
+// follows walks it) and the chunk records, whose .w holds the lower-neighbour
+// axes already added for the chunk.
+struct Touch {
+  int* tflag;
+  int* touched;
+  int* nchunk;  // [1] = touched count
+  int4* chunk;
+  int* cbox;    // [max_chunks] stencil box of the chunk's last P2G (packed, window coordinates)
+  int* tbox;    // [ntiles] the same per tile (the full window when the tile has several chunks)
+};
+
+// Stencil boxes: lo/hi window coordinates (0..11) per axis in 4-bit fields,
+// lo0 | lo1 << 4 | lo2 << 8 | hi0 << 12 | hi1 << 16 | hi2 << 20.  The P2G of
+// a chunk writes only the nodes inside its box, the next G2P of the chunk
+// stages only those (the particles have not moved in between), and the grid
+// update reads a tile's windows only inside its box.
+constexpr int kFullBox = 0 | (0 << 4) | (0 << 8) | ((kFW0 - 1) << 12) | ((kFW1 - 1) << 16) | ((kFW2 - 1) << 20);
+__device__ __forceinline__ void box_unpack(int b, int (&lo)[3], int (&hi)[3]) {
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+    lo[d] = (b >> (4 * d)) & 15;
+    hi[d] = (b >> (12 + 4 * d)) & 15;
+  }
+}
+
+// Lanes 0..26: add the tiles t + a, a_d in {-1 if d in lo, 0, 1}, with some
+// a_d = -1, that are not yet flagged (one append per tile: the flag CAS).
+__device__ __forceinline__ void add_lower_tiles(const Touch& tc, const FTiles& tl, int tx, int ty, int tz, int lo) {
+  const int e = threadIdx.x;
+  if (e < 27) {
+    const int a = e / 9 - 1, b = (e / 3) % 3 - 1, c = e % 3 - 1;
+    const bool need = (a < 0 || b < 0 || c < 0) && (a >= 0 || (lo & 1)) && (b >= 0 || (lo & 2)) && (c >= 0 || (lo & 4));
+    const int x = tx + a, y = ty + b, z = tz + c;
+    if (need && (unsigned)x < (unsigned)tl.td0 && (unsigned)y < (unsigned)tl.td1 && (unsigned)z < (unsigned)tl.td2) {
+      const int t = (x * tl.td1 + y) * tl.td2 + z;
+      if (atomicCAS(&tc.tflag[t], 0, 1) == 0) tc.touched[atomicAdd(&tc.nchunk[1], 1)] = t;
+    }
+  }
 }
 
 // base cell of a particle as bspline() computes it
@@ -113,16 +154,20 @@ __device__ __forceinline__ bool in_grid(const float (&x)[3], const GridDims& g) 
 
 // MODE bit 1: G2P of the previous grid update; bit 2: P2G of this substep.
 // `bin` (uniform): re-bin the particles by their new x into `bo`.
+// Particle storage is in bin order (permuted at every binning), so chunk w's
+// particles are storage rows [first, first + cnt).
 template <int MAT, int MODE>
-__global__ __launch_bounds__(256) void k_fused(Particles ps, GridDims g, FTiles tl, ChunkIn ck, BinOutF bo, int bin,
-                                               const float4* __restrict__ gvel, const BcTable* __restrict__ bct,
-                                               uint32_t mask, float dt, MatConsts mc, float4* __restrict__ slots,
-                                               float4* __restrict__ gacc, int* __restrict__ esc) {
+__global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTiles tl, ChunkIn ck, Touch tc, BinOutF bo,
+                                               int bin, int use_box, const float4* __restrict__ gvel,
+                                               const BcTable* __restrict__ bct, uint32_t mask, float dt, MatConsts mc,
+                                               float4* __restrict__ slots, float4* __restrict__ gacc,
+                                               int* __restrict__ esc) {
   constexpr bool G2P = (MODE & 1) != 0, P2G = (MODE & 2) != 0;
   // channel-planar u64 accumulators; the G2P v window aliases them (it is
   // consumed before the accumulators are zeroed)
   __shared__ unsigned long long s_acc[4 * kFWin];
   __shared__ float s_max[4];
+  __shared__ int s_mxy[4], s_mz[4];
   __shared__ int s_cnt[27], s_base[27];
   float4* s_win = reinterpret_cast<float4*>(s_acc);
   const int ng = g.ng;
@@ -141,7 +186,7 @@ __global__ __launch_bounds__(256) void k_fused(Particles ps, GridDims g, FTiles 
     float x[3] = {0.f, 0.f, 0.f}, v[3] = {0.f, 0.f, 0.f}, C[3][3], F[3][3], m = 0.f;
     // particle loads first: their round trips overlap the window staging
     if (k < cnt) {
-      p = ck.list[first + k];
+      p = first + k;
 #pragma unroll
       for (int d = 0; d < 3; ++d) x[d] = ps.ld(PX + d, p);
       if (G2P || MAT != 0) {
@@ -158,19 +203,29 @@ __global__ __launch_bounds__(256) void k_fused(Particles ps, GridDims g, FTiles 
     }
     if constexpr (G2P) {
       if (!outside) {
+        // the chunk's stencil box from its last P2G (particles unmoved since), else the whole window
+        int lo[3], hi[3];
+        box_unpack((use_box & 1) ? tc.cbox[w] : kFullBox, lo, hi);
+        const int n1 = hi[1] - lo[1] + 1, n2 = hi[2] - lo[2] + 1, n12 = n1 * n2;
+        const int nvol = (hi[0] - lo[0] + 1) * n12;
+        const float r12 = 1.0f / (float)n12, r2 = 1.0f / (float)n2;  // exact floor for q < 2^11
         float4 gv[7];
+        int dst[7];
 #pragma unroll
         for (int u = 0; u < 7; ++u) {
-          const int q = min(k + u * 256, kFWin - 1);
-          const int a = q / (kFW1 * kFW2), b = (q / kFW2) % kFW1, c = q % kFW2;
-          const int ix = o0 + a, iy = o1 + b, iz = o2 + c;
+          const int q = min(k + u * 256, nvol - 1);
+          const int a = (int)(((float)q + 0.5f) * r12), rem = q - a * n12;
+          const int b = (int)(((float)rem + 0.5f) * r2), c = rem - b * n2;
+          const int wa = lo[0] + a, wb = lo[1] + b, wc = lo[2] + c;
+          dst[u] = (wa * kFW1 + wb) * kFW2 + wc;
+          const int ix = o0 + wa, iy = o1 + wb, iz = o2 + wc;
           const bool in = (unsigned)ix < (unsigned)ng && (unsigned)iy < (unsigned)ng && (unsigned)iz < (unsigned)ng;
           gv[u] = gvel[in ? ((size_t)ix * ng + iy) * ng + iz : 0];
           if (!in) gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
         for (int u = 0; u < 7; ++u)
-          if (k + u * 256 < kFWin) s_win[k + u * 256] = gv[u];
+          if (k + u * 256 < nvol) s_win[dst[u]] = gv[u];
       }
       if (k < 27) s_cnt[k] = 0;
       __syncthreads();
@@ -187,7 +242,7 @@ __global__ __launch_bounds__(256) void k_fused(Particles ps, GridDims g, FTiles 
         int b[3];
         base_of(x, g.inv_dx, b);
         float gvd[3][3];
-        if (!outside && in_window(b, o0, o1, o2)) {
+        if (!outside && in_grid(x, g) && in_window(b, o0, o1, o2)) {
           g2p_gather(x, g,
                      [&](const int (&base)[3], int i, int j, int kk) {
                        const float4* wb = s_win + ((base[0] - o0) * kFW1 + (base[1] - o1)) * kFW2 + (base[2] - o2);
@@ -311,18 +366,50 @@ __global__ __launch_bounds__(256) void k_fused(Particles ps, GridDims g, FTiles 
         __syncthreads();
         continue;  // workgroup-uniform
       }
+      int b[3];
+      base_of(x, g.inv_dx, b);
+      const bool win = k < cnt && in_grid(x, g) && in_window(b, o0, o1, o2);
+      // window coordinates covered by this particle's stencil, as per-axis bit masks
+      int mxy = win ? (7 << (b[0] - o0)) | (7 << (16 + b[1] - o1)) : 0;
+      int mz = win ? 7 << (b[2] - o2) : 0;
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) bound = fmaxf(bound, __shfl_xor(bound, o));
-      if ((k & 63) == 0) s_max[k >> 6] = bound;
+      for (int o = 32; o > 0; o >>= 1) {
+        bound = fmaxf(bound, __shfl_xor(bound, o));
+        mxy |= __shfl_xor(mxy, o);
+        mz |= __shfl_xor(mz, o);
+      }
+      if ((k & 63) == 0) {
+        s_max[k >> 6] = bound;
+        s_mxy[k >> 6] = mxy;
+        s_mz[k >> 6] = mz;
+      }
       __syncthreads();  // also orders the zeroing before the adds
       const float bmax = fmaxf(fmaxf(s_max[0], s_max[1]), fmaxf(s_max[2], s_max[3]));
+      const int Mxy = s_mxy[0] | s_mxy[1] | s_mxy[2] | s_mxy[3], Mz = s_mz[0] | s_mz[1] | s_mz[2] | s_mz[3];
+      const int Mx = Mxy & 0xffff, My = (unsigned)Mxy >> 16;
+      // axes on which some stencil reaches below the tile (window coordinate 0)
+      const int lo_all = (Mx & 1) | ((My & 1) << 1) | ((Mz & 1) << 2);
+      if (lo_all & ~cr.w) {  // workgroup-uniform; rare (a new axis since the binning)
+        add_lower_tiles(tc, tl, tx, ty, tz, (lo_all | cr.w) & 7);
+        if (k == 0) tc.chunk[w].w = lo_all | cr.w;
+      }
+      // stencil box of the chunk (empty chunk window: a 1-node box)
+      int box = kFullBox;
+      if (Mx && My && Mz)
+        box = (__builtin_ctz(Mx)) | (__builtin_ctz(My) << 4) | (__builtin_ctz(Mz) << 8) | ((31 - __builtin_clz(Mx)) << 12) |
+              ((31 - __builtin_clz(My)) << 16) | ((31 - __builtin_clz(Mz)) << 20);
+      else
+        box = 0;
+      if (k == 0) {
+        tc.cbox[w] = box;
+        tc.tbox[t] = (cr.w & 8) ? kFullBox : box;  // tiles with several chunks: whole windows
+      }
+      if ((cr.w & 8) || (use_box & 2)) box = kFullBox;
       int ebits;
       frexpf(bmax, &ebits);
       const int S = bmax > 0.f ? 50 - ebits : 0;  // see k_p2g
       if (k < cnt) {
-        int b[3];
-        base_of(x, g.inv_dx, b);
-        if (in_grid(x, g) && in_window(b, o0, o1, o2)) {
+        if (win) {
           int bb[3];
           float fx[3], ww[3][3], dw[3][3];
           bspline(x, g.inv_dx, bb, fx, ww, dw);
@@ -335,92 +422,123 @@ __global__ __launch_bounds__(256) void k_fused(Particles ps, GridDims g, FTiles 
       }
       __syncthreads();
       if (w == (int)blockIdx.x) stamp(SK, 4);
-      float* dst = reinterpret_cast<float*>(slots + (size_t)w * kFWin);
-      for (int q = k; q < kFWin * 4; q += 256)
-        dst[q] = (float)ldexp((double)(long long)s_acc[(q & 3) * kFWin + (q >> 2)], -S);
+      {
+        int lo[3], hi[3];
+        box_unpack(box, lo, hi);
+        const int n1 = hi[1] - lo[1] + 1, n2 = hi[2] - lo[2] + 1, n12 = n1 * n2;
+        const int nvol = (hi[0] - lo[0] + 1) * n12;
+        const float r12 = 1.0f / (float)n12, r2 = 1.0f / (float)n2;
+        float4* dst = slots + (size_t)w * kFWin;
+        for (int q = k; q < nvol; q += 256) {
+          const int a = (int)(((float)q + 0.5f) * r12), rem = q - a * n12;
+          const int bq = (int)(((float)rem + 0.5f) * r2), c = rem - bq * n2;
+          const int node = ((lo[0] + a) * kFW1 + lo[1] + bq) * kFW2 + lo[2] + c;
+          float4 r;
+          r.x = (float)ldexp((double)(long long)s_acc[0 * kFWin + node], -S);
+          r.y = (float)ldexp((double)(long long)s_acc[1 * kFWin + node], -S);
+          r.z = (float)ldexp((double)(long long)s_acc[2 * kFWin + node], -S);
+          r.w = (float)ldexp((double)(long long)s_acc[3 * kFWin + node], -S);
+          dst[node] = r;
+        }
+      }
       __syncthreads();  // LDS reuse by the next chunk
     }
   }
   stamp(SK, 1);
 }
 
-// Chunk ranges of the 27 tiles whose windows reach tile (ti, tj, tk) -> LDS
-// (lanes 0..26; caller syncs).
-__device__ __forceinline__ void load_cover27(const ChunkIn& ck, const FTiles& tl, int ti, int tj, int tk, int* s_c0,
-                                             int* s_nc) {
+// Chunk ranges and stencil boxes of the 27 tiles whose windows reach tile
+// (ti, tj, tk) -> LDS (lanes 0..26; caller syncs).
+__device__ __forceinline__ void load_cover27(const ChunkIn& ck, const int* __restrict__ tbox, const FTiles& tl, int ti,
+                                             int tj, int tk, int* s_c0, int* s_nc, int* s_bx) {
   const int e = threadIdx.x;
   if (e < 27) {
     const int x = ti + e / 9 - 1, y = tj + (e / 3) % 3 - 1, z = tk + e % 3 - 1;
-    int c0 = 0, nc = 0;
+    int c0 = 0, nc = 0, bx = 0;
     if ((unsigned)x < (unsigned)tl.td0 && (unsigned)y < (unsigned)tl.td1 && (unsigned)z < (unsigned)tl.td2) {
       const int t = (x * tl.td1 + y) * tl.td2 + z;
-      nc = (ck.count[t] + kChunk - 1) / kChunk;
+      const int cnt = ck.count[t];
       c0 = ck.cbase[t];
+      bx = tbox ? tbox[t] : kFullBox;
+      nc = (cnt + kChunk - 1) / kChunk;
     }
     s_c0[e] = c0;
     s_nc[e] = nc;
+    s_bx[e] = bx;
   }
 }
 
-// Sum of the chunk windows covering owned node (l0, l1, l2) of a tile.  Per
-// axis a node lies in its own tile's window and, when l < 3, in the lower
-// neighbour's (l + T + 1 < T + 4), when l = T - 1 in the upper one's: <= 8
-// windows, read as 8 unconditional loads (absent ones from the zero slot).
-__device__ __forceinline__ float4 node_sum_f(const float4* __restrict__ slots, int max_chunks, const int* s_c0,
-                                             const int* s_nc, int l0, int l1, int l2) {
+// The <= 8 window reads of owned node (l0, l1, l2) of a tile.  Per axis a node
+// lies in its own tile's window and, when l < 3, in the lower neighbour's
+// (l + T + 1 < T + 4), when l = T - 1 in the upper one's.  A read outside the
+// covering tile's stencil box (nothing was scattered there this substep) is
+// redirected to the all-zero slot, so the 8 loads stay unconditional.
+struct NodeReads {
+  int off[8];  // slot offsets (float4 units) of the first chunk of each covering tile
+  int extra;   // bit e: covering tile e has further chunks
+};
+// covering tile e of node (l0, l1, l2): its index in the 27-neighbourhood and the node's window offset there
+__device__ __forceinline__ void node_cover(int l0, int l1, int l2, int e, int& ci, int& loc) {
   const int sec0 = l0 < 3 ? -1 : (l0 == kFT0 - 1 ? 1 : 0);
   const int sec1 = l1 < 3 ? -1 : (l1 == kFT1 - 1 ? 1 : 0);
   const int sec2 = l2 < 3 ? -1 : (l2 == kFT2 - 1 ? 1 : 0);
-  float4 s8[8];
-  int extra = 0;
-  int loc8[8], ci8[8];
+  const int a = (e >> 2) ? sec0 : 0, b = ((e >> 1) & 1) ? sec1 : 0, c = (e & 1) ? sec2 : 0;
+  ci = (a + 1) * 9 + (b + 1) * 3 + (c + 1);
+  loc = ((l0 - a * kFT0 + 1) * kFW1 + (l1 - b * kFT1 + 1)) * kFW2 + (l2 - c * kFT2 + 1);
+}
+__device__ __forceinline__ void node_reads(int max_chunks, const int* s_c0, const int* s_nc, const int* s_bx, int l0,
+                                           int l1, int l2, NodeReads& r) {
+  const int sec0 = l0 < 3 ? -1 : (l0 == kFT0 - 1 ? 1 : 0);
+  const int sec1 = l1 < 3 ? -1 : (l1 == kFT1 - 1 ? 1 : 0);
+  const int sec2 = l2 < 3 ? -1 : (l2 == kFT2 - 1 ? 1 : 0);
+  r.extra = 0;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int ax = e >> 2, ay = (e >> 1) & 1, az = e & 1;
     const int a = ax ? sec0 : 0, b = ay ? sec1 : 0, c = az ? sec2 : 0;
     bool on = (!ax || sec0) && (!ay || sec1) && (!az || sec2);
     const int ci = (a + 1) * 9 + (b + 1) * 3 + (c + 1);
-    const int nc = s_nc[ci];
-    on = on && nc > 0;
-    const int loc = ((l0 - a * kFT0 + 1) * kFW1 + (l1 - b * kFT1 + 1)) * kFW2 + (l2 - c * kFT2 + 1);
-    loc8[e] = loc;
-    ci8[e] = ci;
-    const size_t off = on ? (size_t)s_c0[ci] * kFWin + loc : (size_t)max_chunks * kFWin;
-    s8[e] = slots[off];
-    extra |= (on && nc > 1) ? (1 << e) : 0;
+    const int nc = s_nc[ci], bx = s_bx[ci];
+    const int w0 = l0 - a * kFT0 + 1, w1 = l1 - b * kFT1 + 1, w2 = l2 - c * kFT2 + 1;
+    on = on && nc > 0 && w0 >= (bx & 15) && w1 >= ((bx >> 4) & 15) && w2 >= ((bx >> 8) & 15) &&
+         w0 <= ((bx >> 12) & 15) && w1 <= ((bx >> 16) & 15) && w2 <= ((bx >> 20) & 15);
+    const int loc = (w0 * kFW1 + w1) * kFW2 + w2;
+    r.off[e] = on ? s_c0[ci] * kFWin + loc : max_chunks * kFWin;
+    r.extra |= (on && nc > 1) ? (1 << e) : 0;
   }
-  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    acc.x += s8[e].x;
-    acc.y += s8[e].y;
-    acc.z += s8[e].z;
-    acc.w += s8[e].w;
-  }
+}
+__device__ __forceinline__ void add4(float4& a, const float4& b) {
+  a.x += b.x;
+  a.y += b.y;
+  a.z += b.z;
+  a.w += b.w;
+}
+// the further chunks of covering tiles with several (rare: tiles of > 256 particles)
+__device__ __forceinline__ void node_extra(const float4* __restrict__ slots, const int* s_c0, const int* s_nc, int l0,
+                                           int l1, int l2, int extra, float4& acc) {
   while (extra) {
     const int e = __builtin_ctz(extra);
     extra &= extra - 1;
-    const int ci = ci8[e], loc = loc8[e];
-    for (int w = s_c0[ci] + 1; w < s_c0[ci] + s_nc[ci]; ++w) {
-      const float4 sv = slots[(size_t)w * kFWin + loc];
-      acc.x += sv.x;
-      acc.y += sv.y;
-      acc.z += sv.z;
-      acc.w += sv.w;
-    }
+    int ci, loc;
+    node_cover(l0, l1, l2, e, ci, loc);
+    for (int w = s_c0[ci] + 1; w < s_c0[ci] + s_nc[ci]; ++w) add4(acc, slots[(size_t)w * kFWin + loc]);
   }
-  return acc;
 }
 
-// Grid update of the fused pipeline.  esc_in: some particle scattered through
-// gacc in the P2G this update consumes -> every tile, plus gacc (re-zeroed).
-// esc_clear: the flag the next P2G raises.  zc / zf (optional): the counts /
-// touched flags the next binning launch accumulates into.
-__global__ __launch_bounds__(512) void k_grid_f(GridDims g, FTiles tl, ChunkIn ck, const float4* __restrict__ slots,
-                                                float4* __restrict__ gacc, float4* __restrict__ gvel,
-                                                const BcTable* __restrict__ bct, GridStep gs,
-                                                const int* __restrict__ esc_in, int* __restrict__ esc_clear,
-                                                int* __restrict__ zc, int* __restrict__ zf) {
+// Grid update of the fused pipeline: one 448-lane workgroup per touched tile,
+// one owned node per lane (all 8 window reads in flight), 4 workgroups per CU
+// (<= 72 VGPRs) so a scene's ~1000 touched tiles run in one round.
+// esc_in: some particle scattered through gacc in the P2G this update consumes
+// -> every tile, plus gacc (re-zeroed).  esc_clear: the flag the next P2G
+// raises.  zc / zf (optional): the counts / touched flags the next binning
+// launch accumulates into.
+__global__ __launch_bounds__(kFTN) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_grid_f(GridDims g, FTiles tl, ChunkIn ck, const int* __restrict__ tbox,
+                                                    const float4* __restrict__ slots, float4* __restrict__ gacc,
+                                                    float4* __restrict__ gvel, const BcTable* __restrict__ bct,
+                                                    GridStep gs, const int* __restrict__ esc_in,
+                                                    int* __restrict__ esc_clear, int* __restrict__ zc,
+                                                    int* __restrict__ zf) {
+  stamp(3, 0);
   if (blockIdx.x == 0 && threadIdx.x == 0) *esc_clear = 0;
   if (zc) {
     for (int t = blockIdx.x * blockDim.x + threadIdx.x; t <= tl.ntiles; t += gridDim.x * blockDim.x) {
@@ -431,31 +549,39 @@ __global__ __launch_bounds__(512) void k_grid_f(GridDims g, FTiles tl, ChunkIn c
   const int ng = g.ng;
   const bool all = *esc_in != 0;
   const int ntouch = all ? tl.ntiles : ck.nchunk[1];
-  __shared__ int s_c0[27], s_nc[27];
+  __shared__ int s_c0[27], s_nc[27], s_bx[27];
+  const int q = threadIdx.x;
+  const int l0 = q / (kFT1 * kFT2), l1 = (q / kFT2) % kFT1, l2 = q % kFT2;
   for (int wt = blockIdx.x; wt < ntouch; wt += gridDim.x) {
     const int T = all ? wt : ck.touched[wt];
     int ti, tj, tk;
     ftile_decode(tl, T, ti, tj, tk);
     __syncthreads();  // readers of the previous tile's ranges are done
-    load_cover27(ck, tl, ti, tj, tk, s_c0, s_nc);
+    if (wt == (int)blockIdx.x) stamp(3, 2);
+    load_cover27(ck, tbox, tl, ti, tj, tk, s_c0, s_nc, s_bx);
     __syncthreads();
-    for (int q = threadIdx.x; q < kFTN; q += blockDim.x) {
-      const int l0 = q / (kFT1 * kFT2), l1 = (q / kFT2) % kFT1, l2 = q % kFT2;
-      const int i = ti * kFT0 + l0, j = tj * kFT1 + l1, k = tk * kFT2 + l2;
-      if (i >= ng || j >= ng || k >= ng) continue;
+    if (wt == (int)blockIdx.x) stamp(3, 3);
+    const int i = ti * kFT0 + l0, j = tj * kFT1 + l1, k = tk * kFT2 + l2;
+    if (i < ng && j < ng && k < ng) {
+      NodeReads r;
+      node_reads(tl.max_chunks, s_c0, s_nc, s_bx, l0, l1, l2, r);
+      float4 v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = slots[r.off[e]];
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) add4(a, v[e]);
+      node_extra(slots, s_c0, s_nc, l0, l1, l2, r.extra, a);
       const size_t idx = ((size_t)i * ng + j) * ng + k;
-      float4 a = node_sum_f(slots, tl.max_chunks, s_c0, s_nc, l0, l1, l2);
       if (all) {
-        const float4 o = gacc[idx];
-        a.x += o.x;
-        a.y += o.y;
-        a.z += o.z;
-        a.w += o.w;
+        add4(a, gacc[idx]);
         gacc[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
       gvel[idx] = node_update(a, i, j, k, g, gs, bct);
     }
+    if (wt == (int)blockIdx.x) stamp(3, 4);
   }
+  stamp(3, 1);
 }
 
 // bin every particle by its current x (set_particles / resort / set x)

@@ -48,7 +48,7 @@ constexpr int kChunk = 256;  // particles per work chunk (one per lane of a 256-
 
 // Workgroup timeline stamps (diagnostics): [kernel][wg][start, end] in
 // s_memrealtime ticks (100 MHz), written by lane 0 of the first 4096 workgroups.
-__device__ unsigned long long g_stamps[3][4096][8];
+__device__ unsigned long long g_stamps[4][4096][8];
 __device__ __forceinline__ void stamp(int kern, int slot) {
   if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[kern][blockIdx.x][slot] = __builtin_amdgcn_s_memrealtime();
 }
@@ -325,7 +325,6 @@ __global__ __launch_bounds__(256) void k_p2g(Particles ps, GridDims g, Tiles tl,
   // every channel on 16 of them: 75 % of LDS cycles were bank conflicts)
   __shared__ unsigned long long s_acc[4 * kWin];
   __shared__ float s_max[4];
-  const int ng = g.ng;
   stamp(0, 0);
   const int nch = ck.nchunk[0];
   for (int w = blockIdx.x; w < nch; w += gridDim.x) {
@@ -966,7 +965,10 @@ __global__ __launch_bounds__(256) void k_finish_bins(Tiles tl, const int* __rest
     const int cb = aux & 0xffff, rk = aux >> 16;
     const bool touched = (t + 1 < E ? (s_aux[t + 1] >> 16) : tot[2]) > rk;
     co.cbase[t] = cb;
-    for (int k = 0; k * kChunk < c; ++k) co.chunk[cb + k] = make_int4(t, off + k * kChunk, min(kChunk, c - k * kChunk), 0);
+    // .w bit 3: the tile has several chunks (the fused pipeline's k_fused keeps
+    // the lower-neighbour axes it added in bits 0..2)
+    for (int k = 0; k * kChunk < c; ++k)
+      co.chunk[cb + k] = make_int4(t, off + k * kChunk, min(kChunk, c - k * kChunk), c > kChunk ? 8 : 0);
     if (touched) {
       co.touched[rk] = t;
       const int tx = t / (tl.td * tl.td);
@@ -1058,7 +1060,7 @@ __global__ __launch_bounds__(1024) void k_scan_tiles(Tiles tl, const int* __rest
     co.cstart[t] = o[0];
     co.cbase[t] = o[1];
     for (int k = 0; k < v[1]; ++k)
-      co.chunk[o[1] + k] = make_int4(t, o[0] + k * kChunk, min(kChunk, v[0] - k * kChunk), 0);
+      co.chunk[o[1] + k] = make_int4(t, o[0] + k * kChunk, min(kChunk, v[0] - k * kChunk), v[0] > kChunk ? 8 : 0);
     if (v[2]) {
       co.touched[o[2]] = t;
       const int tx = t / (tl.td * tl.td);
@@ -1375,12 +1377,24 @@ struct gsmpm_mpm {
   int* ftflag[2] = {nullptr, nullptr};
   int* flist[2] = {nullptr, nullptr};
   int* fesc = nullptr;                    // [2] escape flags (alternating per grid update)
+  int* fcbox[2] = {nullptr, nullptr};     // [max_chunks] per-chunk stencil boxes (fused.h)
+  int* ftbox[2] = {nullptr, nullptr};     // [ntiles] per-tile stencil boxes
+  float* planes_alt = nullptr;            // the other particle-plane buffer: every binning permutes
+  int* orig_alt = nullptr;                //   storage into bin order, alternating planes / planes_alt
   int fbpar = 0;                          // parity of the bins the next k_fused reads
   int fep = 0;                            // escape flag the next P2G raises
   int rebin_interval = 10;                // substeps between re-binnings (fused pipeline)
+  int fdebug = 0;                         // GSMPM_FUSED_DEBUG bits: 1 no G2P box, 2 full-window stores
   std::map<std::vector<uint32_t>, hipGraphExec_t> graphs;
   std::map<std::vector<uint32_t>, int> graph_box_parity;
-  std::map<std::vector<uint32_t>, std::pair<int, int>> graph_fstate;  // (fbpar, fep) after the graph
+  struct FState {
+    int bpar, ep;
+    float* planes;
+    float* planes_alt;
+    int* orig;
+    int* orig_alt;
+  };
+  std::map<std::vector<uint32_t>, FState> graph_fstate;  // fused-pipeline state after the graph
 };
 
 namespace gsmpm {
@@ -1408,6 +1422,9 @@ static ChunkIn chunk_in_f(gsmpm_mpm* h, int c) {
 static ChunkOut chunk_out_f(gsmpm_mpm* h, int c) {
   return ChunkOut{h->fcstart[c], h->fcbase[c], h->fchunk[c], h->fnchunk[c], h->ftflag[c], h->ftouched[c],
                   h->escape, 0, INT_MAX};
+}
+static Touch touch_f(gsmpm_mpm* h, int c) {
+  return Touch{h->ftflag[c], h->ftouched[c], h->fnchunk[c], h->fchunk[c], h->fcbox[c], h->ftbox[c]};
 }
 static BinOutF bin_out_f(gsmpm_mpm* h, int c) { return BinOutF{h->fcount[c], h->ptile, h->pslot, h->ftflag[c], h->ftl}; }
 // k_finish_bins / the scan kernels only use ntiles and max_chunks of a Tiles
@@ -1460,7 +1477,22 @@ static int finish_binning_f(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_
   return finish_bins_on(h, ftiles_flat(h), h->fcount[c], chunk_out_f(h, c), h->flist[c], st, ev);
 }
 
-// (Re)build the fused pipeline's chunk lists of parity `fbpar` from the current x.
+// Storage into the bin order of parity c (list[c]: storage rows grouped by
+// tile): planes / orig gathered into the other buffer, which becomes current.
+static int permute_to_bins(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t* ev = nullptr) {
+  const hipEvent_t e0[2] = {ev ? ev[0] : nullptr, nullptr}, e1[2] = {nullptr, ev ? ev[1] : nullptr};
+  launch(ev ? e0 : nullptr, k_permute, dim3(div_up(h->n, 256), NPLANES), dim3(256), st, (const float*)h->planes,
+         h->planes_alt, h->n, h->np, (const int*)h->flist[c]);
+  launch(ev ? e1 : nullptr, k_permute_i, dim3(div_up(h->n, 256)), dim3(256), st, (const int*)h->orig, h->orig_alt,
+         h->n, (const int*)h->flist[c]);
+  GSMPM_LAUNCH_CHECK();
+  std::swap(h->planes, h->planes_alt);
+  std::swap(h->orig, h->orig_alt);
+  return GSMPM_OK;
+}
+
+// (Re)build the fused pipeline's chunk lists of parity `fbpar` from the current
+// x and permute storage into that bin order.
 static int rebin_f(gsmpm_mpm* h, hipStream_t st) {
   const int c = h->fbpar;
   GSMPM_HIP(hipMemsetAsync(h->fcount[c], 0, sizeof(int) * (h->ftl.ntiles + 1), st));
@@ -1468,7 +1500,8 @@ static int rebin_f(gsmpm_mpm* h, hipStream_t st) {
   GSMPM_HIP(hipMemsetAsync(h->fnchunk[c], 0, sizeof(int) * 2, st));
   hipLaunchKernelGGL(k_bin_all_f, dim3(div_up(h->n, 256)), dim3(256), 0, st, particles_of(h), h->g, bin_out_f(h, c));
   GSMPM_LAUNCH_CHECK();
-  return finish_binning_f(h, c, st);
+  int rc = finish_binning_f(h, c, st);
+  return rc ? rc : permute_to_bins(h, c, st);
 }
 
 // (Re)build the per-phase pipeline's chunk lists of parity `cur_box` from the current x.
@@ -1560,40 +1593,44 @@ static int launch_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc,
 static int fused_grid(gsmpm_mpm* h) { return std::min(h->ftl.max_chunks, 1024); }
 
 template <int MAT, int MODE>
-static void launch_fused_t(gsmpm_mpm* h, int c, const BinOutF& bo, int bin, uint32_t mask, float dt, int* esc,
-                           hipStream_t st, const hipEvent_t* ev) {
+static void launch_fused_t(gsmpm_mpm* h, int c, const BinOutF& bo, int bin, int use_box, uint32_t mask, float dt,
+                           int* esc, hipStream_t st, const hipEvent_t* ev) {
   launch(ev, k_fused<MAT, MODE>, dim3(fused_grid(h)), dim3(256), st, particles_of(h), h->g, h->ftl, chunk_in_f(h, c),
-         bo, bin, (const float4*)h->gvel, (const BcTable*)h->dev_bc, mask, dt, h->mc, h->fslots, h->gacc, esc);
+         touch_f(h, c), bo, bin, use_box, (const float4*)h->gvel, (const BcTable*)h->dev_bc, mask, dt, h->mc, h->fslots, h->gacc,
+         esc);
 }
 template <int MODE>
-static void launch_fused_m(gsmpm_mpm* h, int c, const BinOutF& bo, int bin, uint32_t mask, float dt, int* esc,
+static void launch_fused_m(gsmpm_mpm* h, int c, const BinOutF& bo, int bin, int ub, uint32_t mask, float dt, int* esc,
                            hipStream_t st, const hipEvent_t* ev) {
   switch (h->mat_kernel) {
-    case 0: launch_fused_t<0, MODE>(h, c, bo, bin, mask, dt, esc, st, ev); break;
-    case 1: launch_fused_t<1, MODE>(h, c, bo, bin, mask, dt, esc, st, ev); break;
-    case 2: launch_fused_t<2, MODE>(h, c, bo, bin, mask, dt, esc, st, ev); break;
-    case 3: launch_fused_t<3, MODE>(h, c, bo, bin, mask, dt, esc, st, ev); break;
-    default: launch_fused_t<4, MODE>(h, c, bo, bin, mask, dt, esc, st, ev); break;
+    case 0: launch_fused_t<0, MODE>(h, c, bo, bin, ub, mask, dt, esc, st, ev); break;
+    case 1: launch_fused_t<1, MODE>(h, c, bo, bin, ub, mask, dt, esc, st, ev); break;
+    case 2: launch_fused_t<2, MODE>(h, c, bo, bin, ub, mask, dt, esc, st, ev); break;
+    case 3: launch_fused_t<3, MODE>(h, c, bo, bin, ub, mask, dt, esc, st, ev); break;
+    default: launch_fused_t<4, MODE>(h, c, bo, bin, ub, mask, dt, esc, st, ev); break;
   }
 }
-// mode 1: G2P only, 2: P2G only, 3: G2P of the last grid update + P2G
-static int launch_fused(gsmpm_mpm* h, int mode, int c, bool bin, uint32_t mask, float dt, int* esc, hipStream_t st,
-                        const hipEvent_t* ev) {
+// mode 1: G2P only, 2: P2G only, 3: G2P of the last grid update + P2G.
+// use_box: the previous k_fused launch did the P2G of these same bins, so
+// its per-chunk stencil boxes bound this launch's G2P gathers.
+static int launch_fused(gsmpm_mpm* h, int mode, int c, bool bin, bool use_box, uint32_t mask, float dt, int* esc,
+                        hipStream_t st, const hipEvent_t* ev) {
   const BinOutF bo = bin_out_f(h, c ^ 1);
+  const int ub = (use_box && !(h->fdebug & 1) ? 1 : 0) | (h->fdebug & 2);
   if (mode == 1)
-    launch_fused_t<0, 1>(h, c, bo, bin ? 1 : 0, mask, dt, esc, st, ev);  // G2P does not depend on the material
+    launch_fused_t<0, 1>(h, c, bo, bin ? 1 : 0, ub, mask, dt, esc, st, ev);  // G2P does not depend on the material
   else if (mode == 2)
-    launch_fused_m<2>(h, c, bo, bin ? 1 : 0, mask, dt, esc, st, ev);
+    launch_fused_m<2>(h, c, bo, bin ? 1 : 0, ub, mask, dt, esc, st, ev);
   else
-    launch_fused_m<3>(h, c, bo, bin ? 1 : 0, mask, dt, esc, st, ev);
+    launch_fused_m<3>(h, c, bo, bin ? 1 : 0, ub, mask, dt, esc, st, ev);
   GSMPM_LAUNCH_CHECK();
   return GSMPM_OK;
 }
 
 static int launch_grid_f(gsmpm_mpm* h, int wp, float dt, uint32_t mask, int ep, int* zc, int* zf, hipStream_t st,
                          const hipEvent_t* ev) {
-  launch(ev, k_grid_f, dim3(std::min(h->ftl.ntiles, 1024)), dim3(512), st, h->g, h->ftl, chunk_in_f(h, wp),
-         (const float4*)h->fslots, h->gacc, h->gvel, (const BcTable*)h->dev_bc, grid_step(h, dt, mask),
+  launch(ev, k_grid_f, dim3(std::min(h->ftl.ntiles, 2048)), dim3(kFTN), st, h->g, h->ftl, chunk_in_f(h, wp),
+         (h->fdebug & 2) ? nullptr : (const int*)h->ftbox[wp], (const float4*)h->fslots, h->gacc, h->gvel, (const BcTable*)h->dev_bc, grid_step(h, dt, mask),
          (const int*)(h->fesc + ep), h->fesc + (ep ^ 1), zc, zf);
   GSMPM_LAUNCH_CHECK();
   return GSMPM_OK;
@@ -1609,6 +1646,7 @@ static int launch_substeps_f(gsmpm_mpm* h, float dt, int nsub, const uint32_t* b
   const int R = std::max(1, h->rebin_interval);
   int wp = bp;
   bool zeroed = false;  // counts / flags of parity bp ^ 1 zeroed by a grid launch since the last binning
+  bool boxed = false;   // the last k_fused launch did P2G on the bins parity bp
   for (int s = 0; s <= nsub; ++s) {
     const int mode = s == 0 ? 2 : (s == nsub ? 1 : 3);
     const bool bin = s == nsub || (s > 0 && s % R == 0);
@@ -1618,11 +1656,13 @@ static int launch_substeps_f(gsmpm_mpm* h, float dt, int nsub, const uint32_t* b
       GSMPM_HIP(hipMemsetAsync(h->fcount[bp ^ 1], 0, sizeof(int) * (h->ftl.ntiles + 1), st));
       GSMPM_HIP(hipMemsetAsync(h->ftflag[bp ^ 1], 0, sizeof(int) * h->ftl.ntiles, st));
     }
-    int rc = launch_fused(h, mode, bp, bin, mask, dt, h->fesc + ep, st, e8);
+    int rc = launch_fused(h, mode, bp, bin, boxed, mask, dt, h->fesc + ep, st, e8);
     if (rc) return rc;
     if (mode & 2) wp = bp;
+    boxed = (mode & 2) && !bin;
     if (bin) {
       rc = finish_binning_f(h, bp ^ 1, st, e8 ? e8 + 4 : nullptr);
+      if (!rc) rc = permute_to_bins(h, bp ^ 1, st, e8 ? e8 + 6 : nullptr);
       if (rc) return rc;
       bp ^= 1;
       zeroed = false;
@@ -1644,8 +1684,8 @@ static int launch_substeps_f(gsmpm_mpm* h, float dt, int nsub, const uint32_t* b
     GSMPM_HIP(hipStreamSynchronize(st));
     for (int s = 0; s <= nsub; ++s) {
       const bool bin = s == nsub || (s > 0 && s % R == 0);
-      for (int k = 0; k < 3; ++k) {
-        if ((k == 1 && s == nsub) || (k == 2 && !bin)) continue;
+      for (int k = 0; k < 4; ++k) {
+        if ((k == 1 && s == nsub) || (k >= 2 && !bin)) continue;
         float ms = 0.f;
         GSMPM_HIP(hipEventElapsedTime(&ms, ev[8 * s + 2 * k], ev[8 * s + 2 * k + 1]));
         kernel_ms[k] += ms;
@@ -1803,6 +1843,7 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
   if ((e = hipMalloc(&h->escape, sizeof(int))) != hipSuccess) return fail(e, "hipMalloc escape");
   // fused pipeline: 8 x 8 x 7-cell tiles (fused.h)
   h->fused = !(prm->flags & (GSMPM_FLAG_PHASED | GSMPM_FLAG_KEEP_GRID));
+  if (const char* dbg = std::getenv("GSMPM_FUSED_DEBUG")) h->fdebug = std::atoi(dbg);
   h->ftl.td0 = (h->g.ng + kFT0 - 1) / kFT0;
   h->ftl.td1 = (h->g.ng + kFT1 - 1) / kFT1;
   h->ftl.td2 = (h->g.ng + kFT2 - 1) / kFT2;
@@ -1826,10 +1867,19 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
         return fail(e, "hipMalloc tflag");
       if ((e = hipMalloc(&h->fnchunk[c], sizeof(int) * 2)) != hipSuccess) return fail(e, "hipMalloc nchunk");
       if ((e = hipMalloc(&h->flist[c], sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc list");
+      if ((e = hipMalloc(&h->fcbox[c], sizeof(int) * (size_t)h->ftl.max_chunks)) != hipSuccess)
+        return fail(e, "hipMalloc boxes");
+      if ((e = hipMalloc(&h->ftbox[c], sizeof(int) * (size_t)h->ftl.ntiles)) != hipSuccess)
+        return fail(e, "hipMalloc boxes");
       if ((e = hipMemset(h->fcount[c], 0, sizeof(int) * E)) != hipSuccess) return fail(e, "hipMemset");
       if ((e = hipMemset(h->ftflag[c], 0, sizeof(int) * (size_t)h->ftl.ntiles)) != hipSuccess) return fail(e, "hipMemset");
       if ((e = hipMemset(h->fnchunk[c], 0, sizeof(int) * 2)) != hipSuccess) return fail(e, "hipMemset");
     }
+    if ((e = hipMalloc(&h->planes_alt, sizeof(float) * (size_t)NPLANES * h->np)) != hipSuccess)
+      return fail(e, "hipMalloc planes");
+    if ((e = hipMemset(h->planes_alt, 0, sizeof(float) * (size_t)NPLANES * h->np)) != hipSuccess)
+      return fail(e, "hipMemset");
+    if ((e = hipMalloc(&h->orig_alt, sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc orig");
     if ((e = hipMalloc(&h->fesc, sizeof(int) * 2)) != hipSuccess) return fail(e, "hipMalloc escape flags");
     if ((e = hipMemset(h->fesc, 0, sizeof(int) * 2)) != hipSuccess) return fail(e, "hipMemset");
   }
@@ -1881,9 +1931,13 @@ int gsmpm_mpm_destroy(gsmpm_mpm* h) {
     (void)hipFree(h->ftflag[c]);
     (void)hipFree(h->fnchunk[c]);
     (void)hipFree(h->flist[c]);
+    (void)hipFree(h->fcbox[c]);
+    (void)hipFree(h->ftbox[c]);
   }
   (void)hipFree(h->fslots);
   (void)hipFree(h->fesc);
+  (void)hipFree(h->planes_alt);
+  (void)hipFree(h->orig_alt);
   (void)hipFree(h->ptile);
   (void)hipFree(h->escape);
   (void)hipFree(h->scan_part);
@@ -2017,7 +2071,9 @@ int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t nsub, const uint32_t* bc, voi
   }
   if (nsub == 0) return GSMPM_OK;
   hipStream_t st = (hipStream_t)stream;
-  if (!(h->prm.flags & GSMPM_FLAG_NO_SORT) && h->resort_interval > 0 && h->since_sort >= h->resort_interval) {
+  // the fused pipeline keeps storage in bin order; the per-phase one re-sorts
+  if (!use_fused(h) && !(h->prm.flags & GSMPM_FLAG_NO_SORT) && h->resort_interval > 0 &&
+      h->since_sort >= h->resort_interval) {
     int rc = resort(h, st);
     if (rc) return rc;
   }
@@ -2042,15 +2098,24 @@ int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t nsub, const uint32_t* bc, voi
   key.push_back((uint32_t)h->fbpar);
   key.push_back((uint32_t)h->fep);
   key.push_back((uint32_t)h->rebin_interval);
+  key.push_back(h->planes_alt && h->planes > h->planes_alt ? 1u : 0u);  // which particle buffer is current
   for (int s = 0; s < nsub; ++s) key.push_back(bc ? bc[s] : 0xffffffffu);
   auto it = h->graphs.find(key);
   if (it == h->graphs.end()) {
     if (h->graphs.size() >= 16) drop_graphs(h);
     hipGraph_t graph;
     int parity = h->cur_box, bp = h->fbpar, ep = h->fep;
+    const gsmpm_mpm::FState start{bp, ep, h->planes, h->planes_alt, h->orig, h->orig_alt};
     GSMPM_HIP(hipStreamBeginCapture(h->cap, hipStreamCaptureModeRelaxed));
     int rc = fz ? launch_substeps_f(h, dt, nsub, bc, h->cap, bp, ep) : launch_substeps(h, dt, nsub, bc, h->cap, parity);
     hipError_t e = hipStreamEndCapture(h->cap, &graph);
+    // capture swapped the particle buffers on the host: keep the end state for
+    // the key and start the replay below from the key's state
+    const gsmpm_mpm::FState end{bp, ep, h->planes, h->planes_alt, h->orig, h->orig_alt};
+    h->planes = start.planes;
+    h->planes_alt = start.planes_alt;
+    h->orig = start.orig;
+    h->orig_alt = start.orig_alt;
     if (rc) return rc;
     if (e != hipSuccess) {
       set_error(std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
@@ -2065,12 +2130,17 @@ int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t nsub, const uint32_t* bc, voi
     }
     it = h->graphs.emplace(key, exec).first;
     h->graph_box_parity[key] = parity;
-    h->graph_fstate[key] = std::make_pair(bp, ep);
+    h->graph_fstate[key] = end;
   }
   GSMPM_HIP(hipGraphLaunch(it->second, st));
   h->cur_box = h->graph_box_parity[key];
-  h->fbpar = h->graph_fstate[key].first;
-  h->fep = h->graph_fstate[key].second;
+  const gsmpm_mpm::FState& fs = h->graph_fstate[key];
+  h->fbpar = fs.bpar;
+  h->fep = fs.ep;
+  h->planes = fs.planes;
+  h->planes_alt = fs.planes_alt;
+  h->orig = fs.orig;
+  h->orig_alt = fs.orig_alt;
   return GSMPM_OK;
 }
 
@@ -2167,6 +2237,7 @@ int gsmpm_mpm_resort(gsmpm_mpm* h, int32_t interval, void* stream) {
   GSMPM_REQUIRE(h, "gsmpm_mpm_resort: null handle");
   if (interval >= 0) h->resort_interval = interval;
   if (!h->has_particles || (h->prm.flags & GSMPM_FLAG_NO_SORT)) return GSMPM_OK;
+  if (use_fused(h)) return rebin_f(h, (hipStream_t)stream);  // storage follows the tile bins
   return resort(h, (hipStream_t)stream);
 }
 
@@ -2209,8 +2280,9 @@ int gsmpm_mpm_set(gsmpm_mpm* h, int32_t field, const float* in, void* stream) {
 int gsmpm_mpm_get_grid(gsmpm_mpm* h, int32_t which, float* out, void* stream) {
   GSMPM_REQUIRE(h && out, "gsmpm_mpm_get_grid: null argument");
   GSMPM_REQUIRE(which >= 0 && which <= 2, "gsmpm_mpm_get_grid: unknown grid field");
-  if (!(h->prm.flags & GSMPM_FLAG_KEEP_GRID)) {
-    // without it only the live node box is maintained (see k_grid)
+  if (!(h->prm.flags & GSMPM_FLAG_KEEP_GRID) && !(which == GSMPM_GRID_V_OUT && (h->fdebug & 4))) {
+    // without it only the live node box is maintained (see k_grid); debug bit 4
+    // reads v_out anyway (current on the touched tiles, stale elsewhere)
     set_error("gsmpm_mpm_get_grid: grid readback needs GSMPM_FLAG_KEEP_GRID");
     return GSMPM_ESTATE;
   }
@@ -2278,9 +2350,9 @@ static int time_kernels_f(gsmpm_mpm* h, float dt, uint32_t mask, int reps, float
     return GSMPM_OK;
   };
   ms4[3] = 0.f;
-  int rc = launch_fused(h, 2, c, false, mask, dt, h->fesc + ep, st, nullptr);  // windows of the current x
+  int rc = launch_fused(h, 2, c, false, false, mask, dt, h->fesc + ep, st, nullptr);  // windows of the current x
   if (!rc) rc = launch_grid_f(h, c, dt, mask, ep, nullptr, nullptr, st, nullptr);
-  if (!rc) rc = timed(0, [&]() { return launch_fused(h, 3, c, false, mask, dt, h->fesc + ep, st, nullptr); });
+  if (!rc) rc = timed(0, [&]() { return launch_fused(h, 3, c, false, true, mask, dt, h->fesc + ep, st, nullptr); });
   if (!rc) {
     GSMPM_HIP(hipMemsetAsync(h->fesc, 0, 2 * sizeof(int), st));  // time the touched-tile update
     rc = timed(1, [&]() { return launch_grid_f(h, c, dt, mask, ep, nullptr, nullptr, st, nullptr); });
@@ -2288,7 +2360,7 @@ static int time_kernels_f(gsmpm_mpm* h, float dt, uint32_t mask, int reps, float
   if (!rc) {
     GSMPM_HIP(hipMemsetAsync(h->fcount[c ^ 1], 0, sizeof(int) * (h->ftl.ntiles + 1), st));
     GSMPM_HIP(hipMemsetAsync(h->ftflag[c ^ 1], 0, sizeof(int) * h->ftl.ntiles, st));
-    rc = launch_fused(h, 1, c, true, mask, dt, h->fesc + ep, st, nullptr);
+    rc = launch_fused(h, 1, c, true, true, mask, dt, h->fesc + ep, st, nullptr);
     if (!rc) rc = timed(2, [&]() { return finish_binning_f(h, c ^ 1, st); });
   }
   (void)hipEventDestroy(e[0]);
@@ -2390,7 +2462,7 @@ int gsmpm_mpm_debug_stats(gsmpm_mpm* h, int32_t* out8, void* stream) {
 int gsmpm_debug_stamps(uint64_t* out, void* stream) {
   GSMPM_REQUIRE(out, "gsmpm_debug_stamps: null argument");
   GSMPM_HIP(hipStreamSynchronize((hipStream_t)stream));
-  GSMPM_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 3 * 4096 * 8));
+  GSMPM_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 4 * 4096 * 8));
   return GSMPM_OK;
 }
 

@@ -14,7 +14,7 @@ sa = scene['sargs']
 masks, t = substep_masks(specs, 0.0, sa.substep_dt, 20)
 sim.profile(sa.substep_dt, masks)
 sim.profile(sa.substep_dt, masks[:1])
-buf = np.zeros((3, 4096, 8), np.uint64)
+buf = np.zeros((4, 4096, 8), np.uint64)
 LIB.gsmpm_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), stream_of(dev))
 r = buf[0, 0].astype(np.int64)
 print("scan stamps (us from start): staged %.2f counted %.2f scanned %.2f written %.2f end %.2f" % tuple((r[[2, 3, 4, 5, 1]] - r[0]) / 100))

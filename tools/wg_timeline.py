@@ -14,7 +14,7 @@ sa = scene['sargs']
 masks, t = substep_masks(specs, 0.0, sa.substep_dt, 20)
 sim.profile(sa.substep_dt, masks)
 ms = sim.profile(sa.substep_dt, masks[:1])
-buf = np.zeros((3, 4096, 8), np.uint64)
+buf = np.zeros((4, 4096, 8), np.uint64)
 LIB.gsmpm_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), stream_of(dev))
 print('event ms p2g/grid/g2p', ms)
 for k, name in enumerate(('p2g', 'g2p')):

@@ -16,9 +16,9 @@ sa = scene['sargs']
 masks, t = substep_masks(specs, 0.0, sa.substep_dt, 300)
 sim.step(sa.substep_dt, masks[:100]); sim.step(sa.substep_dt, masks[100:200])
 print('stats', sim.debug_stats(), 'pipeline', sim.pipeline)
-ms = sim.profile(sa.substep_dt, masks[200:203])
+ms = sim.profile(sa.substep_dt, masks[200:203])  # K(P2G), grid, K, grid, K, grid, K(G2P)
 print('event ms K/grid/bins per 3 substeps', ms)
-buf = np.zeros((3, 4096, 8), np.uint64)
+buf = np.zeros((4, 4096, 8), np.uint64)
 LIB.gsmpm_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), stream_of(dev))
 b = buf[0].astype(np.int64)
 b = b[b[:, 0] > 0]
@@ -41,3 +41,16 @@ print("  dur by size >=200 median", np.median(dur[ok][big]).round(2), "<64 media
 # second-chunk WGs (grid-stride): count WGs whose end - start >> single chunk
 ms2 = sim.time_kernels(sa.substep_dt, masks[203], reps=20)
 print('time_kernels K/grid/bins', ms2)
+g = buf[3].astype(np.int64)
+g = g[g[:, 0] > 0]
+t0 = g[:, 0].min()
+okg = g[:, 2] > 0
+print(f"k_grid_f: {len(g)} WGs ({okg.sum()} with a tile); start spread {(g[:,0].max()-t0)/100:.1f} us; end {(g[:,1].max()-t0)/100:.1f} us")
+segg = lambda a, c: (g[okg, c] - g[okg, a]) / 100
+for name, a, c in (("start->tile", 0, 2), ("tile->covers", 2, 3), ("covers->nodes", 3, 4), ("nodes->end", 4, 1)):
+    x = segg(a, c)
+    print(f"  {name}: median {np.median(x):.2f} p90 {np.percentile(x, 90):.2f} max {x.max():.2f}")
+d = (g[okg, 1] - g[okg, 0]) / 100
+print("  WG dur percentiles 50/90/99/max:", np.percentile(d, [50, 90, 99, 100]).round(2))
+st = (g[okg, 0] - t0) / 100
+print("  start histogram", np.histogram(st, bins=10)[0].tolist(), "edges", np.histogram(st, bins=10)[1].round(1).tolist())
