@@ -525,14 +525,16 @@ __device__ __forceinline__ void node_extra(const float4* __restrict__ slots, con
   }
 }
 
-// Grid update of the fused pipeline: one 448-lane workgroup per touched tile,
-// one owned node per lane (all 8 window reads in flight), 4 workgroups per CU
-// (<= 72 VGPRs) so a scene's ~1000 touched tiles run in one round.
+// Grid update of the fused pipeline: two 224-lane workgroups per touched tile
+// (x halves), one owned node per lane (all 8 window reads in flight); at <= 72
+// VGPRs seven workgroups fit a CU, so a scene's ~1000 touched tiles run in
+// one round.
 // esc_in: some particle scattered through gacc in the P2G this update consumes
 // -> every tile, plus gacc (re-zeroed).  esc_clear: the flag the next P2G
 // raises.  zc / zf (optional): the counts / touched flags the next binning
 // launch accumulates into.
-__global__ __launch_bounds__(kFTN) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_grid_f(GridDims g, FTiles tl, ChunkIn ck, const int* __restrict__ tbox,
+constexpr int kGridT = kFTN / 2;  // lanes per grid workgroup: half a tile
+__global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_grid_f(GridDims g, FTiles tl, ChunkIn ck, const int* __restrict__ tbox,
                                                     const float4* __restrict__ slots, float4* __restrict__ gacc,
                                                     float4* __restrict__ gvel, const BcTable* __restrict__ bct,
                                                     GridStep gs, const int* __restrict__ esc_in,
@@ -548,12 +550,12 @@ __global__ __launch_bounds__(kFTN) __attribute__((amdgpu_waves_per_eu(7, 8))) vo
   }
   const int ng = g.ng;
   const bool all = *esc_in != 0;
-  const int ntouch = all ? tl.ntiles : ck.nchunk[1];
+  const int ntouch = 2 * (all ? tl.ntiles : ck.nchunk[1]);
   __shared__ int s_c0[27], s_nc[27], s_bx[27];
-  const int q = threadIdx.x;
-  const int l0 = q / (kFT1 * kFT2), l1 = (q / kFT2) % kFT1, l2 = q % kFT2;
   for (int wt = blockIdx.x; wt < ntouch; wt += gridDim.x) {
-    const int T = all ? wt : ck.touched[wt];
+    const int q = threadIdx.x + (wt & 1) * kGridT;
+    const int l0 = q / (kFT1 * kFT2), l1 = (q / kFT2) % kFT1, l2 = q % kFT2;
+    const int T = all ? wt >> 1 : ck.touched[wt >> 1];
     int ti, tj, tk;
     ftile_decode(tl, T, ti, tj, tk);
     __syncthreads();  // readers of the previous tile's ranges are done

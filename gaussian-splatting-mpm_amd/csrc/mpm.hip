@@ -1629,7 +1629,7 @@ static int launch_fused(gsmpm_mpm* h, int mode, int c, bool bin, bool use_box, u
 
 static int launch_grid_f(gsmpm_mpm* h, int wp, float dt, uint32_t mask, int ep, int* zc, int* zf, hipStream_t st,
                          const hipEvent_t* ev) {
-  launch(ev, k_grid_f, dim3(std::min(h->ftl.ntiles, 2048)), dim3(kFTN), st, h->g, h->ftl, chunk_in_f(h, wp),
+  launch(ev, k_grid_f, dim3(std::min(2 * h->ftl.ntiles, 2048)), dim3(kGridT), st, h->g, h->ftl, chunk_in_f(h, wp),
          (h->fdebug & 2) ? nullptr : (const int*)h->ftbox[wp], (const float4*)h->fslots, h->gacc, h->gvel, (const BcTable*)h->dev_bc, grid_step(h, dt, mask),
          (const int*)(h->fesc + ep), h->fesc + (ep ^ 1), zc, zf);
   GSMPM_LAUNCH_CHECK();
