@@ -13,7 +13,16 @@ import json
 import os
 import sys
 
-KERNELS = ("k_p2g", "k_grid", "k_g2p", "k_finish_bins", "k_render", "k_preprocess")
+# first match wins: k_grid_f before k_grid; k_fused counts its G2P + P2G form (<MAT, 3>) only
+KERNELS = ("k_fused", "k_grid_f", "k_p2g", "k_grid", "k_g2p", "k_finish_bins", "k_permute", "k_render",
+           "k_preprocess")
+
+
+def kernel_key(name):
+    k = next((k for k in KERNELS if k in name), None)
+    if k == "k_fused" and ", 3>" not in name:
+        return None
+    return k
 
 
 def per_dispatch(path, counter):
@@ -21,7 +30,7 @@ def per_dispatch(path, counter):
     for r in csv.DictReader(open(os.path.join(path, "run_counter_collection.csv"))):
         if r["Counter_Name"] != counter:
             continue
-        k = next((k for k in KERNELS if k in r["Kernel_Name"]), None)
+        k = kernel_key(r["Kernel_Name"])
         if k:
             acc[k][r["Dispatch_Id"]] += float(r["Counter_Value"])
     return {k: sum(v.values()) / len(v) for k, v in acc.items()}
