@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--slab", action="store_true", help="strong scaling: one scene in x-slabs with halo exchange")
+    ap.add_argument("--rebin", type=int, default=0, help="fused pipeline: substeps between re-binnings (0: library default)")
     return ap.parse_args()
 
 
@@ -223,6 +224,8 @@ def main():
         sim = SlabSimulator(eng, rank, world, bounds)
     else:
         sim, specs = make_sim(scene, dev)
+        if args.rebin > 0 and sim.pipeline == "fused":
+            sim.set_rebin_interval(args.rebin)
     n_local = sim.n
     bg = torch.zeros(3, device=dev)
     tanx, tany = math.tan(cam.FovX * 0.5), math.tan(cam.FovY * 0.5)
