@@ -229,6 +229,9 @@ def main():
     n_local = sim.n
     bg = torch.zeros(3, device=dev)
     tanx, tany = math.tan(cam.FovX * 0.5), math.tan(cam.FovY * 0.5)
+    # world2grid constants as host floats, once (a per-frame .tolist() / float() of the
+    # device tensors would stall the host on the whole frame)
+    w_scale, w_center = float(scene["s"]), [float(v) for v in scene["c"].reshape(-1).tolist()]
     state = {"t": 0.0, "K": 0}
 
     def frame(render=True):
@@ -237,7 +240,7 @@ def main():
         sim.postprocess()
         if render and not args.no_render:
             # every rank renders its own particles (its scene, or its slab's share)
-            means_r, covs_r = sim.world_outputs(scene["s"], scene["c"].tolist(), render_space=True)
+            means_r, covs_r = sim.world_outputs(w_scale, w_center, render_space=True)
             K, _, _ = raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg,
                                      cam.height, cam.width, tanx, tany, sh_degree=3, shs=feats, cov3D_precomp=covs_r)
             state["K"] = K
@@ -277,7 +280,7 @@ def main():
     state["t"] = t_after
     render_ms = None
     if not args.no_render and rank == 0 and world == 1:
-        means_r, covs_r = sim.world_outputs(scene["s"], scene["c"].tolist(), render_space=True)
+        means_r, covs_r = sim.world_outputs(w_scale, w_center, render_space=True)
         torch.cuda.synchronize()
         r0 = time.perf_counter()
         for _ in range(5):
