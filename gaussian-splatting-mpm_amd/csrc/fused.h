@@ -205,7 +205,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
       if (!outside) {
         // the chunk's stencil box from its last P2G (particles unmoved since), else the whole window
         int lo[3], hi[3];
-        box_unpack((use_box & 1) ? tc.cbox[w] : kFullBox, lo, hi);
+        box_unpack(use_box ? tc.cbox[w] : kFullBox, lo, hi);
         const int n1 = hi[1] - lo[1] + 1, n2 = hi[2] - lo[2] + 1, n12 = n1 * n2;
         const int nvol = (hi[0] - lo[0] + 1) * n12;
         const float r12 = 1.0f / (float)n12, r2 = 1.0f / (float)n2;  // exact floor for q < 2^11
@@ -404,7 +404,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
         tc.cbox[w] = box;
         tc.tbox[t] = (cr.w & 8) ? kFullBox : box;  // tiles with several chunks: whole windows
       }
-      if ((cr.w & 8) || (use_box & 2)) box = kFullBox;
+      if (cr.w & 8) box = kFullBox;
       int ebits;
       frexpf(bmax, &ebits);
       const int S = bmax > 0.f ? 50 - ebits : 0;  // see k_p2g
@@ -459,7 +459,7 @@ __device__ __forceinline__ void load_cover27(const ChunkIn& ck, const int* __res
       const int t = (x * tl.td1 + y) * tl.td2 + z;
       const int cnt = ck.count[t];
       c0 = ck.cbase[t];
-      bx = tbox ? tbox[t] : kFullBox;
+      bx = tbox[t];
       nc = (cnt + kChunk - 1) / kChunk;
     }
     s_c0[e] = c0;

@@ -1085,14 +1085,15 @@ __global__ __launch_bounds__(256) void k_scatter(int n, const int* __restrict__ 
 
 // ------------------------------------------------------------ postprocess --
 // compute_cov_from_F (utils.py:401-433) + compute_R_from_F (utils.py:376-398)
-__global__ __launch_bounds__(256) void k_postprocess(Particles ps) {
+__global__ __launch_bounds__(256) void k_postprocess(Particles ps, const int* __restrict__ orig) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= ps.n) return;
+  const int o = orig[p];  // the cold planes' row
   float F[3][3];
 #pragma unroll
   for (int i = 0; i < 9; ++i) F[i / 3][i % 3] = ps.ld(PF + i, p);
-  const float a0 = ps.ld(PICOV + 0, p), a1 = ps.ld(PICOV + 1, p), a2 = ps.ld(PICOV + 2, p);
-  const float a3 = ps.ld(PICOV + 3, p), a4 = ps.ld(PICOV + 4, p), a5 = ps.ld(PICOV + 5, p);
+  const float a0 = ps.ldc(PICOV + 0, o), a1 = ps.ldc(PICOV + 1, o), a2 = ps.ldc(PICOV + 2, o);
+  const float a3 = ps.ldc(PICOV + 3, o), a4 = ps.ldc(PICOV + 4, o), a5 = ps.ldc(PICOV + 5, o);
   const float A[3][3] = {{a0, a1, a2}, {a1, a3, a4}, {a2, a4, a5}};
   float T[3][3], Cv[3][3];
 #pragma unroll
@@ -1100,12 +1101,12 @@ __global__ __launch_bounds__(256) void k_postprocess(Particles ps) {
 #pragma unroll
     for (int j = 0; j < 3; ++j) T[i][j] = F[i][0] * A[0][j] + F[i][1] * A[1][j] + F[i][2] * A[2][j];
   mmT(T, F, Cv);
-  ps.st(PCOV + 0, p, Cv[0][0]);
-  ps.st(PCOV + 1, p, Cv[0][1]);
-  ps.st(PCOV + 2, p, Cv[0][2]);
-  ps.st(PCOV + 3, p, Cv[1][1]);
-  ps.st(PCOV + 4, p, Cv[1][2]);
-  ps.st(PCOV + 5, p, Cv[2][2]);
+  ps.stc(PCOV + 0, o, Cv[0][0]);
+  ps.stc(PCOV + 1, o, Cv[0][1]);
+  ps.stc(PCOV + 2, o, Cv[0][2]);
+  ps.stc(PCOV + 3, o, Cv[1][1]);
+  ps.stc(PCOV + 4, o, Cv[1][2]);
+  ps.stc(PCOV + 5, o, Cv[2][2]);
   float U[3][3], V[3][3], s[3];
   svd3(F, U, s, V);
   if (det3(U) < 0.f) {
@@ -1123,7 +1124,7 @@ __global__ __launch_bounds__(256) void k_postprocess(Particles ps) {
 #pragma unroll
   for (int i = 0; i < 3; ++i)
 #pragma unroll
-    for (int j = 0; j < 3; ++j) ps.st(PR + i * 3 + j, p, R[j][i]);  // particle_R = (U V^T)^T
+    for (int j = 0; j < 3; ++j) ps.stc(PR + i * 3 + j, o, R[j][i]);  // particle_R = (U V^T)^T
 }
 
 // ------------------------------------------------------------ init / io --
@@ -1147,13 +1148,13 @@ __global__ __launch_bounds__(256) void k_init(Particles ps, InitArgs a) {
   for (int i = 0; i < 9; ++i) {
     ps.st(PC + i, p, 0.0f);
     ps.st(PF + i, p, (i % 4 == 0) ? 1.0f : 0.0f);
-    ps.st(PR + i, p, 0.0f);
+    ps.stc(PR + i, o, 0.0f);
   }
 #pragma unroll
   for (int i = 0; i < 6; ++i) {
     const float c = a.cov6[(size_t)o * 6 + i];
-    ps.st(PICOV + i, p, c);
-    ps.st(PCOV + i, p, c);
+    ps.stc(PICOV + i, o, c);
+    ps.stc(PCOV + i, o, c);
   }
   const float vol = a.vol[o];
   ps.st(PVOL, p, vol);
@@ -1167,19 +1168,26 @@ __global__ __launch_bounds__(256) void k_init(Particles ps, InitArgs a) {
 }
 
 __global__ __launch_bounds__(256) void k_get(Particles ps, const int* __restrict__ orig, int plane0, int width,
-                                             float* __restrict__ out) {
+                                             int cold, float* __restrict__ out) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= ps.n) return;
-  const size_t o = (size_t)orig[p] * width;
-  for (int j = 0; j < width; ++j) out[o + j] = ps.ld(plane0 + j, p);
+  const int r = orig[p];
+  const size_t o = (size_t)r * width;
+  for (int j = 0; j < width; ++j) out[o + j] = cold ? ps.ldc(plane0 + j, r) : ps.ld(plane0 + j, p);
 }
 
 __global__ __launch_bounds__(256) void k_set(Particles ps, const int* __restrict__ orig, int plane0, int width,
-                                             const float* __restrict__ in) {
+                                             int cold, const float* __restrict__ in) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= ps.n) return;
-  const size_t o = (size_t)orig[p] * width;
-  for (int j = 0; j < width; ++j) ps.st(plane0 + j, p, in[o + j]);
+  const int r = orig[p];
+  const size_t o = (size_t)r * width;
+  for (int j = 0; j < width; ++j) {
+    if (cold)
+      ps.stc(plane0 + j, r, in[o + j]);
+    else
+      ps.st(plane0 + j, p, in[o + j]);
+  }
 }
 
 __global__ __launch_bounds__(256) void k_world_out(Particles ps, const int* __restrict__ orig, float half, float s,
@@ -1197,7 +1205,7 @@ __global__ __launch_bounds__(256) void k_world_out(Particles ps, const int* __re
   }
   const float ss = s * s;
 #pragma unroll
-  for (int i = 0; i < 6; ++i) co[o * 6 + i] = ps.ld(PCOV + i, p) / ss;  // transform_utils.py:20
+  for (int i = 0; i < 6; ++i) co[o * 6 + i] = ps.ldc(PCOV + i, (int)o) / ss;  // transform_utils.py:20
 }
 
 __global__ void k_grid_get(const float4* __restrict__ src, size_t nn, int which, float* __restrict__ out) {
@@ -1238,11 +1246,17 @@ __global__ __launch_bounds__(256) void k_morton(Particles ps, float inv_dx, uint
   idx[p] = p;
 }
 
-// dst[plane][i] = src[plane][perm[i]] for every plane (blockIdx.y = plane)
+// dst[plane][i] = src[plane][perm[i]] for every hot plane (blockIdx.y =
+// plane), and the same for the orig map (blockIdx.y = NPLANES)
 __global__ __launch_bounds__(256) void k_permute(const float* __restrict__ src, float* __restrict__ dst, int n, int np,
-                                                 const int* __restrict__ perm) {
+                                                 const int* __restrict__ perm, const int* __restrict__ osrc,
+                                                 int* __restrict__ odst) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  if (blockIdx.y == NPLANES) {
+    odst[i] = osrc[perm[i]];
+    return;
+  }
   const size_t off = (size_t)blockIdx.y * np;
   dst[off + i] = src[off + perm[i]];
 }
@@ -1330,6 +1344,7 @@ struct gsmpm_mpm {
   int mat_kernel = 0;  // template code of k_p2g
   int n = 0, np = 0;
   float* planes = nullptr;
+  float* cold = nullptr;  // [NCOLD][np] init_cov, cov, R in caller order
   int* orig = nullptr;
   float4* gacc = nullptr;   // dense accumulator: outside-grid particles + KEEP_GRID readback
   float4* gvel = nullptr;   // dense v_out
@@ -1384,7 +1399,6 @@ struct gsmpm_mpm {
   int fbpar = 0;                          // parity of the bins the next k_fused reads
   int fep = 0;                            // escape flag the next P2G raises
   int rebin_interval = 10;                // substeps between re-binnings (fused pipeline)
-  int fdebug = 0;                         // GSMPM_FUSED_DEBUG bits: 1 no G2P box, 2 full-window stores
   std::map<std::vector<uint32_t>, hipGraphExec_t> graphs;
   std::map<std::vector<uint32_t>, int> graph_box_parity;
   struct FState {
@@ -1401,7 +1415,7 @@ namespace gsmpm {
 static thread_local std::string g_err;
 void set_error(const std::string& m) { g_err = m; }
 
-static Particles particles_of(gsmpm_mpm* h) { return Particles{h->planes, h->n, h->np}; }
+static Particles particles_of(gsmpm_mpm* h) { return Particles{h->planes, h->n, h->np, h->cold}; }
 
 static ChunkIn chunk_in(gsmpm_mpm* h, int c) {
   return ChunkIn{h->count[c], h->cbase[c], h->chunk[c], h->nchunk[c], h->list[c], h->touched[c]};
@@ -1480,11 +1494,8 @@ static int finish_binning_f(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_
 // Storage into the bin order of parity c (list[c]: storage rows grouped by
 // tile): planes / orig gathered into the other buffer, which becomes current.
 static int permute_to_bins(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t* ev = nullptr) {
-  const hipEvent_t e0[2] = {ev ? ev[0] : nullptr, nullptr}, e1[2] = {nullptr, ev ? ev[1] : nullptr};
-  launch(ev ? e0 : nullptr, k_permute, dim3(div_up(h->n, 256), NPLANES), dim3(256), st, (const float*)h->planes,
-         h->planes_alt, h->n, h->np, (const int*)h->flist[c]);
-  launch(ev ? e1 : nullptr, k_permute_i, dim3(div_up(h->n, 256)), dim3(256), st, (const int*)h->orig, h->orig_alt,
-         h->n, (const int*)h->flist[c]);
+  launch(ev, k_permute, dim3(div_up(h->n, 256), NPLANES + 1), dim3(256), st, (const float*)h->planes, h->planes_alt,
+         h->n, h->np, (const int*)h->flist[c], (const int*)h->orig, h->orig_alt);
   GSMPM_LAUNCH_CHECK();
   std::swap(h->planes, h->planes_alt);
   std::swap(h->orig, h->orig_alt);
@@ -1616,7 +1627,7 @@ static void launch_fused_m(gsmpm_mpm* h, int c, const BinOutF& bo, int bin, int 
 static int launch_fused(gsmpm_mpm* h, int mode, int c, bool bin, bool use_box, uint32_t mask, float dt, int* esc,
                         hipStream_t st, const hipEvent_t* ev) {
   const BinOutF bo = bin_out_f(h, c ^ 1);
-  const int ub = (use_box && !(h->fdebug & 1) ? 1 : 0) | (h->fdebug & 2);
+  const int ub = use_box ? 1 : 0;
   if (mode == 1)
     launch_fused_t<0, 1>(h, c, bo, bin ? 1 : 0, ub, mask, dt, esc, st, ev);  // G2P does not depend on the material
   else if (mode == 2)
@@ -1630,7 +1641,7 @@ static int launch_fused(gsmpm_mpm* h, int mode, int c, bool bin, bool use_box, u
 static int launch_grid_f(gsmpm_mpm* h, int wp, float dt, uint32_t mask, int ep, int* zc, int* zf, hipStream_t st,
                          const hipEvent_t* ev) {
   launch(ev, k_grid_f, dim3(std::min(2 * h->ftl.ntiles, 2048)), dim3(kGridT), st, h->g, h->ftl, chunk_in_f(h, wp),
-         (h->fdebug & 2) ? nullptr : (const int*)h->ftbox[wp], (const float4*)h->fslots, h->gacc, h->gvel, (const BcTable*)h->dev_bc, grid_step(h, dt, mask),
+         (const int*)h->ftbox[wp], (const float4*)h->fslots, h->gacc, h->gvel, (const BcTable*)h->dev_bc, grid_step(h, dt, mask),
          (const int*)(h->fesc + ep), h->fesc + (ep ^ 1), zc, zf);
   GSMPM_LAUNCH_CHECK();
   return GSMPM_OK;
@@ -1708,7 +1719,11 @@ static int upload_bc(gsmpm_mpm* h) {
   return GSMPM_OK;
 }
 
-static int plane_of(int field, int* width) {
+// plane of a field; *cold: a cold plane (caller order)
+static int plane_of(int field, int* width, int* cold = nullptr) {
+  int dummy;
+  if (!cold) cold = &dummy;
+  *cold = field == GSMPM_FIELD_COV || field == GSMPM_FIELD_INIT_COV || field == GSMPM_FIELD_R;
   switch (field) {
     case GSMPM_FIELD_X: *width = 3; return PX;
     case GSMPM_FIELD_V: *width = 3; return PV;
@@ -1762,8 +1777,8 @@ static int resort(gsmpm_mpm* h, hipStream_t st) {
   GSMPM_HIP(rocprim::radix_sort_pairs(h->sort_tmp, bytes, h->sort_keys, h->sort_keys + np, h->sort_idx,
                                       h->sort_idx + np, (size_t)n, 0, 30, st));
   const int* perm = h->sort_idx + np;
-  hipLaunchKernelGGL(k_permute, dim3(div_up(n, 256), NPLANES), dim3(256), 0, st, h->planes, h->planes_tmp, n, np, perm);
-  hipLaunchKernelGGL(k_permute_i, pb, dim3(256), 0, st, h->orig, h->orig_tmp, n, perm);
+  hipLaunchKernelGGL(k_permute, dim3(div_up(n, 256), NPLANES + 1), dim3(256), 0, st, h->planes, h->planes_tmp, n, np,
+                     perm, (const int*)h->orig, h->orig_tmp);
   GSMPM_LAUNCH_CHECK();
   // copy back so pointers baked into cached graphs stay valid
   GSMPM_HIP(hipMemcpyAsync(h->planes, h->planes_tmp, sizeof(float) * (size_t)NPLANES * np, hipMemcpyDeviceToDevice, st));
@@ -1814,6 +1829,8 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
   };
   hipError_t e;
   if ((e = hipMalloc(&h->planes, sizeof(float) * (size_t)NPLANES * h->np)) != hipSuccess) return fail(e, "hipMalloc planes");
+  if ((e = hipMalloc(&h->cold, sizeof(float) * (size_t)NCOLD * h->np)) != hipSuccess) return fail(e, "hipMalloc planes");
+  if ((e = hipMemset(h->cold, 0, sizeof(float) * (size_t)NCOLD * h->np)) != hipSuccess) return fail(e, "hipMemset");
   if ((e = hipMalloc(&h->orig, sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc orig");
   if ((e = hipMalloc(&h->gacc, sizeof(float4) * nn)) != hipSuccess) return fail(e, "hipMalloc grid acc");
   if ((e = hipMalloc(&h->gvel, sizeof(float4) * nn)) != hipSuccess) return fail(e, "hipMalloc grid vel");
@@ -1843,7 +1860,6 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
   if ((e = hipMalloc(&h->escape, sizeof(int))) != hipSuccess) return fail(e, "hipMalloc escape");
   // fused pipeline: 8 x 8 x 7-cell tiles (fused.h)
   h->fused = !(prm->flags & (GSMPM_FLAG_PHASED | GSMPM_FLAG_KEEP_GRID));
-  if (const char* dbg = std::getenv("GSMPM_FUSED_DEBUG")) h->fdebug = std::atoi(dbg);
   h->ftl.td0 = (h->g.ng + kFT0 - 1) / kFT0;
   h->ftl.td1 = (h->g.ng + kFT1 - 1) / kFT1;
   h->ftl.td2 = (h->g.ng + kFT2 - 1) / kFT2;
@@ -1907,6 +1923,7 @@ int gsmpm_mpm_destroy(gsmpm_mpm* h) {
   drop_graphs(h);
   if (h->cap) (void)hipStreamDestroy(h->cap);
   (void)hipFree(h->planes);
+  (void)hipFree(h->cold);
   (void)hipFree(h->orig);
   (void)hipFree(h->gacc);
   (void)hipFree(h->gvel);
@@ -2243,7 +2260,8 @@ int gsmpm_mpm_resort(gsmpm_mpm* h, int32_t interval, void* stream) {
 
 int gsmpm_mpm_postprocess(gsmpm_mpm* h, void* stream) {
   GSMPM_REQUIRE(h, "gsmpm_mpm_postprocess: null handle");
-  hipLaunchKernelGGL(k_postprocess, dim3(div_up(h->n, 256)), dim3(256), 0, (hipStream_t)stream, particles_of(h));
+  hipLaunchKernelGGL(k_postprocess, dim3(div_up(h->n, 256)), dim3(256), 0, (hipStream_t)stream, particles_of(h),
+                     (const int*)h->orig);
   GSMPM_LAUNCH_CHECK();
   return GSMPM_OK;
 }
@@ -2256,22 +2274,22 @@ int gsmpm_mpm_field_width(int32_t field) {
 
 int gsmpm_mpm_get(gsmpm_mpm* h, int32_t field, float* out, void* stream) {
   GSMPM_REQUIRE(h && out, "gsmpm_mpm_get: null argument");
-  int w;
-  const int p0 = plane_of(field, &w);
+  int w, cold;
+  const int p0 = plane_of(field, &w, &cold);
   GSMPM_REQUIRE(p0 >= 0, "gsmpm_mpm_get: unknown field");
   hipLaunchKernelGGL(k_get, dim3(div_up(h->n, 256)), dim3(256), 0, (hipStream_t)stream, particles_of(h), h->orig, p0,
-                     w, out);
+                     w, cold, out);
   GSMPM_LAUNCH_CHECK();
   return GSMPM_OK;
 }
 
 int gsmpm_mpm_set(gsmpm_mpm* h, int32_t field, const float* in, void* stream) {
   GSMPM_REQUIRE(h && in, "gsmpm_mpm_set: null argument");
-  int w;
-  const int p0 = plane_of(field, &w);
+  int w, cold;
+  const int p0 = plane_of(field, &w, &cold);
   GSMPM_REQUIRE(p0 >= 0, "gsmpm_mpm_set: unknown field");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_set, dim3(div_up(h->n, 256)), dim3(256), 0, st, particles_of(h), h->orig, p0, w, in);
+  hipLaunchKernelGGL(k_set, dim3(div_up(h->n, 256)), dim3(256), 0, st, particles_of(h), h->orig, p0, w, cold, in);
   GSMPM_LAUNCH_CHECK();
   if (field == GSMPM_FIELD_X) return rebin(h, st);
   return GSMPM_OK;
@@ -2280,9 +2298,8 @@ int gsmpm_mpm_set(gsmpm_mpm* h, int32_t field, const float* in, void* stream) {
 int gsmpm_mpm_get_grid(gsmpm_mpm* h, int32_t which, float* out, void* stream) {
   GSMPM_REQUIRE(h && out, "gsmpm_mpm_get_grid: null argument");
   GSMPM_REQUIRE(which >= 0 && which <= 2, "gsmpm_mpm_get_grid: unknown grid field");
-  if (!(h->prm.flags & GSMPM_FLAG_KEEP_GRID) && !(which == GSMPM_GRID_V_OUT && (h->fdebug & 4))) {
-    // without it only the live node box is maintained (see k_grid); debug bit 4
-    // reads v_out anyway (current on the touched tiles, stale elsewhere)
+  if (!(h->prm.flags & GSMPM_FLAG_KEEP_GRID)) {
+    // without it only the live node box is maintained (see k_grid)
     set_error("gsmpm_mpm_get_grid: grid readback needs GSMPM_FLAG_KEEP_GRID");
     return GSMPM_ESTATE;
   }

@@ -9,6 +9,8 @@
 namespace gsmpm {
 
 // ------------------------------------------------------------------ layout --
+// Hot planes: what a substep reads and writes, in STORAGE order (re-sorted /
+// permuted into bin order with the particles).
 enum Plane : int {
   PX = 0,      // x y z
   PV = 3,      // v
@@ -19,10 +21,16 @@ enum Plane : int {
   PMU = 26,
   PLAM = 27,
   PYLD = 28,
-  PICOV = 29,  // init cov (upper 6)
-  PCOV = 35,   // cov (upper 6)
-  PR = 41,     // particle_R
-  NPLANES = 50
+  NPLANES = 29
+};
+// Cold planes: only touched at init and by the per-frame postprocess /
+// readback, kept in CALLER order (row = orig[storage row]) so re-sorting and
+// re-binning never move them.
+enum ColdPlane : int {
+  PICOV = 0,   // init cov (upper 6)
+  PCOV = 6,    // cov (upper 6)
+  PR = 12,     // particle_R
+  NCOLD = 21
 };
 
 constexpr int kMaxBC = 32;
@@ -52,10 +60,11 @@ struct BcTable {
 struct Particles {
   float* P;
   int n, np;
+  float* cold;  // [NCOLD][np], caller order
   // Plane access through a buffer resource: SGPR descriptor + SGPR plane
-  // offset + ONE 32-bit VGPR lane offset for all 50 planes (a flat access
+  // offset + ONE 32-bit VGPR lane offset for all hot planes (a flat access
   // holds a 64-bit VGPR address per plane, which costs the transfer kernels
-  // ~48 VGPRs).  Requires NPLANES * np * 4 < 2^32 (np < 10.7M), checked on the host.
+  // ~48 VGPRs).  Requires NPLANES * np * 4 < 2^31, checked on the host.
   __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const {
     return __builtin_amdgcn_make_buffer_rsrc(P, (short)0, NPLANES * np * 4, 0x00020000);
   }
@@ -65,6 +74,9 @@ struct Particles {
   __device__ __forceinline__ void st(int plane, int i, float v) const {
     __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rsrc(), i * 4, plane * np * 4, 0);
   }
+  // cold planes, by caller row
+  __device__ __forceinline__ float ldc(int plane, int row) const { return cold[(size_t)plane * np + row]; }
+  __device__ __forceinline__ void stc(int plane, int row, float v) const { cold[(size_t)plane * np + row] = v; }
 };
 
 struct GridDims {
