@@ -7,16 +7,25 @@
 //   k_preprocess   one lane per Gaussian: frustum test (view z > 0.2), EWA 2D
 //                  covariance (+0.3 low-pass), conic, 3-sigma radius, 16x16
 //                  tile rect, SH(deg<=3) -> RGB, depth, tiles touched
-//   scan           inclusive sum of tiles touched (rocPRIM), one D2H of K
-//   k_duplicate    emit (tile<<32 | depth bits, idx) per touched tile
-//   sort           stable LSD radix sort over 32 + msb(#tiles) key bits
-//   k_ranges       per-tile [start, end) in the sorted list
-//   k_render       one 256-lane workgroup (4 wave64) per 16x16 tile; batches of
-//                  256 Gaussians staged in LDS (xy, conic/opacity, rgb) and
-//                  front-to-back alpha blending with the upstream cut-offs
-//                  (alpha < 1/255 skip, alpha <= 0.99, T < 1e-4 stop), block
-//                  early exit via __syncthreads_count; records each pixel's
-//                  final T and last contributor for the backward pass.
+//   scan           inclusive sum of tiles touched (rocPRIM) -> K, one D2H
+//   depth order    stable sort of the P depths (ties keep index order), then
+//                  the tiles-touched counts scanned in that order; queued
+//                  before the K read-back, so they run behind the simulator
+//   k_emit_by_rank each Gaussian, in depth order, emits (tile, idx) per
+//                  touched tile at its depth-order offset
+//   sort           stable onesweep radix sort on the tile index alone
+//                  (msb(#tiles) bits): each tile's list comes out in (depth,
+//                  index) order, the list upstream's 64-bit
+//                  (tile << 32 | depth bits) sort produces
+//                  (GSMPM_RASTER_WIDE_KEYS=1 runs that upstream path instead)
+//   k_ranges32     per-tile [start, end) in the sorted list
+//   k_render       one wave64 per 8x8 quarter of a 16x16 tile; batches of 64
+//                  list entries are culled against the sub-tile (alpha can't
+//                  reach 1/255 there -> dropped, exactly the entries the blend
+//                  would skip), compacted in LDS and blended front to back
+//                  with the upstream cut-offs (alpha < 1/255 skip, alpha <=
+//                  0.99, T < 1e-4 stop), wave early exit; records each
+//                  pixel's final T and last contributor for the backward.
 //
 // Backward (upstream's BACKWARD::render + preprocess, for extra.py's
 // training loop):
@@ -24,8 +33,9 @@
 //                    last contributor; the 256 pixels' contributions to each
 //                    (Gaussian, tile) pair are summed on chip (wave shuffles +
 //                    LDS) and stored once per pair at the pair's emission
-//                    index -- the sort carries emission indices, so a
-//                    Gaussian's pairs are contiguous (no global atomics);
+//                    index in Gaussian-index order (k_slots derives it for
+//                    the depth-ordered path), so a Gaussian's pairs are
+//                    contiguous (no global atomics);
 //   k_preprocess_bwd one lane per Gaussian: sums its pair records, then the
 //                    2D-covariance / projection / SH / 3D-covariance adjoints.
 #include <hip/hip_runtime.h>
@@ -34,6 +44,7 @@
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -42,6 +53,13 @@
 namespace gsmpm {
 
 constexpr int kBX = 16, kBY = 16, kBlock = kBX * kBY;
+// rocPRIM's onesweep radix sort at every size above one block, for the tile
+// sort (its default switches to block sort + merge passes below 1M keys: ~15
+// launches instead of one per 8-bit digit; measured 0.05 ms/frame slower on the
+// bench's ~500k pairs).  The 100k-key depth sort keeps the default: there the
+// merge path is the faster one (onesweep's look-back chain dominates).
+using OnesweepSort = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                rocprim::default_config, 0>;
 
 __constant__ float kSH_C0 = 0.28209479177387814f;
 __constant__ float kSH_C1 = 0.4886025119029199f;
@@ -256,59 +274,126 @@ __global__ __launch_bounds__(256) void k_ranges(int L, const unsigned long long*
   if (idx == L - 1) ranges[cur].y = L;
 }
 
-__global__ __launch_bounds__(kBlock) void k_render(const uint2* __restrict__ ranges, const unsigned* __restrict__ list,
-                                                   int W, int H, int gx, const float2* __restrict__ xy,
-                                                   const float4* __restrict__ conic_o, const float4* __restrict__ rgbo,
-                                                   const float* __restrict__ bg, float* __restrict__ out,
-                                                   float* __restrict__ final_T, int* __restrict__ n_contrib) {
-  __shared__ float2 s_xy[kBlock];
-  __shared__ float4 s_co[kBlock];
-  __shared__ float4 s_rgb[kBlock];
-  const int tx = threadIdx.x % kBX, ty = threadIdx.x / kBX;
-  const int px = blockIdx.x * kBX + tx, py = blockIdx.y * kBY + ty;
+// k_render: one wave64 workgroup per 8x8 quarter of a 16x16 tile, walking
+// the tile's list front to back in batches of 64 entries (the next batch's
+// gather and the list ids of the one after are in flight while a batch
+// blends).
+//
+// Sub-tile culling.  A tile's list holds every Gaussian whose 3-sigma rect
+// touches the tile, but a faint Gaussian reaches alpha >= 1/255 only inside a
+// much smaller ellipse, q = d^T conic d <= 2 ln(255 o).  Each staged entry is
+// tested once against the 8x8 sub-tile (the ellipse's bounding box, inflated
+// by 2 % and a pixel, so float rounding can never cull a Gaussian the blend
+// would take) and the survivors are compacted in list order; the blend walks
+// only those.  A culled entry is one upstream's loop skips at every pixel of
+// the sub-tile (alpha < 1/255), so pixels, final T and last contributor are
+// unchanged.  On the bench's lego frame this removes ~85 % of the per-pixel
+// work of the heaviest tiles, whose last contributor sits within the first
+// 5-15 % of their list.
+//
+// Per Gaussian the arithmetic and cut-offs are upstream's; kU Gaussians are
+// evaluated independently (their LDS reads and exp2s pipeline) and then folded
+// in order, branch-free.
+constexpr int kU = 8;
+constexpr int kSub = 8;  // pixel sub-tile side: one wave of pixels
+
+// can alpha = o exp(power) reach 1/255 at a pixel centre of the sub-tile
+// [x0, x0 + 7] x [y0, y0 + 7]?  Conservative; NaNs keep the Gaussian.
+__device__ __forceinline__ bool reaches_subtile(float2 g, float4 co, float x0, float y0) {
+  if (co.w * 255.0f < 0.999f) return false;  // o < 1/255: alpha < 1/255 everywhere
+  const float det = co.x * co.z - co.y * co.y;
+  if (!(det > 0.0f)) return true;
+  const float k = fmaxf(2.0f * __logf(255.0f * co.w), 0.0f) * 1.02f + 0.02f;
+  const float ex = sqrtf(k * co.z / det) + 1.0f, ey = sqrtf(k * co.x / det) + 1.0f;
+  return !(g.x + ex < x0 || g.x - ex > x0 + (kSub - 1) || g.y + ey < y0 || g.y - ey > y0 + (kSub - 1));
+}
+
+__global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges, const unsigned* __restrict__ list,
+                                               int W, int H, int gx, const float2* __restrict__ xy,
+                                               const float4* __restrict__ conic_o, const float4* __restrict__ rgbo,
+                                               const float* __restrict__ bg, float* __restrict__ out,
+                                               float* __restrict__ final_T, int* __restrict__ n_contrib, int mode) {
+  __shared__ float2 s_xy[64];
+  __shared__ float4 s_co[64];
+  __shared__ float4 s_rgb[64];  // .w: the entry's tile-list index (as int bits)
+  const int lane = threadIdx.x;
+  const int x0 = blockIdx.x * kSub, y0 = blockIdx.y * kSub;
+  const int px = x0 + (lane & (kSub - 1)), py = y0 + (lane / kSub);
   const bool inside = px < W && py < H;
-  bool done = !inside;
-  const uint2 range = ranges[blockIdx.y * gx + blockIdx.x];
-  const int rounds = (int)((range.y - range.x + kBlock - 1) / kBlock);
-  int todo = (int)(range.y - range.x);
-  const float pfx = (float)px, pfy = (float)py;
+  const uint2 range = ranges[(blockIdx.y >> 1) * gx + (blockIdx.x >> 1)];
+  const int n = (int)(range.y - range.x);
+  const unsigned* lst = list + range.x;
+  const float pfx = (float)px, pfy = (float)py, fx0 = (float)x0, fy0 = (float)y0;
   float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f;
-  int contributor = 0, last = 0;
-  for (int i = 0; i < rounds; ++i, todo -= kBlock) {
-    if (__syncthreads_count(done) == kBlock) break;
-    const int prog = i * kBlock + threadIdx.x;
-    if ((int)range.x + prog < (int)range.y) {
-      const unsigned id = list[range.x + prog];
-      s_xy[threadIdx.x] = xy[id];
-      s_co[threadIdx.x] = conic_o[id];
-      s_rgb[threadIdx.x] = rgbo[id];
+  int last = 0;
+  bool done = !inside;
+  float2 g_xy = make_float2(0.f, 0.f);
+  float4 g_co = make_float4(0.f, 0.f, 0.f, 0.f), g_rgb = g_co;
+  unsigned nid = 0;
+  if (lane < n) {
+    const unsigned id = lst[lane];
+    g_xy = xy[id];
+    g_co = conic_o[id];
+    g_rgb = rgbo[id];
+  }
+  if (64 + lane < n) nid = lst[64 + lane];
+  for (int j0 = 0; j0 < n; j0 += 64) {
+    if (__all(done)) break;
+    // stage the batch's survivors in list order; slots up to the next
+    // multiple of kU are zero (opacity 0: alpha 0, and fma(0, 0, C) = C)
+    const bool keep = j0 + lane < n && ((mode & 1) || reaches_subtile(g_xy, g_co, fx0, fy0));
+    const unsigned long long m = __ballot(keep);
+    const int pos = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+    const int cnt = __popcll(m);
+    if (keep) {
+      s_xy[pos] = g_xy;
+      s_co[pos] = g_co;
+      s_rgb[pos] = make_float4(g_rgb.x, g_rgb.y, g_rgb.z, __int_as_float(j0 + lane));
+    }
+    if (lane < ((cnt + kU - 1) & ~(kU - 1)) - cnt) {
+      s_xy[cnt + lane] = make_float2(0.f, 0.f);
+      s_co[cnt + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+      s_rgb[cnt + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     __syncthreads();
-    const int nb = min(kBlock, todo);
-    for (int j = 0; !done && j < nb; ++j) {
-      ++contributor;
-      const float2 g = s_xy[j];
-      const float dx = g.x - pfx, dy = g.y - pfy;
-      const float4 co = s_co[j];
-      // the blend loop is the renderer's hot loop: FMAs and the hardware
-      // exp2 (v_exp_f32, ~1 ulp) -- pixel parity is 1e-3, not bitwise
-      const float power = __builtin_fmaf(-0.5f, __builtin_fmaf(co.x * dx, dx, co.z * dy * dy), -co.y * dx * dy);
-      if (power > 0.0f) continue;
-      const float alpha = fminf(0.99f, co.w * __builtin_amdgcn_exp2f(power * 1.4426950408889634f));
-      if (alpha < 1.0f / 255.0f) continue;
-      const float test_T = T * (1 - alpha);
-      if (test_T < 0.0001f) {
-        done = true;
-        continue;
-      }
-      const float4 c = s_rgb[j];
-      const float aT = alpha * T;
-      C0 = __builtin_fmaf(c.x, aT, C0);
-      C1 = __builtin_fmaf(c.y, aT, C1);
-      C2 = __builtin_fmaf(c.z, aT, C2);
-      T = test_T;
-      last = contributor;
+    if (j0 + 64 + lane < n) {
+      g_xy = xy[nid];
+      g_co = conic_o[nid];
+      g_rgb = rgbo[nid];
     }
+    if (j0 + 128 + lane < n) nid = lst[j0 + 128 + lane];
+    for (int b = 0; b < cnt; b += kU) {
+      if (__all(done)) break;
+      float al[kU];
+      float4 c[kU];
+#pragma unroll
+      for (int k = 0; k < kU; ++k) {
+        const float2 g = s_xy[b + k];
+        const float4 co = s_co[b + k];
+        c[k] = s_rgb[b + k];
+        const float dx = g.x - pfx, dy = g.y - pfy;
+        // the hardware exp2 (v_exp_f32, ~1 ulp): pixel parity is 1e-3, not bitwise
+        const float power = __builtin_fmaf(-0.5f, __builtin_fmaf(co.x * dx, dx, co.z * dy * dy), -co.y * dx * dy);
+        const float alpha = fminf(0.99f, co.w * __builtin_amdgcn_exp2f(power * 1.4426950408889634f));
+        al[k] = (power > 0.0f || alpha < 1.0f / 255.0f) ? 0.f : alpha;
+      }
+      // front to back, branch-free: a skipped or post-stop Gaussian adds an exact zero
+#pragma unroll
+      for (int k = 0; k < kU; ++k) {
+        const float a = done ? 0.f : al[k];
+        const float test_T = T * (1 - a);
+        const bool stop = a != 0.f && test_T < 0.0001f;
+        done = done || stop;
+        const bool take = a != 0.f && !stop;
+        const float aT = take ? a * T : 0.f;
+        C0 = __builtin_fmaf(c[k].x, aT, C0);
+        C1 = __builtin_fmaf(c[k].y, aT, C1);
+        C2 = __builtin_fmaf(c[k].z, aT, C2);
+        T = take ? test_T : T;
+        last = take ? __float_as_int(c[k].w) + 1 : last;
+      }
+    }
+    __syncthreads();
   }
   if (inside) {
     const size_t pix = (size_t)py * W + px, HW = (size_t)H * W;
@@ -325,6 +410,68 @@ __global__ __launch_bounds__(256) void k_ids(int K, const unsigned* __restrict__
                                              unsigned* __restrict__ ids) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k < K) ids[k] = vals[pos[k]];
+}
+
+// Depth-ordered emission (the default binning path).  The Gaussians are
+// first sorted by depth (stable, so equal depths keep index order); each then
+// emits its rect's pairs at its offset in that order, and a stable sort on the
+// tile index alone (msb(#tiles) bits, two onesweep passes) leaves every tile's
+// list in (depth, Gaussian index) order -- the list upstream's 64-bit
+// (tile << 32 | depth bits) sort produces, with 4-byte keys and 12 bits of
+// radix instead of 32 + 12.
+__global__ __launch_bounds__(256) void k_tiles_by_rank(int P, const unsigned* __restrict__ order,
+                                                       const unsigned* __restrict__ tiles, unsigned* __restrict__ tr) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < P) tr[r] = tiles[order[r]];
+}
+__global__ __launch_bounds__(256) void k_emit_by_rank(int P, const unsigned* __restrict__ order,
+                                                      const unsigned* __restrict__ offr, const float2* __restrict__ xy,
+                                                      const int* __restrict__ radii, int gx, int gy,
+                                                      unsigned* __restrict__ keys, unsigned* __restrict__ ids) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= P) return;
+  const unsigned g = order[r];
+  if (radii[g] <= 0) return;
+  unsigned off = r == 0 ? 0u : offr[r - 1];
+  int rmin[2], rmax[2];
+  get_rect(xy[g].x, xy[g].y, radii[g], gx, gy, rmin, rmax);
+  for (int y = rmin[1]; y < rmax[1]; ++y)
+    for (int x = rmin[0]; x < rmax[0]; ++x) {
+      keys[off] = (unsigned)(y * gx + x);
+      ids[off] = g;
+      ++off;
+    }
+}
+// backward only: sorted pair -> its record slot, the pair's index in
+// Gaussian-index emission order (k_preprocess_bwd sums each Gaussian's
+// contiguous slots without atomics)
+__global__ __launch_bounds__(256) void k_slots(int K, const unsigned* __restrict__ tile_sorted,
+                                               const unsigned* __restrict__ ids, const float2* __restrict__ xy,
+                                               const int* __restrict__ radii, const unsigned* __restrict__ offsets,
+                                               int gx, int gy, unsigned* __restrict__ pos) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  const unsigned id = ids[k], tile = tile_sorted[k];
+  int rmin[2], rmax[2];
+  get_rect(xy[id].x, xy[id].y, radii[id], gx, gy, rmin, rmax);
+  const int tx = (int)(tile % (unsigned)gx), ty = (int)(tile / (unsigned)gx);
+  pos[k] = (id == 0 ? 0u : offsets[id - 1]) + (unsigned)((ty - rmin[1]) * (rmax[0] - rmin[0]) + (tx - rmin[0]));
+}
+__global__ __launch_bounds__(256) void k_ranges32(int L, const unsigned* __restrict__ keys, int rb,
+                                                  uint2* __restrict__ ranges) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= L) return;
+  const unsigned cur = keys[idx] >> rb;
+  if (idx == 0) {
+    ranges[cur].x = 0;
+  } else {
+    const unsigned prev = keys[idx - 1] >> rb;
+    if (cur != prev) {
+      ranges[prev].y = idx;
+      ranges[cur].x = idx;
+    }
+  }
+  if (idx == L - 1) ranges[cur].y = L;
 }
 
 // ------------------------------------------------------------- backward --
@@ -728,6 +875,10 @@ struct gsmpm_raster {
   void* sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
   unsigned* ids_sorted = nullptr;  // Gaussian id per sorted pair (vals_sorted holds emission indices)
+  unsigned *dorder = nullptr, *dsorted = nullptr, *tr = nullptr, *offr = nullptr;  // [capP] depth order, ranked tiles/offsets
+  void* dsort_tmp = nullptr;
+  size_t dsort_tmp_bytes = 0;
+  bool slots_pending = false;  // vals_sorted still to be derived (depth-ordered path)
   float4* rec = nullptr;           // backward pair records, 3 x float4 per pair
   size_t capRec = 0;
   // tile ranges
@@ -770,7 +921,7 @@ int gsmpm_raster_destroy(gsmpm_raster* r) {
   for (void* p : {(void*)r->radii_tmp, (void*)r->depth, (void*)r->xy, (void*)r->conic, (void*)r->rgb, (void*)r->tiles,
                   (void*)r->offsets, r->scan_tmp, (void*)r->keys, (void*)r->keys_sorted, (void*)r->vals,
                   (void*)r->vals_sorted, r->sort_tmp, (void*)r->ranges, (void*)r->ids_sorted, (void*)r->rec,
-                  (void*)r->final_T, (void*)r->n_contrib})
+                  (void*)r->final_T, (void*)r->n_contrib, (void*)r->dorder, (void*)r->dsorted, (void*)r->tr, (void*)r->offr, r->dsort_tmp})
     if (p) (void)hipFree(p);
   if (r->h_count) (void)hipHostFree(r->h_count);
   delete r;
@@ -827,7 +978,17 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     if ((rc = grow((void**)&r->rgb, cap * sizeof(float4)))) return rc;
     if ((rc = grow((void**)&r->tiles, cap * sizeof(unsigned)))) return rc;
     if ((rc = grow((void**)&r->offsets, cap * sizeof(unsigned)))) return rc;
+    if ((rc = grow((void**)&r->dorder, cap * sizeof(unsigned)))) return rc;
+    if ((rc = grow((void**)&r->dsorted, cap * sizeof(unsigned)))) return rc;
+    if ((rc = grow((void**)&r->tr, cap * sizeof(unsigned)))) return rc;
+    if ((rc = grow((void**)&r->offr, cap * sizeof(unsigned)))) return rc;
     size_t bytes = 0;
+    GSMPM_HIP(rocprim::radix_sort_pairs(nullptr, bytes, reinterpret_cast<unsigned*>(r->depth), r->dsorted,
+                                                      rocprim::counting_iterator<unsigned>(0u), r->dorder, cap, 0, 32,
+                                                      st));
+    if ((rc = grow(&r->dsort_tmp, bytes))) return rc;
+    r->dsort_tmp_bytes = bytes;
+    bytes = 0;
     GSMPM_HIP(rocprim::inclusive_scan(nullptr, bytes, r->tiles, r->offsets, cap, rocprim::plus<unsigned>(), st));
     if ((rc = grow(&r->scan_tmp, bytes))) return rc;
     r->scan_tmp_bytes = bytes;
@@ -846,6 +1007,14 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     if ((rc = grow((void**)&r->n_contrib, npix * sizeof(int)))) return rc;
     r->capPix = npix;
   }
+  // GSMPM_RASTER_WIDE_KEYS=1 forces upstream's 64-bit (tile, depth) keys (tests compare the two)
+  const char* wide = std::getenv("GSMPM_RASTER_WIDE_KEYS");
+  const bool depth_ordered = !(wide && wide[0] == '1');
+  // GSMPM_RASTER_RENDER_MODE=1 disables k_render's sub-tile culling (tests
+  // check that culling changes no pixel, final T or last contributor)
+  const char* rm = std::getenv("GSMPM_RASTER_RENDER_MODE");
+  const int render_mode = rm ? std::atoi(rm) & 1 : 0;
+  r->slots_pending = false;
   unsigned K = 0;
   if (P > 0) {
     hipLaunchKernelGGL(k_preprocess, dim3(div_up(P, 256)), dim3(256), 0, st, a, out_radii, r->depth, r->xy, r->conic,
@@ -853,6 +1022,19 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     GSMPM_LAUNCH_CHECK();
     size_t bytes = r->scan_tmp_bytes;
     GSMPM_HIP(rocprim::inclusive_scan(r->scan_tmp, bytes, r->tiles, r->offsets, (size_t)P, rocprim::plus<unsigned>(), st));
+    if (depth_ordered) {
+      // the depth order depends on P only: it runs before the count read-back,
+      // queued behind whatever the stream is still doing
+      bytes = r->dsort_tmp_bytes;
+      GSMPM_HIP(rocprim::radix_sort_pairs(r->dsort_tmp, bytes, reinterpret_cast<unsigned*>(r->depth),
+                                                        r->dsorted, rocprim::counting_iterator<unsigned>(0u),
+                                                        r->dorder, (size_t)P, 0, 32, st));
+      hipLaunchKernelGGL(k_tiles_by_rank, dim3(div_up(P, 256)), dim3(256), 0, st, P, (const unsigned*)r->dorder,
+                         (const unsigned*)r->tiles, r->tr);
+      GSMPM_LAUNCH_CHECK();
+      bytes = r->scan_tmp_bytes;
+      GSMPM_HIP(rocprim::inclusive_scan(r->scan_tmp, bytes, r->tr, r->offr, (size_t)P, rocprim::plus<unsigned>(), st));
+    }
     GSMPM_HIP(hipMemcpyAsync(r->h_count, r->offsets + (P - 1), sizeof(unsigned), hipMemcpyDeviceToHost, st));
     GSMPM_HIP(hipStreamSynchronize(st));
     K = *r->h_count;
@@ -873,10 +1055,34 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       r->sort_tmp_bytes = bytes;
       r->capK = cap;
     }
+    const int bits = msb_bits((unsigned)ntiles);
+    if (depth_ordered) {
+      size_t need = 0;
+      GSMPM_HIP(rocprim::radix_sort_pairs<OnesweepSort>(nullptr, need, reinterpret_cast<unsigned*>(r->keys),
+                                                        reinterpret_cast<unsigned*>(r->keys_sorted), r->vals,
+                                                        r->ids_sorted, (size_t)K, 0, bits, st));
+      if (need > r->sort_tmp_bytes) {
+        int rc;
+        if ((rc = grow(&r->sort_tmp, need))) return rc;
+        r->sort_tmp_bytes = need;
+      }
+      unsigned* tile_keys = reinterpret_cast<unsigned*>(r->keys);
+      unsigned* tile_sorted = reinterpret_cast<unsigned*>(r->keys_sorted);
+      hipLaunchKernelGGL(k_emit_by_rank, dim3(div_up(P, 256)), dim3(256), 0, st, P, (const unsigned*)r->dorder,
+                         (const unsigned*)r->offr, (const float2*)r->xy, (const int*)out_radii, a.grid_x, a.grid_y,
+                         tile_keys, r->vals);
+      GSMPM_LAUNCH_CHECK();
+      size_t bytes = r->sort_tmp_bytes;
+      GSMPM_HIP(rocprim::radix_sort_pairs<OnesweepSort>(r->sort_tmp, bytes, tile_keys, tile_sorted, r->vals,
+                                                        r->ids_sorted, (size_t)K, 0, bits, st));
+      hipLaunchKernelGGL(k_ranges32, dim3(div_up(K, 256)), dim3(256), 0, st, (int)K, (const unsigned*)tile_sorted, 0,
+                         r->ranges);
+      GSMPM_LAUNCH_CHECK();
+      r->slots_pending = true;
+    } else {
     hipLaunchKernelGGL(k_duplicate, dim3(div_up(P, 256)), dim3(256), 0, st, P, r->xy, r->depth, r->offsets, out_radii,
                        a.grid_x, a.grid_y, r->keys, r->vals);
     GSMPM_LAUNCH_CHECK();
-    const int bits = msb_bits((unsigned)ntiles);
     size_t bytes = r->sort_tmp_bytes;
     // values = emission indices (a Gaussian's pairs are contiguous in emission order: the
     // backward sums them without atomics); ids_sorted maps them back to Gaussians
@@ -886,9 +1092,10 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     hipLaunchKernelGGL(k_ids, dim3(div_up(K, 256)), dim3(256), 0, st, (int)K, r->vals_sorted, r->vals, r->ids_sorted);
     hipLaunchKernelGGL(k_ranges, dim3(div_up(K, 256)), dim3(256), 0, st, (int)K, r->keys_sorted, r->ranges);
     GSMPM_LAUNCH_CHECK();
+    }
   }
-  hipLaunchKernelGGL(k_render, dim3(a.grid_x, a.grid_y), dim3(kBlock), 0, st, r->ranges, r->ids_sorted, a.W, a.H,
-                     a.grid_x, r->xy, r->conic, r->rgb, in->bg, out_color, r->final_T, r->n_contrib);
+  hipLaunchKernelGGL(k_render, dim3(2 * a.grid_x, 2 * a.grid_y), dim3(64), 0, st, r->ranges, r->ids_sorted, a.W, a.H,
+                     a.grid_x, r->xy, r->conic, r->rgb, in->bg, out_color, r->final_T, r->n_contrib, render_mode);
   GSMPM_LAUNCH_CHECK();
   if (num_rendered) *num_rendered = (int32_t)K;
   r->P = P;
@@ -925,6 +1132,13 @@ int gsmpm_raster_backward(gsmpm_raster* r, const gsmpm_raster_args* in, const in
     int rc;
     if ((rc = grow((void**)&r->rec, (K + K / 4 + 1024) * 3 * sizeof(float4)))) return rc;
     r->capRec = K + K / 4 + 1024;
+  }
+  if (K > 0 && r->slots_pending) {
+    hipLaunchKernelGGL(k_slots, dim3(div_up(K, 256)), dim3(256), 0, st, (int)K,
+                       (const unsigned*)reinterpret_cast<unsigned*>(r->keys_sorted), (const unsigned*)r->ids_sorted,
+                       (const float2*)r->xy, radii, (const unsigned*)r->offsets, r->gx, r->gy, r->vals_sorted);
+    GSMPM_LAUNCH_CHECK();
+    r->slots_pending = false;
   }
   if (K > 0)
     hipLaunchKernelGGL(k_render_bwd, dim3(r->gx, r->gy), dim3(kBlock), 0, st, r->ranges, r->vals_sorted,

@@ -105,3 +105,102 @@ def test_empty_and_culled(dev):
     with pytest.raises(Exception):
         GaussianRasterizer(st)(means3D=t(means), means2D=None, opacities=t(np.ones((10, 1), np.float32)),
                                cov3D_precomp=t(c6))
+
+
+def test_narrow_keys_match_upstream_keys(dev, monkeypatch):
+    """The narrow (tile << rb | depth rank) 32-bit binning keys give the same
+    sorted pair list as upstream's 64-bit (tile << 32 | depth bits) keys:
+    images, radii and every input gradient bitwise equal; equal depths (ties
+    broken by Gaussian index) included."""
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    P, W, H = 4000, 240, 160
+    means, c6, opa, shs = _scene(P, seed=11)
+    means[1::7, 2] = means[::7, 2][: len(means[1::7])]  # depth ties
+    view, full, campos, tx, ty = _camera(W, H, 0.9)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    st = GaussianRasterizationSettings(image_height=H, image_width=W, tanfovx=tx, tanfovy=ty,
+                                       bg=t(np.zeros(3, np.float32)), scale_modifier=1.0, viewmatrix=t(view),
+                                       projmatrix=t(full), sh_degree=3, campos=t(campos), prefiltered=False,
+                                       debug=False)
+    outs = []
+    for wide in ("0", "1"):
+        monkeypatch.setenv("GSMPM_RASTER_WIDE_KEYS", wide)
+        m, s, o, c = (t(a).requires_grad_(True) for a in (means, shs, opa, c6))
+        color, radii = GaussianRasterizer(st)(means3D=m, means2D=None, opacities=o, shs=s, cov3D_precomp=c)
+        (color * torch.linspace(0.5, 1.5, color.numel(), device=dev).reshape(color.shape)).sum().backward()
+        outs.append([x.detach().cpu().numpy() for x in (color, radii, m.grad, s.grad, o.grad, c.grad)])
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+
+
+def _dense_scene(P, seed, lo, hi):
+    """Heavy tiles (~1000 pairs each) of faint Gaussians (opacity log-uniform in
+    [lo, hi]): most list entries fall to k_render's sub-tile culling, and T
+    falls below the 1e-4 stop at different depths per pixel (11-72 % of the
+    pixels stop for the cases below)."""
+    rng = np.random.default_rng(seed)
+    means = (rng.uniform(-1, 1, size=(P, 3)) * np.array([1.3, 0.975, 0.5])).astype(np.float32)
+    A = rng.normal(0, 1, size=(P, 3, 3)) * 0.05
+    cov = A @ A.transpose(0, 2, 1) + np.eye(3) * 1e-3
+    c6 = np.stack([cov[:, 0, 0], cov[:, 0, 1], cov[:, 0, 2], cov[:, 1, 1], cov[:, 1, 2], cov[:, 2, 2]], 1)
+    opa = np.exp(rng.uniform(np.log(lo), np.log(hi), size=(P, 1))).astype(np.float32)
+    shs = (rng.normal(0, 0.3, size=(P, 16, 3))).astype(np.float32)
+    shs[:, 0] += 0.8
+    return means, c6.astype(np.float32), opa, shs
+
+
+@pytest.mark.parametrize("P,W,H,lo,hi", [(8000, 100, 72, 0.02, 0.3), (8000, 100, 72, 0.03, 0.5),
+                                         (4000, 64, 48, 0.05, 0.7)])
+def test_segmented_blend_vs_oracle(dev, P, W, H, lo, hi):
+    import oracle as O
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    means, c6, opa, shs = _dense_scene(P, P, lo, hi)
+    view, full, campos, tx, ty = _camera(W, H, 0.9)
+    bgv = np.full(3, 0.5, np.float32)
+    oc, orad, oK, _, _ = O.raster_forward(means, opa, view, full, campos, bgv, W, H, tx, ty, shs=shs,
+                                          sh_degree=3, cov3D_precomp=c6)
+    assert oK > 40 * ((W + 15) // 16) * ((H + 15) // 16)  # lists far longer than one 64-entry segment
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    st = GaussianRasterizationSettings(image_height=H, image_width=W, tanfovx=tx, tanfovy=ty, bg=t(bgv),
+                                       scale_modifier=1.0, viewmatrix=t(view), projmatrix=t(full), sh_degree=3,
+                                       campos=t(campos), prefiltered=False, debug=False)
+    color, radii = GaussianRasterizer(st)(means3D=t(means), means2D=None, opacities=t(opa), shs=t(shs),
+                                          cov3D_precomp=t(c6))
+    assert np.array_equal(radii.cpu().numpy(), orad)
+    err = np.abs(color.cpu().numpy() - oc)
+    assert err.max() < 1e-3, (err.max(), (err > 1e-3).sum())
+
+
+@pytest.mark.parametrize("scene", ["dense", "sparse"])
+def test_subtile_culling_changes_nothing(dev, monkeypatch, scene):
+    """k_render's sub-tile culling only drops Gaussians upstream's loop skips
+    (alpha < 1/255 at every pixel of the sub-tile): pixels, final T and last
+    contributor -- hence the backward's gradients -- are bit-identical with
+    culling off (GSMPM_RASTER_RENDER_MODE=1)."""
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    if scene == "dense":
+        P, W, H = 8000, 100, 72
+        means, c6, opa, shs = _dense_scene(P, P, 0.03, 0.5)
+    else:
+        P, W, H = 3000, 256, 192
+        means, c6, opa, shs = _scene(P, seed=7)
+    view, full, campos, tx, ty = _camera(W, H, 0.9)
+    rng = np.random.default_rng(1)
+    wgt = torch.from_numpy(rng.normal(0, 1, (3, H, W)).astype(np.float32)).to(dev)
+    t = lambda a, g=False: torch.from_numpy(np.ascontiguousarray(a)).to(dev).requires_grad_(g)
+    st = GaussianRasterizationSettings(image_height=H, image_width=W, tanfovx=tx, tanfovy=ty,
+                                       bg=t(np.full(3, 0.25, np.float32)), scale_modifier=1.0, viewmatrix=t(view),
+                                       projmatrix=t(full), sh_degree=3, campos=t(campos), prefiltered=False,
+                                       debug=False)
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("GSMPM_RASTER_RENDER_MODE", mode)
+        m3, o1, s1, cv = t(means, True), t(opa, True), t(shs, True), t(c6, True)
+        img, _ = GaussianRasterizer(st)(means3D=m3, means2D=None, opacities=o1, shs=s1, cov3D_precomp=cv)
+        (img * wgt).sum().backward()
+        out[mode] = [x.detach().cpu().numpy() for x in (img, m3.grad, o1.grad, s1.grad, cv.grad)]
+    for a, b in zip(out["0"], out["1"]):
+        assert np.array_equal(a, b)

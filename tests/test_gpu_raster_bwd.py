@@ -16,7 +16,7 @@ import pytest
 import torch
 
 from conftest import rel_err
-from test_gpu_raster import _camera, _scene
+from test_gpu_raster import _camera, _dense_scene, _scene
 
 pytestmark = pytest.mark.gpu
 
@@ -32,11 +32,14 @@ def _close(a, b, what):
 
 
 @pytest.mark.parametrize("P,W,H,D,mode", [(2000, 200, 200, 3, "cov"), (3000, 256, 192, 1, "sr"),
-                                          (1500, 160, 160, 0, "colors"), (5000, 320, 240, 2, "cov")])
+                                          (1500, 160, 160, 0, "colors"), (5000, 320, 240, 2, "cov"),
+                                          (8000, 100, 72, 3, "dense")])
 def test_raster_backward_vs_oracle(dev, P, W, H, D, mode):
     import oracle as O
     from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
-    means, c6, opa, shs = _scene(P, seed=P + W + D)
+    # "dense": ~1300-pair tile lists whose pixels stop in every list segment
+    # (the forward's segmented blend and re-blend path feed final_T/n_contrib)
+    means, c6, opa, shs = _dense_scene(P, P, 0.03, 0.5) if mode == "dense" else _scene(P, seed=P + W + D)
     rng = np.random.default_rng(P)
     scales = np.exp(rng.normal(-3.2, 0.4, (P, 3))).astype(np.float32)
     rots = rng.normal(0, 1, (P, 4)).astype(np.float32)
