@@ -275,9 +275,10 @@ __global__ __launch_bounds__(256) void k_ranges(int L, const unsigned long long*
 }
 
 // k_render: one wave64 workgroup per 8x8 quarter of a 16x16 tile, walking
-// the tile's list front to back in batches of 64 entries (the next batch's
-// gather and the list ids of the one after are in flight while a batch
-// blends).
+// the tile's list front to back in batches of 256 entries, 4 per lane (the
+// next batch's gather and the list ids of the one after are in flight while
+// a batch blends; with most entries culled a batch blends in less than a
+// gather round trip, so batches are sized to cut the round trips).
 //
 // Sub-tile culling.  A tile's list holds every Gaussian whose 3-sigma rect
 // touches the tile, but a faint Gaussian reaches alpha >= 1/255 only inside a
@@ -295,7 +296,9 @@ __global__ __launch_bounds__(256) void k_ranges(int L, const unsigned long long*
 // evaluated independently (their LDS reads and exp2s pipeline) and then folded
 // in order, branch-free.
 constexpr int kU = 8;
-constexpr int kSub = 8;  // pixel sub-tile side: one wave of pixels
+constexpr int kSub = 8;          // pixel sub-tile side: one wave of pixels
+constexpr int kQ = 4;            // list entries per lane per batch
+constexpr int kBatch = 64 * kQ;  // entries staged per batch
 
 // can alpha = o exp(power) reach 1/255 at a pixel centre of the sub-tile
 // [x0, x0 + 7] x [y0, y0 + 7]?  Conservative; NaNs keep the Gaussian.
@@ -313,9 +316,9 @@ __global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges,
                                                const float4* __restrict__ conic_o, const float4* __restrict__ rgbo,
                                                const float* __restrict__ bg, float* __restrict__ out,
                                                float* __restrict__ final_T, int* __restrict__ n_contrib, int mode) {
-  __shared__ float2 s_xy[64];
-  __shared__ float4 s_co[64];
-  __shared__ float4 s_rgb[64];  // .w: the entry's tile-list index (as int bits)
+  __shared__ float2 s_xy[kBatch];
+  __shared__ float4 s_co[kBatch];
+  __shared__ float4 s_rgb[kBatch];  // .w: the entry's tile-list index (as int bits)
   const int lane = threadIdx.x;
   const int x0 = blockIdx.x * kSub, y0 = blockIdx.y * kSub;
   const int px = x0 + (lane & (kSub - 1)), py = y0 + (lane / kSub);
@@ -327,28 +330,41 @@ __global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges,
   float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f;
   int last = 0;
   bool done = !inside;
-  float2 g_xy = make_float2(0.f, 0.f);
-  float4 g_co = make_float4(0.f, 0.f, 0.f, 0.f), g_rgb = g_co;
-  unsigned nid = 0;
-  if (lane < n) {
-    const unsigned id = lst[lane];
-    g_xy = xy[id];
-    g_co = conic_o[id];
-    g_rgb = rgbo[id];
+  // lane holds entries j0 + 64 q + lane, q < kQ
+  float2 g_xy[kQ];
+  float4 g_co[kQ], g_rgb[kQ];
+  unsigned nid[kQ];
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) {
+    g_xy[q] = make_float2(0.f, 0.f);
+    g_co[q] = g_rgb[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    nid[q] = 0;
+    if (64 * q + lane < n) {
+      const unsigned id = lst[64 * q + lane];
+      g_xy[q] = xy[id];
+      g_co[q] = conic_o[id];
+      g_rgb[q] = rgbo[id];
+    }
+    if (kBatch + 64 * q + lane < n) nid[q] = lst[kBatch + 64 * q + lane];
   }
-  if (64 + lane < n) nid = lst[64 + lane];
-  for (int j0 = 0; j0 < n; j0 += 64) {
+  for (int j0 = 0; j0 < n; j0 += kBatch) {
     if (__all(done)) break;
     // stage the batch's survivors in list order; slots up to the next
     // multiple of kU are zero (opacity 0: alpha 0, and fma(0, 0, C) = C)
-    const bool keep = j0 + lane < n && ((mode & 1) || reaches_subtile(g_xy, g_co, fx0, fy0));
-    const unsigned long long m = __ballot(keep);
-    const int pos = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-    const int cnt = __popcll(m);
-    if (keep) {
-      s_xy[pos] = g_xy;
-      s_co[pos] = g_co;
-      s_rgb[pos] = make_float4(g_rgb.x, g_rgb.y, g_rgb.z, __int_as_float(j0 + lane));
+    int cnt = 0;
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      const int j = j0 + 64 * q + lane;
+      const bool keep = j < n && ((mode & 1) || reaches_subtile(g_xy[q], g_co[q], fx0, fy0));
+      const unsigned long long m = __ballot(keep);
+      const int pos =
+          cnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+      if (keep) {
+        s_xy[pos] = g_xy[q];
+        s_co[pos] = g_co[q];
+        s_rgb[pos] = make_float4(g_rgb[q].x, g_rgb[q].y, g_rgb[q].z, __int_as_float(j));
+      }
+      cnt += __popcll(m);
     }
     if (lane < ((cnt + kU - 1) & ~(kU - 1)) - cnt) {
       s_xy[cnt + lane] = make_float2(0.f, 0.f);
@@ -356,12 +372,16 @@ __global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges,
       s_rgb[cnt + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
     __syncthreads();
-    if (j0 + 64 + lane < n) {
-      g_xy = xy[nid];
-      g_co = conic_o[nid];
-      g_rgb = rgbo[nid];
+    // the next batch's gather and the one after's list ids fly while this one blends
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      if (j0 + kBatch + 64 * q + lane < n) {
+        g_xy[q] = xy[nid[q]];
+        g_co[q] = conic_o[nid[q]];
+        g_rgb[q] = rgbo[nid[q]];
+      }
+      if (j0 + 2 * kBatch + 64 * q + lane < n) nid[q] = lst[j0 + 2 * kBatch + 64 * q + lane];
     }
-    if (j0 + 128 + lane < n) nid = lst[j0 + 128 + lane];
     for (int b = 0; b < cnt; b += kU) {
       if (__all(done)) break;
       float al[kU];
