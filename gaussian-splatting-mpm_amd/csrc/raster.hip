@@ -44,6 +44,7 @@
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -423,6 +424,11 @@ __global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges,
     final_T[pix] = T;
     n_contrib[pix] = last;
   }
+}
+
+constexpr unsigned kNoCount = 0xffffffffu;
+__global__ void k_publish_count(const unsigned* __restrict__ src, unsigned* dst) {
+  __hip_atomic_store(dst, *src, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // sorted emission index -> Gaussian id (the sort carries emission indices)
@@ -1055,9 +1061,23 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       bytes = r->scan_tmp_bytes;
       GSMPM_HIP(rocprim::inclusive_scan(r->scan_tmp, bytes, r->tr, r->offr, (size_t)P, rocprim::plus<unsigned>(), st));
     }
-    GSMPM_HIP(hipMemcpyAsync(r->h_count, r->offsets + (P - 1), sizeof(unsigned), hipMemcpyDeviceToHost, st));
-    GSMPM_HIP(hipStreamSynchronize(st));
-    K = *r->h_count;
+    // K straight into pinned (coherent) host memory by a one-lane kernel, and a
+    // spin on it: no copy-engine packet and no sleeping stream sync between
+    // the scan and the post-count launches.  A spin longer than 2 s falls back
+    // to the stream sync (which also surfaces any fault).
+    volatile unsigned* hc = r->h_count;
+    *hc = kNoCount;
+    hipLaunchKernelGGL(k_publish_count, dim3(1), dim3(1), 0, st, (const unsigned*)(r->offsets + (P - 1)), r->h_count);
+    GSMPM_LAUNCH_CHECK();
+    const auto t0 = std::chrono::steady_clock::now();
+    while (*hc == kNoCount) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+        GSMPM_HIP(hipStreamSynchronize(st));
+        break;
+      }
+    }
+    K = *hc;
+    GSMPM_REQUIRE(K != kNoCount, "gsmpm_raster_forward: the pair count never arrived");
   }
   if (K > 0) {
     if (K > r->capK) {
