@@ -40,6 +40,7 @@
 //                    2D-covariance / projection / SH / 3D-covariance adjoints.
 #include <hip/hip_runtime.h>
 
+#include <rocprim/block/block_radix_sort.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
@@ -468,6 +469,73 @@ __global__ __launch_bounds__(256) void k_emit_by_rank(int P, const unsigned* __r
       ++off;
     }
 }
+// Stable tile sort of the depth-ordered emission list for <= kMaxTiles tiles
+// (replaces the two onesweep passes: 2 kernels + a scan instead of ~8
+// launches, no look-back chain).  The list is cut into chunks of kChunk pairs.
+//   k_tile_hist     per chunk, the pair count of every tile (LDS atomics),
+//                   stored tile-major: H[t * nch + c]
+//   exclusive scan  over H -> the output position of chunk c's first pair of
+//                   tile t (tile-major order = sorted order)
+//   k_tile_scatter  per chunk, a stable block radix sort on the tile bits in
+//                   LDS; a pair at sorted position s of run [s0, ..) of tile t
+//                   lands at H'[t * nch + c] + s - s0.  Chunk 0 also writes
+//                   every tile's [start, end).
+constexpr int kMaxTiles = 4096, kSortT = 256, kSortI = 8, kChunk = kSortT * kSortI;
+__global__ __launch_bounds__(kSortT) void k_tile_hist(int K, int ntiles, int nch, const unsigned* __restrict__ keys,
+                                                      unsigned* __restrict__ H) {
+  __shared__ unsigned s_h[kMaxTiles];
+  for (int t = threadIdx.x; t < ntiles; t += kSortT) s_h[t] = 0;
+  __syncthreads();
+  const int c = blockIdx.x;
+  for (int i = threadIdx.x; i < kChunk; i += kSortT) {
+    const int e = c * kChunk + i;
+    if (e < K) atomicAdd(&s_h[keys[e]], 1u);
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < ntiles; t += kSortT) H[(size_t)t * nch + c] = s_h[t];
+}
+__global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int nch, int bits,
+                                                         const unsigned* __restrict__ keys,
+                                                         const unsigned* __restrict__ vals,
+                                                         const unsigned* __restrict__ Hs,
+                                                         unsigned* __restrict__ keys_out, unsigned* __restrict__ vals_out,
+                                                         uint2* __restrict__ ranges) {
+  using BRS = rocprim::block_radix_sort<unsigned, kSortT, kSortI, unsigned>;
+  __shared__ typename BRS::storage_type s_sort;
+  __shared__ unsigned s_key[kChunk];
+  __shared__ int s_start[kMaxTiles];
+  const int c = blockIdx.x;
+  const unsigned pad = (1u << bits) - 1u;  // >= ntiles: sorts last, never stored
+  unsigned k[kSortI], v[kSortI];
+#pragma unroll
+  for (int i = 0; i < kSortI; ++i) {
+    const int e = c * kChunk + threadIdx.x * kSortI + i;  // blocked: the sort is stable in this order
+    k[i] = e < K ? keys[e] : pad;
+    v[i] = e < K ? vals[e] : 0u;
+  }
+  BRS().sort(k, v, s_sort, 0, bits);
+#pragma unroll
+  for (int i = 0; i < kSortI; ++i) s_key[threadIdx.x * kSortI + i] = k[i];
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kSortI; ++i) {
+    const int sp = threadIdx.x * kSortI + i;
+    if (k[i] != pad && (sp == 0 || s_key[sp - 1] != k[i])) s_start[k[i]] = sp;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kSortI; ++i) {
+    if (k[i] == pad) continue;
+    const int sp = threadIdx.x * kSortI + i;
+    const unsigned pos = Hs[(size_t)k[i] * nch + c] + (unsigned)(sp - s_start[k[i]]);
+    keys_out[pos] = k[i];
+    vals_out[pos] = v[i];
+  }
+  if (c == 0)
+    for (int t = threadIdx.x; t < ntiles; t += kSortT)
+      ranges[t] = make_uint2(Hs[(size_t)t * nch], t + 1 < ntiles ? Hs[(size_t)(t + 1) * nch] : (unsigned)K);
+}
+
 // backward only: sorted pair -> its record slot, the pair's index in
 // Gaussian-index emission order (k_preprocess_bwd sums each Gaussian's
 // contiguous slots without atomics)
@@ -903,6 +971,8 @@ struct gsmpm_raster {
   unsigned* ids_sorted = nullptr;  // Gaussian id per sorted pair (vals_sorted holds emission indices)
   unsigned *dorder = nullptr, *dsorted = nullptr, *tr = nullptr, *offr = nullptr;  // [capP] depth order, ranked tiles/offsets
   void* dsort_tmp = nullptr;
+  unsigned* hist = nullptr;  // [2 * capH] tile-major chunk histogram, then its exclusive scan
+  size_t capH = 0;
   size_t dsort_tmp_bytes = 0;
   bool slots_pending = false;  // vals_sorted still to be derived (depth-ordered path)
   float4* rec = nullptr;           // backward pair records, 3 x float4 per pair
@@ -947,7 +1017,7 @@ int gsmpm_raster_destroy(gsmpm_raster* r) {
   for (void* p : {(void*)r->radii_tmp, (void*)r->depth, (void*)r->xy, (void*)r->conic, (void*)r->rgb, (void*)r->tiles,
                   (void*)r->offsets, r->scan_tmp, (void*)r->keys, (void*)r->keys_sorted, (void*)r->vals,
                   (void*)r->vals_sorted, r->sort_tmp, (void*)r->ranges, (void*)r->ids_sorted, (void*)r->rec,
-                  (void*)r->final_T, (void*)r->n_contrib, (void*)r->dorder, (void*)r->dsorted, (void*)r->tr, (void*)r->offr, r->dsort_tmp})
+                  (void*)r->final_T, (void*)r->n_contrib, (void*)r->dorder, (void*)r->dsorted, (void*)r->tr, (void*)r->offr, r->dsort_tmp, (void*)r->hist})
     if (p) (void)hipFree(p);
   if (r->h_count) (void)hipHostFree(r->h_count);
   delete r;
@@ -1097,27 +1167,54 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     }
     const int bits = msb_bits((unsigned)ntiles);
     if (depth_ordered) {
+      unsigned* tile_keys = reinterpret_cast<unsigned*>(r->keys);
+      unsigned* tile_sorted = reinterpret_cast<unsigned*>(r->keys_sorted);
+      // the chunked counting sort needs the tile histogram in LDS; GSMPM_RASTER_ONESWEEP=1 forces rocPRIM
+      const char* os = std::getenv("GSMPM_RASTER_ONESWEEP");
+      const bool chunked = ntiles <= (size_t)kMaxTiles && !(os && os[0] == '1');
+      const int nch = (int)div_up(K, kChunk);
       size_t need = 0;
-      GSMPM_HIP(rocprim::radix_sort_pairs<OnesweepSort>(nullptr, need, reinterpret_cast<unsigned*>(r->keys),
-                                                        reinterpret_cast<unsigned*>(r->keys_sorted), r->vals,
-                                                        r->ids_sorted, (size_t)K, 0, bits, st));
+      if (chunked) {
+        const size_t nh = ntiles * (size_t)nch;
+        if (nh > r->capH) {
+          int rc;
+          if ((rc = grow((void**)&r->hist, 2 * (nh + nh / 4 + 1024) * sizeof(unsigned)))) return rc;
+          r->capH = nh + nh / 4 + 1024;
+        }
+        GSMPM_HIP(rocprim::exclusive_scan(nullptr, need, r->hist, r->hist + r->capH, 0u, nh, rocprim::plus<unsigned>(),
+                                          st));
+      } else {
+        GSMPM_HIP(rocprim::radix_sort_pairs<OnesweepSort>(nullptr, need, tile_keys, tile_sorted, r->vals,
+                                                          r->ids_sorted, (size_t)K, 0, bits, st));
+      }
       if (need > r->sort_tmp_bytes) {
         int rc;
         if ((rc = grow(&r->sort_tmp, need))) return rc;
         r->sort_tmp_bytes = need;
       }
-      unsigned* tile_keys = reinterpret_cast<unsigned*>(r->keys);
-      unsigned* tile_sorted = reinterpret_cast<unsigned*>(r->keys_sorted);
       hipLaunchKernelGGL(k_emit_by_rank, dim3(div_up(P, 256)), dim3(256), 0, st, P, (const unsigned*)r->dorder,
                          (const unsigned*)r->offr, (const float2*)r->xy, (const int*)out_radii, a.grid_x, a.grid_y,
                          tile_keys, r->vals);
       GSMPM_LAUNCH_CHECK();
       size_t bytes = r->sort_tmp_bytes;
-      GSMPM_HIP(rocprim::radix_sort_pairs<OnesweepSort>(r->sort_tmp, bytes, tile_keys, tile_sorted, r->vals,
-                                                        r->ids_sorted, (size_t)K, 0, bits, st));
-      hipLaunchKernelGGL(k_ranges32, dim3(div_up(K, 256)), dim3(256), 0, st, (int)K, (const unsigned*)tile_sorted, 0,
-                         r->ranges);
-      GSMPM_LAUNCH_CHECK();
+      if (chunked) {
+        const size_t nh = ntiles * (size_t)nch;
+        unsigned* Hs = r->hist + r->capH;
+        hipLaunchKernelGGL(k_tile_hist, dim3(nch), dim3(kSortT), 0, st, (int)K, (int)ntiles, nch,
+                           (const unsigned*)tile_keys, r->hist);
+        GSMPM_LAUNCH_CHECK();
+        GSMPM_HIP(rocprim::exclusive_scan(r->sort_tmp, bytes, r->hist, Hs, 0u, nh, rocprim::plus<unsigned>(), st));
+        hipLaunchKernelGGL(k_tile_scatter, dim3(nch), dim3(kSortT), 0, st, (int)K, (int)ntiles, nch, bits,
+                           (const unsigned*)tile_keys, (const unsigned*)r->vals, (const unsigned*)Hs, tile_sorted,
+                           r->ids_sorted, r->ranges);
+        GSMPM_LAUNCH_CHECK();
+      } else {
+        GSMPM_HIP(rocprim::radix_sort_pairs<OnesweepSort>(r->sort_tmp, bytes, tile_keys, tile_sorted, r->vals,
+                                                          r->ids_sorted, (size_t)K, 0, bits, st));
+        hipLaunchKernelGGL(k_ranges32, dim3(div_up(K, 256)), dim3(256), 0, st, (int)K, (const unsigned*)tile_sorted,
+                           0, r->ranges);
+        GSMPM_LAUNCH_CHECK();
+      }
       r->slots_pending = true;
     } else {
     hipLaunchKernelGGL(k_duplicate, dim3(div_up(P, 256)), dim3(256), 0, st, P, r->xy, r->depth, r->offsets, out_radii,

@@ -107,14 +107,17 @@ def test_empty_and_culled(dev):
                                cov3D_precomp=t(c6))
 
 
-def test_narrow_keys_match_upstream_keys(dev, monkeypatch):
-    """The narrow (tile << rb | depth rank) 32-bit binning keys give the same
-    sorted pair list as upstream's 64-bit (tile << 32 | depth bits) keys:
-    images, radii and every input gradient bitwise equal; equal depths (ties
-    broken by Gaussian index) included."""
+@pytest.mark.parametrize("W,H", [(240, 160), (1104, 1000)])
+def test_narrow_keys_match_upstream_keys(dev, monkeypatch, W, H):
+    """The depth-ordered binning (depth sort, then a stable sort on the tile
+    index alone: the chunked counting sort for <= 4096 tiles, rocPRIM onesweep
+    above or with GSMPM_RASTER_ONESWEEP=1) gives the same sorted pair lists as
+    upstream's 64-bit (tile << 32 | depth bits) keys: images, radii and every
+    input gradient bitwise equal; equal depths (ties broken by Gaussian index)
+    included.  1104 x 1000 has 4347 tiles (onesweep fallback)."""
     import torch
     from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
-    P, W, H = 4000, 240, 160
+    P = 4000
     means, c6, opa, shs = _scene(P, seed=11)
     means[1::7, 2] = means[::7, 2][: len(means[1::7])]  # depth ties
     view, full, campos, tx, ty = _camera(W, H, 0.9)
@@ -124,14 +127,16 @@ def test_narrow_keys_match_upstream_keys(dev, monkeypatch):
                                        projmatrix=t(full), sh_degree=3, campos=t(campos), prefiltered=False,
                                        debug=False)
     outs = []
-    for wide in ("0", "1"):
+    for wide, onesweep in (("1", "0"), ("0", "0"), ("0", "1")):
         monkeypatch.setenv("GSMPM_RASTER_WIDE_KEYS", wide)
+        monkeypatch.setenv("GSMPM_RASTER_ONESWEEP", onesweep)
         m, s, o, c = (t(a).requires_grad_(True) for a in (means, shs, opa, c6))
         color, radii = GaussianRasterizer(st)(means3D=m, means2D=None, opacities=o, shs=s, cov3D_precomp=c)
         (color * torch.linspace(0.5, 1.5, color.numel(), device=dev).reshape(color.shape)).sum().backward()
         outs.append([x.detach().cpu().numpy() for x in (color, radii, m.grad, s.grad, o.grad, c.grad)])
-    for a, b in zip(*outs):
-        assert np.array_equal(a, b)
+    for other in outs[1:]:
+        for a, b in zip(outs[0], other):
+            assert np.array_equal(a, b)
 
 
 def _dense_scene(P, seed, lo, hi):
