@@ -313,11 +313,19 @@ __device__ __forceinline__ bool reaches_subtile(float2 g, float4 co, float x0, f
   return !(g.x + ex < x0 || g.x - ex > x0 + (kSub - 1) || g.y + ey < y0 || g.y - ey > y0 + (kSub - 1));
 }
 
+// Tile keys of the depth-ordered path carry, above the tile index, a mask of
+// the tile's four 8x8 sub-tiles the Gaussian can reach (alpha >= 1/255 there,
+// reaches_subtile); a pair that reaches none of them gets kCulledKey and is
+// sorted out of the tile lists (it is one upstream's blend skips at every
+// pixel of the tile).  num_rendered stays upstream's rect count.
+constexpr unsigned kMaskShift = 28, kTileField = (1u << kMaskShift) - 1u, kCulledKey = kTileField;
+constexpr unsigned kNoEntry = 0xffffffffu;  // id of a chunk-tail slot past K
 __global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges, const unsigned* __restrict__ list,
                                                int W, int H, int gx, const float2* __restrict__ xy,
                                                const float4* __restrict__ conic_o, const float4* __restrict__ rgbo,
                                                const float* __restrict__ bg, float* __restrict__ out,
-                                               float* __restrict__ final_T, int* __restrict__ n_contrib, int mode) {
+                                               float* __restrict__ final_T, int* __restrict__ n_contrib,
+                                               const unsigned* __restrict__ tkeys, int mode) {
   __shared__ float2 s_xy[kBatch];
   __shared__ float4 s_co[kBatch];
   __shared__ float4 s_rgb[kBatch];  // .w: the entry's tile-list index (as int bits)
@@ -333,21 +341,34 @@ __global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges,
   int last = 0;
   bool done = !inside;
   // lane holds entries j0 + 64 q + lane, q < kQ
+  // with tkeys (the depth-ordered sort's keys), an entry's sub-tile mask says
+  // whether it reaches this quarter: the gather of one that does not is
+  // skipped; without, the quarter test runs on the gathered conic
+  const unsigned* tk = tkeys ? tkeys + range.x : nullptr;
+  const unsigned qbit = 1u << (kMaskShift + (((blockIdx.y & 1) << 1) | (blockIdx.x & 1)));
   float2 g_xy[kQ];
   float4 g_co[kQ], g_rgb[kQ];
   unsigned nid[kQ];
+  bool g_rel[kQ], n_rel[kQ];
 #pragma unroll
   for (int q = 0; q < kQ; ++q) {
     g_xy[q] = make_float2(0.f, 0.f);
     g_co[q] = g_rgb[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     nid[q] = 0;
+    g_rel[q] = n_rel[q] = false;
     if (64 * q + lane < n) {
-      const unsigned id = lst[64 * q + lane];
-      g_xy[q] = xy[id];
-      g_co[q] = conic_o[id];
-      g_rgb[q] = rgbo[id];
+      g_rel[q] = !tk || (tk[64 * q + lane] & qbit);
+      if (g_rel[q]) {
+        const unsigned id = lst[64 * q + lane];
+        g_xy[q] = xy[id];
+        g_co[q] = conic_o[id];
+        g_rgb[q] = rgbo[id];
+      }
     }
-    if (kBatch + 64 * q + lane < n) nid[q] = lst[kBatch + 64 * q + lane];
+    if (kBatch + 64 * q + lane < n) {
+      nid[q] = lst[kBatch + 64 * q + lane];
+      n_rel[q] = !tk || (tk[kBatch + 64 * q + lane] & qbit);
+    }
   }
   for (int j0 = 0; j0 < n; j0 += kBatch) {
     if (__all(done)) break;
@@ -357,7 +378,7 @@ __global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges,
 #pragma unroll
     for (int q = 0; q < kQ; ++q) {
       const int j = j0 + 64 * q + lane;
-      const bool keep = j < n && ((mode & 1) || reaches_subtile(g_xy[q], g_co[q], fx0, fy0));
+      const bool keep = j < n && g_rel[q] && (tk || (mode & 1) || reaches_subtile(g_xy[q], g_co[q], fx0, fy0));
       const unsigned long long m = __ballot(keep);
       const int pos =
           cnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
@@ -377,12 +398,16 @@ __global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges,
     // the next batch's gather and the one after's list ids fly while this one blends
 #pragma unroll
     for (int q = 0; q < kQ; ++q) {
-      if (j0 + kBatch + 64 * q + lane < n) {
+      g_rel[q] = j0 + kBatch + 64 * q + lane < n && n_rel[q];
+      if (g_rel[q]) {
         g_xy[q] = xy[nid[q]];
         g_co[q] = conic_o[nid[q]];
         g_rgb[q] = rgbo[nid[q]];
       }
-      if (j0 + 2 * kBatch + 64 * q + lane < n) nid[q] = lst[j0 + 2 * kBatch + 64 * q + lane];
+      if (j0 + 2 * kBatch + 64 * q + lane < n) {
+        nid[q] = lst[j0 + 2 * kBatch + 64 * q + lane];
+        n_rel[q] = !tk || (tk[j0 + 2 * kBatch + 64 * q + lane] & qbit);
+      }
     }
     for (int b = 0; b < cnt; b += kU) {
       if (__all(done)) break;
@@ -453,18 +478,29 @@ __global__ __launch_bounds__(256) void k_tiles_by_rank(int P, const unsigned* __
 }
 __global__ __launch_bounds__(256) void k_emit_by_rank(int P, const unsigned* __restrict__ order,
                                                       const unsigned* __restrict__ offr, const float2* __restrict__ xy,
-                                                      const int* __restrict__ radii, int gx, int gy,
+                                                      const float4* __restrict__ conic_o,
+                                                      const int* __restrict__ radii, int gx, int gy, int cull,
                                                       unsigned* __restrict__ keys, unsigned* __restrict__ ids) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= P) return;
   const unsigned g = order[r];
   if (radii[g] <= 0) return;
   unsigned off = r == 0 ? 0u : offr[r - 1];
+  const float2 gp = xy[g];
+  const float4 co = conic_o[g];
   int rmin[2], rmax[2];
-  get_rect(xy[g].x, xy[g].y, radii[g], gx, gy, rmin, rmax);
+  get_rect(gp.x, gp.y, radii[g], gx, gy, rmin, rmax);
   for (int y = rmin[1]; y < rmax[1]; ++y)
     for (int x = rmin[0]; x < rmax[0]; ++x) {
-      keys[off] = (unsigned)(y * gx + x);
+      unsigned m = 0xfu;
+      if (cull) {
+        m = 0u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (reaches_subtile(gp, co, (float)(x * kBX + (q & 1) * kSub), (float)(y * kBY + (q >> 1) * kSub)))
+            m |= 1u << q;
+      }
+      keys[off] = m ? ((unsigned)(y * gx + x) | (m << kMaskShift)) : kCulledKey;
       ids[off] = g;
       ++off;
     }
@@ -481,18 +517,25 @@ __global__ __launch_bounds__(256) void k_emit_by_rank(int P, const unsigned* __r
 //                   lands at H'[t * nch + c] + s - s0.  Chunk 0 also writes
 //                   every tile's [start, end).
 constexpr int kMaxTiles = 4096, kSortT = 256, kSortI = 8, kChunk = kSortT * kSortI;
-__global__ __launch_bounds__(kSortT) void k_tile_hist(int K, int ntiles, int nch, const unsigned* __restrict__ keys,
-                                                      unsigned* __restrict__ H) {
-  __shared__ unsigned s_h[kMaxTiles];
-  for (int t = threadIdx.x; t < ntiles; t += kSortT) s_h[t] = 0;
+// culled pairs count as a virtual tile `ntiles` (sorted after every real
+// tile, so [0, K) of the output stays fully written)
+__device__ __forceinline__ unsigned sort_tile(unsigned key, unsigned lowmask, int ntiles) {
+  const unsigned t = key & lowmask;
+  return t < (unsigned)ntiles ? t : (unsigned)ntiles;
+}
+__global__ __launch_bounds__(kSortT) void k_tile_hist(int K, int ntiles, int nch, int bits,
+                                                      const unsigned* __restrict__ keys, unsigned* __restrict__ H) {
+  __shared__ unsigned s_h[kMaxTiles + 1];
+  const unsigned lowmask = (1u << bits) - 1u;
+  for (int t = threadIdx.x; t <= ntiles; t += kSortT) s_h[t] = 0;
   __syncthreads();
   const int c = blockIdx.x;
   for (int i = threadIdx.x; i < kChunk; i += kSortT) {
     const int e = c * kChunk + i;
-    if (e < K) atomicAdd(&s_h[keys[e]], 1u);
+    if (e < K) atomicAdd(&s_h[sort_tile(keys[e], lowmask, ntiles)], 1u);
   }
   __syncthreads();
-  for (int t = threadIdx.x; t < ntiles; t += kSortT) H[(size_t)t * nch + c] = s_h[t];
+  for (int t = threadIdx.x; t <= ntiles; t += kSortT) H[(size_t)t * nch + c] = s_h[t];
 }
 __global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int nch, int bits,
                                                          const unsigned* __restrict__ keys,
@@ -503,37 +546,41 @@ __global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int 
   using BRS = rocprim::block_radix_sort<unsigned, kSortT, kSortI, unsigned>;
   __shared__ typename BRS::storage_type s_sort;
   __shared__ unsigned s_key[kChunk];
-  __shared__ int s_start[kMaxTiles];
+  __shared__ int s_start[kMaxTiles + 1];
   const int c = blockIdx.x;
-  const unsigned pad = (1u << bits) - 1u;  // >= ntiles: sorts last, never stored
+  const unsigned lowmask = (1u << bits) - 1u;  // >= ntiles
   unsigned k[kSortI], v[kSortI];
 #pragma unroll
   for (int i = 0; i < kSortI; ++i) {
     const int e = c * kChunk + threadIdx.x * kSortI + i;  // blocked: the sort is stable in this order
-    k[i] = e < K ? keys[e] : pad;
-    v[i] = e < K ? vals[e] : 0u;
+    k[i] = e < K ? keys[e] : kNoEntry;
+    v[i] = e < K ? vals[e] : kNoEntry;
   }
   BRS().sort(k, v, s_sort, 0, bits);
-#pragma unroll
-  for (int i = 0; i < kSortI; ++i) s_key[threadIdx.x * kSortI + i] = k[i];
-  __syncthreads();
+  unsigned t[kSortI];
 #pragma unroll
   for (int i = 0; i < kSortI; ++i) {
-    const int sp = threadIdx.x * kSortI + i;
-    if (k[i] != pad && (sp == 0 || s_key[sp - 1] != k[i])) s_start[k[i]] = sp;
+    t[i] = sort_tile(k[i], lowmask, ntiles);
+    s_key[threadIdx.x * kSortI + i] = t[i];
   }
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < kSortI; ++i) {
-    if (k[i] == pad) continue;
     const int sp = threadIdx.x * kSortI + i;
-    const unsigned pos = Hs[(size_t)k[i] * nch + c] + (unsigned)(sp - s_start[k[i]]);
+    if (v[i] != kNoEntry && (sp == 0 || s_key[sp - 1] != t[i])) s_start[t[i]] = sp;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kSortI; ++i) {
+    if (v[i] == kNoEntry) continue;
+    const int sp = threadIdx.x * kSortI + i;
+    const unsigned pos = Hs[(size_t)t[i] * nch + c] + (unsigned)(sp - s_start[t[i]]);
     keys_out[pos] = k[i];
     vals_out[pos] = v[i];
   }
   if (c == 0)
-    for (int t = threadIdx.x; t < ntiles; t += kSortT)
-      ranges[t] = make_uint2(Hs[(size_t)t * nch], t + 1 < ntiles ? Hs[(size_t)(t + 1) * nch] : (unsigned)K);
+    for (int tt = threadIdx.x; tt < ntiles; tt += kSortT)
+      ranges[tt] = make_uint2(Hs[(size_t)tt * nch], Hs[(size_t)(tt + 1) * nch]);
 }
 
 // backward only: sorted pair -> its record slot, the pair's index in
@@ -545,7 +592,8 @@ __global__ __launch_bounds__(256) void k_slots(int K, const unsigned* __restrict
                                                int gx, int gy, unsigned* __restrict__ pos) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= K) return;
-  const unsigned id = ids[k], tile = tile_sorted[k];
+  const unsigned id = ids[k], tile = tile_sorted[k] & kTileField;
+  if (tile >= (unsigned)(gx * gy)) return;  // a culled pair (in no tile list)
   int rmin[2], rmax[2];
   get_rect(xy[id].x, xy[id].y, radii[id], gx, gy, rmin, rmax);
   const int tx = (int)(tile % (unsigned)gx), ty = (int)(tile / (unsigned)gx);
@@ -555,11 +603,11 @@ __global__ __launch_bounds__(256) void k_ranges32(int L, const unsigned* __restr
                                                   uint2* __restrict__ ranges) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= L) return;
-  const unsigned cur = keys[idx] >> rb;
+  const unsigned cur = (keys[idx] & kTileField) >> rb;
   if (idx == 0) {
     ranges[cur].x = 0;
   } else {
-    const unsigned prev = keys[idx - 1] >> rb;
+    const unsigned prev = (keys[idx - 1] & kTileField) >> rb;
     if (cur != prev) {
       ranges[prev].y = idx;
       ranges[cur].x = idx;
@@ -974,7 +1022,8 @@ struct gsmpm_raster {
   unsigned* hist = nullptr;  // [2 * capH] tile-major chunk histogram, then its exclusive scan
   size_t capH = 0;
   size_t dsort_tmp_bytes = 0;
-  bool slots_pending = false;  // vals_sorted still to be derived (depth-ordered path)
+  bool slots_pending = false;
+  bool emit_culled = false;  // the tile lists omit culled pairs: their records must read zero  // vals_sorted still to be derived (depth-ordered path)
   float4* rec = nullptr;           // backward pair records, 3 x float4 per pair
   size_t capRec = 0;
   // tile ranges
@@ -1111,6 +1160,8 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
   const char* rm = std::getenv("GSMPM_RASTER_RENDER_MODE");
   const int render_mode = rm ? std::atoi(rm) & 1 : 0;
   r->slots_pending = false;
+  r->emit_culled = false;
+  const unsigned* tkeys = nullptr;  // sorted tile keys with sub-tile masks (chunked path)
   unsigned K = 0;
   if (P > 0) {
     hipLaunchKernelGGL(k_preprocess, dim3(div_up(P, 256)), dim3(256), 0, st, a, out_radii, r->depth, r->xy, r->conic,
@@ -1175,7 +1226,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       const int nch = (int)div_up(K, kChunk);
       size_t need = 0;
       if (chunked) {
-        const size_t nh = ntiles * (size_t)nch;
+        const size_t nh = (ntiles + 1) * (size_t)nch;
         if (nh > r->capH) {
           int rc;
           if ((rc = grow((void**)&r->hist, 2 * (nh + nh / 4 + 1024) * sizeof(unsigned)))) return rc;
@@ -1192,15 +1243,18 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
         if ((rc = grow(&r->sort_tmp, need))) return rc;
         r->sort_tmp_bytes = need;
       }
+      // sub-tile masks and emission culling ride on the chunked sort (its
+      // virtual culled tile); the onesweep fallback keeps every pair
+      const int cull = chunked && !(render_mode & 1);
       hipLaunchKernelGGL(k_emit_by_rank, dim3(div_up(P, 256)), dim3(256), 0, st, P, (const unsigned*)r->dorder,
-                         (const unsigned*)r->offr, (const float2*)r->xy, (const int*)out_radii, a.grid_x, a.grid_y,
-                         tile_keys, r->vals);
+                         (const unsigned*)r->offr, (const float2*)r->xy, (const float4*)r->conic,
+                         (const int*)out_radii, a.grid_x, a.grid_y, cull, tile_keys, r->vals);
       GSMPM_LAUNCH_CHECK();
       size_t bytes = r->sort_tmp_bytes;
       if (chunked) {
-        const size_t nh = ntiles * (size_t)nch;
+        const size_t nh = (ntiles + 1) * (size_t)nch;
         unsigned* Hs = r->hist + r->capH;
-        hipLaunchKernelGGL(k_tile_hist, dim3(nch), dim3(kSortT), 0, st, (int)K, (int)ntiles, nch,
+        hipLaunchKernelGGL(k_tile_hist, dim3(nch), dim3(kSortT), 0, st, (int)K, (int)ntiles, nch, bits,
                            (const unsigned*)tile_keys, r->hist);
         GSMPM_LAUNCH_CHECK();
         GSMPM_HIP(rocprim::exclusive_scan(r->sort_tmp, bytes, r->hist, Hs, 0u, nh, rocprim::plus<unsigned>(), st));
@@ -1208,6 +1262,8 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
                            (const unsigned*)tile_keys, (const unsigned*)r->vals, (const unsigned*)Hs, tile_sorted,
                            r->ids_sorted, r->ranges);
         GSMPM_LAUNCH_CHECK();
+        tkeys = tile_sorted;
+        r->emit_culled = cull != 0;
       } else {
         GSMPM_HIP(rocprim::radix_sort_pairs<OnesweepSort>(r->sort_tmp, bytes, tile_keys, tile_sorted, r->vals,
                                                           r->ids_sorted, (size_t)K, 0, bits, st));
@@ -1232,7 +1288,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     }
   }
   hipLaunchKernelGGL(k_render, dim3(2 * a.grid_x, 2 * a.grid_y), dim3(64), 0, st, r->ranges, r->ids_sorted, a.W, a.H,
-                     a.grid_x, r->xy, r->conic, r->rgb, in->bg, out_color, r->final_T, r->n_contrib, render_mode);
+                     a.grid_x, r->xy, r->conic, r->rgb, in->bg, out_color, r->final_T, r->n_contrib, tkeys, render_mode);
   GSMPM_LAUNCH_CHECK();
   if (num_rendered) *num_rendered = (int32_t)K;
   r->P = P;
@@ -1277,6 +1333,7 @@ int gsmpm_raster_backward(gsmpm_raster* r, const gsmpm_raster_args* in, const in
     GSMPM_LAUNCH_CHECK();
     r->slots_pending = false;
   }
+  if (K > 0 && r->emit_culled) GSMPM_HIP(hipMemsetAsync(r->rec, 0, K * 3 * sizeof(float4), st));
   if (K > 0)
     hipLaunchKernelGGL(k_render_bwd, dim3(r->gx, r->gy), dim3(kBlock), 0, st, r->ranges, r->vals_sorted,
                        r->ids_sorted, a.W, a.H, r->gx, r->xy, r->conic, r->rgb, in->bg, r->final_T, r->n_contrib,
