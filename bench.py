@@ -234,16 +234,25 @@ def main():
     w_scale, w_center = float(scene["s"]), [float(v) for v in scene["c"].reshape(-1).tolist()]
     state = {"t": 0.0, "K": 0}
 
+    host_t = [] if os.environ.get("GSMPM_BENCH_HOST_TIMING") else None  # per-call host time (diagnostic)
+
     def frame(render=True):
+        t = [time.perf_counter()]
         masks, state["t"] = substep_masks(specs, state["t"], dt, spf)
         sim.step(dt, masks)
+        t.append(time.perf_counter())
         sim.postprocess()
+        t.append(time.perf_counter())
         if render and not args.no_render:
             # every rank renders its own particles (its scene, or its slab's share)
             means_r, covs_r = sim.world_outputs(w_scale, w_center, render_space=True)
+            t.append(time.perf_counter())
             K, _, _ = raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg,
                                      cam.height, cam.width, tanx, tany, sh_degree=3, shs=feats, cov3D_precomp=covs_r)
+            t.append(time.perf_counter())
             state["K"] = K
+        if host_t is not None:
+            host_t.append([1e6 * (b - a) for a, b in zip(t, t[1:])])
 
     def barrier():
         if world > 1:
@@ -258,6 +267,9 @@ def main():
         frame()
     barrier()
     elapsed = time.perf_counter() - t0
+    if host_t:
+        print("host us per call (step, postprocess, world_outputs, raster.forward):",
+              [round(sum(c) / len(host_t[-args.steps:]), 1) for c in zip(*host_t[-args.steps:])], file=sys.stderr)
     if world > 1:
         tt = torch.tensor([elapsed], device=red_dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
