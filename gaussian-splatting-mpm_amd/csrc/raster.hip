@@ -303,14 +303,35 @@ constexpr int kQ = 4;            // list entries per lane per batch
 constexpr int kBatch = 64 * kQ;  // entries staged per batch
 
 // can alpha = o exp(power) reach 1/255 at a pixel centre of the sub-tile
-// [x0, x0 + 7] x [y0, y0 + 7]?  Conservative; NaNs keep the Gaussian.
-__device__ __forceinline__ bool reaches_subtile(float2 g, float4 co, float x0, float y0) {
-  if (co.w * 255.0f < 0.999f) return false;  // o < 1/255: alpha < 1/255 everywhere
+// [x0, x0 + 7] x [y0, y0 + 7]?  Conservative; NaNs keep the Gaussian.  The
+// Gaussian-only part (the ellipse's half extents) is factored out so the
+// emission computes it once per Gaussian, not once per (tile, quarter).
+struct Reach {
+  float ex, ey;  // half extents of the alpha >= 1/255 ellipse's box, + 1 px
+  int mode;      // 0: test the box, 1: reaches nothing (o < 1/255), 2: keep (degenerate conic)
+};
+__device__ __forceinline__ Reach reach_of(float4 co) {
+  Reach r{0.f, 0.f, 0};
+  if (co.w * 255.0f < 0.999f) {  // o < 1/255: alpha < 1/255 everywhere
+    r.mode = 1;
+    return r;
+  }
   const float det = co.x * co.z - co.y * co.y;
-  if (!(det > 0.0f)) return true;
+  if (!(det > 0.0f)) {
+    r.mode = 2;
+    return r;
+  }
   const float k = fmaxf(2.0f * __logf(255.0f * co.w), 0.0f) * 1.02f + 0.02f;
-  const float ex = sqrtf(k * co.z / det) + 1.0f, ey = sqrtf(k * co.x / det) + 1.0f;
-  return !(g.x + ex < x0 || g.x - ex > x0 + (kSub - 1) || g.y + ey < y0 || g.y - ey > y0 + (kSub - 1));
+  r.ex = sqrtf(k * co.z / det) + 1.0f;
+  r.ey = sqrtf(k * co.x / det) + 1.0f;
+  return r;
+}
+__device__ __forceinline__ bool reaches_box(const Reach& r, float2 g, float x0, float y0) {
+  if (r.mode) return r.mode == 2;
+  return !(g.x + r.ex < x0 || g.x - r.ex > x0 + (kSub - 1) || g.y + r.ey < y0 || g.y - r.ey > y0 + (kSub - 1));
+}
+__device__ __forceinline__ bool reaches_subtile(float2 g, float4 co, float x0, float y0) {
+  return reaches_box(reach_of(co), g, x0, y0);
 }
 
 // Tile keys of the depth-ordered path carry, above the tile index, a mask of
@@ -487,7 +508,7 @@ __global__ __launch_bounds__(256) void k_emit_by_rank(int P, const unsigned* __r
   if (radii[g] <= 0) return;
   unsigned off = r == 0 ? 0u : offr[r - 1];
   const float2 gp = xy[g];
-  const float4 co = conic_o[g];
+  const Reach rc = reach_of(conic_o[g]);
   int rmin[2], rmax[2];
   get_rect(gp.x, gp.y, radii[g], gx, gy, rmin, rmax);
   for (int y = rmin[1]; y < rmax[1]; ++y)
@@ -497,7 +518,7 @@ __global__ __launch_bounds__(256) void k_emit_by_rank(int P, const unsigned* __r
         m = 0u;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          if (reaches_subtile(gp, co, (float)(x * kBX + (q & 1) * kSub), (float)(y * kBY + (q >> 1) * kSub)))
+          if (reaches_box(rc, gp, (float)(x * kBX + (q & 1) * kSub), (float)(y * kBY + (q >> 1) * kSub)))
             m |= 1u << q;
       }
       keys[off] = m ? ((unsigned)(y * gx + x) | (m << kMaskShift)) : kCulledKey;
