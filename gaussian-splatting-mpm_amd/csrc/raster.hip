@@ -11,8 +11,8 @@
 //   depth order    stable sort of the P depths (ties keep index order), then
 //                  the tiles-touched counts scanned in that order; queued
 //                  before the K read-back, so they run behind the simulator
-//   k_emit_by_rank each Gaussian, in depth order, emits (tile, idx) per
-//                  touched tile at its depth-order offset
+//   k_emit_pairs   each (Gaussian, tile) pair, in depth order, written at
+//                  its depth-order offset (one lane per pair)
 //   sort           stable onesweep radix sort on the tile index alone
 //                  (msb(#tiles) bits): each tile's list comes out in (depth,
 //                  index) order, the list upstream's 64-bit
@@ -497,34 +497,40 @@ __global__ __launch_bounds__(256) void k_tiles_by_rank(int P, const unsigned* __
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r < P) tr[r] = tiles[order[r]];
 }
-__global__ __launch_bounds__(256) void k_emit_by_rank(int P, const unsigned* __restrict__ order,
-                                                      const unsigned* __restrict__ offr, const float2* __restrict__ xy,
-                                                      const float4* __restrict__ conic_o,
-                                                      const int* __restrict__ radii, int gx, int gy, int cull,
-                                                      unsigned* __restrict__ keys, unsigned* __restrict__ ids) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= P) return;
-  const unsigned g = order[r];
-  if (radii[g] <= 0) return;
-  unsigned off = r == 0 ? 0u : offr[r - 1];
+// Depth-ordered emission, one lane per pair (a lane per Gaussian would
+// serialise the ~1600 stores of the frame's largest Gaussians): the pair's
+// Gaussian is found by binary search over the depth-order offsets, and the
+// pair lands at its depth-order offset + its index in the Gaussian's rect.
+__global__ __launch_bounds__(256) void k_emit_pairs(int K, int P, const unsigned* __restrict__ order,
+                                                    const unsigned* __restrict__ offr, const float2* __restrict__ xy,
+                                                    const float4* __restrict__ conic_o,
+                                                    const int* __restrict__ radii, int gx, int gy, int cull,
+                                                    unsigned* __restrict__ keys, unsigned* __restrict__ ids) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= K) return;
+  int lo = 0, hi = P - 1;  // first r with offr[r] > e (offr: inclusive scan)
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (offr[mid] > (unsigned)e) hi = mid;
+    else lo = mid + 1;
+  }
+  const unsigned g = order[lo];
+  const unsigned local = (unsigned)e - (lo ? offr[lo - 1] : 0u);
   const float2 gp = xy[g];
-  const Reach rc = reach_of(conic_o[g]);
   int rmin[2], rmax[2];
   get_rect(gp.x, gp.y, radii[g], gx, gy, rmin, rmax);
-  for (int y = rmin[1]; y < rmax[1]; ++y)
-    for (int x = rmin[0]; x < rmax[0]; ++x) {
-      unsigned m = 0xfu;
-      if (cull) {
-        m = 0u;
+  const unsigned w = (unsigned)(rmax[0] - rmin[0]);
+  const int x = rmin[0] + (int)(local % w), y = rmin[1] + (int)(local / w);
+  unsigned m = 0xfu;
+  if (cull) {
+    const Reach rc = reach_of(conic_o[g]);
+    m = 0u;
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (reaches_box(rc, gp, (float)(x * kBX + (q & 1) * kSub), (float)(y * kBY + (q >> 1) * kSub)))
-            m |= 1u << q;
-      }
-      keys[off] = m ? ((unsigned)(y * gx + x) | (m << kMaskShift)) : kCulledKey;
-      ids[off] = g;
-      ++off;
-    }
+    for (int q = 0; q < 4; ++q)
+      if (reaches_box(rc, gp, (float)(x * kBX + (q & 1) * kSub), (float)(y * kBY + (q >> 1) * kSub))) m |= 1u << q;
+  }
+  keys[e] = m ? ((unsigned)(y * gx + x) | (m << kMaskShift)) : kCulledKey;
+  ids[e] = g;
 }
 // Stable tile sort of the depth-ordered emission list for <= kMaxTiles tiles
 // (replaces the two onesweep passes: 2 kernels + a scan instead of ~8
@@ -1267,7 +1273,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       // sub-tile masks and emission culling ride on the chunked sort (its
       // virtual culled tile); the onesweep fallback keeps every pair
       const int cull = chunked && !(render_mode & 1);
-      hipLaunchKernelGGL(k_emit_by_rank, dim3(div_up(P, 256)), dim3(256), 0, st, P, (const unsigned*)r->dorder,
+      hipLaunchKernelGGL(k_emit_pairs, dim3(div_up(K, 256)), dim3(256), 0, st, (int)K, P, (const unsigned*)r->dorder,
                          (const unsigned*)r->offr, (const float2*)r->xy, (const float4*)r->conic,
                          (const int*)out_radii, a.grid_x, a.grid_y, cull, tile_keys, r->vals);
       GSMPM_LAUNCH_CHECK();
