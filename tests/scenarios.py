@@ -55,11 +55,18 @@ def world2grid_np(x, grid_extent):
     return xg, c, np.float32(s)
 
 
-def lego_problem(n, n_grid, seed=0, config="lego.json"):
-    """Synthetic lego: grid-space particles + BC list."""
+LEGO_BOX = ((-0.65, -0.65, -0.55), (0.65, 0.65, 0.55))
+BICYCLE_BOX = ((0.05, 0.05, 0.05), (0.95, 0.95, 0.95))
+
+
+def lego_problem(n, n_grid, seed=0, config="lego.json", box=None):
+    """Synthetic lego (config D with config="bicycle.json"):
+    grid-space particles + BC list.  The box defaults to the config's SURVEY 8(d) box."""
     import oracle as O  # test infrastructure only
     cfg = load_config(config)["mpm"]
-    g = synthetic_gaussians(n, seed)
+    if box is None:
+        box = BICYCLE_BOX if config.startswith("bicycle") else LEGO_BOX
+    g = synthetic_gaussians(n, seed, box=box)
     cov = covariance6(g["scale_log"], g["rot"])
     lo, hi = np.asarray(cfg["sim_area"][0]), np.asarray(cfg["sim_area"][1])
     mask = np.all((g["xyz"] >= lo) & (g["xyz"] <= hi), axis=1)
@@ -84,12 +91,15 @@ class BC:
         return self.start <= t < self.end
 
 
-def build_oracle_sim(prob, material=None, jelly_quirk=True, with_collider=True):
+def build_oracle_sim(prob, material=None, jelly_quirk=True, with_collider=True, threaded=False):
+    """threaded=True: the OpenMP build of the same restatement (P2G summation
+    order differs from the serial one by f32 rounding only), for the
+    BASELINE-size parity runs."""
     import oracle as O
     cfg = prob["cfg"]
     sim = O.OracleMPM(prob["x"], prob["cov"], prob["vol"], n_grid=prob["n_grid"], grid_extent=cfg["grid_extent"],
                       material=material or cfg["material"], E=cfg["E"], nu=cfg["nu"], density=cfg["density"],
-                      gravity=cfg["gravity"], jelly_quirk=jelly_quirk)
+                      gravity=cfg["gravity"], jelly_quirk=jelly_quirk, threaded=threaded)
     imps, ops = [], []
     for d in cfg["boundary_conditions"]:
         if d["type"] == "fixed_cube":

@@ -209,3 +209,29 @@ def test_subtile_culling_changes_nothing(dev, monkeypatch, scene):
         out[mode] = [x.detach().cpu().numpy() for x in (img, m3.grad, o1.grad, s1.grad, cv.grad)]
     for a, b in zip(out["0"], out["1"]):
         assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("P,W,H,tiles", [(2000, 200, 200, 169), (20000, 1024, 1024, 4096), (6000, 272, 3856, 4097),
+                                         (8000, 100, 72, 35)])
+def test_num_rendered_and_radii_exact(dev, P, W, H, tiles):
+    """num_rendered (K = sum of tiles touched, upstream's binning count that the
+    backward and the API rely on) and every radius equal the oracle's exactly.
+    Cases: K over many 2048-pair sort chunks; exactly 4096 tiles (the largest
+    grid on the chunked counting sort); 4097 tiles (first on the onesweep
+    fallback); dense tiles with >1000 pairs each."""
+    import oracle as O
+    import torch
+    from gsmpm import raster
+    assert ((W + 15) // 16) * ((H + 15) // 16) == tiles
+    means, c6, opa, shs = _dense_scene(P, P + 1, 0.03, 0.5) if tiles == 35 else _scene(P, seed=P + W)
+    view, full, campos, tx, ty = _camera(W, H, 0.9)
+    bgv = np.zeros(3, np.float32)
+    oc, orad, oK, _, _ = O.raster_forward(means, opa, view, full, campos, bgv, W, H, tx, ty, shs=shs, sh_degree=3,
+                                          cov3D_precomp=c6)
+    assert oK > 4 * 2048
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    K, color, radii = raster.forward(t(means), t(opa), t(view), t(full), t(campos), t(bgv), H, W, tx, ty,
+                                     sh_degree=3, shs=t(shs), cov3D_precomp=t(c6))
+    assert K == oK, (K, oK)
+    assert np.array_equal(radii.cpu().numpy(), orad)
+    assert np.abs(color.cpu().numpy() - oc).max() < 1e-3
