@@ -50,10 +50,19 @@ def parse():
     ap.add_argument("--material", default=None, help="override (e.g. metal) -- not the headline config")
     ap.add_argument("--no-render", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra-configs", action="store_true",
+                    help="skip the driver-timed config C (metal) / D (bicycle 1M, 256^3) side runs")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--slab", action="store_true", help="strong scaling: one scene in x-slabs with halo exchange")
     ap.add_argument("--rebin", type=int, default=0, help="fused pipeline: substeps between re-binnings (0: library default)")
     return ap.parse_args()
+
+
+# models/bicycle/cameras.json record 0 of the reference (intrinsics only: main.py's
+# orbit camera replaces the pose, main.py:84-106) -- data, so the bench needs no
+# reference files on the GPU box
+BICYCLE_CAM0 = {"width": 4946, "height": 3286, "fx": 4649.505977743847, "fy": 4627.300372546341,
+                "position": [0.0, 0.0, 0.0], "rotation": [[1, 0, 0], [0, 1, 0], [0, 0, 1]]}
 
 
 def build_scene(args, dev, rank=0):
@@ -85,8 +94,12 @@ def build_scene(args, dev, rank=0):
     vols = get_particle_volume(xg, sargs)
     center_w, obs = get_center_view_worldspace_and_observant_coordinate(
         torch.tensor([[0.5, 0.5, 0.5]], device=dev), torch.tensor([[0, 0, 1]], device=dev), [], s, c)
-    margs.model_path = "/nonexistent"  # -> lego camera 0 record (800x800, fx 1111.11)
-    cam = drv.modify_cam(drv.load_cameras(margs)[0], center_w, obs, device=dev)
+    if args.config.startswith("bicycle"):
+        cam0 = drv.camera_from_info(BICYCLE_CAM0)
+    else:
+        margs.model_path = "/nonexistent"  # -> lego camera 0 record (800x800, fx 1111.11)
+        cam0 = drv.load_cameras(margs)[0]
+    cam = drv.modify_cam(cam0, center_w, obs, device=dev)
     cam.toCuda(dev)
     return dict(g=g, mask=mask, xg=xg, covs=covs * (s * s), vols=vols, c=c, s=s, cam=cam, sargs=sargs, rargs=rargs)
 
@@ -179,6 +192,65 @@ def cpu_baseline(scene, args, budget_s):
             "sample": f"first {n_done} lego substeps of the same workload ({x.shape[0]} particles, {sa.n_grid}^3, "
                       f"same BCs), C restatement oracle/mpm_oracle.c with OpenMP ({threads} threads), {el:.1f}s",
             "substeps_per_s": n_done / el}
+
+
+def other_configs(args, dev, frames=3):
+    """BASELINE configs[2] (lego-fracture --material metal, 100k, 128^3: the
+    stress-bearing return-map path) and configs[3] on one GPU (bicycle 1M,
+    256^3, rendered at the bicycle camera's 4946x3286) -- timed in the same
+    run as the headline, sim and render separately."""
+    import copy
+    import torch
+    from gsmpm import raster
+    from gsmpm.bc import substep_masks
+    res = {}
+    for key, cfg, mat, n, ng in (("C_lego_fracture_metal", "lego-fracture.json", "metal", 100_000, 128),
+                                 ("D_bicycle_1gpu", "bicycle.json", None, 1_000_000, 256)):
+        a = copy.copy(args)
+        a.config, a.material, a.particles, a.n_grid = cfg, mat, n, ng
+        sc = build_scene(a, dev)
+        sim, specs = make_sim(sc, dev)
+        sa = sc["sargs"]
+        dt, spf, t = sa.substep_dt, sa.steps_per_frame, 0.0
+        masks, t = substep_masks(specs, t, dt, spf)
+        sim.step(dt, masks)  # warm-up frame (graph capture)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(frames):
+            masks, t = substep_masks(specs, t, dt, spf)
+            sim.step(dt, masks)
+        e1.record()
+        torch.cuda.synchronize()
+        sim_ms = e0.elapsed_time(e1) / frames
+        masks, t = substep_masks(specs, t, dt, spf)
+        prof = sim.profile(dt, masks)
+        sim.postprocess()
+        cam, g, mask = sc["cam"], sc["g"], sc["mask"]
+        feats, opac = g.get_features[mask].contiguous(), g.get_opacity[mask].reshape(-1).contiguous()
+        means_r, covs_r = sim.world_outputs(float(sc["s"]), [float(v) for v in sc["c"].reshape(-1).tolist()],
+                                            render_space=True)
+        tx, ty = math.tan(cam.FovX * 0.5), math.tan(cam.FovY * 0.5)
+        bg = torch.zeros(3, device=dev)
+        rf = lambda: raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg, cam.height,
+                                    cam.width, tx, ty, sh_degree=3, shs=feats, cov3D_precomp=covs_r)
+        K, _, _ = rf()
+        torch.cuda.synchronize()
+        r0 = time.perf_counter()
+        for _ in range(frames):
+            rf()
+        torch.cuda.synchronize()
+        render_ms = (time.perf_counter() - r0) / frames * 1e3
+        nsim = sim.n
+        res[key] = {"config": cfg, "material": sa.material, "particles": nsim, "n_grid": sa.n_grid,
+                    "sim_ms_per_frame": round(sim_ms, 4), "sim_substeps_per_s": round(spf / (sim_ms * 1e-3), 1),
+                    "sim_particle_substeps_per_s": nsim * spf / (sim_ms * 1e-3),
+                    "k_fused_us_per_launch": round(prof[0] / (spf + 1) * 1e3, 2),
+                    "k_grid_f_us_per_launch": round(prof[1] / spf * 1e3, 2),
+                    "render": f"{cam.width}x{cam.height} SH3", "render_ms": round(render_ms, 3), "num_rendered": K}
+        del sim, sc, means_r, covs_r, feats, opac
+        torch.cuda.empty_cache()
+    return res
 
 
 def main():
@@ -300,15 +372,25 @@ def main():
                            tanx, tany, sh_degree=3, shs=feats, cov3D_precomp=covs_r)
         torch.cuda.synchronize()
         render_ms = (time.perf_counter() - r0) / 5 * 1e3
-    kern = None
+    kern = frame_prof = None
     if world == 1:
         fused = sim.pipeline == "fused"
         # nodes owned by the grid update: 8x8x7 (fused) / 8^3 cells per touched tile
         live = sim.debug_stats()["touched_tiles"] * (448 if fused else 512)
-        # per-launch kernel time: hipEvents on the simulator's stream around 20
-        # back-to-back launches of each kernel on the current frame's inputs
-        kms = sim.time_kernels(dt, substep_masks(specs, state["t"], dt, 1)[0][0], reps=20)
+        # (1) every launch of one real frame (eager, the same launches the graph
+        # replays, re-binning launches included), each kernel's begin/end stamped
+        # by its own dispatch packet -- the interval rocprofv3's kernel trace
+        # reports, so frame_ms / launches is rocprof's per-launch average
+        masks, state["t"] = substep_masks(specs, state["t"], dt, spf)
+        prof = sim.profile(dt, masks)
         names = ("k_fused", "k_grid_f", "binning") if fused else ("k_p2g", "k_grid", "k_g2p", "binning")
+        # the fused pipeline runs spf + 1 k_fused launches per frame (the first is
+        # P2G only, the last G2P only: together one substep's work)
+        nl = {"k_fused": spf + 1, "k_grid_f": spf, "k_p2g": spf, "k_grid": spf, "k_g2p": spf}
+        frame_prof = {k: prof[i] for i, k in enumerate(names)}
+        # (2) steady state: hipEvents around 20 back-to-back launches of each kernel
+        # on the current frame's inputs (no re-binning launches)
+        kms = sim.time_kernels(dt, substep_masks(specs, state["t"], dt, 1)[0][0], reps=20)
         kern = {k: kms[i] for i, k in enumerate(names)}
         abytes = {k: v for k, v in algorithmic_bytes(n_local, sa.n_grid, sa.material).items() if k in kern}
 
@@ -339,17 +421,30 @@ def main():
         "num_rendered": state["K"],
     }
     if kern is not None:
-        # dominant kernel among the three that carry the reference's work
-        dom = max(abytes, key=lambda k: kern[k])
-        ach = abytes[dom] / (kern[dom] * 1e-3) / 1e9
-        out["kernels_ms_per_launch"] = {k: round(v, 5) for k, v in kern.items()}
+        # dominant kernel: the one with the most time per frame among those that
+        # carry the reference's work
+        dom = max(abytes, key=lambda k: frame_prof[k])
+        frame_s = frame_prof[dom] * 1e-3
+        ach = abytes[dom] * spf / frame_s / 1e9  # one substep's algorithmic bytes per substep
+        avg_launch_s = frame_s / nl[dom]
+        traffic = measured_traffic(dom, {"config": args.config, "particles": args.particles, "n_grid": sa.n_grid,
+                                         "material": sa.material})
+        out["kernels_ms_per_launch"] = {k: round(frame_prof[k] / nl[k], 5) for k in frame_prof if k in nl}
+        out["kernels_ms_per_frame"] = {k: round(v, 4) for k, v in frame_prof.items()}
+        out["kernels_ms_per_launch_steady"] = {k: round(v, 5) for k, v in kern.items()}
         out["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                           "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": measured_traffic(dom, {"config": args.config, "particles": args.particles,
-                                                                   "n_grid": sa.n_grid, "material": sa.material}),
-                           "algorithmic_bytes_per_launch": abytes[dom],
-                           "basis": "SURVEY.md 8(d) B_sub = 208 N + 56 n^3 split per kernel (dense grid)",
+                           "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                           "traffic_frac": None if traffic is None else
+                           round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4),
+                           "avg_launch_us": round(avg_launch_s * 1e6, 2), "launches_per_frame": nl[dom],
+                           "algorithmic_bytes_per_substep": abytes[dom],
+                           "basis": "SURVEY.md 8(d) B_sub = 208 N + 56 n^3 split per kernel (dense grid); "
+                                    "achieved = spf x bytes / the kernel's summed packet-stamped time over one "
+                                    "eager frame (= rocprofv3 avg x launches)",
                            "pipeline": sim.pipeline,
                            "live_nodes": live}
+    if rank == 0 and world == 1 and not args.no_extra_configs:
+        out["other_configs"] = other_configs(args, dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(scene, args, args.cpu_seconds)
     if rank == 0:

@@ -231,11 +231,9 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
       __syncthreads();
       if (w == (int)blockIdx.x) {
         stamp(SK, 2);
-        if (threadIdx.x == 0 && blockIdx.x < 4096) {
-          g_stamps[SK][blockIdx.x][5] = cnt;
-          g_stamps[SK][blockIdx.x][6] = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));  // HW_ID
-          g_stamps[SK][blockIdx.x][7] = __builtin_amdgcn_s_getreg(20 | (0 << 6) | (31 << 11));  // XCC_ID
-        }
+        stamp_val(SK, 5, cnt);
+        stamp_val(SK, 6, GSMPM_HWREG(4));   // HW_ID
+        stamp_val(SK, 7, GSMPM_HWREG(20));  // XCC_ID
       }
       int code = -1, lslot = 0, nt = -1;
       if (k < cnt) {

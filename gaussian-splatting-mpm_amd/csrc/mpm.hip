@@ -48,10 +48,22 @@ constexpr int kChunk = 256;  // particles per work chunk (one per lane of a 256-
 
 // Workgroup timeline stamps (diagnostics): [kernel][wg][start, end] in
 // s_memrealtime ticks (100 MHz), written by lane 0 of the first 4096 workgroups.
+// Compiled in only with -DGSMPM_STAMPS (tools/wg_timeline*.py builds); the
+// production library carries no diagnostic stores in its kernels.
+#ifdef GSMPM_STAMPS
 __device__ unsigned long long g_stamps[4][4096][8];
 __device__ __forceinline__ void stamp(int kern, int slot) {
   if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[kern][blockIdx.x][slot] = __builtin_amdgcn_s_memrealtime();
 }
+__device__ __forceinline__ void stamp_val(int kern, int slot, unsigned long long v) {
+  if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[kern][blockIdx.x][slot] = v;
+}
+#define GSMPM_HWREG(r) __builtin_amdgcn_s_getreg((r) | (0 << 6) | (31 << 11))
+#else
+__device__ __forceinline__ void stamp(int, int) {}
+__device__ __forceinline__ void stamp_val(int, int, unsigned long long) {}
+#define GSMPM_HWREG(r) 0
+#endif
 
 // Chunk work lists (one set per parity).  Every substep G2P re-bins each
 // particle into the tile of its new base cell (LDS-aggregated counters), a
@@ -370,10 +382,8 @@ __global__ __launch_bounds__(256) void k_p2g(Particles ps, GridDims g, Tiles tl,
     __syncthreads();  // also orders the window zeroing before the adds
     if (w == (int)blockIdx.x) {
       stamp(0, 2);
-      if (threadIdx.x == 0 && blockIdx.x < 4096) {
-        g_stamps[0][blockIdx.x][5] = cnt;
-        g_stamps[0][blockIdx.x][6] = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));  // HW_ID
-      }
+      stamp_val(0, 5, cnt);
+      stamp_val(0, 6, GSMPM_HWREG(4));  // HW_ID
     }
     const float bmax = fmaxf(fmaxf(s_max[0], s_max[1]), fmaxf(s_max[2], s_max[3]));
     int ebits;
@@ -789,11 +799,9 @@ __global__ __launch_bounds__(256) void k_g2p(Particles ps, GridDims g, Tiles tl,
     __syncthreads();
     if (w == (int)blockIdx.x) {
       stamp(1, 2);
-      if (threadIdx.x == 0 && blockIdx.x < 4096) {
-        g_stamps[1][blockIdx.x][5] = cnt;
-        g_stamps[1][blockIdx.x][6] = t;
-        g_stamps[1][blockIdx.x][7] = __builtin_amdgcn_s_getreg(4 | (0 << 6) | (31 << 11));  // HW_ID
-      }
+      stamp_val(1, 5, cnt);
+      stamp_val(1, 6, t);
+      stamp_val(1, 7, GSMPM_HWREG(4));  // HW_ID
     }
     int code = -1, lslot = 0, nt = -1;
     if (k < cnt) {
@@ -2478,9 +2486,14 @@ int gsmpm_mpm_debug_stats(gsmpm_mpm* h, int32_t* out8, void* stream) {
 
 int gsmpm_debug_stamps(uint64_t* out, void* stream) {
   GSMPM_REQUIRE(out, "gsmpm_debug_stamps: null argument");
+#ifdef GSMPM_STAMPS
   GSMPM_HIP(hipStreamSynchronize((hipStream_t)stream));
   GSMPM_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 4 * 4096 * 8));
   return GSMPM_OK;
+#else
+  (void)stream;
+  GSMPM_REQUIRE(false, "gsmpm_debug_stamps: library built without -DGSMPM_STAMPS");
+#endif
 }
 
 int gsmpm_mpm_live_box(gsmpm_mpm* h, int32_t* box6, void* stream) {

@@ -1056,7 +1056,8 @@ struct gsmpm_raster {
   // tile ranges
   size_t capT = 0;
   uint2* ranges = nullptr;
-  unsigned* h_count = nullptr;  // pinned
+  unsigned* h_count = nullptr;  // pinned, mapped + coherent (the device writes K into it)
+  hipEvent_t count_ev = nullptr;  // recorded after k_publish_count: surfaces a fault while the host spins
   // per pixel (backward)
   size_t capPix = 0;
   float* final_T = nullptr;
@@ -1078,8 +1079,11 @@ extern "C" {
 int gsmpm_raster_create(gsmpm_raster** out) {
   GSMPM_REQUIRE(out, "gsmpm_raster_create: null argument");
   auto* r = new gsmpm_raster();
-  hipError_t e = hipHostMalloc((void**)&r->h_count, sizeof(unsigned));
+  hipError_t e = hipHostMalloc((void**)&r->h_count, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent);
+  if (e == hipSuccess) e = hipEventCreateWithFlags(&r->count_ev, hipEventDisableTiming);
   if (e != hipSuccess) {
+    if (r->h_count) (void)hipHostFree(r->h_count);
+  if (r->count_ev) (void)hipEventDestroy(r->count_ev);
     delete r;
     set_error(std::string("hipHostMalloc: ") + hipGetErrorString(e));
     return GSMPM_EHIP;
@@ -1096,6 +1100,7 @@ int gsmpm_raster_destroy(gsmpm_raster* r) {
                   (void*)r->final_T, (void*)r->n_contrib, (void*)r->dorder, (void*)r->dsorted, (void*)r->tr, (void*)r->offr, r->dsort_tmp, (void*)r->hist})
     if (p) (void)hipFree(p);
   if (r->h_count) (void)hipHostFree(r->h_count);
+  if (r->count_ev) (void)hipEventDestroy(r->count_ev);
   delete r;
   return GSMPM_OK;
 }
@@ -1209,20 +1214,28 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       bytes = r->scan_tmp_bytes;
       GSMPM_HIP(rocprim::inclusive_scan(r->scan_tmp, bytes, r->tr, r->offr, (size_t)P, rocprim::plus<unsigned>(), st));
     }
-    // K straight into pinned (coherent) host memory by a one-lane kernel, and a
+    // K straight into pinned, coherent host memory by a one-lane kernel, and a
     // spin on it: no copy-engine packet and no sleeping stream sync between
-    // the scan and the post-count launches.  A spin longer than 2 s falls back
-    // to the stream sync (which also surfaces any fault).
+    // the scan and the post-count launches.  Every 256 polls the event
+    // recorded behind the publish is queried, so a device fault surfaces at
+    // once instead of after a timeout; a completed event with no count is an
+    // error.  The count needs the host, so a capturing stream is refused.
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    GSMPM_HIP(hipStreamIsCapturing(st, &cap));
+    GSMPM_REQUIRE(cap == hipStreamCaptureStatusNone,
+                  "gsmpm_raster_forward: the pair count is read on the host; the stream must not be capturing");
     volatile unsigned* hc = r->h_count;
     *hc = kNoCount;
     hipLaunchKernelGGL(k_publish_count, dim3(1), dim3(1), 0, st, (const unsigned*)(r->offsets + (P - 1)), r->h_count);
     GSMPM_LAUNCH_CHECK();
-    const auto t0 = std::chrono::steady_clock::now();
-    while (*hc == kNoCount) {
-      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
-        GSMPM_HIP(hipStreamSynchronize(st));
-        break;
+    GSMPM_HIP(hipEventRecord(r->count_ev, st));
+    for (unsigned polls = 1; *hc == kNoCount; ++polls) {
+      if ((polls & 255) == 0) {
+        const hipError_t q = hipEventQuery(r->count_ev);
+        if (q == hipSuccess) break;  // everything up to the publish finished: K is visible below
+        if (q != hipErrorNotReady) GSMPM_HIP(q);
       }
+      __builtin_ia32_pause();
     }
     K = *hc;
     GSMPM_REQUIRE(K != kNoCount, "gsmpm_raster_forward: the pair count never arrived");

@@ -7,7 +7,8 @@ the HIP kernels in libgsmpm.so.  The backward (upstream's
 _RasterizeGaussians.backward, used by extra.py's loss.backward()) returns the
 gradients of means3D, means2D (w.r.t. NDC, as upstream), shs / colors_precomp,
 opacities, scales / rotations or cov3D_precomp; a forward that needs them runs
-on a context of its own that keeps its binning and per-pixel state.
+on a context of its own (leased from a per-device pool) that keeps its
+binning and per-pixel state until the backward.
 """
 from __future__ import annotations
 
@@ -55,9 +56,10 @@ class _RasterizeGaussians(torch.autograd.Function):
         args = (means3D, opacities.reshape(-1), s.viewmatrix, s.projmatrix, s.campos, s.bg, s.image_height,
                 s.image_width, s.tanfovx, s.tanfovy)
         if any(ctx.needs_input_grad[:8]):
-            context = _raster.RasterContext()
-            num_rendered, color, radii, a, keep = _raster.forward(*args, **kw, context=context, return_args=True)
-            ctx.state = (context, a, keep, radii)
+            lease = _raster.ContextLease(means3D.device.index or 0)
+            num_rendered, color, radii, a, keep = _raster.forward(*args, **kw, context=lease.context,
+                                                                  return_args=True)
+            ctx.state = (lease, a, keep, radii)
             ctx.shapes = [None if t is None else (t.shape, t.dtype) for t in
                           (means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp)]
         else:
@@ -68,7 +70,7 @@ class _RasterizeGaussians(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, grad_out_color, _):
-        context, a, keep, radii = ctx.state
+        lease, a, keep, radii = ctx.state
         shp = ctx.shapes
         P = a.P
 
@@ -78,8 +80,9 @@ class _RasterizeGaussians(torch.autograd.Function):
             return t.reshape(shp[i][0]).to(shp[i][1])
         if P == 0:
             return (None,) * 9
-        g = _raster.backward(context, keep, a, radii, grad_out_color)
-        ctx.state = None  # frees the context's buffers once the graph is released
+        g = _raster.backward(lease.context, keep, a, radii, grad_out_color)
+        lease.release()  # back to the pool: the next iteration's forward reuses its buffers
+        ctx.state = None
         return (cast(g["means3D"], 0), cast(g["means2D"], 1), cast(g["sh"], 2), cast(g["colors"], 3),
                 cast(g["opacity"], 4), cast(g["scales"], 5), cast(g["rotations"], 6), cast(g["cov3D"], 7), None)
 

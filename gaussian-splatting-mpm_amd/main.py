@@ -60,7 +60,6 @@ def load_model(args):
 
 def load_cameras(args):
     """main.py:50-82: cameras.json -> TinyCam list (only cameras[0] is used)."""
-    cams = []
     path = os.path.join(args.model_path, "cameras.json")
     if not os.path.exists(path):
         # synthetic runs without a scene directory: lego camera 0 (800x800, fx = fy = 1111.11)
@@ -69,19 +68,22 @@ def load_cameras(args):
     else:
         with open(path) as f:
             infos = json.load(f)
-    for ci in infos:
-        w, h = ci["width"], ci["height"]
-        fovx, fovy = focal2fov(ci["fx"], w), focal2fov(ci["fy"], h)
-        center = np.array(ci["position"]).astype(np.float32)
-        c2w = np.zeros((4, 4))
-        c2w[:3, :3] = np.array(ci["rotation"])
-        c2w[:3, 3] = center
-        c2w[3, 3] = 1.0
-        view = np.linalg.inv(c2w).transpose().astype(np.float32)
-        proj = getProjectionMatrix(znear=0.01, zfar=100, fovX=fovx, fovY=fovy).numpy().transpose().astype(np.float32)
-        cams.append(TinyCam(width=w, height=h, FovX=fovx, FovY=fovy, cam_center=center, view_mat=view,
-                            full_proj_mat=view @ proj))
-    return cams
+    return [camera_from_info(ci) for ci in infos]
+
+
+def camera_from_info(ci):
+    """One cameras.json record -> TinyCam (main.py:58-80)."""
+    w, h = ci["width"], ci["height"]
+    fovx, fovy = focal2fov(ci["fx"], w), focal2fov(ci["fy"], h)
+    center = np.array(ci["position"]).astype(np.float32)
+    c2w = np.zeros((4, 4))
+    c2w[:3, :3] = np.array(ci["rotation"])
+    c2w[:3, 3] = center
+    c2w[3, 3] = 1.0
+    view = np.linalg.inv(c2w).transpose().astype(np.float32)
+    proj = getProjectionMatrix(znear=0.01, zfar=100, fovX=fovx, fovY=fovy).numpy().transpose().astype(np.float32)
+    return TinyCam(width=w, height=h, FovX=fovx, FovY=fovy, cam_center=center, view_mat=view,
+                   full_proj_mat=view @ proj)
 
 
 def modify_cam(cam: TinyCam, center_view_world_space, observant_coordinates, device="cuda"):
