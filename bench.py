@@ -13,12 +13,16 @@ n_grid 128 (--n_grid override), jelly as written.
     python bench.py [--gpus N --steps K --warmup W]
 
 Multi-GPU (torch.distributed.run, one rank per GPU), two modes:
-* default -- weak scaling: every rank simulates and renders its own lego scene
-  (synthetic seed = rank), independent objects, so no collective in the data
-  path (Multi-GPU); timing is barrier + max over ranks.
-* --slab  -- strong scaling of ONE lego scene cut into x-slabs (gsmpm.dist),
-  halo windows of the shared boundary planes exchanged over RCCL every
-  substep; lego's ~64 occupied planes hold at most 4 slabs.
+* default -- strong scaling of ONE lego scene sharded by spatial slab
+  (gsmpm.dist.SlabDomain, csrc/slab.h): every substep each pair of
+  neighbouring ranks swaps the partial sums of the grid planes around their
+  shared bound over RCCL (the pairwise all-reduce of boundary grid nodes),
+  particles migrate between slabs every 10 substeps; the frame's means/covs
+  are gathered to rank 0, which renders it.  value = scene particles x
+  substeps / time.
+* --dp -- every rank simulates and renders its own lego scene (synthetic seed
+  = rank): independent objects, no collective in the data path.
+Timing is barrier + max over ranks.
 
 Prints ONE JSON line (rank 0).  value = particle-substeps/s over all ranks.
 """
@@ -53,7 +57,8 @@ def parse():
     ap.add_argument("--no-extra-configs", action="store_true",
                     help="skip the driver-timed config C (metal) / D (bicycle 1M, 256^3) side runs")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--slab", action="store_true", help="strong scaling: one scene in x-slabs with halo exchange")
+    ap.add_argument("--dp", action="store_true",
+                    help="N > 1: independent scenes per rank (no exchange) instead of the default slab sharding")
     ap.add_argument("--rebin", type=int, default=0, help="fused pipeline: substeps between re-binnings (0: library default)")
     return ap.parse_args()
 
@@ -104,14 +109,23 @@ def build_scene(args, dev, rank=0):
     return dict(g=g, mask=mask, xg=xg, covs=covs * (s * s), vols=vols, c=c, s=s, cam=cam, sargs=sargs, rargs=rargs)
 
 
-def make_sim(scene, dev, use_graph=True):
+def make_sim(scene, dev, use_graph=True, slab=None):
+    """The scene's simulator and its BC specs.  slab = (rank, world, transport):
+    this rank's gsmpm.dist.SlabDomain of the whole scene instead."""
     from gsmpm.bc import BCSpec
     from gsmpm.sim import Simulator
     sa = scene["sargs"]
     n = scene["xg"].shape[0]
-    sim = Simulator(n, n_grid=sa.n_grid, grid_extent=sa.grid_extent, material=sa.material, E=sa.E, nu=sa.nu,
-                    density=sa.density, gravity=sa.gravity, jelly_fcr=sa.jelly_fcr, use_graph=use_graph, device=dev)
-    sim.set_particles(scene["xg"], scene["covs"], scene["vols"])
+    kw = dict(n_grid=sa.n_grid, grid_extent=sa.grid_extent, material=sa.material, E=sa.E, nu=sa.nu,
+              density=sa.density, gravity=sa.gravity, jelly_fcr=sa.jelly_fcr, device=dev)
+    if slab is not None:
+        from gsmpm.dist import SlabDomain
+        rank, world, xp = slab
+        sim = SlabDomain(scene["xg"], scene["covs"], scene["vols"], rank=rank, world=world, transport=xp,
+                         margin=2, interval=10, **kw)
+    else:
+        sim = Simulator(n, use_graph=use_graph, **kw)
+        sim.set_particles(scene["xg"], scene["covs"], scene["vols"])
     specs = []
     for d in sa.boundary_conditions:
         end = d["start_time"] + sa.substep_dt * d["num_dt"]
@@ -194,61 +208,78 @@ def cpu_baseline(scene, args, budget_s):
             "substeps_per_s": n_done / el}
 
 
-def other_configs(args, dev, frames=3):
+def other_configs(args, dev, frames=3, rank=0, world=1, xp=None, sync=None):
     """BASELINE configs[2] (lego-fracture --material metal, 100k, 128^3: the
-    stress-bearing return-map path) and configs[3] on one GPU (bicycle 1M,
-    256^3, rendered at the bicycle camera's 4946x3286) -- timed in the same
-    run as the headline, sim and render separately."""
+    stress-bearing return-map path) and configs[3] (bicycle 1M, 256^3,
+    rendered at the bicycle camera's 4946x3286): timed in the same run as the
+    headline, sim and render separately.  With a transport (N > 1) both are
+    sharded by slab over the N GPUs, timed barrier-to-barrier (max over ranks),
+    and rank 0 renders the gathered frame."""
     import copy
     import torch
     from gsmpm import raster
     from gsmpm.bc import substep_masks
+    slab = xp is not None
+    sync = sync or torch.cuda.synchronize
     res = {}
     for key, cfg, mat, n, ng in (("C_lego_fracture_metal", "lego-fracture.json", "metal", 100_000, 128),
-                                 ("D_bicycle_1gpu", "bicycle.json", None, 1_000_000, 256)):
+                                 ("D_bicycle", "bicycle.json", None, 1_000_000, 256)):
         a = copy.copy(args)
         a.config, a.material, a.particles, a.n_grid = cfg, mat, n, ng
         sc = build_scene(a, dev)
-        sim, specs = make_sim(sc, dev)
+        sim, specs = make_sim(sc, dev, slab=(rank, world, xp) if slab else None)
         sa = sc["sargs"]
         dt, spf, t = sa.substep_dt, sa.steps_per_frame, 0.0
         masks, t = substep_masks(specs, t, dt, spf)
         sim.step(dt, masks)  # warm-up frame (graph capture)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
+        sync()
+        t0 = time.perf_counter()
         for _ in range(frames):
             masks, t = substep_masks(specs, t, dt, spf)
             sim.step(dt, masks)
-        e1.record()
-        torch.cuda.synchronize()
-        sim_ms = e0.elapsed_time(e1) / frames
-        masks, t = substep_masks(specs, t, dt, spf)
-        prof = sim.profile(dt, masks)
+        sync()
+        sim_ms = (time.perf_counter() - t0) / frames * 1e3
+        if slab:
+            import torch.distributed as dist
+            tt = torch.tensor([sim_ms], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            sim_ms = float(tt.item())
+        nsim = sc["xg"].shape[0]
+        r = {"config": cfg, "material": sa.material, "particles": nsim, "n_grid": sa.n_grid,
+             "parallelism": f"slab{world}" if slab else "single",
+             "sim_ms_per_frame": round(sim_ms, 4), "sim_substeps_per_s": round(spf / (sim_ms * 1e-3), 1),
+             "sim_particle_substeps_per_s": nsim * spf / (sim_ms * 1e-3)}
+        if not slab:
+            masks, t = substep_masks(specs, t, dt, spf)
+            prof = sim.profile(dt, masks)
+            r["k_fused_us_per_launch"] = round(prof[0] / (spf + 1) * 1e3, 2)
+            r["k_grid_f_us_per_launch"] = round(prof[1] / spf * 1e3, 2)
+        else:
+            st = sim.stats()
+            r["rank0_slab_planes"] = [st["lo"], st["hi"]]
         sim.postprocess()
         cam, g, mask = sc["cam"], sc["g"], sc["mask"]
-        feats, opac = g.get_features[mask].contiguous(), g.get_opacity[mask].reshape(-1).contiguous()
-        means_r, covs_r = sim.world_outputs(float(sc["s"]), [float(v) for v in sc["c"].reshape(-1).tolist()],
-                                            render_space=True)
-        tx, ty = math.tan(cam.FovX * 0.5), math.tan(cam.FovY * 0.5)
-        bg = torch.zeros(3, device=dev)
-        rf = lambda: raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg, cam.height,
-                                    cam.width, tx, ty, sh_degree=3, shs=feats, cov3D_precomp=covs_r)
-        K, _, _ = rf()
-        torch.cuda.synchronize()
-        r0 = time.perf_counter()
-        for _ in range(frames):
-            rf()
-        torch.cuda.synchronize()
-        render_ms = (time.perf_counter() - r0) / frames * 1e3
-        nsim = sim.n
-        res[key] = {"config": cfg, "material": sa.material, "particles": nsim, "n_grid": sa.n_grid,
-                    "sim_ms_per_frame": round(sim_ms, 4), "sim_substeps_per_s": round(spf / (sim_ms * 1e-3), 1),
-                    "sim_particle_substeps_per_s": nsim * spf / (sim_ms * 1e-3),
-                    "k_fused_us_per_launch": round(prof[0] / (spf + 1) * 1e3, 2),
-                    "k_grid_f_us_per_launch": round(prof[1] / spf * 1e3, 2),
-                    "render": f"{cam.width}x{cam.height} SH3", "render_ms": round(render_ms, 3), "num_rendered": K}
-        del sim, sc, means_r, covs_r, feats, opac
+        w_args = (float(sc["s"]), [float(v) for v in sc["c"].reshape(-1).tolist()])
+        means_r, covs_r = sim.gather_world(*w_args, render_space=True) if slab else \
+            sim.world_outputs(*w_args, render_space=True)
+        if means_r is not None:
+            feats, opac = g.get_features[mask].contiguous(), g.get_opacity[mask].reshape(-1).contiguous()
+            tx, ty = math.tan(cam.FovX * 0.5), math.tan(cam.FovY * 0.5)
+            bg = torch.zeros(3, device=dev)
+            rf = lambda: raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg,
+                                        cam.height, cam.width, tx, ty, sh_degree=3, shs=feats, cov3D_precomp=covs_r)
+            K, _, _ = rf()
+            torch.cuda.synchronize()
+            r0 = time.perf_counter()
+            for _ in range(frames):
+                rf()
+            torch.cuda.synchronize()
+            r["render"] = f"{cam.width}x{cam.height} SH3"
+            r["render_ms"] = round((time.perf_counter() - r0) / frames * 1e3, 3)
+            r["num_rendered"] = K
+            del feats, opac
+        res[key] = r
+        del sim, sc, means_r, covs_r
         torch.cuda.empty_cache()
     return res
 
@@ -278,27 +309,24 @@ def main():
     from gsmpm import raster
     from gsmpm.bc import substep_masks
 
-    slab = args.slab and world > 1
+    # N > 1: one scene sharded by spatial slab over RCCL (default), or --dp:
+    # independent scenes, one per rank
+    slab = world > 1 and not args.dp
+    xp = None
+    if slab:
+        from gsmpm.dist import make_transport
+        xp = make_transport(rank, world, device=dev)
     scene = build_scene(args, dev, rank=0 if slab else rank)
     sa = scene["sargs"]
     dt, spf = sa.substep_dt, sa.steps_per_frame
     g, mask, cam = scene["g"], scene["mask"], scene["cam"]
     feats = g.get_features[mask].contiguous()
     opac = g.get_opacity[mask].reshape(-1).contiguous()
-    if slab:
-        from gsmpm.dist import SlabSimulator, slab_partition
-        owner, bounds = slab_partition(scene["xg"].cpu().numpy(), sa.n_grid, sa.grid_extent, world)
-        mine = torch.from_numpy((owner == rank).nonzero()[0]).to(dev)
-        for k in ("xg", "covs", "vols"):
-            scene[k] = scene[k][mine].contiguous()
-        feats, opac = feats[mine].contiguous(), opac[mine].contiguous()
-        eng, specs = make_sim(scene, dev)
-        sim = SlabSimulator(eng, rank, world, bounds)
-    else:
-        sim, specs = make_sim(scene, dev)
-        if args.rebin > 0 and sim.pipeline == "fused":
-            sim.set_rebin_interval(args.rebin)
+    sim, specs = make_sim(scene, dev, slab=(rank, world, xp) if slab else None)
+    if not slab and args.rebin > 0 and sim.pipeline == "fused":
+        sim.set_rebin_interval(args.rebin)
     n_local = sim.n
+    n_scene = scene["xg"].shape[0]
     bg = torch.zeros(3, device=dev)
     tanx, tany = math.tan(cam.FovX * 0.5), math.tan(cam.FovY * 0.5)
     # world2grid constants as host floats, once (a per-frame .tolist() / float() of the
@@ -316,13 +344,20 @@ def main():
         sim.postprocess()
         t.append(time.perf_counter())
         if render and not args.no_render:
-            # every rank renders its own particles (its scene, or its slab's share)
-            means_r, covs_r = sim.world_outputs(w_scale, w_center, render_space=True)
+            # slabs: every particle's render-space mean/cov gathered to rank 0, which
+            # renders the frame (compositing order is view-dependent);
+            # --dp / one GPU: every rank renders its own scene
+            if slab:
+                means_r, covs_r = sim.gather_world(w_scale, w_center, render_space=True)
+            else:
+                means_r, covs_r = sim.world_outputs(w_scale, w_center, render_space=True)
             t.append(time.perf_counter())
-            K, _, _ = raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg,
-                                     cam.height, cam.width, tanx, tany, sh_degree=3, shs=feats, cov3D_precomp=covs_r)
+            if means_r is not None:
+                K, _, _ = raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg,
+                                         cam.height, cam.width, tanx, tany, sh_degree=3, shs=feats,
+                                         cov3D_precomp=covs_r)
+                state["K"] = K
             t.append(time.perf_counter())
-            state["K"] = K
         if host_t is not None:
             host_t.append([1e6 * (b - a) for a, b in zip(t, t[1:])])
 
@@ -346,9 +381,12 @@ def main():
         tt = torch.tensor([elapsed], device=red_dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-        nt = torch.tensor([n_local], device=red_dev, dtype=torch.float64)
-        dist.all_reduce(nt)
-        n_total = int(nt.item())
+        if slab:
+            n_total = n_scene  # one scene, every particle simulated once per substep
+        else:
+            nt = torch.tensor([n_local], device=red_dev, dtype=torch.float64)
+            dist.all_reduce(nt)
+            n_total = int(nt.item())
     else:
         n_total = n_local
 
@@ -443,8 +481,11 @@ def main():
                                     "eager frame (= rocprofv3 avg x launches)",
                            "pipeline": sim.pipeline,
                            "live_nodes": live}
-    if rank == 0 and world == 1 and not args.no_extra_configs:
-        out["other_configs"] = other_configs(args, dev)
+    if not args.no_extra_configs:
+        oc = other_configs(args, dev, rank=rank, world=world, xp=xp, sync=barrier) if slab else \
+            (other_configs(args, dev) if world == 1 else None)
+        if oc is not None:
+            out["other_configs"] = oc
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(scene, args, args.cpu_seconds)
     if rank == 0:

@@ -35,6 +35,35 @@ constexpr int kFW0 = kFT0 + 4, kFW1 = kFT1 + 4, kFW2 = kFT2 + 4;  // window node
 constexpr int kFWin = kFW0 * kFW1 * kFW2;                      // 1584
 constexpr int kFTN = kFT0 * kFT1 * kFT2;                       // owned nodes per tile (448)
 
+// ---- multi-GPU slab hooks (slab.h has the exchange and migration kernels) ----
+struct SlabWin {
+  int W;            // window planes (0: not a slab)
+  int a[2];         // first plane of the lower (0) / upper (1) window; window w is [a[w], a[w] + W)
+  int on[2];        // window w present (a neighbour on that side)
+  float4* part[2];  // [W][ng][ng] this rank's partial sums of the window's nodes (k_grid_f writes, k_win_update zeroes)
+  int pass;         // k_grid_f: 0 every touched tile, 1 tiles meeting a window, 2 the others
+};
+
+__device__ __forceinline__ int slab_window_of(const SlabWin& sw, int i) {
+  if (sw.on[0] && i >= sw.a[0] && i < sw.a[0] + sw.W) return 0;
+  if (sw.on[1] && i >= sw.a[1] && i < sw.a[1] + sw.W) return 1;
+  return -1;
+}
+// does tile-x ti (planes [ti * kFT0, ti * kFT0 + kFT0)) meet a window?
+__device__ __forceinline__ bool slab_tile_in_window(const SlabWin& sw, int ti) {
+  const int p0 = ti * kFT0, p1 = p0 + kFT0;
+  bool r = false;
+#pragma unroll
+  for (int w = 0; w < 2; ++w) r = r || (sw.on[w] && p0 < sw.a[w] + sw.W && sw.a[w] < p1);
+  return r;
+}
+
+// drift check of the P2G half of k_fused: base plane allowed in [xlo, xhi)
+struct SlabK {
+  int xlo, xhi;
+  int* drift;
+};
+
 struct FTiles {
   int td0, td1, td2;  // tiles per axis
   int ntiles;         // td0 * td1 * td2 (the pseudo-tile "outside" is index ntiles)
@@ -161,7 +190,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
                                                int bin, int use_box, const float4* __restrict__ gvel,
                                                const BcTable* __restrict__ bct, uint32_t mask, float dt, MatConsts mc,
                                                float4* __restrict__ slots, float4* __restrict__ gacc,
-                                               int* __restrict__ esc) {
+                                               int* __restrict__ esc, SlabK sk) {
   constexpr bool G2P = (MODE & 1) != 0, P2G = (MODE & 2) != 0;
   // channel-planar u64 accumulators; the G2P v window aliases them (it is
   // consumed before the accumulators are zeroed)
@@ -367,6 +396,8 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
       int b[3];
       base_of(x, g.inv_dx, b);
       const bool win = k < cnt && in_grid(x, g) && in_window(b, o0, o1, o2);
+      // slab: a particle past the margin scatters where no window exchange reaches (slab.h)
+      if (k < cnt && (b[0] < sk.xlo || b[0] >= sk.xhi)) *sk.drift = 1;
       // window coordinates covered by this particle's stencil, as per-axis bit masks
       int mxy = win ? (7 << (b[0] - o0)) | (7 << (16 + b[1] - o1)) : 0;
       int mz = win ? 7 << (b[2] - o2) : 0;
@@ -537,10 +568,13 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
                                                     float4* __restrict__ gvel, const BcTable* __restrict__ bct,
                                                     GridStep gs, const int* __restrict__ esc_in,
                                                     int* __restrict__ esc_clear, int* __restrict__ zc,
-                                                    int* __restrict__ zf) {
+                                                    int* __restrict__ zf, SlabWin sw) {
   stamp(3, 0);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *esc_clear = 0;
-  if (zc) {
+  // a slab's grid update runs as two passes (window tiles first, so their
+  // partials can travel while the rest updates): the flag and the zeroing go
+  // with the second
+  if (blockIdx.x == 0 && threadIdx.x == 0 && sw.pass != 1) *esc_clear = 0;
+  if (zc && sw.pass != 1) {
     for (int t = blockIdx.x * blockDim.x + threadIdx.x; t <= tl.ntiles; t += gridDim.x * blockDim.x) {
       zc[t] = 0;
       if (t < tl.ntiles) zf[t] = 0;
@@ -556,6 +590,7 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     const int T = all ? wt >> 1 : ck.touched[wt >> 1];
     int ti, tj, tk;
     ftile_decode(tl, T, ti, tj, tk);
+    if (sw.pass != 0 && slab_tile_in_window(sw, ti) != (sw.pass == 1)) continue;  // workgroup-uniform
     __syncthreads();  // readers of the previous tile's ranges are done
     if (wt == (int)blockIdx.x) stamp(3, 2);
     load_cover27(ck, tbox, tl, ti, tj, tk, s_c0, s_nc, s_bx);
@@ -577,7 +612,11 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
         add4(a, gacc[idx]);
         gacc[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
-      gvel[idx] = node_update(a, i, j, k, g, gs, bct);
+      const int sww = sw.W ? slab_window_of(sw, i) : -1;
+      if (sww >= 0)  // a window node: this rank's partial, totalled after the exchange (k_win_update)
+        sw.part[sww][((size_t)(i - sw.a[sww]) * ng + j) * ng + k] = a;
+      else
+        gvel[idx] = node_update(a, i, j, k, g, gs, bct);
     }
     if (wt == (int)blockIdx.x) stamp(3, 4);
   }

@@ -24,6 +24,7 @@
 // back to the caller's order through `orig`).  Grid: v_out dense float4 n^3;
 // tile slots float4[ntiles][1000]; per-tile buckets int[2][ntiles][cap].
 #include <hip/hip_runtime.h>
+#include <dlfcn.h>
 
 #include <rocprim/device/device_radix_sort.hpp>
 
@@ -519,51 +520,10 @@ __device__ __forceinline__ float4 node_sum(const float4* __restrict__ slots, int
   return a;
 }
 
-// Slab halo windows (multi-GPU, gsmpm/dist.py): planes [x0[w], x0[w] + nx) of
-// the dense grid whose (m, m v) partial sums are exchanged with the rank that
-// shares them; the grid update then uses the reduced sums there.
-struct Halo {
-  int n;               // windows (0, 1 or 2)
-  int x0[2];           // first plane of each window (multiple of kTile)
-  int nx;              // planes per window (multiple of kTile)
-  float4* part;        // [n][nx][ng][ng] this rank's partial sums (k_halo_pack)
-  const float4* sum;   // [n][nx][ng][ng] reduced sums (read by k_grid)
-};
-
-// Partial (m, m v) of every node of the halo windows (zeros where this rank
-// has no particles), plus the gacc contributions of out-of-grid particles.
-__global__ __launch_bounds__(256) void k_halo_pack(GridDims g, Tiles tl, ChunkIn ck, const float4* __restrict__ slots,
-                                                   const float4* __restrict__ gacc, Halo halo, int use_gacc) {
-  __shared__ int s_c0[8], s_nc[8];
-  const int ng = g.ng, td = tl.td;
-  const int tpw = (halo.nx / kTile) * td * td;  // tiles per window
-  for (int wt = blockIdx.x; wt < halo.n * tpw; wt += gridDim.x) {
-    const int w = wt / tpw, r = wt % tpw;
-    const int ti = halo.x0[w] / kTile + r / (td * td), tj = (r / td) % td, tk = r % td;
-    __syncthreads();
-    load_cover(ck, td, ti, tj, tk, s_c0, s_nc);
-    __syncthreads();
-    for (int q = threadIdx.x; q < kTile * kTile * kTile; q += blockDim.x) {
-      const int li = q >> 6, lj = (q >> 3) & 7, lk = q & 7;
-      const int i = ti * kTile + li, j = tj * kTile + lj, k = tk * kTile + lk;
-      if (i >= ng || j >= ng || k >= ng) continue;
-      float4 a = node_sum(slots, tl.max_chunks, s_c0, s_nc, li, lj, lk);
-      if (use_gacc) {
-        const float4 o = gacc[((size_t)i * ng + j) * ng + k];
-        a.x += o.x;
-        a.y += o.y;
-        a.z += o.z;
-        a.w += o.w;
-      }
-      halo.part[(((size_t)w * halo.nx + (i - halo.x0[w])) * ng + j) * ng + k] = a;
-    }
-  }
-}
-
 __global__ __launch_bounds__(512) void k_grid(GridDims g, Tiles tl, ChunkIn ck, const float4* __restrict__ slots,
                                               float4* __restrict__ gacc, float4* __restrict__ gvel,
                                               const BcTable* __restrict__ bct, GridStep gs,
-                                              BinOut nb, Halo halo) {
+                                              BinOut nb) {
   // housekeeping for the G2P that follows (stream order makes this safe)
   for (int t = blockIdx.x * blockDim.x + threadIdx.x; t <= tl.ntiles; t += gridDim.x * blockDim.x) {
     nb.count[t] = 0;
@@ -584,28 +544,19 @@ __global__ __launch_bounds__(512) void k_grid(GridDims g, Tiles tl, ChunkIn ck, 
     __syncthreads();  // readers of the previous tile's ranges are done
     load_cover(ck, td, ti, tj, tk, s_c0, s_nc);
     __syncthreads();
-    int hw = -1;  // halo window holding this tile's planes (windows are tile-aligned)
-    for (int w = 0; w < halo.n; ++w)
-      if (ti * kTile >= halo.x0[w] && ti * kTile < halo.x0[w] + halo.nx) hw = w;
     for (int q = threadIdx.x; q < kTile * kTile * kTile; q += blockDim.x) {
       const int li = q >> 6, lj = (q >> 3) & 7, lk = q & 7;
       const int i = ti * kTile + li, j = tj * kTile + lj, k = tk * kTile + lk;
       if (i >= ng || j >= ng || k >= ng) continue;
       const size_t idx = ((size_t)i * ng + j) * ng + k;
-      float4 a;
-      if (hw >= 0) {
-        a = halo.sum[(((size_t)hw * halo.nx + (i - halo.x0[hw])) * ng + j) * ng + k];  // includes gacc
-        if (outside || gs.keep) gacc[idx] = gs.keep ? a : make_float4(0.f, 0.f, 0.f, 0.f);
-      } else {
-        a = node_sum(slots, tl.max_chunks, s_c0, s_nc, li, lj, lk);
-        if (outside || gs.keep) {
-          const float4 o = gacc[idx];
-          a.x += o.x;
-          a.y += o.y;
-          a.z += o.z;
-          a.w += o.w;
-          gacc[idx] = gs.keep ? a : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+      float4 a = node_sum(slots, tl.max_chunks, s_c0, s_nc, li, lj, lk);
+      if (outside || gs.keep) {
+        const float4 o = gacc[idx];
+        a.x += o.x;
+        a.y += o.y;
+        a.z += o.z;
+        a.w += o.w;
+        gacc[idx] = gs.keep ? a : make_float4(0.f, 0.f, 0.f, 0.f);
       }
       gvel[idx] = node_update(a, i, j, k, g, gs, bct);
     }
@@ -866,8 +817,6 @@ struct ChunkOut {
   int* nchunk;         // [2] {chunks, touched tiles}
   const int* tflag;    // [ntiles] touched flags from the binning
   int* touched;        // [ntiles] compacted touched tiles
-  int* escape;         // [1] set when a touched tile lies outside tile planes [tx_lo, tx_hi]
-  int tx_lo, tx_hi;    // (slab ranks: the planes this rank may touch, own slab + halo windows)
 };
 
 __device__ __forceinline__ int wave_incl_scan(int v) {
@@ -918,7 +867,8 @@ __global__ __launch_bounds__(256) void k_finish_bins(Tiles tl, const int* __rest
   stamp(2, 0);
   // this lane's particle bin, requested first (independent of the scan)
   const int p = blockIdx.x * 256 + threadIdx.x;
-  const int pt = ptile[min(p, n - 1)], psl = pslot[min(p, n - 1)];
+  const int pq = max(0, min(p, n - 1));  // n may be 0 (an empty slab)
+  const int pt = ptile[pq], psl = pslot[pq];
   // tile counts / flags: 16 + 16 unguarded loads in flight per lane per batch
   // (written by other XCDs just before, so each batch is one far round trip)
   for (int q0 = 0; q0 < E; q0 += 256 * 16) {
@@ -977,11 +927,7 @@ __global__ __launch_bounds__(256) void k_finish_bins(Tiles tl, const int* __rest
     // the lower-neighbour axes it added in bits 0..2)
     for (int k = 0; k * kChunk < c; ++k)
       co.chunk[cb + k] = make_int4(t, off + k * kChunk, min(kChunk, c - k * kChunk), c > kChunk ? 8 : 0);
-    if (touched) {
-      co.touched[rk] = t;
-      const int tx = t / (tl.td * tl.td);
-      if (tx < co.tx_lo || tx > co.tx_hi) *co.escape = 1;
-    }
+    if (touched) co.touched[rk] = t;
   }
   if (p < n) list[s_off[pt] + psl] = p;
   stamp(2, 1);
@@ -1069,11 +1015,7 @@ __global__ __launch_bounds__(1024) void k_scan_tiles(Tiles tl, const int* __rest
     co.cbase[t] = o[1];
     for (int k = 0; k < v[1]; ++k)
       co.chunk[o[1] + k] = make_int4(t, o[0] + k * kChunk, min(kChunk, v[0] - k * kChunk), v[0] > kChunk ? 8 : 0);
-    if (v[2]) {
-      co.touched[o[2]] = t;
-      const int tx = t / (tl.td * tl.td);
-      if (tx < co.tx_lo || tx > co.tx_hi) *co.escape = 1;
-    }
+    if (v[2]) co.touched[o[2]] = t;
   }
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 1023) {
     co.nchunk[0] = o[1] + v[1];
@@ -1090,6 +1032,7 @@ __global__ __launch_bounds__(256) void k_scatter(int n, const int* __restrict__ 
 
 
 #include "fused.h"
+#include "slab.h"
 
 // ------------------------------------------------------------ postprocess --
 // compute_cov_from_F (utils.py:401-433) + compute_R_from_F (utils.py:376-398)
@@ -1366,9 +1309,6 @@ struct gsmpm_mpm {
   int* touched[2] = {nullptr, nullptr}; // [ntiles] tiles the grid update owns
   int* tflag[2] = {nullptr, nullptr};   // [ntiles] membership flags of `touched`
   int* list[2] = {nullptr, nullptr};    // [np]
-  Halo halo{};                          // slab halo windows (gsmpm_mpm_set_halo)
-  int tx_lo = 0, tx_hi = 1 << 30;       // tile planes this rank may touch
-  int* escape = nullptr;                // [1] device flag, see ChunkOut
   int4* scan_part = nullptr;            // [ceil((ntiles + 1) / 1024)] block sums (large-grid binning)
   int* ptile = nullptr;                 // [np]
   int* pslot = nullptr;                 // [np]
@@ -1417,6 +1357,29 @@ struct gsmpm_mpm {
     int* orig_alt;
   };
   std::map<std::vector<uint32_t>, FState> graph_fstate;  // fused-pipeline state after the graph
+  // ---- multi-GPU slab (slab.h, slab_host.inc): n varies with migration, np is the capacity ----
+  bool slab = false;
+  int s_lo = 0, s_hi = 0, s_margin = 2, s_interval = 10, s_rank = 0, s_world = 1;
+  int s_has[2] = {0, 0};
+  SlabWin sw{};                              // windows + this rank's partial buffers
+  float4* s_recv[2] = {nullptr, nullptr};    // the neighbours' partials
+  int* s_drift = nullptr;                    // [1] a particle passed the margin (k_fused)
+  int* gid = nullptr;                        // [np] global particle ids, caller order
+  int* gid_alt = nullptr;
+  float* cold_alt = nullptr;
+  int* mig_bcnt = nullptr;                   // [nblk][3] per-block destination counts
+  int* mig_boff = nullptr;                   // [nblk][3] their exclusive scan
+  int* mig_tot = nullptr;                    // [3] + drift flag copy
+  int* mig_host = nullptr;                   // pinned [4]: totals + drift
+  float* mig_send[2] = {nullptr, nullptr};   // [NMIG][count] payloads
+  float* mig_recv[2] = {nullptr, nullptr};
+  size_t mig_send_cap[2] = {0, 0}, mig_recv_cap[2] = {0, 0};  // in particles
+  hipStream_t s_comm = nullptr;              // RCCL exchanges run here, overlapping the interior grid update
+  hipEvent_t s_ev_pack = nullptr, s_ev_x = nullptr;
+  long s_migrations = 0, s_migrated = 0;     // counters (gsmpm_mpm_slab_stats)
+  long s_since = 0;                          // substeps since the last migration
+  float* x_host = nullptr;                   // CALLBACK transport: pinned staging of the exchanged buffers
+  size_t x_host_cap = 0;
 };
 
 namespace gsmpm {
@@ -1429,21 +1392,19 @@ static ChunkIn chunk_in(gsmpm_mpm* h, int c) {
   return ChunkIn{h->count[c], h->cbase[c], h->chunk[c], h->nchunk[c], h->list[c], h->touched[c]};
 }
 static ChunkOut chunk_out(gsmpm_mpm* h, int c) {
-  return ChunkOut{h->cstart[c], h->cbase[c], h->chunk[c], h->nchunk[c], h->tflag[c], h->touched[c],
-                  h->escape, h->tx_lo, h->tx_hi};
+  return ChunkOut{h->cstart[c], h->cbase[c], h->chunk[c], h->nchunk[c], h->tflag[c], h->touched[c]};
 }
 static BinOut bin_out(gsmpm_mpm* h, int c) {
   return BinOut{h->count[c], h->ptile, h->pslot, h->tflag[c], h->tl.td, h->tl.ntiles};
 }
 
-static bool use_fused(const gsmpm_mpm* h) { return h->fused && h->halo.n == 0; }
+static bool use_fused(const gsmpm_mpm* h) { return h->fused; }
 
 static ChunkIn chunk_in_f(gsmpm_mpm* h, int c) {
   return ChunkIn{h->fcount[c], h->fcbase[c], h->fchunk[c], h->fnchunk[c], h->flist[c], h->ftouched[c]};
 }
 static ChunkOut chunk_out_f(gsmpm_mpm* h, int c) {
-  return ChunkOut{h->fcstart[c], h->fcbase[c], h->fchunk[c], h->fnchunk[c], h->ftflag[c], h->ftouched[c],
-                  h->escape, 0, INT_MAX};
+  return ChunkOut{h->fcstart[c], h->fcbase[c], h->fchunk[c], h->fnchunk[c], h->ftflag[c], h->ftouched[c]};
 }
 static Touch touch_f(gsmpm_mpm* h, int c) {
   return Touch{h->ftflag[c], h->ftouched[c], h->fnchunk[c], h->fchunk[c], h->fcbox[c], h->ftbox[c]};
@@ -1478,7 +1439,7 @@ static int finish_bins_on(gsmpm_mpm* h, const Tiles& tl, const int* count, const
                           hipStream_t st, const hipEvent_t* ev) {
   // fused path: tile table fits LDS, first-chunk indices fit 16 bits (s_aux)
   if (tl.ntiles + 1 <= kFuseTiles && tl.max_chunks < 65536) {
-    launch(ev, k_finish_bins, dim3(div_up(h->n, 256)), dim3(256), st, tl, count, co, h->n, (const int*)h->ptile,
+    launch(ev, k_finish_bins, dim3(std::max(1, div_up(h->n, 256))), dim3(256), st, tl, count, co, h->n, (const int*)h->ptile,
            (const int*)h->pslot, list);
   } else {
     const hipEvent_t e0[2] = {ev ? ev[0] : nullptr, nullptr}, e1[2] = {nullptr, ev ? ev[1] : nullptr};
@@ -1486,7 +1447,7 @@ static int finish_bins_on(gsmpm_mpm* h, const Tiles& tl, const int* count, const
     launch(ev ? e0 : nullptr, k_scan_partials, dim3(nblk), dim3(1024), st, tl, count, (const int*)co.tflag,
            h->scan_part);
     launch(nullptr, k_scan_tiles, dim3(nblk), dim3(1024), st, tl, count, co, (const int4*)h->scan_part);
-    launch(ev ? e1 : nullptr, k_scatter, dim3(div_up(h->n, 256)), dim3(256), st, h->n, (const int*)h->ptile,
+    launch(ev ? e1 : nullptr, k_scatter, dim3(std::max(1, div_up(h->n, 256))), dim3(256), st, h->n, (const int*)h->ptile,
            (const int*)h->pslot, (const int*)co.cstart, list);
   }
   GSMPM_LAUNCH_CHECK();
@@ -1502,7 +1463,7 @@ static int finish_binning_f(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_
 // Storage into the bin order of parity c (list[c]: storage rows grouped by
 // tile): planes / orig gathered into the other buffer, which becomes current.
 static int permute_to_bins(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t* ev = nullptr) {
-  launch(ev, k_permute, dim3(div_up(h->n, 256), NPLANES + 1), dim3(256), st, (const float*)h->planes, h->planes_alt,
+  launch(ev, k_permute, dim3(std::max(1, div_up(h->n, 256)), NPLANES + 1), dim3(256), st, (const float*)h->planes, h->planes_alt,
          h->n, h->np, (const int*)h->flist[c], (const int*)h->orig, h->orig_alt);
   GSMPM_LAUNCH_CHECK();
   std::swap(h->planes, h->planes_alt);
@@ -1517,7 +1478,7 @@ static int rebin_f(gsmpm_mpm* h, hipStream_t st) {
   GSMPM_HIP(hipMemsetAsync(h->fcount[c], 0, sizeof(int) * (h->ftl.ntiles + 1), st));
   GSMPM_HIP(hipMemsetAsync(h->ftflag[c], 0, sizeof(int) * h->ftl.ntiles, st));
   GSMPM_HIP(hipMemsetAsync(h->fnchunk[c], 0, sizeof(int) * 2, st));
-  hipLaunchKernelGGL(k_bin_all_f, dim3(div_up(h->n, 256)), dim3(256), 0, st, particles_of(h), h->g, bin_out_f(h, c));
+  hipLaunchKernelGGL(k_bin_all_f, dim3(std::max(1, div_up(h->n, 256))), dim3(256), 0, st, particles_of(h), h->g, bin_out_f(h, c));
   GSMPM_LAUNCH_CHECK();
   int rc = finish_binning_f(h, c, st);
   return rc ? rc : permute_to_bins(h, c, st);
@@ -1548,8 +1509,7 @@ static GridStep grid_step(gsmpm_mpm* h, float dt, uint32_t mask) {
   return gs;
 }
 
-// First half of a substep (parity c): P2G, and the halo partial sums when the
-// simulator is one slab of a multi-GPU domain.
+// First half of a per-phase substep (parity c): P2G.
 static int substep_begin(gsmpm_mpm* h, float dt, uint32_t mask, int c, hipStream_t st, const hipEvent_t* e8) {
   const bool keep = (h->prm.flags & GSMPM_FLAG_KEEP_GRID) != 0;
   if (keep) {
@@ -1564,21 +1524,14 @@ static int substep_begin(gsmpm_mpm* h, float dt, uint32_t mask, int c, hipStream
     default: launch_p2g<4>(h, c, mask, dt, st, e8); break;
   }
   GSMPM_LAUNCH_CHECK();
-  if (h->halo.n > 0) {
-    // gacc holds out-of-grid contributions only when particles left the grid; include it always (cheap)
-    hipLaunchKernelGGL(k_halo_pack, dim3(1024), dim3(256), 0, st, h->g, h->tl, chunk_in(h, c),
-                       (const float4*)h->slots, (const float4*)h->gacc, h->halo, 1);
-    GSMPM_LAUNCH_CHECK();
-  }
   return GSMPM_OK;
 }
 
-// Second half: grid update (reduced halo sums in the windows), G2P, binning of parity nx.
+// Second half: grid update, G2P, binning of parity nx.
 static int substep_end(gsmpm_mpm* h, float dt, uint32_t mask, int c, hipStream_t st, const hipEvent_t* e8) {
   const int nx = c ^ 1;
   launch(e8 ? e8 + 2 : nullptr, k_grid, dim3(grid_grid(h)), dim3(512), st, h->g, h->tl, chunk_in(h, c),
-         (const float4*)h->slots, h->gacc, h->gvel, (const BcTable*)h->dev_bc, grid_step(h, dt, mask), bin_out(h, nx),
-         h->halo);
+         (const float4*)h->slots, h->gacc, h->gvel, (const BcTable*)h->dev_bc, grid_step(h, dt, mask), bin_out(h, nx));
   GSMPM_LAUNCH_CHECK();
   launch(e8 ? e8 + 4 : nullptr, k_g2p, dim3(g2p_grid(h)), dim3(kChunk), st, particles_of(h), h->g, h->tl,
          chunk_in(h, c), bin_out(h, nx), (const float4*)h->gvel, dt);
@@ -1614,9 +1567,11 @@ static int fused_grid(gsmpm_mpm* h) { return std::min(h->ftl.max_chunks, 1024); 
 template <int MAT, int MODE>
 static void launch_fused_t(gsmpm_mpm* h, int c, const BinOutF& bo, int bin, int use_box, uint32_t mask, float dt,
                            int* esc, hipStream_t st, const hipEvent_t* ev) {
+  const SlabK sk = h->slab ? SlabK{h->s_lo - h->s_margin, h->s_hi + h->s_margin, h->s_drift}
+                          : SlabK{INT_MIN, INT_MAX, nullptr};
   launch(ev, k_fused<MAT, MODE>, dim3(fused_grid(h)), dim3(256), st, particles_of(h), h->g, h->ftl, chunk_in_f(h, c),
          touch_f(h, c), bo, bin, use_box, (const float4*)h->gvel, (const BcTable*)h->dev_bc, mask, dt, h->mc, h->fslots, h->gacc,
-         esc);
+         esc, sk);
 }
 template <int MODE>
 static void launch_fused_m(gsmpm_mpm* h, int c, const BinOutF& bo, int bin, int ub, uint32_t mask, float dt, int* esc,
@@ -1647,10 +1602,11 @@ static int launch_fused(gsmpm_mpm* h, int mode, int c, bool bin, bool use_box, u
 }
 
 static int launch_grid_f(gsmpm_mpm* h, int wp, float dt, uint32_t mask, int ep, int* zc, int* zf, hipStream_t st,
-                         const hipEvent_t* ev) {
+                         const hipEvent_t* ev, const SlabWin* swp = nullptr) {
+  const SlabWin sw = swp ? *swp : SlabWin{};
   launch(ev, k_grid_f, dim3(std::min(2 * h->ftl.ntiles, 2048)), dim3(kGridT), st, h->g, h->ftl, chunk_in_f(h, wp),
          (const int*)h->ftbox[wp], (const float4*)h->fslots, h->gacc, h->gvel, (const BcTable*)h->dev_bc, grid_step(h, dt, mask),
-         (const int*)(h->fesc + ep), h->fesc + (ep ^ 1), zc, zf);
+         (const int*)(h->fesc + ep), h->fesc + (ep ^ 1), zc, zf, sw);
   GSMPM_LAUNCH_CHECK();
   return GSMPM_OK;
 }
@@ -1660,8 +1616,11 @@ static int launch_grid_f(gsmpm_mpm* h, int wp, float dt, uint32_t mask, int ep, 
 // rebin_interval substeps and at the end, so the bins are fresh for the next
 // call.  bp / ep: bins parity / escape flag, updated.  ev: 8 events per
 // k_fused launch ({K, grid, binning} pairs), summed into kernel_ms[0..2].
+static int slab_grid_phase(gsmpm_mpm* h, int wp, float dt, uint32_t mask, int ep, int* zc, int* zf, hipStream_t st,
+                           const gsmpm_transport* xp);  // slab_host.inc
 static int launch_substeps_f(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc, hipStream_t st, int& bp, int& ep,
-                             hipEvent_t* ev = nullptr, float* kernel_ms = nullptr) {
+                             hipEvent_t* ev = nullptr, float* kernel_ms = nullptr,
+                             const gsmpm_transport* xp = nullptr) {
   const int R = std::max(1, h->rebin_interval);
   int wp = bp;
   bool zeroed = false;  // counts / flags of parity bp ^ 1 zeroed by a grid launch since the last binning
@@ -1694,7 +1653,8 @@ static int launch_substeps_f(gsmpm_mpm* h, float dt, int nsub, const uint32_t* b
         zf = h->ftflag[bp ^ 1];
         zeroed = true;
       }
-      rc = launch_grid_f(h, wp, dt, mask, ep, zc, zf, st, e8 ? e8 + 2 : nullptr);
+      rc = h->slab ? slab_grid_phase(h, wp, dt, mask, ep, zc, zf, st, xp)
+                   : launch_grid_f(h, wp, dt, mask, ep, zc, zf, st, e8 ? e8 + 2 : nullptr);
       if (rc) return rc;
       ep ^= 1;
     }
@@ -1865,7 +1825,6 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
     if ((e = hipMemset(h->count[c], 0, sizeof(int) * E)) != hipSuccess) return fail(e, "hipMemset");
     if ((e = hipMemset(h->nchunk[c], 0, sizeof(int) * 2)) != hipSuccess) return fail(e, "hipMemset");
   }
-  if ((e = hipMalloc(&h->escape, sizeof(int))) != hipSuccess) return fail(e, "hipMalloc escape");
   // fused pipeline: 8 x 8 x 7-cell tiles (fused.h)
   h->fused = !(prm->flags & (GSMPM_FLAG_PHASED | GSMPM_FLAG_KEEP_GRID));
   h->ftl.td0 = (h->g.ng + kFT0 - 1) / kFT0;
@@ -1910,7 +1869,6 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
   const int scan_tiles = std::max(h->tl.ntiles, h->ftl.ntiles) + 1;
   if ((e = hipMalloc(&h->scan_part, sizeof(int4) * (size_t)div_up(scan_tiles, 1024))) != hipSuccess)
     return fail(e, "hipMalloc scan partials");
-  if ((e = hipMemset(h->escape, 0, sizeof(int))) != hipSuccess) return fail(e, "hipMemset");
   if ((e = hipMalloc(&h->ptile, sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc ptile");
   if ((e = hipMalloc(&h->pslot, sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc pslot");
   if ((e = hipMalloc(&h->dev_bc, sizeof(BcTable))) != hipSuccess) return fail(e, "hipMalloc bc table");
@@ -1964,7 +1922,6 @@ int gsmpm_mpm_destroy(gsmpm_mpm* h) {
   (void)hipFree(h->planes_alt);
   (void)hipFree(h->orig_alt);
   (void)hipFree(h->ptile);
-  (void)hipFree(h->escape);
   (void)hipFree(h->scan_part);
   (void)hipFree(h->pslot);
   (void)hipFree(h->planes_tmp);
@@ -1972,6 +1929,24 @@ int gsmpm_mpm_destroy(gsmpm_mpm* h) {
   (void)hipFree(h->sort_keys);
   (void)hipFree(h->sort_idx);
   (void)hipFree(h->sort_tmp);
+  for (int w = 0; w < 2; ++w) {
+    (void)hipFree(h->sw.part[w]);
+    (void)hipFree(h->s_recv[w]);
+    (void)hipFree(h->mig_send[w]);
+    (void)hipFree(h->mig_recv[w]);
+  }
+  (void)hipFree(h->s_drift);
+  (void)hipFree(h->gid);
+  (void)hipFree(h->gid_alt);
+  (void)hipFree(h->cold_alt);
+  (void)hipFree(h->mig_bcnt);
+  (void)hipFree(h->mig_boff);
+  (void)hipFree(h->mig_tot);
+  if (h->mig_host) (void)hipHostFree(h->mig_host);
+  if (h->x_host) (void)hipHostFree(h->x_host);
+  if (h->s_ev_pack) (void)hipEventDestroy(h->s_ev_pack);
+  if (h->s_ev_x) (void)hipEventDestroy(h->s_ev_x);
+  if (h->s_comm) (void)hipStreamDestroy(h->s_comm);
   delete h;
   return GSMPM_OK;
 }
@@ -2089,9 +2064,8 @@ int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t nsub, const uint32_t* bc, voi
     return GSMPM_ESTATE;
   }
   GSMPM_REQUIRE(nsub >= 0, "gsmpm_mpm_step: n_substeps < 0");
-  if (h->halo.n > 0) {
-    set_error("gsmpm_mpm_step: this simulator is a slab with halo windows; step it with "
-              "gsmpm_mpm_substep_begin / exchange / gsmpm_mpm_substep_end");
+  if (h->slab) {
+    set_error("gsmpm_mpm_step: this simulator is one slab of a multi-GPU domain; step it with gsmpm_mpm_slab_step");
     return GSMPM_ESTATE;
   }
   if (nsub == 0) return GSMPM_OK;
@@ -2166,83 +2140,6 @@ int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t nsub, const uint32_t* bc, voi
   h->planes_alt = fs.planes_alt;
   h->orig = fs.orig;
   h->orig_alt = fs.orig_alt;
-  return GSMPM_OK;
-}
-
-int gsmpm_mpm_set_halo(gsmpm_mpm* h, int32_t n_windows, const int32_t* x0, int32_t nx, float* part, const float* sum,
-                       int32_t allow_lo, int32_t allow_hi) {
-  GSMPM_REQUIRE(h, "gsmpm_mpm_set_halo: null handle");
-  GSMPM_REQUIRE(n_windows >= 0 && n_windows <= 2, "gsmpm_mpm_set_halo: 0..2 windows");
-  GSMPM_REQUIRE(allow_lo < allow_hi, "gsmpm_mpm_set_halo: empty allowed plane range");
-  Halo hl{};
-  hl.n = n_windows;
-  if (n_windows > 0) {
-    GSMPM_REQUIRE(x0 && part && sum, "gsmpm_mpm_set_halo: null window argument");
-    GSMPM_REQUIRE(nx > 0 && nx % kTile == 0, "gsmpm_mpm_set_halo: nx must be a positive multiple of 8");
-    for (int w = 0; w < n_windows; ++w) {
-      GSMPM_REQUIRE(x0[w] >= 0 && x0[w] % kTile == 0 && x0[w] + nx <= h->tl.td * kTile,
-                    "gsmpm_mpm_set_halo: window must be tile-aligned and inside the grid");
-      hl.x0[w] = x0[w];
-    }
-    if (n_windows == 2) GSMPM_REQUIRE(x0[0] + nx <= x0[1], "gsmpm_mpm_set_halo: windows overlap / out of order");
-    hl.nx = nx;
-    hl.part = reinterpret_cast<float4*>(part);
-    hl.sum = reinterpret_cast<const float4*>(sum);
-  }
-  h->halo = hl;
-  h->tx_lo = std::max(0, allow_lo) / kTile;
-  h->tx_hi = std::max(0, allow_hi - 1) / kTile;
-  drop_graphs(h);  // kernel arguments changed
-  // slabs run the per-phase pipeline (halo windows between P2G and the grid
-  // update); its bins must describe the current x
-  if (h->has_particles) {
-    int rc = rebin(h, nullptr);
-    if (rc) return rc;
-    GSMPM_HIP(hipStreamSynchronize(nullptr));
-  }
-  return GSMPM_OK;
-}
-
-int gsmpm_mpm_substep_begin(gsmpm_mpm* h, float dt, uint32_t bc_active, void* stream) {
-  GSMPM_REQUIRE(h, "gsmpm_mpm_substep_begin: null handle");
-  if (!h->has_particles) {
-    set_error("gsmpm_mpm_substep_begin: particles not set");
-    return GSMPM_ESTATE;
-  }
-  hipStream_t st = (hipStream_t)stream;
-  if (use_fused(h)) {
-    set_error("gsmpm_mpm_substep_begin: the split substep is the slab path; set halo windows first "
-              "(gsmpm_mpm_set_halo) or create the simulator with GSMPM_FLAG_PHASED");
-    return GSMPM_ESTATE;
-  }
-  if (!(h->prm.flags & GSMPM_FLAG_NO_SORT) && h->resort_interval > 0 && h->since_sort >= h->resort_interval) {
-    int rc = resort(h, st);
-    if (rc) return rc;
-  }
-  return substep_begin(h, dt, bc_active, h->cur_box, st, nullptr);
-}
-
-int gsmpm_mpm_substep_end(gsmpm_mpm* h, float dt, uint32_t bc_active, void* stream) {
-  GSMPM_REQUIRE(h, "gsmpm_mpm_substep_end: null handle");
-  if (use_fused(h)) {
-    set_error("gsmpm_mpm_substep_end: the split substep is the slab path (see gsmpm_mpm_substep_begin)");
-    return GSMPM_ESTATE;
-  }
-  int rc = substep_end(h, dt, bc_active, h->cur_box, (hipStream_t)stream, nullptr);
-  if (rc) return rc;
-  h->cur_box ^= 1;
-  h->since_sort += 1;
-  return GSMPM_OK;
-}
-
-int gsmpm_mpm_halo_status(gsmpm_mpm* h, int32_t* escaped, void* stream) {
-  GSMPM_REQUIRE(h && escaped, "gsmpm_mpm_halo_status: null argument");
-  hipStream_t st = (hipStream_t)stream;
-  int v = 0;
-  GSMPM_HIP(hipMemcpyAsync(&v, h->escape, sizeof(int), hipMemcpyDeviceToHost, st));
-  GSMPM_HIP(hipStreamSynchronize(st));
-  GSMPM_HIP(hipMemsetAsync(h->escape, 0, sizeof(int), st));
-  *escaped = v;
   return GSMPM_OK;
 }
 
@@ -2415,7 +2312,7 @@ int gsmpm_mpm_time_kernels(gsmpm_mpm* h, float dt, uint32_t bc_active, int32_t r
   GSMPM_HIP(hipEventCreate(&e[1]));
   auto grid = [&]() {
     launch(nullptr, k_grid, dim3(grid_grid(h)), dim3(512), st, h->g, h->tl, chunk_in(h, c), (const float4*)h->slots,
-           h->gacc, h->gvel, (const BcTable*)h->dev_bc, gs, bin_out(h, nx), h->halo);
+           h->gacc, h->gvel, (const BcTable*)h->dev_bc, gs, bin_out(h, nx));
   };
   auto g2p = [&]() {
     launch(nullptr, k_g2p, dim3(g2p_grid(h)), dim3(kChunk), st, particles_of(h), h->g, h->tl, chunk_in(h, c),
@@ -2583,3 +2480,5 @@ int gsmpm_particle_volume(const float* x, int32_t n, int32_t ng, double extent, 
 }
 
 }  // extern "C"
+
+#include "slab_host.inc"

@@ -79,11 +79,18 @@ _SIGS = {
                                                     ctypes.c_double]),
     "gsmpm_mpm_step": (ctypes.c_int, [c_void_p, ctypes.c_float, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint32),
                                       c_void_p]),
-    "gsmpm_mpm_set_halo": (ctypes.c_int, [c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32,
-                                          c_void_p, c_void_p, ctypes.c_int32, ctypes.c_int32]),
-    "gsmpm_mpm_substep_begin": (ctypes.c_int, [c_void_p, ctypes.c_float, ctypes.c_uint32, c_void_p]),
-    "gsmpm_mpm_substep_end": (ctypes.c_int, [c_void_p, ctypes.c_float, ctypes.c_uint32, c_void_p]),
-    "gsmpm_mpm_halo_status": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int32), c_void_p]),
+    "gsmpm_rccl_unique_id": (ctypes.c_int, [c_void_p]),
+    "gsmpm_rccl_comm_init": (ctypes.c_int, [c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(c_void_p)]),
+    "gsmpm_rccl_comm_destroy": (ctypes.c_int, [c_void_p]),
+    "gsmpm_mpm_slab_init": (ctypes.c_int, [c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                           ctypes.c_int32, ctypes.c_int32]),
+    "gsmpm_mpm_slab_set_particles": (ctypes.c_int, [c_void_p, ctypes.c_int32, c_void_p, c_void_p, c_void_p, c_void_p,
+                                                    c_void_p, c_void_p]),
+    "gsmpm_mpm_slab_step": (ctypes.c_int, [c_void_p, ctypes.c_float, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint32),
+                                           c_void_p, c_void_p]),
+    "gsmpm_mpm_count": (ctypes.c_int, [c_void_p]),
+    "gsmpm_mpm_get_gid": (ctypes.c_int, [c_void_p, c_void_p, c_void_p]),
+    "gsmpm_mpm_slab_stats": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int64)]),
     "gsmpm_mpm_resort": (ctypes.c_int, [c_void_p, ctypes.c_int32, c_void_p]),
     "gsmpm_mpm_set_rebin_interval": (ctypes.c_int, [c_void_p, ctypes.c_int32]),
     "gsmpm_mpm_pipeline": (ctypes.c_int, [c_void_p]),
@@ -132,6 +139,18 @@ _SIGS = {
                               [c_void_p] * 8 + [c_void_p]),
     "gsmpm_raster_mark_visible": (ctypes.c_int, [c_void_p, ctypes.c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
+
+# slab transports (include/gsmpm.h)
+XPORT_NONE, XPORT_RCCL, XPORT_CALLBACK = 0, 1, 2
+EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int32),
+                               ctypes.POINTER(c_void_p), ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(c_void_p),
+                               ctypes.POINTER(ctypes.c_size_t))
+
+
+class Transport(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("rank", ctypes.c_int32), ("world", ctypes.c_int32), ("comm", c_void_p),
+                ("fn", EXCHANGE_FN), ("user", c_void_p)]
+
 
 # field ids (include/gsmpm.h)
 FIELD = {"x": 0, "v": 1, "C": 2, "F_trial": 3, "cov": 4, "init_cov": 5, "R": 6, "mass": 7, "vol": 8, "mu": 9,

@@ -1,134 +1,247 @@
-"""Multi-GPU MPM: one shared grid split into x-slabs, one rank per GPU.
+"""Multi-GPU MPM: one scene cut into spatial slabs, one rank per GPU.
 
-SURVEY.md 8(e).  The reference is single-GPU; this is the MI355X-side
-decomposition of its substep (mpm_solver/solver.py:27-52):
+SURVEY.md 8(e).  The reference runs its substep (mpm_solver/solver.py:27-52)
+on one device (main.py:28); here it is sharded by slab along grid axis 0
+(csrc/slab.h has the kernels, csrc/slab_host.inc the per-substep sequence):
 
-* Particles are owned by rank: ``slab_partition`` splits them into ``world``
-  x-slabs of about equal count by their base plane
-  (trunc(x * inv_dx - 0.5), utils.py:95), slab bounds rounded to 8-plane tiles.
-  Every rank runs a full-size grid but only its particles touch it, so the work
-  (tiles, chunks) is its slab's.
-* A node receives contributions from two ranks only near a shared slab bound
-  b: the halo window [b - H, b + H) (H = 8 planes by default).  After P2G each
-  rank writes its partial (m, m v) of every window node; the two ranks sharing
-  the window exchange partials with one send/recv pair (RCCL over xGMI, or
-  gloo), and both add them in the same order (a + b == b + a in f32), so the
-  grid update, BCs and G2P see the same node values on both sides -- the
-  "all-reduce of boundary grid nodes" of the north star, done pairwise.
-* No particle migration: a rank may touch only planes [b_r - H, b_{r+1} + H).
-  The library flags any touched tile outside that range and ``step`` raises
-  (never a silently wrong answer); re-partition (``repartition``) when that
-  happens.
+* ``slab_bounds`` cuts the planes [0, n_grid) into ``world`` slabs of about
+  equal particle count (quantiles of the particles' base planes,
+  trunc(x * inv_dx - 0.5), utils.py:95), each at least 2 * margin + 2 planes
+  thick.  Rank r owns planes [bounds[r], bounds[r+1]) and the particles whose
+  base plane lies there.
+* Every substep the partial (m v, m) sums of the 2 * margin + 2 planes around
+  each shared bound are swapped with the neighbour and both sides update the
+  node from the same f32 sum (lower rank's partial + upper rank's): the
+  pairwise all-reduce of boundary grid nodes, over RCCL (``RcclTransport``,
+  grouped ncclSend/ncclRecv on the simulator's comm stream, overlapping the
+  interior grid update) or, for tests, a host callback over
+  torch.distributed (``CallbackTransport``, gloo).
+* Every ``interval`` substeps the particles whose base plane left the slab
+  migrate to the neighbour (wave-ballot compaction on the GPU, counts then
+  payloads through the transport).  A particle drifting more than ``margin``
+  planes between migrations would have scattered outside the exchanged
+  windows; the library detects it and ``step`` raises.
 
-The engine is anything with ``set_halo / substep_begin / substep_end /
-halo_escaped`` -- ``gsmpm.sim.Simulator`` on the GPU, or a CPU engine in the
-tests.
+``SlabDomain`` is one rank's view: the engine (``gsmpm.sim.Simulator`` in
+slab mode), the transport, and ``gather`` of per-particle outputs to one rank
+in global particle order (the renderer does not shard by slab: compositing
+order is view-dependent).
 """
 from __future__ import annotations
+
+import ctypes
 
 import numpy as np
 import torch
 import torch.distributed as dist
 
-TILE = 8
+from . import _lib
+from ._lib import LIB, check
 
 
 def base_planes(x_grid, inv_dx: float):
-    """trunc(x * inv_dx - 0.5) of the x coordinate, f32 as the kernels compute it."""
-    xs = np.asarray(x_grid, dtype=np.float32)[:, 0]
-    return np.trunc(xs * np.float32(inv_dx) - np.float32(0.5)).astype(np.int64)
+    """trunc(x * inv_dx - 0.5) of the axis-0 coordinate, f32 as the kernels compute it."""
+    xs = np.asarray(x_grid, dtype=np.float32).reshape(-1, 3)[:, 0]
+    with np.errstate(invalid="ignore"):
+        return np.trunc(xs * np.float32(inv_dx) - np.float32(0.5)).astype(np.int64)
 
 
-def slab_partition(x_grid, n_grid: int, grid_extent: float, world: int, halo: int = TILE):
-    """Split particles into `world` x-slabs of about equal count.
-
-    Returns (owner[N] int32, bounds[world + 1]) with bounds[0] = 0,
-    bounds[world] = n_grid rounded up to a tile, every bound a multiple of 8,
-    and slabs at least 2 * halo planes thick (so the two windows of a rank never
-    overlap).  Raises ValueError if the grid cannot hold that many slabs.
-    """
-    inv_dx = n_grid / grid_extent
-    bx = base_planes(x_grid, inv_dx)
-    top = (n_grid + TILE - 1) // TILE * TILE
+def slab_bounds(x_grid, n_grid: int, grid_extent: float, world: int, margin: int = 2):
+    """Plane bounds [0 = b_0 < b_1 < ... < b_world = n_grid] of `world` slabs of
+    about equal particle count, each >= 2 * margin + 2 planes thick.  Raises
+    ValueError if the grid cannot hold that many slabs."""
+    thick = 2 * margin + 2
     if world == 1:
-        return np.zeros(len(bx), np.int32), [0, top]
-    qs = np.quantile(np.clip(bx, 0, n_grid - 1), [r / world for r in range(1, world)])
-    bounds = [0]
-    for q in qs:
-        b = int(round(q / TILE)) * TILE
-        b = max(b, bounds[-1] + 2 * halo)
-        bounds.append(b)
-    bounds.append(top)
-    for r in range(world):
-        if bounds[r + 1] - bounds[r] < 2 * halo or (r + 1 < world and bounds[r + 1] + halo > top):
-            raise ValueError(f"cannot cut {n_grid} planes into {world} slabs of >= {2 * halo} planes "
-                             f"around the particles (bounds {bounds})")
-    owner = (np.searchsorted(np.asarray(bounds[1:-1]), bx, side="right")).astype(np.int32)
-    return owner, bounds
+        return [0, n_grid]
+    if world * thick > n_grid:
+        raise ValueError(f"cannot cut {n_grid} planes into {world} slabs of >= {thick} planes")
+    bx = np.clip(base_planes(x_grid, n_grid / grid_extent), 0, n_grid - 1)
+    q = np.quantile(bx, [r / world for r in range(1, world)]) if len(bx) else \
+        np.linspace(0, n_grid, world + 1)[1:-1]
+    b = [0] + [int(round(v)) for v in q] + [n_grid]
+    for r in range(1, world):  # forward: every slab at least `thick`
+        b[r] = max(b[r], b[r - 1] + thick)
+    for r in range(world - 1, 0, -1):  # backward: room for the slabs above
+        b[r] = min(b[r], b[r + 1] - thick)
+    return b
 
 
-def windows_of(rank: int, world: int, bounds, halo: int = TILE):
-    """Halo windows of `rank` in increasing x: lower (shared with rank - 1) and upper (rank + 1)."""
-    w = []
-    if rank > 0:
-        w.append(bounds[rank] - halo)
-    if rank < world - 1:
-        w.append(bounds[rank + 1] - halo)
-    return w
+def owner_of(x_grid, bounds, n_grid: int, grid_extent: float):
+    """Rank owning each particle: the slab holding its base plane (clipped to the grid)."""
+    bx = np.clip(base_planes(x_grid, n_grid / grid_extent), 0, n_grid - 1)
+    return np.searchsorted(np.asarray(bounds[1:-1]), bx, side="right").astype(np.int32)
 
 
-class SlabSimulator:
-    """One rank's slab of a shared-grid MPM domain (see module docstring)."""
+# ------------------------------------------------------------- transports --
+class RcclTransport:
+    """GSMPM_XPORT_RCCL: an RCCL communicator of the library's own (unique id
+    from rank 0, broadcast over the torch.distributed group), used by
+    gsmpm_mpm_slab_step for grouped ncclSend/ncclRecv between neighbours."""
 
-    def __init__(self, engine, rank: int, world: int, bounds, halo: int = TILE, group=None):
-        self.engine, self.rank, self.world, self.bounds, self.halo = engine, rank, world, list(bounds), halo
-        self.group = group
-        self.x0s = windows_of(rank, world, bounds, halo)
-        lo = max(0, bounds[rank] - halo) if rank > 0 else 0
-        hi = bounds[rank + 1] + halo if rank < world - 1 else 1 << 30
-        self.part, self.total = engine.set_halo(self.x0s, 2 * halo, allow=(lo, hi))
-        self.n = engine.n
-        self._host = None
-        if world > 1 and dist.get_backend(group) == "gloo" and self.part.is_cuda:
-            # gloo moves host memory: stage the windows through pinned buffers
-            self._host = (torch.empty(self.part.shape, pin_memory=True), torch.empty(self.part.shape, pin_memory=True))
-        self.recv = torch.empty_like(self.part) if self.part is not None else None
+    def __init__(self, rank: int, world: int, group=None, device=None):
+        uid = (ctypes.c_uint8 * 128)()
+        if rank == 0:
+            check(LIB.gsmpm_rccl_unique_id(uid), "gsmpm_rccl_unique_id")
+        obj = [bytes(uid)]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        uid = (ctypes.c_uint8 * 128).from_buffer_copy(obj[0])
+        comm = ctypes.c_void_p()
+        with torch.cuda.device(device if device is not None else torch.cuda.current_device()):
+            check(LIB.gsmpm_rccl_comm_init(uid, int(rank), int(world), ctypes.byref(comm)), "gsmpm_rccl_comm_init")
+        self.comm = comm
+        self.struct = _lib.Transport(_lib.XPORT_RCCL, int(rank), int(world), comm, _lib.EXCHANGE_FN(), None)
 
-    # ------------------------------------------------------------ exchange --
-    def _exchange(self):
-        if self.part is None:  # world == 1
-            return
-        part, recv = self.part, self.recv
-        if self._host is not None:
-            hp, hr = self._host
-            hp.copy_(part)
-            part, recv = hp, hr
+    def close(self):
+        if self.comm is not None and self.comm.value:
+            check(LIB.gsmpm_rccl_comm_destroy(self.comm), "gsmpm_rccl_comm_destroy")
+            self.comm = None
+
+
+class CallbackTransport:
+    """GSMPM_XPORT_CALLBACK over torch.distributed point-to-point: the library
+    hands pinned host copies of the buffers to `exchange` (gloo moves host
+    memory).  Used to run several slab ranks on one GPU in tests; the
+    protocol (sizes, order, peers) is the one the RCCL transport runs."""
+
+    def __init__(self, rank: int, world: int, group=None):
+        self.rank, self.world, self.group = int(rank), int(world), group
+        self.error = None
+        self._fn = _lib.EXCHANGE_FN(self._callback)  # kept alive with the object
+        self.struct = _lib.Transport(_lib.XPORT_CALLBACK, self.rank, self.world, None, self._fn, None)
+
+    def exchange(self, peers, sends, recvs):
+        """send sends[i] to peers[i] and receive recvs[i] from it (CPU tensors)."""
         ops = []
-        k = 0
-        if self.rank > 0:
-            ops.append(dist.P2POp(dist.isend, part[k], self.rank - 1, self.group))
-            ops.append(dist.P2POp(dist.irecv, recv[k], self.rank - 1, self.group))
-            k += 1
-        if self.rank < self.world - 1:
-            ops.append(dist.P2POp(dist.isend, part[k], self.rank + 1, self.group))
-            ops.append(dist.P2POp(dist.irecv, recv[k], self.rank + 1, self.group))
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
-        if self._host is not None:
-            self.recv.copy_(recv, non_blocking=True)
-        # both sharing ranks add the same two partials: identical window sums
-        torch.add(self.part, self.recv, out=self.total)
+        for p, s, r in zip(peers, sends, recvs):
+            if s.numel():
+                ops.append(dist.P2POp(dist.isend, s, int(p), self.group))
+            if r.numel():
+                ops.append(dist.P2POp(dist.irecv, r, int(p), self.group))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
 
-    # ---------------------------------------------------------------- step --
+    def _callback(self, user, n, peers, send, sb, recv, rb):
+        try:
+            view = lambda addr, nb: torch.frombuffer((ctypes.c_uint8 * nb).from_address(addr), dtype=torch.uint8) \
+                if nb else torch.empty(0, dtype=torch.uint8)
+            self.exchange([peers[i] for i in range(n)], [view(send[i], sb[i]) for i in range(n)],
+                          [view(recv[i], rb[i]) for i in range(n)])
+            return 0
+        except Exception as e:  # surfaced by the library as a failed exchange; kept for the caller
+            self.error = e
+            return 1
+
+    def close(self):
+        pass
+
+
+def make_transport(rank: int, world: int, group=None, device=None):
+    """RCCL when the process group is nccl (one rank per GPU), else the host callback."""
+    if world > 1 and dist.get_backend(group) == "nccl":
+        return RcclTransport(rank, world, group, device)
+    return CallbackTransport(rank, world, group)
+
+
+# ------------------------------------------------------------------ domain --
+class SlabDomain:
+    """Rank `rank`'s slab of one MPM scene.
+
+    Every rank passes the WHOLE scene (grid-space x, cov6, vol, optional v;
+    the same arrays on every rank, e.g. built from the same seed / PLY); the
+    slab keeps its particles, with their index in those arrays as global id.
+    ``sim_kwargs`` go to gsmpm.sim.Simulator (material, E, nu, density,
+    gravity, ...); ``engine_factory`` replaces Simulator (tests: a CPU engine
+    built on the oracle that runs the same slab protocol)."""
+
+    def __init__(self, x_grid, cov6, vol, *, rank: int, world: int, transport, n_grid: int, grid_extent: float = 2.0,
+                 margin: int = 2, interval: int = 10, capacity: int | None = None, v=None, device=None,
+                 engine_factory=None, **sim_kwargs):
+        from .sim import Simulator
+        engine_factory = engine_factory or Simulator
+        self.rank, self.world, self.transport = int(rank), int(world), transport
+        self.n_grid, self.grid_extent = int(n_grid), float(grid_extent)
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        self.margin, self.interval = int(margin), int(interval)
+        xh = (x_grid.detach().cpu().numpy() if torch.is_tensor(x_grid) else np.asarray(x_grid)).reshape(-1, 3)
+        self.n_total = len(xh)
+        self.bounds = slab_bounds(xh, self.n_grid, self.grid_extent, self.world, margin)
+        owner = owner_of(xh, self.bounds, self.n_grid, self.grid_extent)
+        mine = torch.from_numpy(np.nonzero(owner == self.rank)[0]).to(self.device)
+        cap = capacity or max(4096, 2 * (self.n_total // self.world) + 4096)
+        self.engine = engine_factory(cap, n_grid=self.n_grid, grid_extent=self.grid_extent, device=self.device,
+                                     **sim_kwargs)
+        self.engine.slab_init(self.rank, self.world, self.bounds[self.rank], self.bounds[self.rank + 1], margin,
+                              interval)
+        t = lambda a: (a if torch.is_tensor(a) else torch.from_numpy(np.ascontiguousarray(a))).to(self.device)
+        sel = lambda a: None if a is None else t(a).reshape(self.n_total, -1)[mine]
+        self.engine.slab_set_particles(sel(x_grid), sel(cov6), sel(vol), mine.to(torch.int32), v=sel(v))
+
+    # configuration and stepping: the engine's, with the transport
+    def add_fixed_cube(self, center, size):
+        return self.engine.add_fixed_cube(center, size)
+
+    def add_impulse(self, center, size, force, substep_dt):
+        return self.engine.add_impulse(center, size, force, substep_dt)
+
+    def add_plane_collider(self, point, normal, friction=0.0):
+        return self.engine.add_plane_collider(point, normal, friction)
+
     def step(self, dt: float, masks):
-        for m in masks:
-            self.engine.substep_begin(dt, m)
-            self._exchange()
-            self.engine.substep_end(dt, m)
-        if self.engine.halo_escaped():
-            raise RuntimeError(f"rank {self.rank}: particles left planes [{self.bounds[self.rank]} - {self.halo}, "
-                               f"{self.bounds[self.rank + 1]} + {self.halo}); re-partition the slabs")
+        try:
+            self.engine.slab_step(dt, masks, self.transport)
+        except _lib.GsmpmError:
+            err = getattr(self.transport, "error", None)
+            if err is not None:
+                raise RuntimeError(f"rank {self.rank}: slab exchange failed") from err
+            raise
 
-    def __getattr__(self, name):
-        # postprocess / get / world_outputs / ... act on this rank's particles
-        return getattr(self.engine, name)
+    def postprocess(self):
+        self.engine.postprocess()
+
+    @property
+    def n(self) -> int:
+        return self.engine.count
+
+    def stats(self):
+        return self.engine.slab_stats()
+
+    # outputs in global order on one rank
+    def gather(self, rows: torch.Tensor, dst: int = 0):
+        """Per-particle rows of this rank ([n, w] in the engine's row order)
+        -> on rank `dst` the [n_total, w] tensor in global particle order
+        (None elsewhere).  all_gather of count-padded blocks + global ids."""
+        gid = self.engine.get_gid().to(torch.int64)
+        rows = rows.reshape(gid.numel(), -1).to(torch.float32)
+        w = rows.shape[1]
+        on_dev = dist.get_backend() == "nccl"
+        dev = self.device if on_dev else torch.device("cpu")
+        cnt = torch.tensor([gid.numel()], dtype=torch.int64, device=dev)
+        cnts = [torch.zeros_like(cnt) for _ in range(self.world)]
+        dist.all_gather(cnts, cnt)
+        nmax = int(max(int(c.item()) for c in cnts))
+        blk = torch.zeros((nmax, w + 1), dtype=torch.float32, device=dev)
+        blk[: gid.numel(), :w] = rows.to(dev)
+        blk[: gid.numel(), w] = gid.to(dev).to(torch.float32)  # exact below 2^24 particles
+        assert self.n_total < (1 << 24)
+        parts = [torch.empty_like(blk) for _ in range(self.world)]
+        dist.all_gather(parts, blk)
+        if self.rank != dst:
+            return None
+        out = torch.empty((self.n_total, w), dtype=torch.float32, device=self.device)
+        for c, p in zip(cnts, parts):
+            k = int(c.item())
+            if k:
+                p = p[:k].to(self.device)
+                out[p[:, w].to(torch.int64)] = p[:, :w]
+        return out
+
+    def gather_field(self, name: str, dst: int = 0):
+        return self.gather(self.engine.get(name), dst)
+
+    def gather_world(self, scale, center, render_space: bool, dst: int = 0):
+        """Fused grid2world (+ render shift) of every particle, on rank `dst`:
+        (means [N, 3], cov6 [N, 6]) in global order."""
+        m, c = self.engine.world_outputs(scale, center, render_space)
+        full = self.gather(torch.cat([m, c], 1), dst)
+        return (None, None) if full is None else (full[:, :3].contiguous(), full[:, 3:].contiguous())

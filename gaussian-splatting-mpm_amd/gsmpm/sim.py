@@ -95,35 +95,51 @@ class Simulator:
         check(LIB.gsmpm_mpm_step(self._h, ctypes.c_float(dt), n, arr, stream_of(self.device)), "gsmpm_mpm_step")
 
     # ---------------------------------------------------------- slab mode --
-    def set_halo(self, x0s, nx: int, part=None, total=None, allow=(0, 1 << 30)):
-        """Halo windows of a multi-GPU slab (gsmpm/dist.py): planes
-        [x0, x0 + nx) for x0 in x0s.  Returns (part, total) device buffers
-        [len(x0s), nx, n, n, 4]: the library writes this rank's partial sums to
-        `part` and reads the reduced sums from `total`."""
-        nw, ng = len(x0s), self.n_grid
-        shape = (nw, nx, ng, ng, 4)
-        if nw and part is None:
-            part = torch.zeros(shape, dtype=torch.float32, device=self.device)
-        if nw and total is None:
-            total = torch.zeros(shape, dtype=torch.float32, device=self.device)
-        arr = (ctypes.c_int32 * max(1, nw))(*[int(v) for v in x0s])
-        check(LIB.gsmpm_mpm_set_halo(self._h, nw, arr, int(nx), ptr(part) if nw else None,
-                                     ptr(total) if nw else None, int(allow[0]), int(allow[1])), "gsmpm_mpm_set_halo")
-        self._halo = (part, total)  # keep the buffers alive
-        return part, total
+    def slab_init(self, rank: int, world: int, lo: int, hi: int, margin: int = 2, interval: int = 10):
+        """Make this simulator (created with n_particles = capacity) rank `rank`
+        of a `world`-slab domain owning grid planes [lo, hi) (csrc/slab.h)."""
+        check(LIB.gsmpm_mpm_slab_init(self._h, int(rank), int(world), int(lo), int(hi), int(margin), int(interval)),
+              "gsmpm_mpm_slab_init")
 
-    def substep_begin(self, dt: float, mask: int):
-        check(LIB.gsmpm_mpm_substep_begin(self._h, ctypes.c_float(dt), int(mask) & 0xFFFFFFFF,
-                                          stream_of(self.device)), "gsmpm_mpm_substep_begin")
+    def slab_set_particles(self, x, cov6, vol, gid, v=None):
+        f = lambda t: None if t is None else t.detach().to(self.device, torch.float32).contiguous()
+        x, cov6, vol, v = f(x), f(cov6), f(vol), f(v)
+        gid = gid.detach().to(self.device, torch.int32).contiguous()
+        n = int(gid.numel())
+        assert x.numel() == 3 * n and cov6.numel() == 6 * n and vol.numel() == n
+        check(LIB.gsmpm_mpm_slab_set_particles(self._h, n, ptr(x) if n else None, ptr(cov6) if n else None,
+                                               ptr(vol) if n else None, ptr(v) if n and v is not None else None,
+                                               ptr(gid) if n else None, stream_of(self.device)),
+              "gsmpm_mpm_slab_set_particles")
 
-    def substep_end(self, dt: float, mask: int):
-        check(LIB.gsmpm_mpm_substep_end(self._h, ctypes.c_float(dt), int(mask) & 0xFFFFFFFF,
-                                        stream_of(self.device)), "gsmpm_mpm_substep_end")
+    def slab_step(self, dt: float, masks, transport):
+        """`len(masks)` substeps with the window exchange every substep and the
+        particle migration every `interval` substeps through `transport`
+        (gsmpm.dist.RcclTransport / CallbackTransport)."""
+        n = len(masks)
+        if n == 0:
+            return
+        arr = (ctypes.c_uint32 * n)(*[int(m) & 0xFFFFFFFF for m in masks])
+        xp = None if transport is None else ctypes.byref(transport.struct)
+        check(LIB.gsmpm_mpm_slab_step(self._h, ctypes.c_float(dt), n, arr, xp, stream_of(self.device)),
+              "gsmpm_mpm_slab_step")
 
-    def halo_escaped(self) -> bool:
-        v = ctypes.c_int32(0)
-        check(LIB.gsmpm_mpm_halo_status(self._h, ctypes.byref(v), stream_of(self.device)), "gsmpm_mpm_halo_status")
-        return bool(v.value)
+    @property
+    def count(self) -> int:
+        """Particles this simulator holds now (a slab's count changes with migration)."""
+        return check(LIB.gsmpm_mpm_count(self._h), "gsmpm_mpm_count")
+
+    def get_gid(self) -> torch.Tensor:
+        out = torch.empty(self.count, dtype=torch.int32, device=self.device)
+        if out.numel():
+            check(LIB.gsmpm_mpm_get_gid(self._h, ptr(out), stream_of(self.device)), "gsmpm_mpm_get_gid")
+        return out
+
+    def slab_stats(self):
+        b = (ctypes.c_int64 * 8)()
+        check(LIB.gsmpm_mpm_slab_stats(self._h, b), "gsmpm_mpm_slab_stats")
+        keys = ("migrations", "migrated", "lo", "hi", "margin", "interval", "window_planes", "capacity")
+        return dict(zip(keys, [int(v) for v in b]))
 
     def profile(self, dt: float, masks):
         """Eager substeps with a hipEvent pair per kernel -> summed ms of
@@ -170,13 +186,16 @@ class Simulator:
         check(LIB.gsmpm_mpm_resort(self._h, int(interval), stream_of(self.device)), "gsmpm_mpm_resort")
 
     def postprocess(self):
+        if self.count == 0:
+            return
         check(LIB.gsmpm_mpm_postprocess(self._h, stream_of(self.device)), "gsmpm_mpm_postprocess")
 
     # ------------------------------------------------------------------ io --
     def get(self, name: str) -> torch.Tensor:
-        w = _WIDTH[name]
-        out = torch.empty((self.n, w) if w > 1 else (self.n,), dtype=torch.float32, device=self.device)
-        check(LIB.gsmpm_mpm_get(self._h, _lib.FIELD[name], ptr(out), stream_of(self.device)), f"get {name}")
+        w, n = _WIDTH[name], self.count
+        out = torch.empty((n, w) if w > 1 else (n,), dtype=torch.float32, device=self.device)
+        if n:
+            check(LIB.gsmpm_mpm_get(self._h, _lib.FIELD[name], ptr(out), stream_of(self.device)), f"get {name}")
         return out
 
     def set(self, name: str, t: torch.Tensor):
@@ -194,8 +213,11 @@ class Simulator:
 
     def world_outputs(self, scale, center, render_space: bool, means_out=None, cov_out=None):
         """Fused grid2world (+ render shift) of x and cov, in caller order."""
-        means_out = torch.empty((self.n, 3), dtype=torch.float32, device=self.device) if means_out is None else means_out
-        cov_out = torch.empty((self.n, 6), dtype=torch.float32, device=self.device) if cov_out is None else cov_out
+        n = self.count
+        means_out = torch.empty((n, 3), dtype=torch.float32, device=self.device) if means_out is None else means_out
+        cov_out = torch.empty((n, 6), dtype=torch.float32, device=self.device) if cov_out is None else cov_out
+        if n == 0:
+            return means_out, cov_out
         c = (ctypes.c_float * 3)(*[float(a) for a in center])
         check(LIB.gsmpm_mpm_world_outputs(self._h, ctypes.c_float(float(scale)), c, int(bool(render_space)),
                                           ptr(means_out), ptr(cov_out), stream_of(self.device)), "world_outputs")

@@ -44,7 +44,7 @@ typedef struct gsmpm_mpm gsmpm_mpm;
 #define GSMPM_FLAG_NO_GRAPH 4u    /* launch substeps eagerly instead of through a cached hipGraph */
 #define GSMPM_FLAG_NO_SORT 8u     /* keep particles in input order (no spatial sort) */
 #define GSMPM_FLAG_PHASED 16u     /* per-phase substep (P2G, grid, G2P, binning: 4 launches) instead of the
-                                     fused G2P2G pipeline (2 launches); also implied by KEEP_GRID and slabs */
+                                     fused G2P2G pipeline (2 launches); also implied by KEEP_GRID */
 
 /* substep pipelines (gsmpm_mpm_pipeline) */
 #define GSMPM_PIPE_PHASED 0
@@ -91,21 +91,67 @@ int gsmpm_mpm_add_plane_collider(gsmpm_mpm* h, const double point[3], const doub
  * all active.  Asynchronous on `stream`. */
 int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t n_substeps, const uint32_t* bc_active, void* stream);
 
-/* Multi-GPU slab (driver gsmpm/dist.py, no reference counterpart:
- * the reference is single-GPU).  Up to two halo windows of nx planes starting
- * at planes x0[w] (tile-aligned): after P2G, gsmpm_mpm_substep_begin writes
- * this rank's partial (m, m v) of every window node to part[n][nx][n_grid^2][4];
- * the caller sums the partials of the ranks sharing the window into
- * sum[n][nx][n_grid^2][4] (RCCL/gloo send-recv), then gsmpm_mpm_substep_end
- * runs the grid update with those sums, G2P and the binning.  Particles must
- * stay within planes [allow_lo, allow_hi) (own slab + windows): a touched tile
- * outside sets the flag read by gsmpm_mpm_halo_status.  n_windows = 0 turns
- * the slab mode off.  part / sum are caller-owned device buffers. */
-int gsmpm_mpm_set_halo(gsmpm_mpm* h, int32_t n_windows, const int32_t* x0, int32_t nx, float* part, const float* sum,
-                       int32_t allow_lo, int32_t allow_hi);
-int gsmpm_mpm_substep_begin(gsmpm_mpm* h, float dt, uint32_t bc_active, void* stream);
-int gsmpm_mpm_substep_end(gsmpm_mpm* h, float dt, uint32_t bc_active, void* stream);
-int gsmpm_mpm_halo_status(gsmpm_mpm* h, int32_t* escaped, void* stream);
+/* ------------------------------------------------- multi-GPU slabs ---
+ * SURVEY 8(e); no reference counterpart (the reference is one device,
+ * main.py:28): the substep of mpm_solver/solver.py:27-52 sharded by spatial
+ * slab along grid axis 0, one rank per GPU (csrc/slab.h, gsmpm/dist.py).
+ *
+ * A transport moves the boundary-node partial sums (every substep) and the
+ * migrating particles (every `interval` substeps) between neighbouring ranks:
+ *   GSMPM_XPORT_RCCL      comm is an ncclComm_t (gsmpm_rccl_comm_init):
+ *                         grouped ncclSend/ncclRecv with ranks r-1 / r+1 on
+ *                         a stream of the simulator's, overlapping the
+ *                         interior grid update;
+ *   GSMPM_XPORT_CALLBACK  fn(user, n, peers, send, send_bytes, recv,
+ *                         recv_bytes) is called on the host after the stream
+ *                         is synchronised, with pinned HOST copies of the
+ *                         buffers (tests: gloo, several ranks on one GPU).
+ * Both sides of every pair post the same sizes in the same order. */
+#define GSMPM_XPORT_NONE 0
+#define GSMPM_XPORT_RCCL 1
+#define GSMPM_XPORT_CALLBACK 2
+typedef int (*gsmpm_exchange_fn)(void* user, int32_t n, const int32_t* peers, void* const* send,
+                                 const size_t* send_bytes, void* const* recv, const size_t* recv_bytes);
+typedef struct {
+  int32_t kind;          /* GSMPM_XPORT_* */
+  int32_t rank, world;
+  void* comm;            /* ncclComm_t (RCCL) */
+  gsmpm_exchange_fn fn;  /* CALLBACK */
+  void* user;
+} gsmpm_transport;
+
+/* RCCL communicator for the slab exchange (ncclGetUniqueId / ncclCommInitRank
+ * of the RCCL already loaded in the process, dlopen'ed -- torch's when torch
+ * is imported).  id is 128 bytes: rank 0 creates it, every rank receives it
+ * (e.g. torch.distributed broadcast) and calls comm_init on its own GPU. */
+int gsmpm_rccl_unique_id(uint8_t id[128]);
+int gsmpm_rccl_comm_init(const uint8_t id[128], int32_t rank, int32_t world, void** comm);
+int gsmpm_rccl_comm_destroy(void* comm);
+
+/* Make `h` (created with n_particles = this rank's particle CAPACITY) rank
+ * `rank` of a `world`-slab domain owning grid planes [lo, hi) of axis 0;
+ * particles may drift `margin` planes between migrations, which happen every
+ * `interval` substeps inside gsmpm_mpm_slab_step.  Call before
+ * gsmpm_mpm_slab_set_particles.  Neighbouring slabs must be >= 2*margin+2
+ * planes thick. */
+int gsmpm_mpm_slab_init(gsmpm_mpm* h, int32_t rank, int32_t world, int32_t lo, int32_t hi, int32_t margin,
+                        int32_t interval);
+/* This rank's initial particles (n <= capacity) with their global ids
+ * (device int32[n]); otherwise as gsmpm_mpm_set_particles. */
+int gsmpm_mpm_slab_set_particles(gsmpm_mpm* h, int32_t n, const float* x, const float* cov6, const float* vol,
+                                 const float* v_or_null, const int32_t* gid, void* stream);
+/* n_substeps substeps of the slab (bc masks as gsmpm_mpm_step), window
+ * exchange every substep and particle migration every `interval` substeps
+ * through `xp`.  Returns GSMPM_ESTATE if a particle drifted past the margin
+ * (its contributions were not exchanged: the state is invalid). */
+int gsmpm_mpm_slab_step(gsmpm_mpm* h, float dt, int32_t n_substeps, const uint32_t* bc_active_mask,
+                        const gsmpm_transport* xp, void* stream);
+/* current particle count of this rank (changes with migration) */
+int gsmpm_mpm_count(gsmpm_mpm* h);
+/* global ids of this rank's particles, in the order gsmpm_mpm_get returns rows */
+int gsmpm_mpm_get_gid(gsmpm_mpm* h, int32_t* out, void* stream);
+/* {migrations, particles migrated (sent), lo, hi, margin, interval, window planes, capacity} */
+int gsmpm_mpm_slab_stats(gsmpm_mpm* h, int64_t out8[8]);
 
 /* Re-sort particle storage into Morton order of the current cells now (only
  * summation order changes; rows stay in caller order).  interval >= 0 also sets

@@ -1,0 +1,106 @@
+"""Multi-GPU slabs on the HIP library (csrc/slab.h, slab_host.inc), SURVEY 8(e).
+
+Several ranks share cuda:0 (one process each, gloo + the library's CALLBACK
+transport, host-staged): the library's native sequence runs -- k_grid_f's
+window pass, the exchange, the interior pass, k_win_update, and every 10
+substeps the k_mig_* migration -- 200 substeps of a scene drifting along the
+slab axis, gathered in global order and compared with the single-domain CPU
+oracle (the same scene as tests/test_dist_slab.py).  The RCCL transport
+differs only in moving the same buffers with ncclSend/ncclRecv; its test needs
+two GPUs (RCCL refuses two ranks on one device) and is skipped otherwise.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import rel_err
+from test_dist_slab import DT, EXT, FIXED, KW, NG, STEPS, TOL, free_port, reference, scene
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu_worker(rank, world, port, out, backend, steps):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev_index = rank if backend == "nccl" else 0
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gsmpm.dist import SlabDomain, make_transport
+        x, v, cov, vol = scene()
+        xp = make_transport(rank, world, device=dev)
+        dom = SlabDomain(x, cov, vol, v=v, rank=rank, world=world, transport=xp, n_grid=NG, grid_extent=EXT,
+                         margin=2, interval=10, device=dev, jelly_fcr=True, **KW)
+        dom.add_fixed_cube(*FIXED)
+        dom.add_plane_collider([0, 0, 0.4], [0, 0, 1])
+        for s in range(0, steps, 50):  # several calls: chunks continue across calls
+            dom.step(DT, [0b11] * min(50, steps - s))
+        got = {k: dom.gather_field(k) for k in ("x", "v", "C", "F_trial")}
+        dom.postprocess()
+        got["cov"] = dom.gather_field("cov")
+        st = dom.stats()
+        mig = torch.tensor([st["migrated"]], dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(mig)
+        if rank == 0:
+            np.savez(os.path.join(out, "res.npz"), migrated=int(mig.item()), bounds=np.array(dom.bounds),
+                     **{k: g.cpu().numpy() for k, g in got.items()})
+        xp.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(world, tmp_path, backend="gloo", steps=STEPS):
+    mp.spawn(_gpu_worker, args=(world, free_port(), str(tmp_path), backend, steps), nprocs=world, join=True)
+    return np.load(os.path.join(tmp_path, "res.npz"))
+
+
+def _check(r, steps=STEPS):
+    x, v, cov, vol = scene()
+    ref = reference(x, v, cov, vol, steps)
+    errs = {k: rel_err(r[k], getattr(ref, k)) for k in TOL}
+    ref.postprocess()
+    errs["cov"] = rel_err(r["cov"], ref.cov)
+    for k, e in errs.items():
+        assert e < TOL.get(k, 1e-4), (k, e, errs)
+    return errs
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_gpu_slabs_match_single_domain_oracle(dev, tmp_path, world):
+    r = _run(world, tmp_path)
+    if world > 1:
+        assert int(r["migrated"]) > 50  # particles crossed slab bounds and migrated
+    errs = _check(r)
+    print("slab", world, errs, "migrated", int(r["migrated"]), "bounds", r["bounds"].tolist())
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="RCCL needs one GPU per rank")
+def test_gpu_slabs_rccl_two_gpus(dev, tmp_path):
+    r = _run(2, tmp_path, backend="nccl")
+    assert int(r["migrated"]) > 50
+    _check(r)
+
+
+def test_slab_refuses_thin_slab_and_plain_step(dev):
+    from gsmpm._lib import GsmpmError
+    from gsmpm.sim import Simulator
+    sim = Simulator(1000, n_grid=NG, grid_extent=EXT, **KW)
+    with pytest.raises(GsmpmError):
+        sim.slab_init(1, 3, 10, 14, margin=2, interval=10)  # 4 planes < 2 * 2 + 2
+    sim.slab_init(0, 2, 0, 32, margin=2, interval=10)
+    x, v, cov, vol = scene(500)
+    t = lambda a: torch.from_numpy(a).to(dev)
+    sim.slab_set_particles(t(x), t(cov), t(vol), torch.arange(500, dtype=torch.int32, device=dev), v=t(v))
+    with pytest.raises(GsmpmError):
+        sim.step(DT, [1])  # a slab steps through gsmpm_mpm_slab_step only
+    with pytest.raises(GsmpmError):
+        sim.slab_step(DT, [1], None)  # rank 0 of 2 has a neighbour: no transport, no step

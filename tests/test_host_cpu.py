@@ -36,7 +36,7 @@ def test_header_declares_the_boundary():
     for must in ("gsmpm_mpm_create", "gsmpm_mpm_set_particles", "gsmpm_mpm_step", "gsmpm_mpm_postprocess",
                  "gsmpm_mpm_get", "gsmpm_mpm_add_fixed_cube", "gsmpm_mpm_add_impulse",
                  "gsmpm_mpm_add_plane_collider", "gsmpm_raster_forward", "gsmpm_particle_volume",
-                 "gsmpm_mpm_set_halo", "gsmpm_last_error"):
+                 "gsmpm_mpm_slab_init", "gsmpm_mpm_slab_step", "gsmpm_rccl_comm_init", "gsmpm_last_error"):
         assert must in names
 
 
