@@ -490,6 +490,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline(scene, args, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if xp is not None:
+        xp.close()
     if world > 1:
         dist.destroy_process_group()
 

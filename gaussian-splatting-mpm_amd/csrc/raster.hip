@@ -657,6 +657,21 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// Test mode (GSMPM_RASTER_POISON=1): every listed pair's record set to NaN
+// before k_render_bwd, which must overwrite each one (a record left unwritten
+// would otherwise hold whatever the reused buffer held -- the round-1
+// 5.98e25 means3D gradients); culled pairs keep the zeros of the memset.
+__global__ __launch_bounds__(256) void k_poison_listed(const uint2* __restrict__ ranges,
+                                                       const unsigned* __restrict__ pos_sorted,
+                                                       float4* __restrict__ rec) {
+  const uint2 r = ranges[blockIdx.x];
+  const float nan = __int_as_float(0x7fc00000);
+  for (unsigned k = r.x + threadIdx.x; k < r.y; k += 256) {
+    float4* p = rec + (size_t)pos_sorted[k] * 3;
+    p[0] = p[1] = p[2] = make_float4(nan, nan, nan, nan);
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_render_bwd(const uint2* __restrict__ ranges,
                                                        const unsigned* __restrict__ pos_sorted,
                                                        const unsigned* __restrict__ ids, int W, int H, int gx,
@@ -1374,6 +1389,12 @@ int gsmpm_raster_backward(gsmpm_raster* r, const gsmpm_raster_args* in, const in
     r->slots_pending = false;
   }
   if (K > 0 && r->emit_culled) GSMPM_HIP(hipMemsetAsync(r->rec, 0, K * 3 * sizeof(float4), st));
+  const char* poison = std::getenv("GSMPM_RASTER_POISON");
+  if (K > 0 && poison && poison[0] == '1') {
+    hipLaunchKernelGGL(k_poison_listed, dim3(r->gx * r->gy), dim3(256), 0, st, (const uint2*)r->ranges,
+                       (const unsigned*)r->vals_sorted, r->rec);
+    GSMPM_LAUNCH_CHECK();
+  }
   if (K > 0)
     hipLaunchKernelGGL(k_render_bwd, dim3(r->gx, r->gy), dim3(kBlock), 0, st, r->ranges, r->vals_sorted,
                        r->ids_sorted, a.W, a.H, r->gx, r->xy, r->conic, r->rgb, in->bg, r->final_T, r->n_contrib,

@@ -98,8 +98,9 @@ class Simulator:
     def slab_init(self, rank: int, world: int, lo: int, hi: int, margin: int = 2, interval: int = 10):
         """Make this simulator (created with n_particles = capacity) rank `rank`
         of a `world`-slab domain owning grid planes [lo, hi) (csrc/slab.h)."""
-        check(LIB.gsmpm_mpm_slab_init(self._h, int(rank), int(world), int(lo), int(hi), int(margin), int(interval)),
-              "gsmpm_mpm_slab_init")
+        with torch.cuda.device(self.device):  # the slab's comm stream / buffers live on this device
+            check(LIB.gsmpm_mpm_slab_init(self._h, int(rank), int(world), int(lo), int(hi), int(margin),
+                                          int(interval)), "gsmpm_mpm_slab_init")
 
     def slab_set_particles(self, x, cov6, vol, gid, v=None):
         f = lambda t: None if t is None else t.detach().to(self.device, torch.float32).contiguous()
@@ -121,8 +122,9 @@ class Simulator:
             return
         arr = (ctypes.c_uint32 * n)(*[int(m) & 0xFFFFFFFF for m in masks])
         xp = None if transport is None else ctypes.byref(transport.struct)
-        check(LIB.gsmpm_mpm_slab_step(self._h, ctypes.c_float(dt), n, arr, xp, stream_of(self.device)),
-              "gsmpm_mpm_slab_step")
+        with torch.cuda.device(self.device):
+            check(LIB.gsmpm_mpm_slab_step(self._h, ctypes.c_float(dt), n, arr, xp, stream_of(self.device)),
+                  "gsmpm_mpm_slab_step")
 
     @property
     def count(self) -> int:
