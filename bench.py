@@ -336,14 +336,39 @@ def main():
 
     host_t = [] if os.environ.get("GSMPM_BENCH_HOST_TIMING") else None  # per-call host time (diagnostic)
 
-    def frame(render=True):
+    # Frames are pipelined as main.py's loop allows: frame f's render-space
+    # snapshot (world_outputs) is taken on the simulator's stream, then the
+    # render of frame f - 1 runs on a second stream while frame f simulates
+    # (the rasterizer's pair-count read-back waits on the host for frame f - 1
+    # only).  Every timed step still simulates AND renders one frame: the
+    # timed region ends with the last frame's render.
+    render_stream = torch.cuda.Stream(dev)
+    pending = []
+
+    def render(item):
+        means_r, covs_r, ev = item
+        if means_r is None or args.no_render:
+            return
+        with torch.cuda.stream(render_stream):
+            render_stream.wait_event(ev)
+            K, _, _ = raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg,
+                                     cam.height, cam.width, tanx, tany, sh_degree=3, shs=feats, cov3D_precomp=covs_r)
+        means_r.record_stream(render_stream)  # allocated on the simulator's stream
+        covs_r.record_stream(render_stream)
+        state["K"] = K
+
+    def flush():
+        while pending:
+            render(pending.pop(0))
+
+    def frame(render_frame=True):
         t = [time.perf_counter()]
         masks, state["t"] = substep_masks(specs, state["t"], dt, spf)
         sim.step(dt, masks)
         t.append(time.perf_counter())
         sim.postprocess()
         t.append(time.perf_counter())
-        if render and not args.no_render:
+        if render_frame and not args.no_render:
             # slabs: every particle's render-space mean/cov gathered to rank 0, which
             # renders the frame (compositing order is view-dependent);
             # --dp / one GPU: every rank renders its own scene
@@ -351,12 +376,11 @@ def main():
                 means_r, covs_r = sim.gather_world(w_scale, w_center, render_space=True)
             else:
                 means_r, covs_r = sim.world_outputs(w_scale, w_center, render_space=True)
+            ev = torch.cuda.Event()
+            ev.record()
             t.append(time.perf_counter())
-            if means_r is not None:
-                K, _, _ = raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg,
-                                         cam.height, cam.width, tanx, tany, sh_degree=3, shs=feats,
-                                         cov3D_precomp=covs_r)
-                state["K"] = K
+            flush()  # the previous frame renders while this one simulates
+            pending.append((means_r, covs_r, ev))
             t.append(time.perf_counter())
         if host_t is not None:
             host_t.append([1e6 * (b - a) for a, b in zip(t, t[1:])])
@@ -368,14 +392,16 @@ def main():
 
     for _ in range(args.warmup):
         frame()
+    flush()
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         frame()
+    flush()
     barrier()
     elapsed = time.perf_counter() - t0
     if host_t:
-        print("host us per call (step, postprocess, world_outputs, raster.forward):",
+        print("host us per call (step, postprocess, world_outputs, render of the previous frame):",
               [round(sum(c) / len(host_t[-args.steps:]), 1) for c in zip(*host_t[-args.steps:])], file=sys.stderr)
     if world > 1:
         tt = torch.tensor([elapsed], device=red_dev, dtype=torch.float64)

@@ -129,7 +129,32 @@ struct Touch {
   int4* chunk;
   int* cbox;    // [max_chunks] stencil box of the chunk's last P2G (packed, window coordinates)
   int* tbox;    // [ntiles] the same per tile (the full window when the tile has several chunks)
+  unsigned char* perm;  // [max_chunks][256] lane -> particle of the chunk (lane balance, below); null: off
 };
+
+// Lane balance.  A wave's LDS accesses to the chunk window (G2P's ds_read_b128
+// of float4 nodes, P2G's 64-bit atomics into channel planes) are serviced in
+// lane groups of 16 whose banks follow the node index mod 16 -- and with the
+// same stencil offset added by every lane, a group is conflict-free exactly
+// when its 16 particles' base nodes are distinct mod 16.  Every P2G records,
+// per chunk, the lane assignment that puts a particle whose base node has
+// residue r on a lane L with L mod 16 = r wherever the residue counts allow
+// (the leftovers fill the remaining lanes in order); the next launch on the
+// same bins (the particles moved < 1 cell) runs its lanes through it.  Both
+// b128 and b64 lane groups hold 16 lanes of distinct L mod 16.
+__device__ __forceinline__ int balanced_lane(const int* __restrict__ rcnt, int cnt, int r, int rank) {
+  const int Lr = (cnt - r + 15) >> 4;  // lanes of residue r in [0, cnt)
+  if (rank < Lr) return rank * 16 + r;
+  int o = rank - Lr;
+  for (int q = 0; q < r; ++q) o += max(0, rcnt[q] - ((cnt - q + 15) >> 4));
+  int acc = 0;
+  for (int q = 0; q < 16; ++q) {
+    const int Lq = (cnt - q + 15) >> 4, d = max(0, Lq - rcnt[q]);
+    if (o < acc + d) return (rcnt[q] + (o - acc)) * 16 + q;
+    acc += d;
+  }
+  return rank * 16 + r;  // unreachable: overflow == deficit
+}
 
 // Stencil boxes: lo/hi window coordinates (0..11) per axis in 4-bit fields,
 // lo0 | lo1 << 4 | lo2 << 8 | hi0 << 12 | hi1 << 16 | hi2 << 20.  The P2G of
@@ -198,6 +223,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
   __shared__ float s_max[4];
   __shared__ int s_mxy[4], s_mz[4];
   __shared__ int s_cnt[27], s_base[27];
+  __shared__ int s_rcnt[16];
   float4* s_win = reinterpret_cast<float4*>(s_acc);
   const int ng = g.ng;
   constexpr int SK = MODE == 3 ? 0 : 1;  // diagnostics slot (k_p2g's / k_g2p's in the per-phase pipeline)
@@ -213,9 +239,11 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
     const int o0 = tx * kFT0 - 1, o1 = ty * kFT1 - 1, o2 = tz * kFT2 - 1;  // first window node
     int p = -1;
     float x[3] = {0.f, 0.f, 0.f}, v[3] = {0.f, 0.f, 0.f}, C[3][3], F[3][3], m = 0.f;
+    // this lane's particle: the lane balance of the last P2G on these bins (use_box), else in order
+    const int q = (use_box && tc.perm && k < cnt) ? (int)tc.perm[(size_t)w * 256 + k] : k;
     // particle loads first: their round trips overlap the window staging
     if (k < cnt) {
-      p = first + k;
+      p = first + q;
 #pragma unroll
       for (int d = 0; d < 3; ++d) x[d] = ps.ld(PX + d, p);
       if (G2P || MAT != 0) {
@@ -242,8 +270,8 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
         int dst[7];
 #pragma unroll
         for (int u = 0; u < 7; ++u) {
-          const int q = min(k + u * 256, nvol - 1);
-          const int a = (int)(((float)q + 0.5f) * r12), rem = q - a * n12;
+          const int qn = min(k + u * 256, nvol - 1);
+          const int a = (int)(((float)qn + 0.5f) * r12), rem = qn - a * n12;
           const int b = (int)(((float)rem + 0.5f) * r2), c = rem - b * n2;
           const int wa = lo[0] + a, wb = lo[1] + b, wc = lo[2] + c;
           dst[u] = (wa * kFW1 + wb) * kFW2 + wc;
@@ -337,7 +365,8 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
     }
     if constexpr (P2G) {
       if (!outside)
-        for (int q = k; q < kFWin * 4; q += 256) s_acc[q] = 0ull;
+        for (int e = k; e < kFWin * 4; e += 256) s_acc[e] = 0ull;
+      if (k < 16) s_rcnt[k] = 0;
       float nvt[3][3];
 #pragma unroll
       for (int i = 0; i < 9; ++i) nvt[i / 3][i % 3] = 0.f;
@@ -413,6 +442,9 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
         s_mz[k >> 6] = mz;
       }
       __syncthreads();  // also orders the zeroing before the adds
+      // lane balance for the next launch: this particle's rank among those of its base-node residue
+      const int res = win ? (((b[0] - o0) * kFW1 + (b[1] - o1)) * kFW2 + (b[2] - o2)) & 15 : (q & 15);
+      const int rrank = (tc.perm && k < cnt) ? atomicAdd(&s_rcnt[res], 1) : 0;
       const float bmax = fmaxf(fmaxf(s_max[0], s_max[1]), fmaxf(s_max[2], s_max[3]));
       const int Mxy = s_mxy[0] | s_mxy[1] | s_mxy[2] | s_mxy[3], Mz = s_mz[0] | s_mz[1] | s_mz[2] | s_mz[3];
       const int Mx = Mxy & 0xffff, My = (unsigned)Mxy >> 16;
@@ -451,6 +483,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
       }
       __syncthreads();
       if (w == (int)blockIdx.x) stamp(SK, 4);
+      if (tc.perm && k < cnt) tc.perm[(size_t)w * 256 + balanced_lane(s_rcnt, cnt, res, rrank)] = (unsigned char)q;
       {
         int lo[3], hi[3];
         box_unpack(box, lo, hi);
@@ -458,8 +491,8 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
         const int nvol = (hi[0] - lo[0] + 1) * n12;
         const float r12 = 1.0f / (float)n12, r2 = 1.0f / (float)n2;
         float4* dst = slots + (size_t)w * kFWin;
-        for (int q = k; q < nvol; q += 256) {
-          const int a = (int)(((float)q + 0.5f) * r12), rem = q - a * n12;
+        for (int qn = k; qn < nvol; qn += 256) {
+          const int a = (int)(((float)qn + 0.5f) * r12), rem = qn - a * n12;
           const int bq = (int)(((float)rem + 0.5f) * r2), c = rem - bq * n2;
           const int node = ((lo[0] + a) * kFW1 + lo[1] + bq) * kFW2 + lo[2] + c;
           float4 r;

@@ -1342,6 +1342,8 @@ struct gsmpm_mpm {
   int* fesc = nullptr;                    // [2] escape flags (alternating per grid update)
   int* fcbox[2] = {nullptr, nullptr};     // [max_chunks] per-chunk stencil boxes (fused.h)
   int* ftbox[2] = {nullptr, nullptr};     // [ntiles] per-tile stencil boxes
+  unsigned char* fperm[2] = {nullptr, nullptr};  // [max_chunks][256] lane balance (fused.h); null: off
+  bool lane_balance = true;               // GSMPM_LANE_BALANCE=0 turns it off (A/B)
   float* planes_alt = nullptr;            // the other particle-plane buffer: every binning permutes
   int* orig_alt = nullptr;                //   storage into bin order, alternating planes / planes_alt
   int fbpar = 0;                          // parity of the bins the next k_fused reads
@@ -1407,7 +1409,8 @@ static ChunkOut chunk_out_f(gsmpm_mpm* h, int c) {
   return ChunkOut{h->fcstart[c], h->fcbase[c], h->fchunk[c], h->fnchunk[c], h->ftflag[c], h->ftouched[c]};
 }
 static Touch touch_f(gsmpm_mpm* h, int c) {
-  return Touch{h->ftflag[c], h->ftouched[c], h->fnchunk[c], h->fchunk[c], h->fcbox[c], h->ftbox[c]};
+  return Touch{h->ftflag[c], h->ftouched[c], h->fnchunk[c], h->fchunk[c], h->fcbox[c], h->ftbox[c],
+               h->lane_balance ? h->fperm[c] : nullptr};
 }
 static BinOutF bin_out_f(gsmpm_mpm* h, int c) { return BinOutF{h->fcount[c], h->ptile, h->pslot, h->ftflag[c], h->ftl}; }
 // k_finish_bins / the scan kernels only use ntiles and max_chunks of a Tiles
@@ -1827,6 +1830,7 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
   }
   // fused pipeline: 8 x 8 x 7-cell tiles (fused.h)
   h->fused = !(prm->flags & (GSMPM_FLAG_PHASED | GSMPM_FLAG_KEEP_GRID));
+  if (const char* lb = std::getenv("GSMPM_LANE_BALANCE")) h->lane_balance = lb[0] != '0';
   h->ftl.td0 = (h->g.ng + kFT0 - 1) / kFT0;
   h->ftl.td1 = (h->g.ng + kFT1 - 1) / kFT1;
   h->ftl.td2 = (h->g.ng + kFT2 - 1) / kFT2;
@@ -1854,6 +1858,8 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
         return fail(e, "hipMalloc boxes");
       if ((e = hipMalloc(&h->ftbox[c], sizeof(int) * (size_t)h->ftl.ntiles)) != hipSuccess)
         return fail(e, "hipMalloc boxes");
+      if ((e = hipMalloc(&h->fperm[c], (size_t)h->ftl.max_chunks * 256)) != hipSuccess)
+        return fail(e, "hipMalloc lane balance");
       if ((e = hipMemset(h->fcount[c], 0, sizeof(int) * E)) != hipSuccess) return fail(e, "hipMemset");
       if ((e = hipMemset(h->ftflag[c], 0, sizeof(int) * (size_t)h->ftl.ntiles)) != hipSuccess) return fail(e, "hipMemset");
       if ((e = hipMemset(h->fnchunk[c], 0, sizeof(int) * 2)) != hipSuccess) return fail(e, "hipMemset");
@@ -1916,6 +1922,7 @@ int gsmpm_mpm_destroy(gsmpm_mpm* h) {
     (void)hipFree(h->flist[c]);
     (void)hipFree(h->fcbox[c]);
     (void)hipFree(h->ftbox[c]);
+    (void)hipFree(h->fperm[c]);
   }
   (void)hipFree(h->fslots);
   (void)hipFree(h->fesc);
