@@ -516,8 +516,9 @@ def main():
         out["cpu_baseline"] = cpu_baseline(scene, args, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if xp is not None:
-        xp.close()
+    # the slab transport's RCCL communicator is left to process exit: captured
+    # chunk graphs still reference it (ncclCommDestroy behind a live graph
+    # that used the communicator blocked in tools/probe/rccl_graph_probe.cpp)
     if world > 1:
         dist.destroy_process_group()
 

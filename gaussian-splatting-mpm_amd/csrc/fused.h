@@ -229,8 +229,16 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
   constexpr int SK = MODE == 3 ? 0 : 1;  // diagnostics slot (k_p2g's / k_g2p's in the per-phase pipeline)
   stamp(SK, 0);
   const int nch = ck.nchunk[0];
+  // the first chunk's record, box and lane order are requested with the chunk
+  // count (clamped: a workgroup past the last chunk discards them), which
+  // takes one dependent round trip off every workgroup's chain
+  const int w0 = min((int)blockIdx.x, tl.max_chunks - 1);
+  const int4 cr0 = ck.chunk[w0];
+  const int box0 = use_box ? tc.cbox[w0] : kFullBox;
+  const int q0 = (use_box && tc.perm) ? (int)tc.perm[(size_t)w0 * 256 + threadIdx.x] : (int)threadIdx.x;
   for (int w = blockIdx.x; w < nch; w += gridDim.x) {
-    const int4 cr = ck.chunk[w];
+    const bool first_chunk = w == (int)blockIdx.x;
+    const int4 cr = first_chunk ? cr0 : ck.chunk[w];
     const int t = cr.x, first = cr.y, cnt = cr.z;
     const int k = threadIdx.x;
     const bool outside = t == tl.ntiles;  // workgroup-uniform
@@ -240,7 +248,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
     int p = -1;
     float x[3] = {0.f, 0.f, 0.f}, v[3] = {0.f, 0.f, 0.f}, C[3][3], F[3][3], m = 0.f;
     // this lane's particle: the lane balance of the last P2G on these bins (use_box), else in order
-    const int q = (use_box && tc.perm && k < cnt) ? (int)tc.perm[(size_t)w * 256 + k] : k;
+    const int q = k >= cnt ? k : first_chunk ? q0 : (use_box && tc.perm) ? (int)tc.perm[(size_t)w * 256 + k] : k;
     // particle loads first: their round trips overlap the window staging
     if (k < cnt) {
       p = first + q;
@@ -262,7 +270,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
       if (!outside) {
         // the chunk's stencil box from its last P2G (particles unmoved since), else the whole window
         int lo[3], hi[3];
-        box_unpack(use_box ? tc.cbox[w] : kFullBox, lo, hi);
+        box_unpack(first_chunk ? box0 : use_box ? tc.cbox[w] : kFullBox, lo, hi);
         const int n1 = hi[1] - lo[1] + 1, n2 = hi[2] - lo[2] + 1, n12 = n1 * n2;
         const int nvol = (hi[0] - lo[0] + 1) * n12;
         const float r12 = 1.0f / (float)n12, r2 = 1.0f / (float)n2;  // exact floor for q < 2^11
@@ -616,11 +624,13 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
   const int ng = g.ng;
   const bool all = *esc_in != 0;
   const int ntouch = 2 * (all ? tl.ntiles : ck.nchunk[1]);
+  // the first touched tile requested with the count (clamped), one round trip less
+  const int T0 = ck.touched[min((int)blockIdx.x >> 1, tl.ntiles - 1)];
   __shared__ int s_c0[27], s_nc[27], s_bx[27];
   for (int wt = blockIdx.x; wt < ntouch; wt += gridDim.x) {
     const int q = threadIdx.x + (wt & 1) * kGridT;
     const int l0 = q / (kFT1 * kFT2), l1 = (q / kFT2) % kFT1, l2 = q % kFT2;
-    const int T = all ? wt >> 1 : ck.touched[wt >> 1];
+    const int T = all ? wt >> 1 : wt == (int)blockIdx.x ? T0 : ck.touched[wt >> 1];
     int ti, tj, tk;
     ftile_decode(tl, T, ti, tj, tk);
     if (sw.pass != 0 && slab_tile_in_window(sw, ti) != (sw.pass == 1)) continue;  // workgroup-uniform

@@ -1380,6 +1380,7 @@ struct gsmpm_mpm {
   hipEvent_t s_ev_pack = nullptr, s_ev_x = nullptr;
   long s_migrations = 0, s_migrated = 0;     // counters (gsmpm_mpm_slab_stats)
   long s_since = 0;                          // substeps since the last migration
+  bool s_graph = true;                       // capture RCCL chunks in hipGraphs (GSMPM_SLAB_GRAPH=0: eager)
   float* x_host = nullptr;                   // CALLBACK transport: pinned staging of the exchanged buffers
   size_t x_host_cap = 0;
 };
@@ -1760,6 +1761,77 @@ static int resort(gsmpm_mpm* h, hipStream_t st) {
 
 }  // namespace gsmpm
 
+namespace gsmpm {
+// nsub substeps through a cached hipGraph: captured once per (dt, BC masks,
+// bins / escape / buffer parities, transport) key and replayed.  A slab with
+// the RCCL transport captures its window exchanges too (grouped
+// ncclSend/ncclRecv on the comm stream, joined into the capture by events).
+static int graph_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc, hipStream_t st,
+                          const gsmpm_transport* xp) {
+  const bool fz = use_fused(h);
+  std::vector<uint32_t> key;
+  key.reserve(nsub + 9);
+  uint32_t dtb;
+  std::memcpy(&dtb, &dt, 4);
+  key.push_back(dtb);
+  key.push_back((uint32_t)nsub);
+  key.push_back((uint32_t)h->cur_box);
+  key.push_back(fz ? 1u : 0u);
+  key.push_back((uint32_t)h->fbpar);
+  key.push_back((uint32_t)h->fep);
+  key.push_back((uint32_t)h->rebin_interval);
+  key.push_back(h->planes_alt && h->planes > h->planes_alt ? 1u : 0u);  // which particle buffer is current
+  key.push_back(xp ? (uint32_t)(((uintptr_t)xp->comm >> 4) ^ (uint32_t)xp->kind) : 0u);
+  for (int s = 0; s < nsub; ++s) key.push_back(bc ? bc[s] : 0xffffffffu);
+  auto it = h->graphs.find(key);
+  if (it == h->graphs.end()) {
+    if (h->graphs.size() >= 16) drop_graphs(h);
+    hipGraph_t graph;
+    int parity = h->cur_box, bp = h->fbpar, ep = h->fep;
+    const gsmpm_mpm::FState start{bp, ep, h->planes, h->planes_alt, h->orig, h->orig_alt};
+    GSMPM_HIP(hipStreamBeginCapture(h->cap, hipStreamCaptureModeRelaxed));
+    int rc = fz ? launch_substeps_f(h, dt, nsub, bc, h->cap, bp, ep, nullptr, nullptr, xp)
+                : launch_substeps(h, dt, nsub, bc, h->cap, parity);
+    hipError_t e = hipStreamEndCapture(h->cap, &graph);
+    // capture swapped the particle buffers on the host: keep the end state for
+    // the key and start the replay below from the key's state
+    const gsmpm_mpm::FState end{bp, ep, h->planes, h->planes_alt, h->orig, h->orig_alt};
+    h->planes = start.planes;
+    h->planes_alt = start.planes_alt;
+    h->orig = start.orig;
+    h->orig_alt = start.orig_alt;
+    if (rc) {
+      if (e == hipSuccess) (void)hipGraphDestroy(graph);
+      return rc;
+    }
+    if (e != hipSuccess) {
+      set_error(std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
+      return GSMPM_EHIP;
+    }
+    hipGraphExec_t exec;
+    e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    if (e != hipSuccess) {
+      set_error(std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+      return GSMPM_EHIP;
+    }
+    it = h->graphs.emplace(key, exec).first;
+    h->graph_box_parity[key] = parity;
+    h->graph_fstate[key] = end;
+  }
+  GSMPM_HIP(hipGraphLaunch(it->second, st));
+  h->cur_box = h->graph_box_parity[key];
+  const gsmpm_mpm::FState& fs = h->graph_fstate[key];
+  h->fbpar = fs.bpar;
+  h->fep = fs.ep;
+  h->planes = fs.planes;
+  h->planes_alt = fs.planes_alt;
+  h->orig = fs.orig;
+  h->orig_alt = fs.orig_alt;
+  return GSMPM_OK;
+}
+}  // namespace gsmpm
+
 extern "C" {
 
 const char* gsmpm_last_error(void) { return g_err.c_str(); }
@@ -2085,69 +2157,14 @@ int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t nsub, const uint32_t* bc, voi
   }
   h->since_sort += nsub;
   const bool use_graph = !(h->prm.flags & GSMPM_FLAG_NO_GRAPH) && nsub >= 2;
-  const bool fz = use_fused(h);
   if (!use_graph) {
     int parity = h->cur_box;
-    int rc = fz ? launch_substeps_f(h, dt, nsub, bc, st, h->fbpar, h->fep)
-                : launch_substeps(h, dt, nsub, bc, st, parity);
+    int rc = use_fused(h) ? launch_substeps_f(h, dt, nsub, bc, st, h->fbpar, h->fep)
+                          : launch_substeps(h, dt, nsub, bc, st, parity);
     h->cur_box = parity;
     return rc;
   }
-  std::vector<uint32_t> key;
-  key.reserve(nsub + 7);
-  uint32_t dtb;
-  std::memcpy(&dtb, &dt, 4);
-  key.push_back(dtb);
-  key.push_back((uint32_t)nsub);
-  key.push_back((uint32_t)h->cur_box);
-  key.push_back(fz ? 1u : 0u);
-  key.push_back((uint32_t)h->fbpar);
-  key.push_back((uint32_t)h->fep);
-  key.push_back((uint32_t)h->rebin_interval);
-  key.push_back(h->planes_alt && h->planes > h->planes_alt ? 1u : 0u);  // which particle buffer is current
-  for (int s = 0; s < nsub; ++s) key.push_back(bc ? bc[s] : 0xffffffffu);
-  auto it = h->graphs.find(key);
-  if (it == h->graphs.end()) {
-    if (h->graphs.size() >= 16) drop_graphs(h);
-    hipGraph_t graph;
-    int parity = h->cur_box, bp = h->fbpar, ep = h->fep;
-    const gsmpm_mpm::FState start{bp, ep, h->planes, h->planes_alt, h->orig, h->orig_alt};
-    GSMPM_HIP(hipStreamBeginCapture(h->cap, hipStreamCaptureModeRelaxed));
-    int rc = fz ? launch_substeps_f(h, dt, nsub, bc, h->cap, bp, ep) : launch_substeps(h, dt, nsub, bc, h->cap, parity);
-    hipError_t e = hipStreamEndCapture(h->cap, &graph);
-    // capture swapped the particle buffers on the host: keep the end state for
-    // the key and start the replay below from the key's state
-    const gsmpm_mpm::FState end{bp, ep, h->planes, h->planes_alt, h->orig, h->orig_alt};
-    h->planes = start.planes;
-    h->planes_alt = start.planes_alt;
-    h->orig = start.orig;
-    h->orig_alt = start.orig_alt;
-    if (rc) return rc;
-    if (e != hipSuccess) {
-      set_error(std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
-      return GSMPM_EHIP;
-    }
-    hipGraphExec_t exec;
-    e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(graph);
-    if (e != hipSuccess) {
-      set_error(std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
-      return GSMPM_EHIP;
-    }
-    it = h->graphs.emplace(key, exec).first;
-    h->graph_box_parity[key] = parity;
-    h->graph_fstate[key] = end;
-  }
-  GSMPM_HIP(hipGraphLaunch(it->second, st));
-  h->cur_box = h->graph_box_parity[key];
-  const gsmpm_mpm::FState& fs = h->graph_fstate[key];
-  h->fbpar = fs.bpar;
-  h->fep = fs.ep;
-  h->planes = fs.planes;
-  h->planes_alt = fs.planes_alt;
-  h->orig = fs.orig;
-  h->orig_alt = fs.orig_alt;
-  return GSMPM_OK;
+  return graph_substeps(h, dt, nsub, bc, st, nullptr);
 }
 
 int gsmpm_mpm_set_rebin_interval(gsmpm_mpm* h, int32_t substeps) {

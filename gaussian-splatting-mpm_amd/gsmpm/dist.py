@@ -92,6 +92,10 @@ class RcclTransport:
         self.struct = _lib.Transport(_lib.XPORT_RCCL, int(rank), int(world), comm, _lib.EXCHANGE_FN(), None)
 
     def close(self):
+        """Destroy the communicator.  Every simulator that stepped with it must be
+        closed first: its captured chunk graphs hold RCCL work on the
+        communicator (ncclCommDestroy behind a live graph blocked in
+        tools/probe/rccl_graph_probe.cpp)."""
         if self.comm is not None and self.comm.value:
             check(LIB.gsmpm_rccl_comm_destroy(self.comm), "gsmpm_rccl_comm_destroy")
             self.comm = None

@@ -53,6 +53,7 @@ def _gpu_worker(rank, world, port, out, backend, steps):
         if rank == 0:
             np.savez(os.path.join(out, "res.npz"), migrated=int(mig.item()), bounds=np.array(dom.bounds),
                      **{k: g.cpu().numpy() for k, g in got.items()})
+        dom.engine.close()  # its graphs before the communicator
         xp.close()
     finally:
         dist.destroy_process_group()
