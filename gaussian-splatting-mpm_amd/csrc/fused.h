@@ -372,8 +372,10 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
       if (w == (int)blockIdx.x) stamp(SK, 3);
     }
     if constexpr (P2G) {
-      if (!outside)
-        for (int e = k; e < kFWin * 4; e += 256) s_acc[e] = 0ull;
+      if (!outside) {  // 16-byte stores: half the LDS write instructions of u64 ones
+        uint4* z = reinterpret_cast<uint4*>(s_acc);
+        for (int e = k; e < kFWin * 2; e += 256) z[e] = make_uint4(0u, 0u, 0u, 0u);
+      }
       if (k < 16) s_rcnt[k] = 0;
       float nvt[3][3];
 #pragma unroll
@@ -504,11 +506,14 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
           const int bq = (int)(((float)rem + 0.5f) * r2), c = rem - bq * n2;
           const int node = ((lo[0] + a) * kFW1 + lo[1] + bq) * kFW2 + lo[2] + c;
           float4 r;
-          r.x = (float)ldexp((double)(long long)s_acc[0 * kFWin + node], -S);
-          r.y = (float)ldexp((double)(long long)s_acc[1 * kFWin + node], -S);
-          r.z = (float)ldexp((double)(long long)s_acc[2 * kFWin + node], -S);
-          r.w = (float)ldexp((double)(long long)s_acc[3 * kFWin + node], -S);
-          dst[node] = r;
+          r.x = from_fixed32(s_acc[0 * kFWin + node], S);
+          r.y = from_fixed32(s_acc[1 * kFWin + node], S);
+          r.z = from_fixed32(s_acc[2 * kFWin + node], S);
+          r.w = from_fixed32(s_acc[3 * kFWin + node], S);
+          // write-through: a slot is read by other XCDs' grid updates, and a dirty
+          // line left in this XCD's L2 would be written back by the end-of-kernel
+          // release (k_fused 21.9 -> 18.2 us on the lego frame)
+          wt_store4(dst + node, r);
         }
       }
       __syncthreads();  // LDS reuse by the next chunk

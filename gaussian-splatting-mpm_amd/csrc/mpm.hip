@@ -261,6 +261,13 @@ __device__ __forceinline__ unsigned long long to_fixed(float v, double scale) {
   return (unsigned long long)__double_as_longlong(d) - 0x4338000000000000ull;
 }
 
+// fixed point -> f32 from the two 32-bit halves (full-rate f32 converts; the
+// f64 path rounds once, this one at most twice: <= 1 ulp)
+__device__ __forceinline__ float from_fixed32(unsigned long long a, int S) {
+  const float hi = (float)(int)(a >> 32), lo = (float)(unsigned)a;
+  return ldexpf(__builtin_fmaf(hi, 4294967296.0f, lo), -S);
+}
+
 __device__ __forceinline__ void lds_add(unsigned long long* a, unsigned long long v) {
   __hip_atomic_fetch_add(a, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }

@@ -72,7 +72,7 @@ struct Particles {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc(), i * 4, plane * np * 4, 0));
   }
   __device__ __forceinline__ void st(int plane, int i, float v) const {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rsrc(), i * 4, plane * np * 4, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rsrc(), i * 4, plane * np * 4, 2);  // nt
   }
   // cold planes, by caller row
   __device__ __forceinline__ float ldc(int plane, int row) const { return cold[(size_t)plane * np + row]; }
@@ -94,6 +94,13 @@ struct Box {
 };
 
 // -------------------------------------------------------- device helpers --
+typedef float nt_f4 __attribute__((ext_vector_type(4)));
+// write-through store (sc1): the line leaves the XCD's L2 with the store, so
+// the end-of-kernel release has no dirty line of it to write back
+__device__ __forceinline__ void wt_store4(float4* p, const float4& v) {
+  nt_f4 t = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(t) : "memory");
+}
 __device__ __forceinline__ void bspline(const float x[3], float inv_dx, int base[3], float fx[3], float w[3][3],
                                         float dw[3][3]) {
   // utils.py:92-109: base = (x*inv_dx - 0.5).cast(int) (truncation), quadratic B-spline
