@@ -38,6 +38,21 @@ cnt = b[ok, 5]
 print("  chunk sizes: mean", cnt.mean().round(1), "<=64:", (cnt <= 64).sum(), ">=200:", (cnt >= 200).sum())
 big = cnt >= 200
 print("  dur by size >=200 median", np.median(dur[ok][big]).round(2), "<64 median", np.median(dur[ok][cnt < 64]).round(2))
+# per-CU load: HW_ID (slot 6) cu_id [11:8], sh_id [12], se_id [15:13]; XCC (slot 7)
+hw = b[:, 6]; xcc = b[:, 7] & 0xf
+cu = (xcc << 8) | (((hw >> 13) & 7) << 5) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 15)
+cuk = cu[ok]; sizes = cnt.astype(np.int64); durs = dur[ok]
+u, inv = np.unique(cuk, return_inverse=True)
+load = np.bincount(inv, weights=sizes); nwg = np.bincount(inv)
+print(f"  CUs used {len(u)}; WGs per CU hist {np.bincount(nwg).tolist()}; particles per CU p50/p90/max {np.percentile(load,[50,90,100]).round(0).tolist()}")
+maxdur = np.zeros(len(u)); np.maximum.at(maxdur, inv, durs)
+for lo_, hi_ in ((0, 300), (300, 450), (450, 600), (600, 2000)):
+    m = (load >= lo_) & (load < hi_)
+    if m.any(): print(f"    CU load [{lo_},{hi_}): {m.sum()} CUs, max WG dur median {np.median(maxdur[m]):.2f} max {maxdur[m].max():.2f}")
+same = {}
+for i in np.nonzero(ok)[0]:
+    same.setdefault(int(cu[i]), []).append(int(i))
+print("  WG sets sharing a CU (sample):", list(same.values())[:8])
 # second-chunk WGs (grid-stride): count WGs whose end - start >> single chunk
 ms2 = sim.time_kernels(sa.substep_dt, masks[203], reps=20)
 print('time_kernels K/grid/bins', ms2)
