@@ -8,7 +8,11 @@ namespace gsmpm {
 
 // ---------------------------------------------------- constitutive models --
 // Material codes as template: 0 = jelly as written (zero stress),
-// 1 metal, 2 sand, 3 foam, 4 = jelly with FCR (F3 fixed).
+// 1 metal, 2 sand, 3 foam, 4 = jelly with FCR (F3 fixed), 5 = the cohesive
+// fluid of fluid_return_mapping (constitutive_models.py:142-213), which the
+// reference defines but never dispatches (utils.py:13-54 has no branch for
+// it); here it is paired with the StVK Kirchhoff stress its viscoplastic
+// sibling (material 3) uses.
 template <int MAT>
 __device__ __forceinline__ void return_map_and_stress(float (&F)[3][3], float mu, float lam, float& yld, float dt,
                                                       const MatConsts& mc, float (&tau)[3][3]) {
@@ -92,6 +96,28 @@ __device__ __forceinline__ void return_map_and_stress(float (&F)[3][3], float mu
         }
     }
   }
+  else if constexpr (MAT == 5) {
+    // fluid_return_mapping, constitutive_models.py:142-213
+    svd3(F, U, s, V);
+    float eps[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) eps[d] = logf(fmaxf(fabsf(s[d]), 0.01f));
+    const float tr = eps[0] + eps[1] + eps[2];
+    float stv[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) stv[d] = 2.0f * mu * (eps[d] - tr / 3.0f);
+    const float stn = sqrtf(stv[0] * stv[0] + stv[1] * stv[1] + stv[2] * stv[2]);
+    const float y = stn - sqrtf(2.0f / 3.0f) * yld;
+    if (y > 0.0f) {
+      const float mu_hat = mu * (s[0] * s[0] + s[1] * s[1] + s[2] * s[2]) / 3.0f;
+      const float pf = 1.0f + mc.pvisc / (2.0f * mu_hat * dt);
+      const float snn = stn - y / pf;
+      float se[3];
+#pragma unroll
+      for (int d = 0; d < 3; ++d) se[d] = expf(1.0f / (2.0f * mu) * ((snn / stn) * stv[d]) + tr / 3.0f);
+      usv(U, se, V, F);  // a true matrix product here (U @ sig_elastic @ V^T, :205)
+    }
+  }
   // Kirchhoff stress of the (returned) F, utils.py:32-52
   float T[3][3];
 #pragma unroll
@@ -100,7 +126,7 @@ __device__ __forceinline__ void return_map_and_stress(float (&F)[3][3], float mu
     for (int j = 0; j < 3; ++j) T[i][j] = 0.0f;
   if constexpr (MAT != 0) {
     svd3(F, U, s, V);
-    if constexpr (MAT == 1 || MAT == 3) {
+    if constexpr (MAT == 1 || MAT == 3 || MAT == 5) {
       // kirchoff_stress_StVK, constitutive_models.py:23-38
       float tv[3];
       float ls[3];

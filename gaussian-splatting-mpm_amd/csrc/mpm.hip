@@ -2468,7 +2468,7 @@ int gsmpm_mpm_live_box(gsmpm_mpm* h, int32_t* box6, void* stream) {
 int gsmpm_constitutive(int32_t material, const float* Ft, int32_t n, const float* mu, const float* lam, float* yld,
                        float dt, float* Fo, float* To, void* stream) {
   GSMPM_REQUIRE(Ft && mu && lam && yld && Fo && To && n >= 0, "gsmpm_constitutive: bad argument");
-  GSMPM_REQUIRE(material >= 0 && material <= 4, "gsmpm_constitutive: material must be 0..4");
+  GSMPM_REQUIRE(material >= 0 && material <= 5, "gsmpm_constitutive: material must be 0..5");
   if (n == 0) return GSMPM_OK;
   MatConsts mc;
   const double sin_phi = std::sin(25.0 / 180.0 * 3.141592653589793);
@@ -2483,7 +2483,8 @@ int gsmpm_constitutive(int32_t material, const float* Ft, int32_t n, const float
     case 1: hipLaunchKernelGGL(k_constitutive<1>, g, b, 0, st, Ft, n, mu, lam, yld, dt, mc, Fo, To); break;
     case 2: hipLaunchKernelGGL(k_constitutive<2>, g, b, 0, st, Ft, n, mu, lam, yld, dt, mc, Fo, To); break;
     case 3: hipLaunchKernelGGL(k_constitutive<3>, g, b, 0, st, Ft, n, mu, lam, yld, dt, mc, Fo, To); break;
-    default: hipLaunchKernelGGL(k_constitutive<4>, g, b, 0, st, Ft, n, mu, lam, yld, dt, mc, Fo, To); break;
+    case 4: hipLaunchKernelGGL(k_constitutive<4>, g, b, 0, st, Ft, n, mu, lam, yld, dt, mc, Fo, To); break;
+    default: hipLaunchKernelGGL(k_constitutive<5>, g, b, 0, st, Ft, n, mu, lam, yld, dt, mc, Fo, To); break;
   }
   GSMPM_LAUNCH_CHECK();
   return GSMPM_OK;

@@ -238,7 +238,9 @@ int gsmpm_svd3(const float* A, int32_t n, float* U, float* sig, float* V, void* 
 /* Constitutive step alone (compute_stress_from_F_trial, utils.py:13-54) on n
  * particles: F_trial[n*9], mu[n], lam[n], yield[n] (updated in place for
  * metal) -> F[n*9] (return-mapped), tau[n*9] (symmetrised Kirchhoff stress).
- * material: GSMPM_MAT_*, or 4 = jelly with FCR (F3 fixed).  Test entry point. */
+ * material: GSMPM_MAT_*, or 4 = jelly with FCR (F3 fixed), or 5 = the cohesive
+ * fluid of fluid_return_mapping (constitutive_models.py:142-213; defined but
+ * never dispatched by the reference) with StVK stress.  Test entry point. */
 int gsmpm_constitutive(int32_t material, const float* F_trial, int32_t n, const float* mu, const float* lam,
                        float* yield, float dt, float* F_out, float* tau_out, void* stream);
 

@@ -313,6 +313,49 @@ static void stress_fcr(const float F[9], const float U[9], const float V[9], flo
   out[0] += l; out[4] += l; out[8] += l;
 }
 
+/* fluid_return_mapping, constitutive_models.py:142-213.  Defined by the
+ * reference but dispatched nowhere (utils.py:13-54 has no branch for it); the
+ * GPU build pairs it with kirchoff_stress_StVK (as material 3), so om_fluid
+ * returns that stress too (symmetrised, utils.py:52).  Unlike :256 the
+ * product at :205 is a true matrix product U @ diag @ V^T. */
+void om_fluid(int n, const float* Ft_all, const float* mu_all, const float* lam_all, const float* yield_all,
+              float pvisc, float dt, float* Fout_all, float* tau_all) {
+  for (int p = 0; p < n; ++p) {
+    const float* Ft = Ft_all + p * 9;
+    float* Fo = Fout_all + p * 9;
+    const float mu = mu_all[p], lam = lam_all[p];
+    float U[9], V[9], sig[3];
+    om_svd3(Ft, U, sig, V);
+    float eps[3];
+    for (int d = 0; d < 3; ++d) eps[d] = logf(fmaxf_(fabsf(sig[d]), 0.01f));   /* :163-167 */
+    float tr = eps[0] + eps[1] + eps[2];
+    float eh[3];
+    for (int d = 0; d < 3; ++d) eh[d] = eps[d] - tr / 3.0f;                       /* :169 */
+    float st[3];
+    for (int d = 0; d < 3; ++d) st[d] = 2.0f * mu * eh[d];                        /* :172 */
+    float stn = sqrtf(st[0] * st[0] + st[1] * st[1] + st[2] * st[2]);
+    float yv = stn - sqrtf(2.0f / 3.0f) * yield_all[p];                           /* :177 */
+    if (yv > 0.0f) {
+      float mu_hat = mu * (sig[0] * sig[0] + sig[1] * sig[1] + sig[2] * sig[2]) / 3.0f;  /* :185 */
+      float pf = 1.0f + pvisc / (2.0f * mu_hat * dt);                            /* :186 */
+      float snn = stn - yv / pf;                                                  /* :189 */
+      float se[3];
+      for (int d = 0; d < 3; ++d) {
+        float sn = (snn / stn) * st[d];                                           /* :190 */
+        se[d] = expf((1.0f / (2.0f * mu)) * sn + tr / 3.0f);                      /* :193 */
+      }
+      diag_sandwich(U, se, V, Fo);                                                /* :205 */
+    } else {
+      memcpy(Fo, Ft, 36);                                                         /* :210 */
+    }
+    float U2[9], V2[9], s2[3], T[9];
+    om_svd3(Fo, U2, s2, V2);
+    stress_stvk(Fo, U2, V2, s2, mu, lam, T);
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) tau_all[p * 9 + i * 3 + j] = (T[i * 3 + j] + T[j * 3 + i]) / 2.0f;
+  }
+}
+
 /* compute_stress_from_F_trial, utils.py:13-54 */
 void om_stress(om_state* s, float dt) {
   const int mat = s->material;

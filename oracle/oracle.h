@@ -62,6 +62,8 @@ void om_svd3(const float A[9], float U[9], float sig[3], float V[9]);
 void om_mu_lam(int n, const float* logE, const float* y, float* mu, float* lam);
 void om_particle_volume(int n, const float* x, int ng, float grid_dx, int32_t* count_grid, float* vol);
 void om_stress(om_state* s, float dt);
+void om_fluid(int n, const float* F_trial, const float* mu, const float* lam, const float* yield, float pvisc, float dt,
+              float* F_out, float* tau_out);
 void om_p2g(om_state* s, float dt);
 void om_grid_normalize(om_state* s, float dt);
 void om_grid_ops(om_state* s, int n_ops, const om_gridop* ops, const int32_t* active);

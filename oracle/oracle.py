@@ -105,6 +105,20 @@ def svd3(A):
 MATERIALS = {"jelly": 0, "metal": 1, "sand": 2, "foam": 3}
 
 
+def fluid_return_mapping(F_trial, mu, lam, yield_stress, dt, plastic_viscosity=0.008):
+    """fluid_return_mapping (constitutive_models.py:142-213) on n particles,
+    plus the StVK Kirchhoff stress of the returned F the GPU build pairs it
+    with (symmetrised).  The reference never dispatches it (utils.py:13-54)."""
+    F = np.ascontiguousarray(F_trial, np.float32).reshape(-1, 9)
+    n = F.shape[0]
+    a = lambda v: np.ascontiguousarray(np.broadcast_to(np.asarray(v, np.float32), (n,)))
+    mu, lam, y = a(mu), a(lam), a(yield_stress)
+    Fo = np.zeros_like(F); tau = np.zeros_like(F)
+    lib().om_fluid(ctypes.c_int(n), _p(F), _p(mu), _p(lam), _p(y), ctypes.c_float(plastic_viscosity),
+                   ctypes.c_float(dt), _p(Fo), _p(tau))
+    return Fo.reshape(n, 3, 3), tau.reshape(n, 3, 3)
+
+
 def mu_lam(E: float, nu: float, n: int):
     """model.py:42-44 (host f64 -> f32 storage) + utils.py:349-362 (device f32)."""
     logE = np.full(n, math.log10(E), np.float32)

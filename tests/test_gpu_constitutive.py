@@ -74,3 +74,29 @@ def test_constitutive_vs_oracle(dev, code, material, quirk):
     assert rel_err(Fg, Fo) < 1e-4
     assert rel_err(Tg, To) < 1e-4
     assert rel_err(yy, yo) < 1e-4
+
+
+@pytest.mark.parametrize("yld", [0.005, 1e9])
+def test_fluid_return_mapping_vs_oracle(dev, yld):
+    """gsmpm_constitutive material 5: fluid_return_mapping
+    (constitutive_models.py:142-213, never dispatched by the reference) + StVK
+    stress, against oracle/mpm_oracle.c:om_fluid; plastic and elastic branches."""
+    import torch
+    from gsmpm._lib import LIB, check, ptr, stream_of
+    rng = np.random.default_rng(5)
+    n = 5000
+    Q, _ = np.linalg.qr(rng.standard_normal((n, 3, 3)))
+    st = np.stack([rng.uniform(1.1, 1.3, n), rng.uniform(0.9, 1.05, n), rng.uniform(0.7, 0.85, n)], 1)
+    F = (Q * st[:, None, :] @ np.linalg.qr(rng.standard_normal((n, 3, 3)))[0]).astype(np.float32)
+    F *= np.sign(np.linalg.det(F))[:, None, None]
+    mu = np.full(n, 8.3e4, np.float32)
+    lam = np.full(n, 5.6e4, np.float32)
+    y = np.full(n, yld, np.float32)
+    dt = 1e-4
+    Fo, To = O.fluid_return_mapping(F, mu, lam, y, dt, 0.008)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    Ft, ymu, ylam, yy = t(F.reshape(n, 9)), t(mu), t(lam), t(y)
+    Fg, Tg = torch.empty_like(Ft), torch.empty_like(Ft)
+    check(LIB.gsmpm_constitutive(5, ptr(Ft), n, ptr(ymu), ptr(ylam), ptr(yy), dt, ptr(Fg), ptr(Tg), stream_of(dev)))
+    assert rel_err(Fg.cpu().numpy(), Fo.reshape(n, 9)) < 1e-4
+    assert rel_err(Tg.cpu().numpy(), To.reshape(n, 9)) < 1e-4

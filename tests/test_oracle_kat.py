@@ -229,3 +229,43 @@ def test_raster_depth_order_composite():
     # pixel 15 is 0.5 px from centre: alpha = o * exp(-0.5*conic*d^2) ~ o (within 1e-4)
     assert px[1] == pytest.approx(0.6, abs=2e-3)
     assert px[0] == pytest.approx(0.5 * 0.4, abs=2e-3)
+
+
+def test_fluid_return_mapping_known_answers():
+    """fluid_return_mapping (constitutive_models.py:142-213), from its own
+    algebra in float64: below the yield surface F_trial comes back unchanged;
+    above it the returned F keeps F_trial's singular vectors and the volumetric
+    log-strain, and its deviatoric Kirchhoff norm is s_trial - yield_value /
+    plastic_factor.  The StVK stress it is paired with is symmetric."""
+    rng = np.random.default_rng(11)
+    n, mu, lam, dt, pv = 400, 8.3e4, 5.6e4, 1e-4, 0.008
+    Q1 = np.linalg.qr(rng.standard_normal((n, 3, 3)))[0]
+    Q2 = np.linalg.qr(rng.standard_normal((n, 3, 3)))[0]
+    s = np.stack([rng.uniform(1.15, 1.3, n), rng.uniform(0.95, 1.05, n), rng.uniform(0.7, 0.85, n)], 1)
+    F = (Q1 * s[:, None, :]) @ Q2.transpose(0, 2, 1)
+    F *= np.sign(np.linalg.det(F))[:, None, None]
+    F = F.astype(np.float32)
+    # elastic: a yield stress far above any trial deviatoric stress
+    Fo, tau = O.fluid_return_mapping(F, mu, lam, 1e9, dt, pv)
+    assert np.array_equal(Fo, F)
+    assert np.abs(tau - tau.transpose(0, 2, 1)).max() == 0.0
+    # plastic
+    yld = 0.005
+    Fo, _ = O.fluid_return_mapping(F, mu, lam, yld, dt, pv)
+    for i in range(n):
+        U, sig, Vt = np.linalg.svd(F[i].astype(np.float64))
+        eps = np.log(np.maximum(np.abs(sig), 0.01))
+        tr = eps.sum()
+        st = 2 * mu * (eps - tr / 3)
+        stn = np.linalg.norm(st)
+        y = stn - math.sqrt(2 / 3) * yld
+        assert y > 0
+        pf = 1 + pv / (2 * mu * (sig ** 2).sum() / 3 * dt)
+        want_dev = stn - y / pf
+        so = np.linalg.svd(Fo[i].astype(np.float64), compute_uv=False)
+        eo = np.log(so)
+        assert abs(eo.sum() - tr) < 2e-5
+        assert abs(2 * mu * np.linalg.norm(eo - eo.sum() / 3) - want_dev) < 1e-4 * stn
+        # same singular vectors: U^T Fo V is diagonal
+        D = U.T @ Fo[i].astype(np.float64) @ Vt.T
+        assert np.abs(D - np.diag(np.diag(D))).max() < 2e-5
