@@ -199,3 +199,48 @@ def test_to8b_truncates():
     from utils.render_utils import to8b
     x = np.array([-1.0, 0.0, 0.5, 1 / 255, 0.999, 1.0, 7.0])
     assert to8b(x).tolist() == [0, 0, 127, 1, 254, 255, 255]  # uint8(255 * clip(x)) truncates
+
+
+def test_camera_known_answers():
+    """Hand-derived answers for the orbit camera (transform_utils.py:136-216,
+    main.py:84-106) and the projection (graphics_utils getProjectionMatrix).
+    Vertical axis z: generate_local_coord gives h1 = (1,1,0)/sqrt2 and
+    h2 = h1 x z = (1,-1,0)/sqrt2; azimuth 0 / elevation 0 puts the camera at
+    center + r h1 looking back along -h1 with its y axis along -z, so
+    R = [(-1,1,0)/sqrt2 | (0,0,-1) | (-1,-1,0)/sqrt2].  modify_cam's W2C maps
+    the view center to (0, 0, r), and its campos is the W2C translation
+    (SURVEY F8), (0, 0, r) - R^T center."""
+    import math as _m
+    import torch
+    from gaussian_splatting.utils.graphics_utils import getProjectionMatrix
+    from utils.render_utils import TinyCam
+    from utils.transform_utils import generate_local_coord, get_camera_position_and_rotation
+    import main as M
+    s2 = 1.0 / _m.sqrt(2.0)
+    v, h1, h2 = generate_local_coord(np.array([0.0, 0.0, 2.0]))
+    np.testing.assert_allclose(v, [0, 0, 1], atol=1e-15)
+    np.testing.assert_allclose(h1, [s2, s2, 0], atol=1e-15)
+    np.testing.assert_allclose(h2, [s2, -s2, 0], atol=1e-15)
+    obs = np.column_stack((h1, h2, v))
+    r = 5.75
+    pos, R = get_camera_position_and_rotation(0.0, 0.0, r, np.zeros(3), obs)
+    np.testing.assert_allclose(pos, [r * s2, r * s2, 0], atol=1e-14)
+    np.testing.assert_allclose(R, np.column_stack(([-s2, s2, 0], [0, 0, -1], [-s2, -s2, 0])), atol=1e-15)
+    pos, R = get_camera_position_and_rotation(90.0, 0.0, r, np.zeros(3), obs)
+    np.testing.assert_allclose(pos, [r * s2, -r * s2, 0], atol=1e-14)
+    # projection at 90 degrees both ways: diag(1, 1, f/(f-n)), P[2,3] = -f n/(f-n), P[3,2] = 1
+    P = getProjectionMatrix(znear=0.01, zfar=100, fovX=_m.pi / 2, fovY=_m.pi / 2).numpy()
+    n_, f_ = 0.01, 100.0
+    want = np.array([[1, 0, 0, 0], [0, 1, 0, 0], [0, 0, f_ / (f_ - n_), -f_ * n_ / (f_ - n_)], [0, 0, 1, 0]])
+    np.testing.assert_allclose(P, want, rtol=1e-6, atol=1e-7)
+    # modify_cam (azimuth 130, elevation 10, radius 5.75) around two centers
+    for center in (np.zeros(3), np.array([0.3, -0.2, 0.9])):
+        cam = TinyCam(width=64, height=48, FovX=_m.pi / 2, FovY=_m.pi / 2, cam_center=np.zeros(3, np.float32),
+                      view_mat=None, full_proj_mat=None)
+        cam = M.modify_cam(cam, center, obs, device="cpu")
+        W2C = cam.view_mat.numpy().T  # the rasterizer's transposed convention
+        pc = W2C @ np.append(center, 1.0)
+        np.testing.assert_allclose(pc[:3], [0, 0, r], atol=1e-5)
+        _, Rc = get_camera_position_and_rotation(130, 10, r, center, obs)
+        np.testing.assert_allclose(cam.cam_center, np.array([0, 0, r]) - Rc.T @ center, atol=1e-5)
+        np.testing.assert_allclose(cam.full_proj_mat.numpy(), cam.view_mat.numpy() @ want.T, rtol=1e-5, atol=1e-5)
