@@ -127,6 +127,41 @@ def save_frame(frame, save_path, fid, save_seq):
     Image.fromarray(to8b(frame)).save(os.path.join(save_path, f"{fid:04d}.png"))
 
 
+class FrameWriter:
+    """main.py:157-161 without the stalls: each rendered image is copied into a
+    pinned host buffer on the render's stream (non-blocking) and encoded to PNG
+    on a worker thread once its copy event completes, while the GPU already
+    simulates the next frame.  Same files, same frame order."""
+
+    def __init__(self, save_path, save_seq, workers=4):
+        from concurrent.futures import ThreadPoolExecutor
+        self.path, self.seq = save_path, save_seq
+        self.pool = ThreadPoolExecutor(max_workers=workers)
+        self.jobs = []
+
+    def submit(self, image, fid):
+        host = torch.empty(image.shape, dtype=image.dtype, pin_memory=True)
+        host.copy_(image, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        slot = len(self.seq)
+        self.seq.append(None)
+
+        def work():
+            ev.synchronize()
+            frame = host.numpy().transpose(1, 2, 0)
+            self.seq[slot] = frame
+            from PIL import Image
+            Image.fromarray(to8b(frame)).save(os.path.join(self.path, f"{fid:04d}.png"))
+
+        self.jobs.append(self.pool.submit(work))
+
+    def close(self):
+        for j in self.jobs:
+            j.result()
+        self.pool.shutdown()
+
+
 def simulate(model_args, sim_args, render_args):
     dev = torch.device("cuda")
     gaussians = load_model(model_args)
@@ -157,8 +192,9 @@ def simulate(model_args, sim_args, render_args):
     solver.set_boundary_conditions(sim_args.boundary_conditions, sim_args)
     solver.add_surface_collider((0.0, 0.0, 0.4), (0.0, 0.0, 1.0))
 
-    save_frame(render_frame(cam, gaussians, mask, sim_means3D, sim_covs, background, model_args, rot, pos_center),
-               out_images, 0, seq)
+    writer = FrameWriter(out_images, seq)
+    writer.submit(render_frame(cam, gaussians, mask, sim_means3D, sim_covs, background, model_args, rot, pos_center,
+                               to_host=False), 0)
     t0 = time.time()
     for fid in range(1, render_args.num_frames + 1):
         for _ in range(sim_args.steps_per_frame):
@@ -172,11 +208,13 @@ def simulate(model_args, sim_args, render_args):
                                                           gaussians._scaling, gaussians._rotation)])
             g2._xyz[mask] = sim_means3D
             g2.save_ply(os.path.join(render_args.output_path, "point_cloud", f"iteration_{fid}", "point_cloud.ply"))
-        save_frame(render_frame(cam, gaussians, mask, sim_means3D, sim_covs, background, model_args, rot, pos_center),
-                   out_images, fid, seq)
+        writer.submit(render_frame(cam, gaussians, mask, sim_means3D, sim_covs, background, model_args, rot,
+                                   pos_center, to_host=False), fid)
         if fid % 10 == 0 or fid == render_args.num_frames:
             el = time.time() - t0
             print(f"frame {fid}/{render_args.num_frames}  {fid / el:.1f} fps (sim+render+png)", flush=True)
+    writer.close()
+    print(f"{render_args.num_frames / (time.time() - t0):.1f} fps with every PNG written", flush=True)
     if render_args.save_pcd:
         for name in ("cameras.json", "cfg_args", "input.ply"):
             src = os.path.join(model_args.model_path, name)
