@@ -30,7 +30,10 @@
 // (counts + touched flags), `k_finish_bins` turns the counts into chunk
 // records, exactly as in the per-phase pipeline.
 
-constexpr int kFT0 = 8, kFT1 = 8, kFT2 = 7;                  // tile cells per axis
+#ifndef GSMPM_FT2
+#define GSMPM_FT2 7
+#endif
+constexpr int kFT0 = 8, kFT1 = 8, kFT2 = GSMPM_FT2;          // tile cells per axis
 constexpr int kFW0 = kFT0 + 4, kFW1 = kFT1 + 4, kFW2 = kFT2 + 4;  // window nodes per axis
 constexpr int kFWin = kFW0 * kFW1 * kFW2;                      // 1584
 constexpr int kFTN = kFT0 * kFT1 * kFT2;                       // owned nodes per tile (448)
@@ -274,10 +277,11 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
         const int n1 = hi[1] - lo[1] + 1, n2 = hi[2] - lo[2] + 1, n12 = n1 * n2;
         const int nvol = (hi[0] - lo[0] + 1) * n12;
         const float r12 = 1.0f / (float)n12, r2 = 1.0f / (float)n2;  // exact floor for q < 2^11
-        float4 gv[7];
-        int dst[7];
+        constexpr int kStageU = (kFWin + 255) / 256;  // window nodes per lane, at most
+        float4 gv[kStageU];
+        int dst[kStageU];
 #pragma unroll
-        for (int u = 0; u < 7; ++u) {
+        for (int u = 0; u < kStageU; ++u) {
           const int qn = min(k + u * 256, nvol - 1);
           const int a = (int)(((float)qn + 0.5f) * r12), rem = qn - a * n12;
           const int b = (int)(((float)rem + 0.5f) * r2), c = rem - b * n2;
@@ -289,7 +293,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
           if (!in) gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
-        for (int u = 0; u < 7; ++u)
+        for (int u = 0; u < kStageU; ++u)
           if (k + u * 256 < nvol) s_win[dst[u]] = gv[u];
       }
       if (k < 27) s_cnt[k] = 0;
