@@ -38,6 +38,12 @@ cnt = b[ok, 5]
 print("  chunk sizes: mean", cnt.mean().round(1), "<=64:", (cnt <= 64).sum(), ">=200:", (cnt >= 200).sum())
 big = cnt >= 200
 print("  dur by size >=200 median", np.median(dur[ok][big]).round(2), "<64 median", np.median(dur[ok][cnt < 64]).round(2))
+order = np.argsort(-dur[ok])[:12]
+print("  slowest WGs: (dur, cnt, staged, g2p, scatter, store)")
+for i in order:
+    r = b[ok][i]
+    print("   ", round(dur[ok][i], 2), int(r[5]), [round((r[c] - r[a]) / 100, 2) for a, c in ((0, 2), (2, 3), (3, 4), (4, 1))],
+          "start", round((r[0] - t0) / 100, 2))
 # per-CU load: HW_ID (slot 6) cu_id [11:8], sh_id [12], se_id [15:13]; XCC (slot 7)
 hw = b[:, 6]; xcc = b[:, 7] & 0xf
 cu = (xcc << 8) | (((hw >> 13) & 7) << 5) | (((hw >> 12) & 1) << 4) | ((hw >> 8) & 15)
