@@ -865,9 +865,19 @@ __device__ __forceinline__ void block_scan3(const int (&v)[3], int (&o)[3], int 
 // one-workgroup scan kernel followed by a scatter launch.  Workgroup b writes
 // the chunk records of its slice of tiles, then each lane places one particle.
 constexpr int kFuseTiles = 8192;
+// Permute (optional, fused pipeline): instead of the list entry, the lane's
+// particle itself moves to its bin-order row -- every hot plane and its
+// caller row (orig) -- which spares the separate k_permute launch.
+struct BinPermute {
+  const float* src;
+  float* dst;
+  int np;
+  const int* osrc;
+  int* odst;
+};
 __global__ __launch_bounds__(256) void k_finish_bins(Tiles tl, const int* __restrict__ count, ChunkOut co, int n,
                                                      const int* __restrict__ ptile, const int* __restrict__ pslot,
-                                                     int* __restrict__ list) {
+                                                     int* __restrict__ list, BinPermute bp) {
   __shared__ int s_off[kFuseTiles];  // count | touched << 31, then list offsets
   __shared__ int s_aux[kFuseTiles];  // first chunk (low 16 bits) | touched-list rank (high 16 bits)
   const int E = tl.ntiles + 1;
@@ -936,7 +946,20 @@ __global__ __launch_bounds__(256) void k_finish_bins(Tiles tl, const int* __rest
       co.chunk[cb + k] = make_int4(t, off + k * kChunk, min(kChunk, c - k * kChunk), c > kChunk ? 8 : 0);
     if (touched) co.touched[rk] = t;
   }
-  if (p < n) list[s_off[pt] + psl] = p;
+  if (p < n) {
+    const int d = s_off[pt] + psl;
+    if (bp.dst) {
+      float v[NPLANES];
+#pragma unroll
+      for (int q = 0; q < NPLANES; ++q) v[q] = bp.src[(size_t)q * bp.np + p];
+      const int o = bp.osrc[p];
+#pragma unroll
+      for (int q = 0; q < NPLANES; ++q) bp.dst[(size_t)q * bp.np + d] = v[q];
+      bp.odst[d] = o;
+    } else {
+      list[d] = p;
+    }
+  }
   stamp(2, 1);
 }
 
@@ -1351,6 +1374,7 @@ struct gsmpm_mpm {
   int* ftbox[2] = {nullptr, nullptr};     // [ntiles] per-tile stencil boxes
   unsigned char* fperm[2] = {nullptr, nullptr};  // [max_chunks][256] lane balance (fused.h); null: off
   bool lane_balance = true;               // GSMPM_LANE_BALANCE=0 turns it off (A/B)
+  bool fuse_permute = true;               // GSMPM_FUSE_PERMUTE=0: separate k_permute (A/B)
   float* planes_alt = nullptr;            // the other particle-plane buffer: every binning permutes
   int* orig_alt = nullptr;                //   storage into bin order, alternating planes / planes_alt
   int fbpar = 0;                          // parity of the bins the next k_fused reads
@@ -1446,12 +1470,14 @@ static void launch_p2g(gsmpm_mpm* h, int c, uint32_t mask, float dt, hipStream_t
 }
 
 // counts -> list offsets + chunk list, then the per-tile lists
+// fused path of the binning: tile table fits LDS, first-chunk indices fit 16 bits (s_aux)
+static bool bins_fused(const Tiles& tl) { return tl.ntiles + 1 <= kFuseTiles && tl.max_chunks < 65536; }
+// bp.dst non-null (fused path only): the particles are permuted into bin order by the same launch
 static int finish_bins_on(gsmpm_mpm* h, const Tiles& tl, const int* count, const ChunkOut& co, int* list,
-                          hipStream_t st, const hipEvent_t* ev) {
-  // fused path: tile table fits LDS, first-chunk indices fit 16 bits (s_aux)
-  if (tl.ntiles + 1 <= kFuseTiles && tl.max_chunks < 65536) {
+                          hipStream_t st, const hipEvent_t* ev, const BinPermute& bp = BinPermute{}) {
+  if (bins_fused(tl)) {
     launch(ev, k_finish_bins, dim3(std::max(1, div_up(h->n, 256))), dim3(256), st, tl, count, co, h->n, (const int*)h->ptile,
-           (const int*)h->pslot, list);
+           (const int*)h->pslot, list, bp);
   } else {
     const hipEvent_t e0[2] = {ev ? ev[0] : nullptr, nullptr}, e1[2] = {nullptr, ev ? ev[1] : nullptr};
     const int nblk = div_up(tl.ntiles + 1, 1024);
@@ -1470,10 +1496,30 @@ static int finish_binning(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t*
 static int finish_binning_f(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t* ev = nullptr) {
   return finish_bins_on(h, ftiles_flat(h), h->fcount[c], chunk_out_f(h, c), h->flist[c], st, ev);
 }
+// the binning of parity c and the storage permutation into its order: one
+// launch on the fused path (k_finish_bins moves the particles), else the
+// list kernels followed by k_permute
+static int permute_to_bins(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t* ev);
+static int rebin_permute_f(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t* ev = nullptr) {
+  if (bins_fused(ftiles_flat(h)) && h->fuse_permute) {
+    const BinPermute bp{h->planes, h->planes_alt, h->np, h->orig, h->orig_alt};
+    int rc = finish_bins_on(h, ftiles_flat(h), h->fcount[c], chunk_out_f(h, c), h->flist[c], st, ev, bp);
+    if (rc) return rc;
+    if (ev) {  // the permute's timing pair: nothing left to time
+      GSMPM_HIP(hipEventRecord(ev[2], st));
+      GSMPM_HIP(hipEventRecord(ev[3], st));
+    }
+    std::swap(h->planes, h->planes_alt);
+    std::swap(h->orig, h->orig_alt);
+    return GSMPM_OK;
+  }
+  int rc = finish_binning_f(h, c, st, ev);
+  return rc ? rc : permute_to_bins(h, c, st, ev ? ev + 2 : nullptr);
+}
 
 // Storage into the bin order of parity c (list[c]: storage rows grouped by
 // tile): planes / orig gathered into the other buffer, which becomes current.
-static int permute_to_bins(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t* ev = nullptr) {
+static int permute_to_bins(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t* ev) {
   launch(ev, k_permute, dim3(std::max(1, div_up(h->n, 256)), NPLANES + 1), dim3(256), st, (const float*)h->planes, h->planes_alt,
          h->n, h->np, (const int*)h->flist[c], (const int*)h->orig, h->orig_alt);
   GSMPM_LAUNCH_CHECK();
@@ -1491,8 +1537,7 @@ static int rebin_f(gsmpm_mpm* h, hipStream_t st) {
   GSMPM_HIP(hipMemsetAsync(h->fnchunk[c], 0, sizeof(int) * 2, st));
   hipLaunchKernelGGL(k_bin_all_f, dim3(std::max(1, div_up(h->n, 256))), dim3(256), 0, st, particles_of(h), h->g, bin_out_f(h, c));
   GSMPM_LAUNCH_CHECK();
-  int rc = finish_binning_f(h, c, st);
-  return rc ? rc : permute_to_bins(h, c, st);
+  return rebin_permute_f(h, c, st);
 }
 
 // (Re)build the per-phase pipeline's chunk lists of parity `cur_box` from the current x.
@@ -1650,8 +1695,7 @@ static int launch_substeps_f(gsmpm_mpm* h, float dt, int nsub, const uint32_t* b
     if (mode & 2) wp = bp;
     boxed = (mode & 2) && !bin;
     if (bin) {
-      rc = finish_binning_f(h, bp ^ 1, st, e8 ? e8 + 4 : nullptr);
-      if (!rc) rc = permute_to_bins(h, bp ^ 1, st, e8 ? e8 + 6 : nullptr);
+      rc = rebin_permute_f(h, bp ^ 1, st, e8 ? e8 + 4 : nullptr);
       if (rc) return rc;
       bp ^= 1;
       zeroed = false;
@@ -1910,6 +1954,7 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
   // fused pipeline: 8 x 8 x 7-cell tiles (fused.h)
   h->fused = !(prm->flags & (GSMPM_FLAG_PHASED | GSMPM_FLAG_KEEP_GRID));
   if (const char* lb = std::getenv("GSMPM_LANE_BALANCE")) h->lane_balance = lb[0] != '0';
+  if (const char* fp = std::getenv("GSMPM_FUSE_PERMUTE")) h->fuse_permute = fp[0] != '0';
   h->ftl.td0 = (h->g.ng + kFT0 - 1) / kFT0;
   h->ftl.td1 = (h->g.ng + kFT1 - 1) / kFT1;
   h->ftl.td2 = (h->g.ng + kFT2 - 1) / kFT2;
