@@ -171,10 +171,11 @@ def measured_traffic(kernel, workload):
 
 
 def cpu_baseline(scene, args, budget_s):
-    """The CPU restatement (oracle/mpm_oracle.c built with OpenMP:
-    liboracle_omp.so) on a bounded sample of the same workload -- as many lego
-    substeps at N particles / n^3 as fit in ~budget_s -- timed on this host's
-    cores (OMP_NUM_THREADS, else all cores in the affinity mask)."""
+    """The CPU restatement (oracle/mpm_oracle.c built with OpenMP at -O3
+    -ffast-math for AVX2/FMA: liboracle_fast.so, as Taichi's arch=cpu compiles
+    the reference's kernels) on a bounded sample of the same workload -- as
+    many lego substeps at N particles / n^3 as fit in ~budget_s -- timed on
+    this host's cores (OMP_NUM_THREADS, else all cores in the affinity mask)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle as O  # cpu_baseline leg only
@@ -183,8 +184,8 @@ def cpu_baseline(scene, args, budget_s):
     os.environ.setdefault("OMP_NUM_THREADS", str(len(os.sched_getaffinity(0))))
     sim = O.OracleMPM(x, scene["covs"].cpu().numpy(), scene["vols"].cpu().numpy(), n_grid=sa.n_grid,
                       grid_extent=sa.grid_extent, material=sa.material, E=sa.E, nu=sa.nu, density=sa.density,
-                      gravity=sa.gravity, jelly_quirk=not sa.jelly_fcr, threaded=True)
-    threads = int(O.lib(True).om_threads())
+                      gravity=sa.gravity, jelly_quirk=not sa.jelly_fcr, threaded="fast")
+    threads = int(O.lib("fast").om_threads())
     ops = []
     for d in sa.boundary_conditions:
         if d["type"] == "fixed_cube":
@@ -204,7 +205,8 @@ def cpu_baseline(scene, args, budget_s):
             break
     return {"value": n_done * x.shape[0] / el, "unit": "particle-substeps/s", "cores": threads, "kind": "port",
             "sample": f"first {n_done} lego substeps of the same workload ({x.shape[0]} particles, {sa.n_grid}^3, "
-                      f"same BCs), C restatement oracle/mpm_oracle.c with OpenMP ({threads} threads), {el:.1f}s",
+                      f"same BCs), C restatement oracle/mpm_oracle.c, OpenMP ({threads} threads) -O3 -ffast-math "
+                      f"-march=x86-64-v3, {el:.1f}s",
             "substeps_per_s": n_done / el}
 
 

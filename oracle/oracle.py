@@ -70,10 +70,12 @@ class _RArgs(ctypes.Structure):
                 ("tanfovx", ctypes.c_float), ("tanfovy", ctypes.c_float)]
 
 
-def lib(threaded: bool = False):
-    """Load (building if needed) liboracle.so, or with threaded=True the OpenMP
-    build liboracle_omp.so (bench.py's CPU-baseline leg only)."""
-    name = "liboracle_omp.so" if threaded else "liboracle.so"
+def lib(threaded=False):
+    """Load (building if needed) liboracle.so, with threaded=True the OpenMP
+    build liboracle_omp.so (checker of the BASELINE-size parity runs), or with
+    threaded="fast" liboracle_fast.so (OpenMP, -O3 -ffast-math, AVX2/FMA:
+    bench.py's timed CPU baseline only)."""
+    name = "liboracle_fast.so" if threaded == "fast" else ("liboracle_omp.so" if threaded else "liboracle.so")
     if name not in _LIBS:
         path = os.path.join(_HERE, name)
         if not os.path.exists(path):
