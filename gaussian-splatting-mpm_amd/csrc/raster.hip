@@ -1191,7 +1191,9 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     if ((rc = grow((void**)&r->ranges, ntiles * sizeof(uint2)))) return rc;
     r->capT = ntiles;
   }
-  GSMPM_HIP(hipMemsetAsync(r->ranges, 0, ntiles * sizeof(uint2), st));
+  // tile ranges: the chunked tile sort writes every tile's; the other paths
+  // (and K = 0) start from empty ranges
+  bool ranges_written = false;
   const size_t npix = (size_t)in->W * in->H;
   if (npix > r->capPix) {
     int rc;
@@ -1319,9 +1321,11 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
         GSMPM_LAUNCH_CHECK();
         tkeys = tile_sorted;
         r->emit_culled = cull != 0;
+        ranges_written = true;
       } else {
         GSMPM_HIP(rocprim::radix_sort_pairs<OnesweepSort>(r->sort_tmp, bytes, tile_keys, tile_sorted, r->vals,
                                                           r->ids_sorted, (size_t)K, 0, bits, st));
+        GSMPM_HIP(hipMemsetAsync(r->ranges, 0, ntiles * sizeof(uint2), st));
         hipLaunchKernelGGL(k_ranges32, dim3(div_up(K, 256)), dim3(256), 0, st, (int)K, (const unsigned*)tile_sorted,
                            0, r->ranges);
         GSMPM_LAUNCH_CHECK();
@@ -1338,10 +1342,12 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
                                         rocprim::counting_iterator<unsigned>(0u), r->vals_sorted, (size_t)K, 0,
                                         32 + bits, st));
     hipLaunchKernelGGL(k_ids, dim3(div_up(K, 256)), dim3(256), 0, st, (int)K, r->vals_sorted, r->vals, r->ids_sorted);
+    GSMPM_HIP(hipMemsetAsync(r->ranges, 0, ntiles * sizeof(uint2), st));
     hipLaunchKernelGGL(k_ranges, dim3(div_up(K, 256)), dim3(256), 0, st, (int)K, r->keys_sorted, r->ranges);
     GSMPM_LAUNCH_CHECK();
     }
   }
+  if (!ranges_written && K == 0) GSMPM_HIP(hipMemsetAsync(r->ranges, 0, ntiles * sizeof(uint2), st));
   hipLaunchKernelGGL(k_render, dim3(2 * a.grid_x, 2 * a.grid_y), dim3(64), 0, st, r->ranges, r->ids_sorted, a.W, a.H,
                      a.grid_x, r->xy, r->conic, r->rgb, in->bg, out_color, r->final_T, r->n_contrib, tkeys, render_mode);
   GSMPM_LAUNCH_CHECK();

@@ -133,7 +133,7 @@ def forward(means3D, opacities, viewmatrix, projmatrix, campos, bg, image_height
                     prefiltered)
     P = a.P
     color = torch.empty((3, image_height, image_width), dtype=torch.float32, device=dev)
-    radii = torch.zeros(P, dtype=torch.int32, device=dev)
+    radii = torch.empty(P, dtype=torch.int32, device=dev)  # k_preprocess writes every entry (0 when culled)
     nr = ctypes.c_int32(0)
     if P == 0:
         # nothing to splat: the image is the background (upstream behaviour)

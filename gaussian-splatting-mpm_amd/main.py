@@ -98,7 +98,7 @@ def modify_cam(cam: TinyCam, center_view_world_space, observant_coordinates, dev
     T = w2c[:3, 3]
     proj = getProjectionMatrix(znear=0.01, zfar=100, fovX=cam.FovX, fovY=cam.FovY).transpose(0, 1).to(device)
     cam.view_mat = torch.tensor(getWorld2View2(Rv, T, np.array([0.0, 0.0, 0.0]), 1.0)).transpose(0, 1).to(device)
-    cam.view_mat = cam.view_mat.to(torch.float32)
+    cam.view_mat = cam.view_mat.to(torch.float32).contiguous()  # once here, not per render (the rasterizer needs it dense)
     cam.cam_center = T.astype(np.float32)
     cam.full_proj_mat = (cam.view_mat.unsqueeze(0).bmm(proj.unsqueeze(0))).squeeze(0).to(torch.float32)
     return cam
