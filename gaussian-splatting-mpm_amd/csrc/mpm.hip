@@ -903,7 +903,7 @@ __global__ __launch_bounds__(256) void k_finish_bins(Tiles tl, const int* __rest
     }
   }
   __syncthreads();
-  const int per = (E + 255) / 256;
+  const int per = ((E + 255) / 256) | 1;  // odd: lane-strided LDS segments hit distinct banks
   const int t0 = min(E, threadIdx.x * per), t1 = min(E, t0 + per);
   stamp(2, 2);
   int v[3] = {0, 0, 0};
