@@ -604,15 +604,21 @@ __device__ __forceinline__ void node_extra(const float4* __restrict__ slots, con
   }
 }
 
-// Grid update of the fused pipeline: two 224-lane workgroups per touched tile
-// (x halves), one owned node per lane (all 8 window reads in flight); at <= 72
-// VGPRs seven workgroups fit a CU, so a scene's ~1000 touched tiles run in
-// one round.
+// Grid update of the fused pipeline: kGridParts one-wave workgroups per
+// touched tile (64 consecutive owned nodes each), one owned node per lane (all
+// 8 window reads in flight); a scene's ~900 touched tiles run in one round.
+// Measured (lego frame): one 448-lane workgroup per tile 17.4 us, two 224-lane
+// 12.45, four 112-lane 12.1, seven 64-lane 12.2 with k_fused unaffected
+// (sim 3.27-3.28 against 3.29-3.32 ms/frame for two).
 // esc_in: some particle scattered through gacc in the P2G this update consumes
 // -> every tile, plus gacc (re-zeroed).  esc_clear: the flag the next P2G
 // raises.  zc / zf (optional): the counts / touched flags the next binning
 // launch accumulates into.
-constexpr int kGridT = kFTN / 2;  // lanes per grid workgroup: half a tile
+#ifndef GSMPM_GRID_PARTS
+#define GSMPM_GRID_PARTS 7
+#endif
+constexpr int kGridParts = GSMPM_GRID_PARTS;  // workgroups per touched tile
+constexpr int kGridT = kFTN / kGridParts;     // lanes per grid workgroup
 __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_grid_f(GridDims g, FTiles tl, ChunkIn ck, const int* __restrict__ tbox,
                                                     const float4* __restrict__ slots, float4* __restrict__ gacc,
                                                     float4* __restrict__ gvel, const BcTable* __restrict__ bct,
@@ -632,14 +638,14 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
   }
   const int ng = g.ng;
   const bool all = *esc_in != 0;
-  const int ntouch = 2 * (all ? tl.ntiles : ck.nchunk[1]);
+  const int ntouch = kGridParts * (all ? tl.ntiles : ck.nchunk[1]);
   // the first touched tile requested with the count (clamped), one round trip less
-  const int T0 = ck.touched[min((int)blockIdx.x >> 1, tl.ntiles - 1)];
+  const int T0 = ck.touched[min((int)blockIdx.x / kGridParts, tl.ntiles - 1)];
   __shared__ int s_c0[27], s_nc[27], s_bx[27];
   for (int wt = blockIdx.x; wt < ntouch; wt += gridDim.x) {
-    const int q = threadIdx.x + (wt & 1) * kGridT;
+    const int q = threadIdx.x + (wt % kGridParts) * kGridT;
     const int l0 = q / (kFT1 * kFT2), l1 = (q / kFT2) % kFT1, l2 = q % kFT2;
-    const int T = all ? wt >> 1 : wt == (int)blockIdx.x ? T0 : ck.touched[wt >> 1];
+    const int T = all ? wt / kGridParts : wt == (int)blockIdx.x ? T0 : ck.touched[wt / kGridParts];
     int ti, tj, tk;
     ftile_decode(tl, T, ti, tj, tk);
     if (sw.pass != 0 && slab_tile_in_window(sw, ti) != (sw.pass == 1)) continue;  // workgroup-uniform

@@ -1660,7 +1660,7 @@ static int launch_fused(gsmpm_mpm* h, int mode, int c, bool bin, bool use_box, u
 static int launch_grid_f(gsmpm_mpm* h, int wp, float dt, uint32_t mask, int ep, int* zc, int* zf, hipStream_t st,
                          const hipEvent_t* ev, const SlabWin* swp = nullptr) {
   const SlabWin sw = swp ? *swp : SlabWin{};
-  launch(ev, k_grid_f, dim3(std::min(2 * h->ftl.ntiles, 2048)), dim3(kGridT), st, h->g, h->ftl, chunk_in_f(h, wp),
+  launch(ev, k_grid_f, dim3(std::min(kGridParts * h->ftl.ntiles, 1024 * kGridParts)), dim3(kGridT), st, h->g, h->ftl, chunk_in_f(h, wp),
          (const int*)h->ftbox[wp], (const float4*)h->fslots, h->gacc, h->gvel, (const BcTable*)h->dev_bc, grid_step(h, dt, mask),
          (const int*)(h->fesc + ep), h->fesc + (ep ^ 1), zc, zf, sw);
   GSMPM_LAUNCH_CHECK();

@@ -2,7 +2,7 @@
 #   bash tools/ab_libs.sh name1 name2 ...   (name "base" = libgsmpm.so, else libgsmpm_<name>.so)
 # extra bench args via BENCH_ARGS
 set -e
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
   for v in "$@"; do
     if [ "$v" = base ]; then L=$PWD/gaussian-splatting-mpm_amd/libgsmpm.so; else L=$PWD/gaussian-splatting-mpm_amd/libgsmpm_$v.so; fi
     GSMPM_LIB=$L timeout -k 10 120 python3 bench.py --no-cpu-baseline --no-extra-configs --steps 20 --warmup 3 $BENCH_ARGS > gpurun_out/ab_${v}_${rep}.json 2> gpurun_out/ab_${v}_${rep}.err
