@@ -13,13 +13,28 @@ namespace gsmpm {
 // reference defines but never dispatches (utils.py:13-54 has no branch for
 // it); here it is paired with the StVK Kirchhoff stress its viscoplastic
 // sibling (material 3) uses.
+//
+// The stress needs the SVD of the returned F (utils.py:32-52 takes a second
+// ti.svd).  Where the return map left F unchanged that is the SVD it already
+// took (the same input, so the same factors, bit for bit); where it set
+// F = U diag(se) V^T the factors are U, se, V, and the stresses below are
+// isotropic functions of F (any SVD of it gives the same U f(s) V^T), so the
+// second SVD is skipped on both branches.  The difference from a fresh SVD of
+// the rounded product is rounding-level.  Foam (material 3) forms its new F
+// element-wise, which is no SVD of anything, so its plastic lanes
+// take the second SVD.  GSMPM_SVD_REUSE=0 at build time: always two SVDs.
+#ifndef GSMPM_SVD_REUSE
+#define GSMPM_SVD_REUSE 1
+#endif
 template <int MAT>
 __device__ __forceinline__ void return_map_and_stress(float (&F)[3][3], float mu, float lam, float& yld, float dt,
                                                       const MatConsts& mc, float (&tau)[3][3]) {
   float U[3][3], V[3][3], s[3];
+  bool fresh = false;  // F changed in a way U, s, V do not describe: take its SVD
+  constexpr bool kFast = MAT != 3;  // foam's plastic F depends on the SVD basis (svd3.h)
   if constexpr (MAT == 1) {
     // von_mises_return_mapping, constitutive_models.py:62-103
-    svd3(F, U, s, V);
+    svd3<kFast>(F, U, s, V);
     float eps[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) eps[d] = logf(fmaxf(s[d], 0.01f));
@@ -43,11 +58,13 @@ __device__ __forceinline__ void return_map_and_stress(float (&F)[3][3], float mu
 #pragma unroll
       for (int d = 0; d < 3; ++d) se[d] = expf(eps[d] - (dg / ehn) * eh[d]);
       usv(U, se, V, F);
+#pragma unroll
+      for (int d = 0; d < 3; ++d) s[d] = se[d];
       if (mc.hardening == 1.0f) yld += 2.0f * mu * mc.xi * dg;
     }
   } else if constexpr (MAT == 2) {
     // sand_return_mapping, constitutive_models.py:105-140
-    svd3(F, U, s, V);
+    svd3<kFast>(F, U, s, V);
     float eps[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) eps[d] = logf(fmaxf(fabsf(s[d]), 1e-14f));
@@ -60,16 +77,20 @@ __device__ __forceinline__ void return_map_and_stress(float (&F)[3][3], float mu
     if (dg > 0.0f) {
       if (tr > 0.0f) {
         mmT(U, V, F);
+#pragma unroll
+        for (int d = 0; d < 3; ++d) s[d] = 1.0f;
       } else {
         float sn[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) sn[d] = expf(eps[d] - eh[d] * (dg / ehn));
         usv(U, sn, V, F);
+#pragma unroll
+        for (int d = 0; d < 3; ++d) s[d] = sn[d];
       }
     }
   } else if constexpr (MAT == 3) {
     // viscoplasticity_return_mapping_with_StVK, constitutive_models.py:216-259
-    svd3(F, U, s, V);
+    svd3<kFast>(F, U, s, V);
     float sg[3], eps[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
@@ -94,11 +115,12 @@ __device__ __forceinline__ void return_map_and_stress(float (&F)[3][3], float mu
           const float se = (i == j) ? expf(en) : 0.0f;
           F[i][j] = U[i][j] * se * V[j][i];
         }
+      fresh = true;
     }
   }
   else if constexpr (MAT == 5) {
     // fluid_return_mapping, constitutive_models.py:142-213
-    svd3(F, U, s, V);
+    svd3<kFast>(F, U, s, V);
     float eps[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) eps[d] = logf(fmaxf(fabsf(s[d]), 0.01f));
@@ -116,6 +138,8 @@ __device__ __forceinline__ void return_map_and_stress(float (&F)[3][3], float mu
 #pragma unroll
       for (int d = 0; d < 3; ++d) se[d] = expf(1.0f / (2.0f * mu) * ((snn / stn) * stv[d]) + tr / 3.0f);
       usv(U, se, V, F);  // a true matrix product here (U @ sig_elastic @ V^T, :205)
+#pragma unroll
+      for (int d = 0; d < 3; ++d) s[d] = se[d];
     }
   }
   // Kirchhoff stress of the (returned) F, utils.py:32-52
@@ -125,7 +149,7 @@ __device__ __forceinline__ void return_map_and_stress(float (&F)[3][3], float mu
 #pragma unroll
     for (int j = 0; j < 3; ++j) T[i][j] = 0.0f;
   if constexpr (MAT != 0) {
-    svd3(F, U, s, V);
+    if (MAT == 4 || !GSMPM_SVD_REUSE || fresh) svd3<kFast>(F, U, s, V);
     if constexpr (MAT == 1 || MAT == 3 || MAT == 5) {
       // kirchoff_stress_StVK, constitutive_models.py:23-38
       float tv[3];

@@ -16,10 +16,33 @@
 
 namespace gsmpm {
 
+// FAST: reciprocal square roots and square roots by the hardware
+// instructions (v_rsq_f32 / v_sqrt_f32, ~1 ulp) instead of the correctly
+// rounded sequences (27 / 18 VALU each, 25 per SVD).  Sifakis' algorithm is
+// written around an approximate rsqrt, and Taichi builds it with fast math.
+// Where a result depends on the SVD basis itself (foam's element-wise
+// U * diag * V^T, SURVEY F13: for F ~ I the basis is ill-defined and one ulp
+// picks another) the correctly rounded form is used, as in the oracle.
+// GSMPM_SVD_FAST=0 at build time: correctly rounded everywhere.
+#ifndef GSMPM_SVD_FAST
+#define GSMPM_SVD_FAST 1
+#endif
+template <bool FAST>
+__device__ __forceinline__ float svd_rsqrt(float x) {
+  if constexpr (FAST && GSMPM_SVD_FAST) return __builtin_amdgcn_rsqf(x);
+  return 1.0f / sqrtf(x);
+}
+template <bool FAST>
+__device__ __forceinline__ float svd_sqrt(float x) {
+  if constexpr (FAST && GSMPM_SVD_FAST) return __builtin_amdgcn_sqrtf(x);
+  return sqrtf(x);
+}
+
 struct M3 {
   float m[3][3];
 };
 
+template <bool FAST>
 __device__ __forceinline__ void svd_jacobi(float (&S)[3][3], float (&q)[4], int p, int r) {
   constexpr float kGamma = 5.828427124746190f;  // 3 + 2 sqrt(2)
   constexpr float kCStar = 0.923879532511287f;  // cos(pi/8)
@@ -27,7 +50,7 @@ __device__ __forceinline__ void svd_jacobi(float (&S)[3][3], float (&q)[4], int 
   float ch = 2.0f * (S[p][p] - S[r][r]);
   float sh = S[r][p];
   const bool b = (kGamma * sh * sh) < (ch * ch);
-  const float w = 1.0f / sqrtf(ch * ch + sh * sh);
+  const float w = svd_rsqrt<FAST>(ch * ch + sh * sh);
   ch = b ? w * ch : kCStar;
   sh = b ? w * sh : kSStar;
   const float c = ch * ch - sh * sh, s = 2.0f * sh * ch;
@@ -68,17 +91,18 @@ __device__ __forceinline__ void svd_cond_swap(bool c, float (&B)[3][3], float (&
   rho[j] = c ? ri : rj;
 }
 
+template <bool FAST>
 __device__ __forceinline__ void svd_qr_givens(float (&B)[3][3], float (&U)[3][3], int p, int r) {
   constexpr float kEps = 1.0e-12f;
   const float a1 = B[p][p], a2 = B[r][p];
-  const float rho = sqrtf(a1 * a1 + a2 * a2);
+  const float rho = svd_sqrt<FAST>(a1 * a1 + a2 * a2);
   float sh = rho > kEps ? a2 : 0.0f;
   float ch = fabsf(a1) + fmaxf(rho, kEps);
   const bool neg = a1 < 0.0f;
   const float t = sh;
   sh = neg ? ch : sh;
   ch = neg ? t : ch;
-  const float w = 1.0f / sqrtf(ch * ch + sh * sh);
+  const float w = svd_rsqrt<FAST>(ch * ch + sh * sh);
   ch *= w;
   sh *= w;
   const float c = ch * ch - sh * sh, s = 2.0f * sh * ch;
@@ -97,6 +121,7 @@ __device__ __forceinline__ void svd_qr_givens(float (&B)[3][3], float (&U)[3][3]
 }
 
 // A = U diag(sig) V^T
+template <bool FAST = true>
 __device__ __forceinline__ void svd3(const float (&A)[3][3], float (&U)[3][3], float (&sig)[3], float (&V)[3][3]) {
   float S[3][3];
 #pragma unroll
@@ -106,11 +131,11 @@ __device__ __forceinline__ void svd3(const float (&A)[3][3], float (&U)[3][3], f
   float q[4] = {1.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int it = 0; it < 5; ++it) {
-    svd_jacobi(S, q, 0, 1);
-    svd_jacobi(S, q, 1, 2);
-    svd_jacobi(S, q, 2, 0);
+    svd_jacobi<FAST>(S, q, 0, 1);
+    svd_jacobi<FAST>(S, q, 1, 2);
+    svd_jacobi<FAST>(S, q, 2, 0);
   }
-  const float qn = 1.0f / sqrtf(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+  const float qn = svd_rsqrt<FAST>(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
   const float w = q[0] * qn, x = q[1] * qn, y = q[2] * qn, z = q[3] * qn;
   V[0][0] = 1.f - 2.f * (y * y + z * z); V[0][1] = 2.f * (x * y - w * z); V[0][2] = 2.f * (x * z + w * y);
   V[1][0] = 2.f * (x * y + w * z); V[1][1] = 1.f - 2.f * (x * x + z * z); V[1][2] = 2.f * (y * z - w * x);
@@ -130,9 +155,9 @@ __device__ __forceinline__ void svd3(const float (&A)[3][3], float (&U)[3][3], f
   for (int i = 0; i < 3; ++i)
 #pragma unroll
     for (int j = 0; j < 3; ++j) U[i][j] = (i == j) ? 1.f : 0.f;
-  svd_qr_givens(B, U, 0, 1);
-  svd_qr_givens(B, U, 0, 2);
-  svd_qr_givens(B, U, 1, 2);
+  svd_qr_givens<FAST>(B, U, 0, 1);
+  svd_qr_givens<FAST>(B, U, 0, 2);
+  svd_qr_givens<FAST>(B, U, 1, 2);
   sig[0] = B[0][0];
   sig[1] = B[1][1];
   sig[2] = B[2][2];
