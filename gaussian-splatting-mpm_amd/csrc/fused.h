@@ -235,13 +235,21 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
   // the first chunk's record, box and lane order are requested with the chunk
   // count (clamped: a workgroup past the last chunk discards them), which
   // takes one dependent round trip off every workgroup's chain
+  // (the same for every further chunk: its record, box and lane order are
+  // requested while the chunk before it is processed)
   const int w0 = min((int)blockIdx.x, tl.max_chunks - 1);
-  const int4 cr0 = ck.chunk[w0];
-  const int box0 = use_box ? tc.cbox[w0] : kFullBox;
-  const int q0 = (use_box && tc.perm) ? (int)tc.perm[(size_t)w0 * 256 + threadIdx.x] : (int)threadIdx.x;
+  int4 cr_n = ck.chunk[w0];
+  int box_n = use_box ? tc.cbox[w0] : kFullBox;
+  int q_n = (use_box && tc.perm) ? (int)tc.perm[(size_t)w0 * 256 + threadIdx.x] : (int)threadIdx.x;
   for (int w = blockIdx.x; w < nch; w += gridDim.x) {
-    const bool first_chunk = w == (int)blockIdx.x;
-    const int4 cr = first_chunk ? cr0 : ck.chunk[w];
+    const int4 cr = cr_n;
+    const int cbox = box_n, q_lane = q_n;
+    if (w + (int)gridDim.x < nch) {  // workgroup-uniform; chunk w + grid is only ever touched by this workgroup
+      const int wn = w + gridDim.x;
+      cr_n = ck.chunk[wn];
+      box_n = use_box ? tc.cbox[wn] : kFullBox;
+      q_n = (use_box && tc.perm) ? (int)tc.perm[(size_t)wn * 256 + threadIdx.x] : (int)threadIdx.x;
+    }
     const int t = cr.x, first = cr.y, cnt = cr.z;
     const int k = threadIdx.x;
     const bool outside = t == tl.ntiles;  // workgroup-uniform
@@ -251,7 +259,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
     int p = -1;
     float x[3] = {0.f, 0.f, 0.f}, v[3] = {0.f, 0.f, 0.f}, C[3][3], F[3][3], m = 0.f;
     // this lane's particle: the lane balance of the last P2G on these bins (use_box), else in order
-    const int q = k >= cnt ? k : first_chunk ? q0 : (use_box && tc.perm) ? (int)tc.perm[(size_t)w * 256 + k] : k;
+    const int q = k >= cnt ? k : q_lane;
     // particle loads first: their round trips overlap the window staging
     if (k < cnt) {
       p = first + q;
@@ -273,7 +281,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
       if (!outside) {
         // the chunk's stencil box from its last P2G (particles unmoved since), else the whole window
         int lo[3], hi[3];
-        box_unpack(first_chunk ? box0 : use_box ? tc.cbox[w] : kFullBox, lo, hi);
+        box_unpack(cbox, lo, hi);
         const int n1 = hi[1] - lo[1] + 1, n2 = hi[2] - lo[2] + 1, n12 = n1 * n2;
         const int nvol = (hi[0] - lo[0] + 1) * n12;
         const float r12 = 1.0f / (float)n12, r2 = 1.0f / (float)n2;  // exact floor for q < 2^11

@@ -1375,6 +1375,7 @@ struct gsmpm_mpm {
   unsigned char* fperm[2] = {nullptr, nullptr};  // [max_chunks][256] lane balance (fused.h); null: off
   bool lane_balance = true;               // GSMPM_LANE_BALANCE=0 turns it off (A/B)
   bool fuse_permute = true;               // GSMPM_FUSE_PERMUTE=0: separate k_permute (A/B)
+  int fused_wgs = 1024;                   // k_fused grid cap: the workgroups resident at once (init)
   float* planes_alt = nullptr;            // the other particle-plane buffer: every binning permutes
   int* orig_alt = nullptr;                //   storage into bin order, alternating planes / planes_alt
   int fbpar = 0;                          // parity of the bins the next k_fused reads
@@ -1618,7 +1619,12 @@ static int launch_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc,
 }
 
 // ------------------------------------------------------ fused pipeline --
-static int fused_grid(gsmpm_mpm* h) { return std::min(h->ftl.max_chunks, 1024); }
+// Chunks are dealt w, w + grid, ... to the workgroups, so a grid larger than
+// the workgroups resident at once (LDS: 3 per CU) leaves the surplus to start
+// only when a resident one has finished ALL its chunks; capped at residency,
+// every workgroup starts at once and the chunks of a scene that needs several
+// rounds (config D) are spread evenly.
+static int fused_grid(gsmpm_mpm* h) { return std::min(h->ftl.max_chunks, h->fused_wgs); }
 
 template <int MAT, int MODE>
 static void launch_fused_t(gsmpm_mpm* h, int c, const BinOutF& bo, int bin, int use_box, uint32_t mask, float dt,
@@ -1955,6 +1961,15 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
   h->fused = !(prm->flags & (GSMPM_FLAG_PHASED | GSMPM_FLAG_KEEP_GRID));
   if (const char* lb = std::getenv("GSMPM_LANE_BALANCE")) h->lane_balance = lb[0] != '0';
   if (const char* fp = std::getenv("GSMPM_FUSE_PERMUTE")) h->fuse_permute = fp[0] != '0';
+  {
+    int dev = 0, ncu = 0, per_cu = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_fused<0, 3>, 256, 0) == hipSuccess && ncu > 0 &&
+        per_cu > 0)
+      h->fused_wgs = ncu * per_cu;
+    if (const char* fw = std::getenv("GSMPM_FUSED_WGS")) h->fused_wgs = std::max(1, std::atoi(fw));
+  }
   h->ftl.td0 = (h->g.ng + kFT0 - 1) / kFT0;
   h->ftl.td1 = (h->g.ng + kFT1 - 1) / kFT1;
   h->ftl.td2 = (h->g.ng + kFT2 - 1) / kFT2;
