@@ -283,7 +283,56 @@ def other_configs(args, dev, frames=3, rank=0, world=1, xp=None, sync=None):
         res[key] = r
         del sim, sc, means_r, covs_r
         torch.cuda.empty_cache()
+    if not slab:
+        res["E_extra_fit"] = config_e(dev)
     return res
+
+
+def config_e(dev, iters=5):
+    """BASELINE configs[4] (extra.py system identification): extra.py training
+    iterations of the differentiable MPM (30 forward substeps + postprocess,
+    its backward, 30 backward substeps, learn, cycle_init; extra.py:205-241
+    without the renderer) on tools/bench_fit.py's synthetic 20k-particle torus,
+    n_grid 50.  One iteration is the unit; value counts the forward and the
+    backward substeps of every particle."""
+    import numpy as np
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench_fit as bf
+    from gsmpm.fit import FitSimulator
+    n = 20_000
+    x, cov, v = bf.torus(n)
+    t = lambda arr: torch.from_numpy(np.ascontiguousarray(arr)).to(dev)
+    g = FitSimulator(n, n_grid=bf.NG, grid_extent=bf.EXT, gravity=bf.GRAV, **bf.MAT)
+    g.set_particles(t(x), t(cov), t(bf.volumes(x)), t(v))
+    g.set_bc_ground_only()
+    gx = t(np.random.default_rng(1).normal(0, 1, (n, 3)).astype(np.float32))
+    gc = t(np.full(n * 6, 10.0, np.float32))
+
+    def iteration():
+        for s in range(bf.NSUB):
+            g.forward(bf.DT, s)
+        g.postprocess_forward()
+        g.clear_grads()
+        g.set_grads(gx, gc)
+        g.postprocess_backward()
+        for s in reversed(range(bf.NSUB)):
+            g.backward(bf.DT, s)
+        g.learn()
+        g.cycle_init()
+
+    iteration()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        iteration()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / iters * 1e3
+    del g
+    torch.cuda.empty_cache()
+    return {"config": "extra.py (synthetic torus)", "particles": n, "n_grid": bf.NG, "substeps": bf.NSUB,
+            "ms_per_iteration": round(ms, 4), "iterations_per_s": round(1e3 / ms, 1),
+            "particle_substeps_per_s_fwd_bwd": 2 * bf.NSUB * n / (ms * 1e-3)}
 
 
 def main():

@@ -34,4 +34,13 @@ void set_error(const std::string& msg);
 
 inline int div_up(long a, long b) { return (int)((a + b - 1) / b); }
 
+typedef float nt_f4 __attribute__((ext_vector_type(4)));
+// write-through vector store (sc1): the line leaves the XCD's L2 with the
+// store, so the end-of-kernel release has no dirty line of it to write back.
+// For data the next launch reads from other XCDs (chunk windows).
+__device__ __forceinline__ void wt_store4(float4* p, const float4& v) {
+  nt_f4 t = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(t) : "memory");
+}
+
 }  // namespace gsmpm

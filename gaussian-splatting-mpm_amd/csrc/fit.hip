@@ -40,6 +40,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -65,10 +66,14 @@ struct View {
   float *vol, *mass, *logE, *y, *mu, *lam, *glogE, *gy, *gmu, *glam;  // [np]
   float *icov, *cov, *gcov;           // [6][np]
   float *gm, *vin, *vout, *gvin, *gvout;  // grid planes
+  long gstride;  // level stride of gm | vin | vout (7 nn: one grid per level), or 0 (one grid)
   int *count, *cbase, *cstart, *tl, *rk, *perm, *nchunks;  // count, cbase: [L][ntiles]
   int4* chunks;
   float4* slots;  // [max_chunks + 1][kWin3] chunk windows; slot max_chunks stays 0
 };
+
+// the (m | v_in | v_out) planes of level s
+__device__ __forceinline__ float* glv(float* base, const View& V, int s) { return base + (size_t)s * V.gstride; }
 
 __device__ __forceinline__ float* pl(float* base, const View& V, int s, int w, int c) {
   return base + ((size_t)s * w + c) * V.np;
@@ -259,7 +264,8 @@ __device__ __forceinline__ void store_window(const View& V, const unsigned long 
   for (int l = threadIdx.x; l < kWin3; l += kChunk) {
     float c[4] = {0.f, 0.f, 0.f, 0.f};
     for (int ch = 0; ch < nch; ++ch) c[ch] = (float)ldexp((double)(long long)win[ch * kWin3 + l], -S[ch]);
-    dst[l] = make_float4(c[0], c[1], c[2], c[3]);
+    // write-through: the grid kernels read the slots from other XCDs (common.h)
+    wt_store4(dst + l, make_float4(c[0], c[1], c[2], c[3]));
   }
 }
 
@@ -400,10 +406,13 @@ __global__ __launch_bounds__(kGridWG) void k_grid(View V, int s, float dt) {
   const long g = ((long)ix * V.ng + iy) * V.ng + iz;
   const float4 a = window_sum(V, s_c0, s_nc, li, lj, lk);
   const float m = a.w;
-  V.gm[g] = m;
-  V.vin[g] = a.x;
-  V.vin[V.nn + g] = a.y;
-  V.vin[2 * V.nn + g] = a.z;
+  float* const gm = glv(V.gm, V, s);
+  float* const vin = glv(V.vin, V, s);
+  float* const vout = glv(V.vout, V, s);
+  gm[g] = m;
+  vin[g] = a.x;
+  vin[V.nn + g] = a.y;
+  vin[2 * V.nn + g] = a.z;
   float o[3] = {0.f, 0.f, 0.f};
   if (m > 1e-15f) {
     const float gr[3] = {V.gx_, V.gy_, V.gz_};
@@ -414,7 +423,7 @@ __global__ __launch_bounds__(kGridWG) void k_grid(View V, int s, float dt) {
     const float px = (float)ix * V.dx, py = (float)iy * V.dx, pz = (float)iz * V.dx;
     if (fabsf(px - V.bc0) < V.bs0 && fabsf(py - V.bc1) < V.bs1 && fabsf(pz - V.bc2) < V.bs2) o[0] = o[1] = o[2] = 0.f;
   }
-  for (int d = 0; d < 3; ++d) V.vout[d * V.nn + g] = o[d];
+  for (int d = 0; d < 3; ++d) vout[d * V.nn + g] = o[d];
 }
 
 __device__ __forceinline__ long node_of(const View& V, const int base[3], int i, int j, int k) {
@@ -427,6 +436,7 @@ __device__ __forceinline__ long node_of(const View& V, const int base[3], int i,
 __global__ __launch_bounds__(256) void k_g2p(View V, int s, float dt) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= V.n) return;
+  const float* const vout = glv(V.vout, V, s);
   float x[3], Fm[9];
   load_x(V, s, p, x);
   load9(V.F, V, s, p, Fm);
@@ -443,7 +453,7 @@ __global__ __launch_bounds__(256) void k_g2p(View V, int s, float dt) {
         float dpos[3];
         for (int d = 0; d < 3; ++d) dpos[d] = (float)o[d] - fx[d];
         const float weight = w[0][i] * w[1][j] * w[2][k];
-        const float gv[3] = {V.vout[g], V.vout[V.nn + g], V.vout[2 * V.nn + g]};
+        const float gv[3] = {vout[g], vout[V.nn + g], vout[2 * V.nn + g]};
         const float gw[3] = {V.inv_dx * dw[0][i] * w[1][j] * w[2][k], V.inv_dx * w[0][i] * dw[1][j] * w[2][k],
                              V.inv_dx * w[0][i] * w[1][j] * dw[2][k]};
         for (int r = 0; r < 3; ++r) {
@@ -497,6 +507,7 @@ __device__ __forceinline__ void weight_fx_adjoint(const float w[3][3], const flo
 __global__ __launch_bounds__(kChunk) void k_g2p_bwd(View V, int s, float dt) {
   __shared__ unsigned long long win[3 * kWin3];
   __shared__ float s_max[4];
+  const float* const vout = glv(V.vout, V, s);
   const int c = blockIdx.x;
   if (c >= V.nchunks[s]) return;
   const int4 rec = V.chunks[(size_t)s * V.max_chunks + c];
@@ -519,7 +530,7 @@ __global__ __launch_bounds__(kChunk) void k_g2p_bwd(View V, int s, float dt) {
         for (int k = 0; k < 3; ++k) {
           const long g = node_of(V, base, i, j, k);
           if (g < 0) continue;
-          const float gv[3] = {V.vout[g], V.vout[V.nn + g], V.vout[2 * V.nn + g]};
+          const float gv[3] = {vout[g], vout[V.nn + g], vout[2 * V.nn + g]};
           const float gw[3] = {V.inv_dx * dw[0][i] * w[1][j] * w[2][k], V.inv_dx * w[0][i] * dw[1][j] * w[2][k],
                                V.inv_dx * w[0][i] * w[1][j] * dw[2][k]};
           for (int r = 0; r < 3; ++r)
@@ -579,7 +590,7 @@ __global__ __launch_bounds__(kChunk) void k_g2p_bwd(View V, int s, float dt) {
           const float weight = w[0][i] * w[1][j] * w[2][k];
           const float gw[3] = {V.inv_dx * dw[0][i] * w[1][j] * w[2][k], V.inv_dx * w[0][i] * dw[1][j] * w[2][k],
                                V.inv_dx * w[0][i] * w[1][j] * dw[2][k]};
-          const float gv[3] = {V.vout[g], V.vout[V.nn + g], V.vout[2 * V.nn + g]};
+          const float gv[3] = {vout[g], vout[V.nn + g], vout[2 * V.nn + g]};
           const float cw = weight * V.inv_dx * 4.0f;
           float g_weight = 0.f, g_dpos[3] = {0.f, 0.f, 0.f}, g_gw[3] = {0.f, 0.f, 0.f};
           const int a = lb0 + i, b = lb1 + j, c3 = lb2 + k;
@@ -621,7 +632,7 @@ __global__ __launch_bounds__(kGridWG) void k_grid_bwd(View V, int s) {
   const long g = ((long)ix * V.ng + iy) * V.ng + iz;
   const float4 a = window_sum(V, s_c0, s_nc, li, lj, lk);
   const float add[3] = {a.x, a.y, a.z};
-  const float m = V.gm[g];
+  const float m = glv(V.gm, V, s)[g];
   for (int d = 0; d < 3; ++d) {
     const float go = V.gvout[d * V.nn + g] + add[d];
     V.gvout[d * V.nn + g] = go;
@@ -871,6 +882,15 @@ struct gsmpm_fit {
   int has_box = 0;
   float box_c[3] = {0, 0, 0}, box_s[3] = {0, 0, 0};
   std::vector<char> binned;  // per level: bins of x[level] are current
+  // One grid per level (memory allowing): the backward pass then reads the
+  // grid its forward pass computed instead of recomputing it (the reference's
+  // P2G + grid update redo in p2g2p_backward gives the same values from the
+  // same inputs).  gvalid[s]: level s's grid is that of the current x/v/C/S[s]
+  // (forward(s) with dt gdt[s]); any state change through the API drops it.
+  int glevels = 1;
+  std::vector<char> gvalid;
+  std::vector<float> gdt;
+  int glast = 0;             // the level whose grid was computed last (get_grid)
   void* mem = nullptr;       // one allocation for everything
   View V{};
   int* order = nullptr;
@@ -897,6 +917,8 @@ int require_ready(gsmpm_fit* h, const char* fn) {
   return GSMPM_OK;
 }
 
+void drop_grids(gsmpm_fit* h) { std::fill(h->gvalid.begin(), h->gvalid.end(), 0); }
+
 int bin_level(gsmpm_fit* h, int s, hipStream_t st) {
   GSMPM_HIP(hipMemsetAsync(h->V.count + (size_t)s * h->ntiles, 0, sizeof(int) * h->ntiles, st));
   hipLaunchKernelGGL(k_count, dim3(blocks(h->n)), dim3(256), 0, st, h->V, s);
@@ -910,6 +932,8 @@ int bin_level(gsmpm_fit* h, int s, hipStream_t st) {
 // p2g (+ stress) into chunk windows + window sums and grid update of level s
 // (the reset_grid_state of the reference is implicit: k_grid writes every node)
 int grid_of_level(gsmpm_fit* h, int s, float dt, bool recompute, hipStream_t st) {
+  h->glast = h->glevels > 1 ? s : 0;
+  if (recompute && h->glevels > 1 && h->gvalid[s] && h->gdt[s] == dt && h->binned[s]) return GSMPM_OK;
   if (!h->binned[s]) {
     int rc = bin_level(h, s, st);
     if (rc) return rc;
@@ -920,6 +944,8 @@ int grid_of_level(gsmpm_fit* h, int s, float dt, bool recompute, hipStream_t st)
     hipLaunchKernelGGL(k_p2g<false>, dim3(h->max_chunks), dim3(kChunk), 0, st, h->V, s, dt);
   hipLaunchKernelGGL(k_grid, dim3(grid_blocks(h)), dim3(kGridWG), 0, st, h->V, s, dt);
   GSMPM_LAUNCH_CHECK();
+  h->gvalid[s] = 1;
+  h->gdt[s] = dt;
   return GSMPM_OK;
 }
 
@@ -982,7 +1008,12 @@ int gsmpm_fit_create(const gsmpm_fit_params* p, gsmpm_fit** out) {
   h->max_chunks = div_up(h->n, kChunk) + h->ntiles;
   h->binned.assign(h->L, 0);
   const size_t np = h->np, L = h->L, nn = h->nn;
-  const size_t nf = L * np * (3 + 3 + 9 + 9 + 9) * 2 + np * 10 + np * 6 * 3 + nn * 13;
+  // per-level grids up to 4 GiB (GSMPM_FIT_GRID_LEVELS=0: one grid, recomputed in the backward pass)
+  const char* glenv = std::getenv("GSMPM_FIT_GRID_LEVELS");
+  h->glevels = (glenv && glenv[0] == '0') || 7 * nn * 4 * L > (size_t(4) << 30) ? 1 : h->L;
+  h->gvalid.assign(h->L, 0);
+  h->gdt.assign(h->L, 0.f);
+  const size_t nf = L * np * (3 + 3 + 9 + 9 + 9) * 2 + np * 10 + np * 6 * 3 + nn * (7 * (size_t)h->glevels + 6);
   const size_t ni = (size_t)h->ntiles * (2 * L + 1) + np * 3 + L * np + L + 64;
   const size_t nslot = (size_t)(h->max_chunks + 1) * kWin3;
   const size_t bytes = nf * 4 + ni * 4 + L * h->max_chunks * sizeof(int4) + nslot * sizeof(float4) + 64 * 256;  // + per-take alignment
@@ -1010,9 +1041,11 @@ int gsmpm_fit_create(const gsmpm_fit_params* p, gsmpm_fit** out) {
   V.vol = F(np); V.mass = F(np); V.logE = F(np); V.y = F(np); V.mu = F(np); V.lam = F(np);
   V.glogE = F(np); V.gy = F(np); V.gmu = F(np); V.glam = F(np);
   V.icov = F(6 * np); V.cov = F(6 * np); V.gcov = F(6 * np);
-  V.gm = F(4 * nn);  // m | v_in (one memset resets both)
+  V.gm = F(7 * nn * h->glevels);  // per level: m | v_in | v_out
   V.vin = V.gm + nn;
-  V.vout = F(3 * nn); V.gvin = F(3 * nn); V.gvout = F(3 * nn);
+  V.vout = V.gm + 4 * nn;
+  V.gstride = h->glevels > 1 ? 7 * (long)nn : 0;
+  V.gvin = F(3 * nn); V.gvout = F(3 * nn);
   V.count = I(L * h->ntiles); V.cbase = I(L * h->ntiles); V.cstart = I(h->ntiles); V.tl = I(np); V.rk = I(np); V.perm = I(L * np);
   V.nchunks = I(L);
   h->order = I(np);
@@ -1048,8 +1081,9 @@ int gsmpm_fit_set_particles(gsmpm_fit* h, const float* xyz, const float* cov6, c
   // zero every plane once (padding lanes stay 0), then level-0 bins in input
   // order define the internal (tile-sorted) order
   GSMPM_HIP(hipMemsetAsync(V.x, 0, (char*)(V.icov + 6 * (size_t)np * 3) - (char*)V.x, st));
-  for (float* g : {V.gm, V.vout, V.gvin, V.gvout})
-    GSMPM_HIP(hipMemsetAsync(g, 0, sizeof(float) * (g == V.gm ? 4 : 3) * h->nn, st));
+  GSMPM_HIP(hipMemsetAsync(V.gm, 0, sizeof(float) * 7 * h->nn * h->glevels, st));
+  for (float* g : {V.gvin, V.gvout}) GSMPM_HIP(hipMemsetAsync(g, 0, sizeof(float) * 3 * h->nn, st));
+  drop_grids(h);
   hipLaunchKernelGGL(k_iota, dim3(blocks(n)), dim3(256), 0, st, h->order, n);
   hipLaunchKernelGGL(k_scatter_in, dim3(blocks(n)), dim3(256), 0, st, V.x, 3, n, np, (const int*)h->order, xyz);
   GSMPM_LAUNCH_CHECK();
@@ -1079,6 +1113,7 @@ int gsmpm_fit_set_fixed_cube(gsmpm_fit* h, const double center[3], const double 
   V.has_box = 1;
   V.bc0 = (float)center[0]; V.bc1 = (float)center[1]; V.bc2 = (float)center[2];
   V.bs0 = (float)size[0]; V.bs1 = (float)size[1]; V.bs2 = (float)size[2];
+  drop_grids(h);
   return GSMPM_OK;
 }
 
@@ -1090,6 +1125,7 @@ int gsmpm_fit_forward(gsmpm_fit* h, float dt, int32_t s, void* stream) {
   hipLaunchKernelGGL(k_g2p, dim3(blocks(h->n)), dim3(256), 0, st, h->V, (int)s, dt);
   GSMPM_LAUNCH_CHECK();
   h->binned[s + 1] = 0;
+  std::fill(h->gvalid.begin() + s + 1, h->gvalid.end(), 0);  // x/v/C/F of the later levels change
   return GSMPM_OK;
 }
 
@@ -1136,6 +1172,7 @@ int gsmpm_fit_learn(gsmpm_fit* h, void* stream) {
   if (int rc = require_ready(h, "gsmpm_fit_learn")) return rc;
   hipLaunchKernelGGL(k_learn, dim3(blocks(h->n)), dim3(256), 0, S(stream), h->V);
   GSMPM_LAUNCH_CHECK();
+  drop_grids(h);
   return GSMPM_OK;
 }
 
@@ -1143,6 +1180,7 @@ int gsmpm_fit_mu_lam(gsmpm_fit* h, void* stream) {
   if (int rc = require_ready(h, "gsmpm_fit_mu_lam")) return rc;
   hipLaunchKernelGGL(k_mu_lam, dim3(blocks(h->n)), dim3(256), 0, S(stream), h->V);
   GSMPM_LAUNCH_CHECK();
+  drop_grids(h);
   return GSMPM_OK;
 }
 
@@ -1157,6 +1195,7 @@ int gsmpm_fit_cycle_init(gsmpm_fit* h, void* stream) {
     GSMPM_HIP(hipMemcpyAsync(planes[i], planes[i] + last * widths[i] * np, sizeof(float) * widths[i] * np,
                              hipMemcpyDeviceToDevice, st));
   h->binned[0] = 0;
+  drop_grids(h);
   return GSMPM_OK;
 }
 
@@ -1197,6 +1236,7 @@ static int fit_io(gsmpm_fit* h, int32_t field, int32_t level, float* out, const 
                        (const int*)h->order, in);
   GSMPM_LAUNCH_CHECK();
   if (in && field == GSMPM_FIT_X) h->binned[level] = 0;
+  if (in) drop_grids(h);
   return GSMPM_OK;
 }
 
@@ -1217,11 +1257,12 @@ int gsmpm_fit_get_grid(gsmpm_fit* h, int32_t which, float* out, void* stream) {
   GSMPM_REQUIRE(out && which >= 0 && which <= 4, "gsmpm_fit_get_grid: bad argument");
   hipStream_t st = S(stream);
   View& V = h->V;
+  const size_t lo = (size_t)h->glast * V.gstride;  // the grid computed last
   if (which == GSMPM_GRID_MASS) {
-    GSMPM_HIP(hipMemcpyAsync(out, V.gm, sizeof(float) * h->nn, hipMemcpyDeviceToDevice, st));
+    GSMPM_HIP(hipMemcpyAsync(out, V.gm + lo, sizeof(float) * h->nn, hipMemcpyDeviceToDevice, st));
     return GSMPM_OK;
   }
-  const float* src = which == GSMPM_GRID_V_IN ? V.vin : which == GSMPM_GRID_V_OUT ? V.vout : which == 3 ? V.gvin : V.gvout;
+  const float* src = which == GSMPM_GRID_V_IN ? V.vin + lo : which == GSMPM_GRID_V_OUT ? V.vout + lo : which == 3 ? V.gvin : V.gvout;
   hipLaunchKernelGGL(k_interleave, dim3(blocks(h->nn)), dim3(256), 0, st, src, h->nn, 3, out);
   GSMPM_LAUNCH_CHECK();
   return GSMPM_OK;

@@ -6,6 +6,8 @@
 #include <climits>
 #include <cstdint>
 
+#include "common.h"
+
 namespace gsmpm {
 
 // ------------------------------------------------------------------ layout --
@@ -94,13 +96,6 @@ struct Box {
 };
 
 // -------------------------------------------------------- device helpers --
-typedef float nt_f4 __attribute__((ext_vector_type(4)));
-// write-through store (sc1): the line leaves the XCD's L2 with the store, so
-// the end-of-kernel release has no dirty line of it to write back
-__device__ __forceinline__ void wt_store4(float4* p, const float4& v) {
-  nt_f4 t = {v.x, v.y, v.z, v.w};
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(t) : "memory");
-}
 __device__ __forceinline__ void bspline(const float x[3], float inv_dx, int base[3], float fx[3], float w[3][3],
                                         float dw[3][3]) {
   // utils.py:92-109: base = (x*inv_dx - 0.5).cast(int) (truncation), quadratic B-spline

@@ -137,6 +137,50 @@ def test_fit_backward_learn_cycle_match_oracle(dev):
     assert rel_err(g.get("x", 3).cpu().numpy(), o.x[3]) < 1e-4
 
 
+def test_fit_grid_levels_equal_recompute(dev):
+    """The backward pass reading the grid its forward pass stored per level
+    (the default) gives bit-identical adjoints to recomputing P2G + the grid
+    update as the reference's p2g2p_backward does: one simulator, one forward
+    pass and its bins, the backward pass run twice from the same adjoint seed,
+    the second time after mu_lam() (same mu/lam bits) dropped the stored
+    grids.  Then a state change between the passes (set x at a level) is seen
+    by that level's backward (its grid is recomputed)."""
+    import oracle as O
+    from gsmpm.fit import FitSimulator
+    x, cov, v = _scene(3000, 3)
+    vol = O.particle_volume(x, NG, EXT)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    g = FitSimulator(len(x), n_grid=NG, grid_extent=EXT, gravity=GRAV, **MAT)
+    g.set_particles(t(x), t(cov), t(vol), t(v))
+    g.set_bc_ground_only()
+    rng = np.random.default_rng(5)
+    gx = t(rng.normal(0, 1, (len(x), 3)).astype(np.float32))
+    gc = t((rng.normal(0, 1, len(x) * 6) * 1e3).astype(np.float32))
+    for s in range(NSUB):
+        g.forward(DT, s)
+    g.postprocess_forward()
+    keys = [(k, None) for k in ("glogE", "gy", "gmu", "glam")] + \
+           [(k, lvl) for k in ("gx", "gv", "gF", "gC") for lvl in (0, 7, NSUB - 1)]
+    runs = []
+    for drop in (False, True):
+        if drop:
+            g.mu_lam()
+        g.clear_grads(); g.set_grads(gx, gc); g.postprocess_backward()
+        for s in reversed(range(NSUB)):
+            g.backward(DT, s)
+        r = {(k, l): (g.get(k) if l is None else g.get(k, l)).cpu().numpy() for k, l in keys}
+        r.update({w: g.get_grid(w).cpu().numpy() for w in ("mass", "v_in", "v_out")})  # level 0's
+        runs.append(r)
+    for key in runs[0]:
+        np.testing.assert_array_equal(runs[0][key], runs[1][key], err_msg=str(key))
+    # x changed at level 4 after the forward pass: backward(4) recomputes level 4's grid
+    m_before = g.get_grid("mass").cpu().numpy()
+    g.set("x", g.get("x", 4) + 2e-2, 4)
+    g.clear_grads(); g.set_grads(gx, gc)
+    g.backward(DT, 4)
+    assert not np.array_equal(g.get_grid("mass").cpu().numpy(), m_before)
+
+
 def test_fit_ragged_and_tiny(dev):
     """n not a multiple of 256, a handful of particles, a small grid."""
     import oracle as O
