@@ -111,21 +111,16 @@ __device__ __forceinline__ float det3(const float F[9]) {
 }
 
 // ------------------------------------------------------------- binning ---
-// Tile of every particle of level s and its rank inside the tile.  Lanes of a
-// wave that share a tile (the common case: particles are stored tile-sorted)
-// take their ranks from ONE returning atomic per distinct tile.
-__global__ __launch_bounds__(256) void k_count(View V, int s) {
-  const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool on = p < V.n;
-  int tile = -1;
-  if (on) {
-    float x[3];
-    load_x(V, s, p, x);
-    int t[3];
-    for (int d = 0; d < 3; ++d) t[d] = tile_axis((int)(x[d] * V.inv_dx - 0.5f), V);
-    tile = (t[0] * V.nta + t[1]) * V.nta + t[2];
-  }
-  int* count = V.count + (size_t)s * V.ntiles;
+__device__ __forceinline__ int tile_of_x(const float x[3], const View& V) {
+  int t[3];
+  for (int d = 0; d < 3; ++d) t[d] = tile_axis((int)(x[d] * V.inv_dx - 0.5f), V);
+  return (t[0] * V.nta + t[1]) * V.nta + t[2];
+}
+// Rank of each active lane's particle inside its tile (count: that level's
+// per-tile counters, zero before the level's first call).  Lanes of a wave
+// that share a tile (the common case: particles are stored tile-sorted) take
+// their ranks from ONE returning atomic per distinct tile.
+__device__ __forceinline__ void count_rank(const View& V, int* count, int p, bool on, int tile) {
   const int lane = __lane_id();
   const unsigned long long below = (1ull << lane) - 1ull;
   unsigned long long pending = __ballot(on);
@@ -144,6 +139,19 @@ __global__ __launch_bounds__(256) void k_count(View V, int s) {
     V.tl[p] = tile;
     V.rk[p] = rank;
   }
+}
+
+// Tile of every particle of level s and its rank inside the tile.
+__global__ __launch_bounds__(256) void k_count(View V, int s) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool on = p < V.n;
+  int tile = -1;
+  if (on) {
+    float x[3];
+    load_x(V, s, p, x);
+    tile = tile_of_x(x, V);
+  }
+  count_rank(V, V.count + (size_t)s * V.ntiles, p, on, tile);
 }
 
 // inclusive scan of one value per thread over a 1024-thread block
@@ -207,6 +215,67 @@ __global__ __launch_bounds__(256) void k_place(View V, int s) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= V.n) return;
   V.perm[(size_t)s * V.np + V.cstart[V.tl[p]] + V.rk[p]] = p;
+}
+
+// k_scan + k_place in one launch for grids of <= kScanTiles tiles: every
+// workgroup scans the (L2-resident) tile counts itself, workgroup 0 writes the
+// chunk records; then each lane places its particle.  zero_next: zero the
+// next level's counters (the G2P that produces that level counts into them).
+constexpr int kScanTiles = 8192;
+__global__ __launch_bounds__(256) void k_scanplace(View V, int s, int zero_next) {
+  __shared__ int s_start[kScanTiles];
+  __shared__ int s_w[8];
+  const int* count = V.count + (size_t)s * V.ntiles;
+  const int nt = V.ntiles, per = (nt + 255) / 256;
+  const int t0 = min((int)threadIdx.x * per, nt), t1 = min(t0 + per, nt);
+  int sc = 0, sh = 0;
+  for (int t = t0; t < t1; ++t) {
+    const int c = count[t];
+    sc += c;
+    sh += (c + kChunk - 1) / kChunk;
+  }
+  // exclusive scans of (particles, chunks) over the 256 segments
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int ic = sc, ih = sh;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int yc = __shfl_up(ic, o), yh = __shfl_up(ih, o);
+    if (lane >= o) {
+      ic += yc;
+      ih += yh;
+    }
+  }
+  if (lane == 63) {
+    s_w[wid] = ic;
+    s_w[4 + wid] = ih;
+  }
+  __syncthreads();
+  int bc = 0, bh = 0;
+  for (int q = 0; q < wid; ++q) {
+    bc += s_w[q];
+    bh += s_w[4 + q];
+  }
+  int c0 = bc + ic - sc, h0 = bh + ih - sh;
+  int4* chunks = V.chunks + (size_t)s * V.max_chunks;
+  int* cbase = V.cbase + (size_t)s * V.ntiles;
+  for (int t = t0; t < t1; ++t) {
+    const int c = count[t], nch = (c + kChunk - 1) / kChunk;
+    s_start[t] = c0;
+    if (blockIdx.x == 0) {
+      cbase[t] = h0;
+      for (int j = 0; j < nch; ++j) chunks[h0 + j] = make_int4(t, c0 + j * kChunk, min(kChunk, c - j * kChunk), 0);
+    }
+    c0 += c;
+    h0 += nch;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 255) V.nchunks[s] = h0;
+  __syncthreads();
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < V.n) V.perm[(size_t)s * V.np + s_start[V.tl[p]] + V.rk[p]] = p;
+  if (zero_next) {
+    int* cn = V.count + (size_t)(s + 1) * V.ntiles;
+    for (int t = p; t < nt; t += gridDim.x * blockDim.x) cn[t] = 0;
+  }
 }
 
 // ------------------------------------------------------------- forward ---
@@ -433,7 +502,9 @@ __device__ __forceinline__ long node_of(const View& V, const int base[3], int i,
 }
 
 // g2p_opt (utils.py:284-347): level s -> s+1 (v, x, C, F; no cov update).
-__global__ __launch_bounds__(256) void k_g2p(View V, int s, float dt) {
+// count_next: also count level s+1's particles into its (zeroed) tile
+// counters, k_count's work for the next binning.
+__global__ __launch_bounds__(256) void k_g2p(View V, int s, float dt, int count_next) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= V.n) return;
   const float* const vout = glv(V.vout, V, s);
@@ -464,10 +535,13 @@ __global__ __launch_bounds__(256) void k_g2p(View V, int s, float dt) {
           }
         }
       }
+  float x1[3];
   for (int d = 0; d < 3; ++d) {
+    x1[d] = x[d] + dt * nv[d];
     pl(V.v, V, s + 1, 3, d)[p] = nv[d];
-    pl(V.x, V, s + 1, 3, d)[p] = x[d] + dt * nv[d];
+    pl(V.x, V, s + 1, 3, d)[p] = x1[d];
   }
+  if (count_next) count_rank(V, V.count + (size_t)(s + 1) * V.ntiles, p, true, tile_of_x(x1, V));
   store9(V.C, V, s + 1, p, nC);
   float F1[9];
   for (int r = 0; r < 3; ++r)
@@ -891,6 +965,10 @@ struct gsmpm_fit {
   std::vector<char> gvalid;
   std::vector<float> gdt;
   int glast = 0;             // the level whose grid was computed last (get_grid)
+  // Binning state: tl/rk (one set) and count[counted] are complete for level
+  // `counted` (-1: none); czero[l]: count[l] is all zero.
+  int counted = -1;
+  std::vector<char> czero;
   void* mem = nullptr;       // one allocation for everything
   View V{};
   int* order = nullptr;
@@ -919,11 +997,27 @@ int require_ready(gsmpm_fit* h, const char* fn) {
 
 void drop_grids(gsmpm_fit* h) { std::fill(h->gvalid.begin(), h->gvalid.end(), 0); }
 
+// Bins of level s.  Its counts come from the G2P that produced the level when
+// it counted (forward), else k_count; the scan and the placement are one launch
+// on grids of <= kScanTiles tiles, which also zeroes level s+1's counters.
 int bin_level(gsmpm_fit* h, int s, hipStream_t st) {
-  GSMPM_HIP(hipMemsetAsync(h->V.count + (size_t)s * h->ntiles, 0, sizeof(int) * h->ntiles, st));
-  hipLaunchKernelGGL(k_count, dim3(blocks(h->n)), dim3(256), 0, st, h->V, s);
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, h->V, s);
-  hipLaunchKernelGGL(k_place, dim3(blocks(h->n)), dim3(256), 0, st, h->V, s);
+  if (h->counted != s) {
+    if (!h->czero[s]) GSMPM_HIP(hipMemsetAsync(h->V.count + (size_t)s * h->ntiles, 0, sizeof(int) * h->ntiles, st));
+    hipLaunchKernelGGL(k_count, dim3(blocks(h->n)), dim3(256), 0, st, h->V, s);
+    h->counted = s;
+    h->czero[s] = 0;
+  }
+  if (h->ntiles <= kScanTiles) {
+    const int zn = s + 1 < h->L ? 1 : 0;
+    hipLaunchKernelGGL(k_scanplace, dim3(blocks(h->n)), dim3(256), 0, st, h->V, s, zn);
+    if (zn) {
+      h->czero[s + 1] = 1;
+      h->binned[s + 1] = 0;
+    }
+  } else {
+    hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, h->V, s);
+    hipLaunchKernelGGL(k_place, dim3(blocks(h->n)), dim3(256), 0, st, h->V, s);
+  }
   GSMPM_LAUNCH_CHECK();
   h->binned[s] = 1;
   return GSMPM_OK;
@@ -1007,6 +1101,7 @@ int gsmpm_fit_create(const gsmpm_fit_params* p, gsmpm_fit** out) {
   h->ntiles = h->nta * h->nta * h->nta;
   h->max_chunks = div_up(h->n, kChunk) + h->ntiles;
   h->binned.assign(h->L, 0);
+  h->czero.assign(h->L, 0);
   const size_t np = h->np, L = h->L, nn = h->nn;
   // per-level grids up to 4 GiB (GSMPM_FIT_GRID_LEVELS=0: one grid, recomputed in the backward pass)
   const char* glenv = std::getenv("GSMPM_FIT_GRID_LEVELS");
@@ -1088,9 +1183,12 @@ int gsmpm_fit_set_particles(gsmpm_fit* h, const float* xyz, const float* cov6, c
   hipLaunchKernelGGL(k_scatter_in, dim3(blocks(n)), dim3(256), 0, st, V.x, 3, n, np, (const int*)h->order, xyz);
   GSMPM_LAUNCH_CHECK();
   std::fill(h->binned.begin(), h->binned.end(), 0);
+  std::fill(h->czero.begin(), h->czero.end(), 0);
+  h->counted = -1;
   int rc = bin_level(h, 0, st);
   if (rc) return rc;
   GSMPM_HIP(hipMemcpyAsync(h->order, V.perm, sizeof(int) * n, hipMemcpyDeviceToDevice, st));
+  h->counted = -1;  // the particles are re-stored in tile order below
   const int* ord = h->order;
   hipLaunchKernelGGL(k_scatter_in, dim3(blocks(n)), dim3(256), 0, st, V.x, 3, n, np, ord, xyz);
   hipLaunchKernelGGL(k_scatter_in, dim3(blocks(n)), dim3(256), 0, st, V.v, 3, n, np, ord, init_v);
@@ -1122,9 +1220,12 @@ int gsmpm_fit_forward(gsmpm_fit* h, float dt, int32_t s, void* stream) {
   GSMPM_REQUIRE(s >= 0 && s < h->L - 1, "gsmpm_fit_forward: level out of range");
   hipStream_t st = S(stream);
   if (int rc = grid_of_level(h, s, dt, false, st)) return rc;
-  hipLaunchKernelGGL(k_g2p, dim3(blocks(h->n)), dim3(256), 0, st, h->V, (int)s, dt);
+  const int cn = h->czero[s + 1];  // count level s+1 on the way (its counters are zero)
+  hipLaunchKernelGGL(k_g2p, dim3(blocks(h->n)), dim3(256), 0, st, h->V, (int)s, dt, cn);
   GSMPM_LAUNCH_CHECK();
   h->binned[s + 1] = 0;
+  h->czero[s + 1] = 0;
+  h->counted = cn ? s + 1 : (h->counted == s + 1 ? -1 : h->counted);
   std::fill(h->gvalid.begin() + s + 1, h->gvalid.end(), 0);  // x/v/C/F of the later levels change
   return GSMPM_OK;
 }
@@ -1195,6 +1296,7 @@ int gsmpm_fit_cycle_init(gsmpm_fit* h, void* stream) {
     GSMPM_HIP(hipMemcpyAsync(planes[i], planes[i] + last * widths[i] * np, sizeof(float) * widths[i] * np,
                              hipMemcpyDeviceToDevice, st));
   h->binned[0] = 0;
+  if (h->counted == 0) h->counted = -1;
   drop_grids(h);
   return GSMPM_OK;
 }
@@ -1235,7 +1337,10 @@ static int fit_io(gsmpm_fit* h, int32_t field, int32_t level, float* out, const 
     hipLaunchKernelGGL(k_scatter_in, dim3(blocks(h->n)), dim3(256), 0, st, plane, d.width, h->n, h->np,
                        (const int*)h->order, in);
   GSMPM_LAUNCH_CHECK();
-  if (in && field == GSMPM_FIT_X) h->binned[level] = 0;
+  if (in && field == GSMPM_FIT_X) {
+    h->binned[level] = 0;
+    if (h->counted == level) h->counted = -1;
+  }
   if (in) drop_grids(h);
   return GSMPM_OK;
 }
