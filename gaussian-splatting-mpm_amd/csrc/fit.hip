@@ -500,6 +500,17 @@ __device__ __forceinline__ long node_of(const View& V, const int base[3], int i,
   if ((unsigned)a >= (unsigned)V.ng || (unsigned)b >= (unsigned)V.ng || (unsigned)c >= (unsigned)V.ng) return -1;
   return ((long)a * V.ng + b) * V.ng + c;
 }
+// The 3 planes of a grid vector at node g, 0 off the grid (g < 0).  The loads
+// are unconditional (clamped index), so a stencil loop's 27 gathers are not
+// each behind a branch (one round trip apiece); a node off the grid then adds
+// zeros where the reference skips it.
+__device__ __forceinline__ void grid3(const float* b, const View& V, long g, float out[3]) {
+  const long gg = g < 0 ? 0 : g;
+  const float a0 = b[gg], a1 = b[V.nn + gg], a2 = b[2 * V.nn + gg];
+  out[0] = g < 0 ? 0.f : a0;
+  out[1] = g < 0 ? 0.f : a1;
+  out[2] = g < 0 ? 0.f : a2;
+}
 
 // g2p_opt (utils.py:284-347): level s -> s+1 (v, x, C, F; no cov update).
 // count_next: also count level s+1's particles into its (zeroed) tile
@@ -515,16 +526,19 @@ __global__ __launch_bounds__(256) void k_g2p(View V, int s, float dt, int count_
   float fx[3], w[3][3], dw[3][3];
   bsp(x, V.inv_dx, base, fx, w, dw);
   float nv[3] = {0.f, 0.f, 0.f}, nC[9] = {0.f}, nF[9] = {0.f};
+#pragma unroll
   for (int i = 0; i < 3; ++i)
+#pragma unroll
     for (int j = 0; j < 3; ++j)
+#pragma unroll
       for (int k = 0; k < 3; ++k) {
         const long g = node_of(V, base, i, j, k);
-        if (g < 0) continue;
         const int o[3] = {i, j, k};
         float dpos[3];
         for (int d = 0; d < 3; ++d) dpos[d] = (float)o[d] - fx[d];
         const float weight = w[0][i] * w[1][j] * w[2][k];
-        const float gv[3] = {vout[g], vout[V.nn + g], vout[2 * V.nn + g]};
+        float gv[3];
+        grid3(vout, V, g, gv);
         const float gw[3] = {V.inv_dx * dw[0][i] * w[1][j] * w[2][k], V.inv_dx * w[0][i] * dw[1][j] * w[2][k],
                              V.inv_dx * w[0][i] * w[1][j] * dw[2][k]};
         for (int r = 0; r < 3; ++r) {
@@ -599,12 +613,15 @@ __global__ __launch_bounds__(kChunk) void k_g2p_bwd(View V, int s, float dt) {
     load9(V.F, V, s, p, Fm);
     bsp(x, V.inv_dx, base, fx, w, dw);
     float nF[9] = {0.f};
+#pragma unroll
     for (int i = 0; i < 3; ++i)
+#pragma unroll
       for (int j = 0; j < 3; ++j)
+#pragma unroll
         for (int k = 0; k < 3; ++k) {
           const long g = node_of(V, base, i, j, k);
-          if (g < 0) continue;
-          const float gv[3] = {vout[g], vout[V.nn + g], vout[2 * V.nn + g]};
+          float gv[3];
+          grid3(vout, V, g, gv);
           const float gw[3] = {V.inv_dx * dw[0][i] * w[1][j] * w[2][k], V.inv_dx * w[0][i] * dw[1][j] * w[2][k],
                                V.inv_dx * w[0][i] * w[1][j] * dw[2][k]};
           for (int r = 0; r < 3; ++r)
@@ -653,22 +670,26 @@ __global__ __launch_bounds__(kChunk) void k_g2p_bwd(View V, int s, float dt) {
     const double sc = ldexp(1.0, S[0]);
     const int lb0 = base[0] - ox, lb1 = base[1] - oy, lb2 = base[2] - oz;
     float gfx[3] = {0.f, 0.f, 0.f};
+#pragma unroll
     for (int i = 0; i < 3; ++i)
+#pragma unroll
       for (int j = 0; j < 3; ++j)
+#pragma unroll
         for (int k = 0; k < 3; ++k) {
           const long g = node_of(V, base, i, j, k);
-          if (g < 0) continue;
           const int o[3] = {i, j, k};
           float dpos[3];
           for (int d = 0; d < 3; ++d) dpos[d] = (float)o[d] - fx[d];
           const float weight = w[0][i] * w[1][j] * w[2][k];
           const float gw[3] = {V.inv_dx * dw[0][i] * w[1][j] * w[2][k], V.inv_dx * w[0][i] * dw[1][j] * w[2][k],
                                V.inv_dx * w[0][i] * w[1][j] * dw[2][k]};
-          const float gv[3] = {vout[g], vout[V.nn + g], vout[2 * V.nn + g]};
+          float gv[3];
+          grid3(vout, V, g, gv);
           const float cw = weight * V.inv_dx * 4.0f;
           float g_weight = 0.f, g_dpos[3] = {0.f, 0.f, 0.f}, g_gw[3] = {0.f, 0.f, 0.f};
           const int a = lb0 + i, b = lb1 + j, c3 = lb2 + k;
-          const bool in_win = (unsigned)a < (unsigned)kWin && (unsigned)b < (unsigned)kWin && (unsigned)c3 < (unsigned)kWin;
+          const bool in_win = g >= 0 && (unsigned)a < (unsigned)kWin && (unsigned)b < (unsigned)kWin &&
+                              (unsigned)c3 < (unsigned)kWin;
           const int l = (a * kWin + b) * kWin + c3;
           for (int r = 0; r < 3; ++r) {
             float g_g = g_nv[r] * weight;
@@ -733,18 +754,21 @@ __global__ __launch_bounds__(256) void k_p2g_bwd(View V, int s, float dt) {
   bsp(x, V.inv_dx, base, fx, w, dw);
   const float m = V.mass[p], vol = V.vol[p];
   float gfx[3] = {0.f, 0.f, 0.f};
+#pragma unroll
   for (int i = 0; i < 3; ++i)
+#pragma unroll
     for (int j = 0; j < 3; ++j)
+#pragma unroll
       for (int k = 0; k < 3; ++k) {
         const long g = node_of(V, base, i, j, k);
-        if (g < 0) continue;
         const int o[3] = {i, j, k};
         float dpos[3];
         for (int d = 0; d < 3; ++d) dpos[d] = ((float)o[d] - fx[d]) * V.dx;
         const float weight = w[0][i] * w[1][j] * w[2][k];
         const float gw[3] = {V.inv_dx * dw[0][i] * w[1][j] * w[2][k], V.inv_dx * w[0][i] * dw[1][j] * w[2][k],
                              V.inv_dx * w[0][i] * w[1][j] * dw[2][k]};
-        const float G[3] = {V.gvin[g], V.gvin[V.nn + g], V.gvin[2 * V.nn + g]};
+        float G[3];
+        grid3(V.gvin, V, g, G);
         float g_weight = 0.f, g_dpos[3] = {0.f, 0.f, 0.f}, g_gw[3] = {0.f, 0.f, 0.f};
         for (int r = 0; r < 3; ++r) {
           const float cd = Cm[r * 3 + 0] * dpos[0] + Cm[r * 3 + 1] * dpos[1] + Cm[r * 3 + 2] * dpos[2];
