@@ -48,16 +48,17 @@ namespace gsmpm {
 constexpr int kChunk = 256;  // particles per work chunk (one per lane of a 256-lane workgroup)
 
 // Workgroup timeline stamps (diagnostics): [kernel][wg][start, end] in
-// s_memrealtime ticks (100 MHz), written by lane 0 of the first 4096 workgroups.
+// s_memrealtime ticks (100 MHz), written by lane 0 of the first kStampWGs workgroups.
 // Compiled in only with -DGSMPM_STAMPS (tools/wg_timeline*.py builds); the
 // production library carries no diagnostic stores in its kernels.
 #ifdef GSMPM_STAMPS
-__device__ unsigned long long g_stamps[4][4096][8];
+constexpr int kStampWGs = 8192;
+__device__ unsigned long long g_stamps[4][kStampWGs][8];
 __device__ __forceinline__ void stamp(int kern, int slot) {
-  if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[kern][blockIdx.x][slot] = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0 && blockIdx.x < kStampWGs) g_stamps[kern][blockIdx.x][slot] = __builtin_amdgcn_s_memrealtime();
 }
 __device__ __forceinline__ void stamp_val(int kern, int slot, unsigned long long v) {
-  if (threadIdx.x == 0 && blockIdx.x < 4096) g_stamps[kern][blockIdx.x][slot] = v;
+  if (threadIdx.x == 0 && blockIdx.x < kStampWGs) g_stamps[kern][blockIdx.x][slot] = v;
 }
 #define GSMPM_HWREG(r) __builtin_amdgcn_s_getreg((r) | (0 << 6) | (31 << 11))
 #else
@@ -2476,7 +2477,7 @@ int gsmpm_debug_stamps(uint64_t* out, void* stream) {
   GSMPM_REQUIRE(out, "gsmpm_debug_stamps: null argument");
 #ifdef GSMPM_STAMPS
   GSMPM_HIP(hipStreamSynchronize((hipStream_t)stream));
-  GSMPM_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 4 * 4096 * 8));
+  GSMPM_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * 4 * kStampWGs * 8));
   return GSMPM_OK;
 #else
   (void)stream;

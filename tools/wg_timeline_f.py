@@ -18,7 +18,7 @@ sim.step(sa.substep_dt, masks[:100]); sim.step(sa.substep_dt, masks[100:200])
 print('stats', sim.debug_stats(), 'pipeline', sim.pipeline)
 ms = sim.profile(sa.substep_dt, masks[200:203])  # K(P2G), grid, K, grid, K, grid, K(G2P)
 print('event ms K/grid/bins per 3 substeps', ms)
-buf = np.zeros((4, 4096, 8), np.uint64)
+buf = np.zeros((4, 8192, 8), np.uint64)
 LIB.gsmpm_debug_stamps(buf.ctypes.data_as(ctypes.c_void_p), stream_of(dev))
 b = buf[0].astype(np.int64)
 b = b[b[:, 0] > 0]
