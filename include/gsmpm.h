@@ -226,7 +226,7 @@ int gsmpm_mpm_time_kernels(gsmpm_mpm* h, float dt, uint32_t bc_active, int32_t r
  * re-sort}.  Synchronises `stream`. */
 int gsmpm_mpm_debug_stats(gsmpm_mpm* h, int32_t* out8, void* stream);
 /* Workgroup timelines of the last k_p2g / k_g2p / k_finish_bins launches:
- * out[4][4096][8] phase stamps in s_memrealtime ticks (100 MHz).  Diagnostics. */
+ * out[4][8192][8] phase stamps in s_memrealtime ticks (100 MHz).  Diagnostics. */
 int gsmpm_debug_stamps(uint64_t* out, void* stream);
 /* Node box (lo[3], hi[3]) of the tiles the next grid update owns; synchronises `stream`. */
 int gsmpm_mpm_live_box(gsmpm_mpm* h, int32_t* box6, void* stream);
