@@ -204,6 +204,43 @@ def test_fit_ragged_and_tiny(dev):
         assert rel_err(g.get("F", 5).cpu().numpy(), o.F[5]) < 1e-4
 
 
+def test_fit_binning_paths(dev):
+    """The binning bookkeeping (csrc/fit.hip bin_level): a grid of more than
+    8,192 tiles (k_scan + k_place instead of the fused k_scanplace), a level
+    stepped forward twice (its counters were already consumed), and x set at a
+    level between forward steps (counts taken again by k_count); the oracle
+    runs the same call sequence."""
+    import oracle as O
+    from gsmpm.fit import FitSimulator
+    # 176: 22^3 = 10,648 tiles (dense enough blob, dt under the CFL limit of dx = 0.011)
+    for n, ng, lo, hi, dt in ((3000, 24, 0.8, 1.2, 1e-3), (3000, 176, 0.95, 1.05, 1e-4)):
+        rng = np.random.default_rng(ng)
+        x = rng.uniform(lo, hi, (n, 3)).astype(np.float32)
+        cov = np.tile(np.array([1e-4, 0, 0, 1e-4, 0, 1e-4], np.float32), (n, 1))
+        v = rng.normal(0, 0.05, (n, 3)).astype(np.float32)
+        vol = O.particle_volume(x, ng, EXT)
+        o = O.OracleDiff(x, cov, vol, n_grid=ng, grid_extent=EXT, gravity=GRAV, init_v=v, levels=8,
+                         ground_only=True, **MAT)
+        g = FitSimulator(n, n_grid=ng, grid_extent=EXT, levels=8, gravity=GRAV, **MAT)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        g.set_particles(t(x), t(cov), t(vol), t(v))
+        g.set_bc_ground_only()
+        seq = [0, 1, 2, 2, 3]  # level 2 twice
+        for s in seq:
+            o.p2g2p_forward(dt, s)
+            g.forward(dt, s)
+        assert rel_err(g.get("x", 4).cpu().numpy(), o.x[4]) < 1e-4, ng
+        # x of level 4 moved between forward steps
+        xs = o.x[4] + np.float32(1e-3)
+        o.x[4][:] = xs
+        g.set("x", t(xs), 4)
+        for s in (4, 5, 6):
+            o.p2g2p_forward(dt, s)
+            g.forward(dt, s)
+        assert rel_err(g.get("x", 7).cpu().numpy(), o.x[7]) < 1e-4, ng
+        assert rel_err(g.get("F", 7).cpu().numpy(), o.F[7]) < 1e-4, ng
+
+
 def test_fit_dropin_extra_py_loop(dev):
     """The extra.py train loop (extra.py:189-241) through the drop-in API."""
     import oracle as O
