@@ -650,10 +650,30 @@ __global__ __launch_bounds__(256) void k_ranges32(int L, const unsigned* __restr
 // with upstream's conventions: dmean2D w.r.t. NDC (x W/2, H/2), the conic's
 // off-diagonal term halved, alpha's 0.99 clamp not differentiated.
 constexpr int kRec = 9;
+#ifndef GSMPM_RBWD_DPP
+#define GSMPM_RBWD_DPP 1  // 0: __shfl_xor wave sums (A/B)
+#endif
+
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+// Sum over the wave, valid in lane 63 only: six DPP adds (quad swaps, row
+// shifts, row broadcasts) instead of six LDS-crossbar permutes (__shfl_xor is
+// ds_bpermute_b32 here).  Lanes whose DPP source is out of range add 0.
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ float dpp_src(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK, 0xf, false));
+}
+__device__ __forceinline__ float wave_total63(float v) {
+  v += dpp_src<0xb1>(v);         // quad_perm [1,0,3,2]
+  v += dpp_src<0x4e>(v);         // quad_perm [2,3,0,1]
+  v += dpp_src<0x114>(v);        // row_shr:4
+  v += dpp_src<0x118>(v);        // row_shr:8
+  v += dpp_src<0x142, 0xa>(v);   // row_bcast:15 into rows 1, 3
+  v += dpp_src<0x143, 0xc>(v);   // row_bcast:31 into rows 2, 3
   return v;
 }
 
@@ -685,10 +705,10 @@ __global__ __launch_bounds__(kBlock) void k_render_bwd(const uint2* __restrict__
   __shared__ float4 s_rgb[kBlock];
   __shared__ float s_part[kBlock / 64][kRec][kBlock];
   __shared__ int s_maxlast;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int tx = threadIdx.x % kBX, ty = threadIdx.x / kBX;
   const int px = blockIdx.x * kBX + tx, py = blockIdx.y * kBY + ty;
   const bool inside = px < W && py < H;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint2 range = ranges[blockIdx.y * gx + blockIdx.x];
   const int todo0 = (int)(range.y - range.x);
   const size_t pix = (size_t)py * W + px, HW = (size_t)H * W;
@@ -721,8 +741,10 @@ __global__ __launch_bounds__(kBlock) void k_render_bwd(const uint2* __restrict__
     __syncthreads();
     if ((int)threadIdx.x < nb) {
       const unsigned id = ids[range.x + myp];
-      s_xy[threadIdx.x] = xy[id];
-      s_co[threadIdx.x] = conic_o[id];
+      const float2 gxy = xy[id];
+      const float4 gco = conic_o[id];
+      s_xy[threadIdx.x] = gxy;
+      s_co[threadIdx.x] = gco;
       s_rgb[threadIdx.x] = rgbo[id];
     }
     __syncthreads();
@@ -767,6 +789,15 @@ __global__ __launch_bounds__(kBlock) void k_render_bwd(const uint2* __restrict__
           }
         }
       }
+#if GSMPM_RBWD_DPP
+      if (__ballot(act)) {
+#pragma unroll
+        for (int q = 0; q < kRec; ++q) g[q] = wave_total63(g[q]);
+      }
+      if (lane == 63)
+#pragma unroll
+        for (int q = 0; q < kRec; ++q) s_part[wave][q][j] = g[q];
+#else
       if (__ballot(act)) {
 #pragma unroll
         for (int q = 0; q < kRec; ++q) g[q] = wave_sum(g[q]);
@@ -774,6 +805,7 @@ __global__ __launch_bounds__(kBlock) void k_render_bwd(const uint2* __restrict__
       if (lane == 0)
 #pragma unroll
         for (int q = 0; q < kRec; ++q) s_part[wave][q][j] = g[q];
+#endif
     }
     __syncthreads();
     if ((int)threadIdx.x < nb) {
