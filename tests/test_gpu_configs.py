@@ -65,9 +65,11 @@ def _errs(s, ref):
     return e
 
 
-def _check(errs, where, extra=None):
+def _check(errs, where, extra=None, stress=False):
+    if os.environ.get('GSMPM_PRINT_ERRS'):
+        print('ERRS', where, {k: f'{e:.2e}' for k, e in errs.items()})
     for k, e in errs.items():
-        bound = (extra or {}).get(k, TOL_DERIVED.get(k, TOL))
+        bound = (extra or {}).get(k, TOL_DERIVED.get(k, TOL) if stress else TOL)
         assert e < bound, f"{where}: {k} rel err {e:.3e} > {bound} (all: {errs})"
 
 
@@ -80,7 +82,7 @@ def _dump(name, record):
             json.dump(record, f, indent=1)
 
 
-def _run_curve(s, ref, imps, ops, dt, checkpoints, extra=None):
+def _run_curve(s, ref, imps, ops, dt, checkpoints, extra=None, stress=False):
     """Advance both sides to each checkpoint substep; the error at every one."""
     curve, done, t = {}, 0, 0.0
     for c in checkpoints:
@@ -90,7 +92,7 @@ def _run_curve(s, ref, imps, ops, dt, checkpoints, extra=None):
         done = c
         assert abs(s.time - t) == 0.0
         curve[c] = _errs(s, ref)
-        _check(curve[c], f"substep {c}", extra)
+        _check(curve[c], f"substep {c}", extra, stress)
     return curve
 
 
@@ -212,7 +214,7 @@ def test_config_C_lego_fracture(dev, material):
     s, _ = dropin_sim(prob, dev, material=material)
     extra = {"yield": 5e-3} if material == "metal" else {}
     rec = {"config": "lego-fracture.json", "material": material, "N": len(prob["x"]), "n_grid": 128}
-    rec["curve"] = _run_curve(s, ref, imps, ops, dt, (1, 10, 50, 100), extra)
+    rec["curve"] = _run_curve(s, ref, imps, ops, dt, (1, 10, 50, 100), extra, stress=material == "metal")
     # the impulse moved the particles in its box (a real dynamic, not a resting state)
     assert np.abs(ref.v).max() > 1e-3
     if material == "metal":
@@ -275,7 +277,7 @@ def test_dense_tiles_multi_chunk(dev, material, fcr):
     errs = {k: rel_err(got[k].cpu().numpy().reshape(exp[k].shape), exp[k]) for k in got}
     errs["C"] = _c_err(got["C"].cpu().numpy(), ref.C, ref.v, ng / ext)
     extra = {"F_trial": 1e-4}
-    _check(errs, "dense tiles", extra)
+    _check(errs, "dense tiles", extra, stress=True)  # FCR jelly and metal
     sim.postprocess()
     ref.postprocess()
     assert rel_err(sim.get("cov").cpu().numpy(), ref.cov) < TOL

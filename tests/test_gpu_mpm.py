@@ -28,9 +28,12 @@ def _set_rebin(s, pipe):
         s._sim.set_rebin_interval(int(pipe[len("fused_r"):]))
 
 TOL = 1e-4
-# v and C are grid-velocity gradients (C = sum v_i dpos^T w 4/dx^2): with a stiff
-# stress model they amplify the float-atomic summation order by ~1/dx, so they get
-# their own bound; x / F_trial / cov carry the north_star 1e-4.
+# Every field of a stress-free run (jelly as written) is held to the
+# north_star 1e-4 (measured: v, C <= 3e-6).  With a stiff stress model v and C
+# (C = sum v_i dpos^T w 4/dx^2) amplify the summation-order difference of the
+# grid sums by ~1/dx, so stress-bearing runs (FCR jelly, metal, sand, foam) get
+# their own bound for those two (measured on these 48^3 scenes: v <= 1.8e-3,
+# C <= 3.2e-3); x / F_trial / cov carry 1e-4 everywhere.
 TOL_DERIVED = {"v": 2e-3, "C": 5e-3}
 
 
@@ -43,7 +46,7 @@ TOL_DERIVED = {"v": 2e-3, "C": 5e-3}
 MATERIAL_TOL = {"metal": {"yield": 5e-3}, "foam": {"F_trial": 2e-2}}
 
 
-def _compare(s, ref, fields=("x", "v", "C", "F_trial"), tol=TOL, extra=None):
+def _compare(s, ref, fields=("x", "v", "C", "F_trial"), tol=TOL, extra=None, stress=False):
     st = s.mpm_state
     got = {
         "x": st.particle_xyz.to_torch().cpu().numpy(),
@@ -53,9 +56,11 @@ def _compare(s, ref, fields=("x", "v", "C", "F_trial"), tol=TOL, extra=None):
     }
     exp = {"x": ref.x, "v": ref.v, "C": ref.C, "F_trial": ref.F_trial}
     errs = {k: rel_err(got[k], exp[k]) for k in fields}
+    if __import__('os').environ.get('GSMPM_PRINT_ERRS'):
+        print('ERRS', __import__('os').environ.get('PYTEST_CURRENT_TEST', '').split(' ')[0], {k: f'{e:.2e}' for k, e in errs.items()})
     for k, e in errs.items():
-        bound = (extra or {}).get(k, TOL_DERIVED.get(k, tol))
-        assert e < bound, f"{k}: rel err {e:.3e} (all: {errs})"
+        bound = (extra or {}).get(k, TOL_DERIVED.get(k, tol) if stress else tol)
+        assert e < bound, f"{k}: rel err {e:.3e} > {bound} (all: {errs})"
     return errs
 
 
@@ -95,7 +100,7 @@ def test_materials_parity(dev, material, quirk, pipe):
     for _ in range(30):
         s.p2g2p(dt)
     extra = MATERIAL_TOL.get(material, {})
-    _compare(s, ref, extra=extra)
+    _compare(s, ref, extra=extra, stress=True)  # every case here carries stress
     if material == "metal":
         y = s.mpm_model.yield_stress.to_torch().cpu().numpy()
         assert rel_err(y, ref.yield_stress) < extra["yield"]
