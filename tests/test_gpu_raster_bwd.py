@@ -3,11 +3,14 @@ GaussianRasterizer -> gsmpm_raster_backward) vs the oracle's backward
 (oracle/raster_oracle.c or_backward, itself checked against float64 autograd
 in test_oracle_raster_bwd.py).
 
-Tolerance: per element 1e-2 of its magnitude (+1e-3 of the max) for all but
-0.5 % of the entries, and 5e-2 of the max everywhere.  The forward blends with
-the hardware exp2 and FMAs (pixels agree to 1e-3, test_gpu_raster.py), so a
-pair at the alpha >= 1/255 or T >= 1e-4 cut-off can be kept by one side and
-skipped by the other; that moves a few gradients, not the bulk.
+Tolerance: 2e-4 of the max everywhere; per element (relative to its own
+magnitude + 1e-3 of the max) 1e-3 for all but 0.1 % of the entries and 1e-2
+for all but 0.01 %.  Measured on these scenes (GSMPM_PRINT_ERRS=1): max
+<= 6e-5, <= 0.01 % of entries beyond 1e-3, none beyond 1e-2.  The forward
+blends with the hardware exp2 and FMAs, so a pair at the alpha >= 1/255 or
+T >= 1e-4 cut-off can be kept by one side and skipped by the other; that
+moves a few gradients, not the bulk (the GPU path is deterministic, so a scene
+either has such a flip or not).
 """
 from __future__ import annotations
 
@@ -26,8 +29,12 @@ def _close(a, b, what):
     b = np.asarray(b, np.float64).reshape(-1)
     r = np.abs(a - b) / (np.abs(b) + 1e-3 * np.abs(b).max() + 1e-30)
     frac = float((r > 1e-2).mean())
+    frac3 = float((r > 1e-3).mean())
     e = rel_err(a, b)
-    assert frac <= 5e-3 and e < 5e-2, (what, frac, e, float(np.median(r)))
+    if __import__("os").environ.get("GSMPM_PRINT_ERRS"):
+        print("ERRS", what, f"max {e:.2e} median {np.median(r):.2e} >1e-4 {(r > 1e-4).mean():.4f} "
+              f">1e-3 {(r > 1e-3).mean():.4f} >1e-2 {frac:.4f}")
+    assert frac <= 1e-4 and frac3 <= 1e-3 and e < 2e-4, (what, frac, frac3, e, float(np.median(r)))
     return e
 
 
