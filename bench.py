@@ -259,6 +259,7 @@ def other_configs(args, dev, frames=3, rank=0, world=1, xp=None, sync=None):
         else:
             st = sim.stats()
             r["rank0_slab_planes"] = [st["lo"], st["hi"]]
+            r["rank0_window_rects"] = sim.engine.slab_rects()  # exchanged (y0, ny, z0, nz) per window
         sim.postprocess()
         cam, g, mask = sc["cam"], sc["g"], sc["mask"]
         w_args = (float(sc["s"]), [float(v) for v in sc["c"].reshape(-1).tolist()])
@@ -565,6 +566,10 @@ def main():
             out["other_configs"] = oc
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(scene, args, args.cpu_seconds)
+    if slab:
+        st = sim.stats()
+        out["config"]["rank0_slab_planes"] = [st["lo"], st["hi"]]
+        out["config"]["rank0_window_rects"] = sim.engine.slab_rects()
     if rank == 0:
         print(json.dumps(out), flush=True)
     # the slab transport's RCCL communicator is left to process exit: captured

@@ -43,8 +43,12 @@ struct SlabWin {
   int W;            // window planes (0: not a slab)
   int a[2];         // first plane of the lower (0) / upper (1) window; window w is [a[w], a[w] + W)
   int on[2];        // window w present (a neighbour on that side)
-  float4* part[2];  // [W][ng][ng] this rank's partial sums of the window's nodes (k_grid_f writes, k_win_update zeroes)
-  int pass;         // k_grid_f: 0 every touched tile, 1 tiles meeting a window, 2 the others
+  float4* part[2];  // [W][ny][nz] this rank's partial sums of the window's nodes in its rect (k_grid_f writes,
+                    // k_win_update zeroes)
+  int y0[2], ny[2];  // window w's rect of nodes [y0, y0 + ny) x [z0, z0 + nz): what the two ranks of the bound can
+  int z0[2], nz[2];  // touch before the next migration (agreed at every migration); only it is exchanged
+  int* oob;          // set when a window node outside the rect has mass (the exchange would miss it)
+  int pass;          // k_grid_f: 0 every touched tile, 1 tiles meeting a window, 2 the others
 };
 
 __device__ __forceinline__ int slab_window_of(const SlabWin& sw, int i) {
@@ -679,8 +683,11 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
         gacc[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
       const int sww = sw.W ? slab_window_of(sw, i) : -1;
-      if (sww >= 0)  // a window node: this rank's partial, totalled after the exchange (k_win_update)
-        sw.part[sww][((size_t)(i - sw.a[sww]) * ng + j) * ng + k] = a;
+      const bool inrect = sww >= 0 && (unsigned)(j - sw.y0[sww]) < (unsigned)sw.ny[sww] &&
+                          (unsigned)(k - sw.z0[sww]) < (unsigned)sw.nz[sww];
+      if (sww >= 0 && !inrect && a.w != 0.f) *sw.oob = 1;
+      if (inrect)  // a window node: this rank's partial, totalled after the exchange (k_win_update)
+        sw.part[sww][((size_t)(i - sw.a[sww]) * sw.ny[sww] + (j - sw.y0[sww])) * sw.nz[sww] + (k - sw.z0[sww])] = a;
       else
         gvel[idx] = node_update(a, i, j, k, g, gs, bct);
     }

@@ -1398,14 +1398,17 @@ struct gsmpm_mpm {
   int s_has[2] = {0, 0};
   SlabWin sw{};                              // windows + this rank's partial buffers
   float4* s_recv[2] = {nullptr, nullptr};    // the neighbours' partials
-  int* s_drift = nullptr;                    // [1] a particle passed the margin (k_fused)
+  int* s_drift = nullptr;                    // [2]: a particle passed the margin (k_fused); a window node
+                                             // outside its rect got mass (k_grid_f)
+  int* s_rect_dev = nullptr;                 // [12]: this rank's particle yz box, the neighbours' (rect handshake)
+  bool s_rect_set = false;                   // the windows' rects have been agreed once
   int* gid = nullptr;                        // [np] global particle ids, caller order
   int* gid_alt = nullptr;
   float* cold_alt = nullptr;
   int* mig_bcnt = nullptr;                   // [nblk][3] per-block destination counts
   int* mig_boff = nullptr;                   // [nblk][3] their exclusive scan
   int* mig_tot = nullptr;                    // [3] + drift flag copy
-  int* mig_host = nullptr;                   // pinned [4]: totals + drift
+  int* mig_host = nullptr;                   // pinned [16]: totals + drift flags + rect handshake
   float* mig_send[2] = {nullptr, nullptr};   // [NMIG][count] payloads
   float* mig_recv[2] = {nullptr, nullptr};
   size_t mig_send_cap[2] = {0, 0}, mig_recv_cap[2] = {0, 0};  // in particles
@@ -2083,6 +2086,7 @@ int gsmpm_mpm_destroy(gsmpm_mpm* h) {
     (void)hipFree(h->mig_recv[w]);
   }
   (void)hipFree(h->s_drift);
+  (void)hipFree(h->s_rect_dev);
   (void)hipFree(h->gid);
   (void)hipFree(h->gid_alt);
   (void)hipFree(h->cold_alt);

@@ -38,15 +38,17 @@ __global__ __launch_bounds__(256) void k_win_update(GridDims g, SlabWin sw, cons
                                                    const float4* __restrict__ recv1, float4* __restrict__ gvel,
                                                    const BcTable* __restrict__ bct, GridStep gs) {
   const int ng = g.ng;
-  const size_t per = (size_t)sw.W * ng * ng;
-  for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < 2 * per; q += (size_t)gridDim.x * blockDim.x) {
-    const int w = q < per ? 0 : 1;
-    if (!sw.on[w]) continue;
-    const size_t r = q - (size_t)w * per;
-    const int pl = (int)(r / ((size_t)ng * ng));
+  const size_t per0 = sw.on[0] ? (size_t)sw.W * sw.ny[0] * sw.nz[0] : 0;
+  const size_t per1 = sw.on[1] ? (size_t)sw.W * sw.ny[1] * sw.nz[1] : 0;
+  for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < per0 + per1;
+       q += (size_t)gridDim.x * blockDim.x) {
+    const int w = q < per0 ? 0 : 1;
+    const size_t r = q - (w ? per0 : 0);
+    const int ny = sw.ny[w], nz = sw.nz[w];
+    const int pl = (int)(r / ((size_t)ny * nz));
     const int i = sw.a[w] + pl;
     if (i < 0 || i >= ng) continue;
-    const int j = (int)((r / ng) % ng), k = (int)(r % ng);
+    const int j = sw.y0[w] + (int)((r / nz) % ny), k = sw.z0[w] + (int)(r % nz);
     const float4 mine = sw.part[w][r];
     const float4 other = w == 0 ? recv0[r] : recv1[r];
     float4 a = w == 0 ? other : mine;  // lower rank's partial first
@@ -57,6 +59,32 @@ __global__ __launch_bounds__(256) void k_win_update(GridDims g, SlabWin sw, cons
     a.w += b.w;
     gvel[((size_t)i * ng + j) * ng + k] = node_update(a, i, j, k, g, gs, bct);
     sw.part[w][r] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// yz box of the particles' base nodes (trunc(x * inv_dx - 0.5), utils.py:95)
+// -> out4 {min y, max y, min z, max z} (initialised to INT_MAX / INT_MIN).
+__global__ __launch_bounds__(256) void k_slab_bbox(Particles ps, float inv_dx, int* __restrict__ out4) {
+  int v[4] = {INT_MAX, INT_MIN, INT_MAX, INT_MIN};
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < ps.n; p += gridDim.x * 256) {
+    const int by = (int)(ps.ld(PX + 1, p) * inv_dx - 0.5f), bz = (int)(ps.ld(PX + 2, p) * inv_dx - 0.5f);
+    v[0] = min(v[0], by);
+    v[1] = max(v[1], by);
+    v[2] = min(v[2], bz);
+    v[3] = max(v[3], bz);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    v[0] = min(v[0], __shfl_xor(v[0], o));
+    v[1] = max(v[1], __shfl_xor(v[1], o));
+    v[2] = min(v[2], __shfl_xor(v[2], o));
+    v[3] = max(v[3], __shfl_xor(v[3], o));
+  }
+  if ((threadIdx.x & 63) == 0 && v[0] <= v[1]) {
+    atomicMin(out4 + 0, v[0]);
+    atomicMax(out4 + 1, v[1]);
+    atomicMin(out4 + 2, v[2]);
+    atomicMax(out4 + 3, v[3]);
   }
 }
 

@@ -91,6 +91,7 @@ _SIGS = {
     "gsmpm_mpm_count": (ctypes.c_int, [c_void_p]),
     "gsmpm_mpm_get_gid": (ctypes.c_int, [c_void_p, c_void_p, c_void_p]),
     "gsmpm_mpm_slab_stats": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int64)]),
+    "gsmpm_mpm_slab_rects": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int32)]),
     "gsmpm_mpm_resort": (ctypes.c_int, [c_void_p, ctypes.c_int32, c_void_p]),
     "gsmpm_mpm_set_rebin_interval": (ctypes.c_int, [c_void_p, ctypes.c_int32]),
     "gsmpm_mpm_pipeline": (ctypes.c_int, [c_void_p]),

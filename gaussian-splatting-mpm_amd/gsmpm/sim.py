@@ -143,6 +143,12 @@ class Simulator:
         keys = ("migrations", "migrated", "lo", "hi", "margin", "interval", "window_planes", "capacity")
         return dict(zip(keys, [int(v) for v in b]))
 
+    def slab_rects(self):
+        """The exchanged yz rect of the lower and upper window: [(y0, ny, z0, nz)] * 2."""
+        b = (ctypes.c_int32 * 8)()
+        check(LIB.gsmpm_mpm_slab_rects(self._h, b), "gsmpm_mpm_slab_rects")
+        return [tuple(int(v) for v in b[4 * w:4 * w + 4]) for w in (0, 1)]
+
     def profile(self, dt: float, masks):
         """Eager substeps with a hipEvent pair per kernel -> summed ms of
         (k_p2g, k_grid, k_g2p, binning); fused pipeline: (k_fused, k_grid_f, binning, 0)."""

@@ -152,6 +152,11 @@ int gsmpm_mpm_count(gsmpm_mpm* h);
 int gsmpm_mpm_get_gid(gsmpm_mpm* h, int32_t* out, void* stream);
 /* {migrations, particles migrated (sent), lo, hi, margin, interval, window planes, capacity} */
 int gsmpm_mpm_slab_stats(gsmpm_mpm* h, int64_t out8[8]);
+/* The yz rect of each window that the exchange moves, agreed by the two ranks of
+ * the bound at every migration: {y0, ny, z0, nz} of the lower window, then of the
+ * upper one (ny = nz = 0: nothing to exchange; before the first slab_step, the
+ * whole cross-section). */
+int gsmpm_mpm_slab_rects(gsmpm_mpm* h, int32_t out8[8]);
 
 /* Re-sort particle storage into Morton order of the current cells now (only
  * summation order changes; rows stay in caller order).  interval >= 0 also sets

@@ -48,10 +48,14 @@ def _gpu_worker(rank, world, port, out, backend, steps):
         dom.postprocess()
         got["cov"] = dom.gather_field("cov")
         st = dom.stats()
+        rects = np.array(dom.engine.slab_rects(), np.int64).reshape(-1)
         mig = torch.tensor([st["migrated"]], dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(mig)
+        rect_all = [None] * world
+        dist.all_gather_object(rect_all, rects.tolist())
         if rank == 0:
             np.savez(os.path.join(out, "res.npz"), migrated=int(mig.item()), bounds=np.array(dom.bounds),
+                     rects=np.array(rect_all, np.int64),
                      **{k: g.cpu().numpy() for k, g in got.items()})
         dom.engine.close()  # its graphs before the communicator
         xp.close()
@@ -80,6 +84,12 @@ def test_gpu_slabs_match_single_domain_oracle(dev, tmp_path, world):
     r = _run(world, tmp_path)
     if world > 1:
         assert int(r["migrated"]) > 50  # particles crossed slab bounds and migrated
+        # the exchanged rects: agreed by both ranks of a bound, inside the cross-section, smaller than it
+        rc = r["rects"].reshape(world, 2, 4)
+        for b in range(world - 1):
+            assert (rc[b, 1] == rc[b + 1, 0]).all(), rc
+            y0, ny, z0, nz = rc[b, 1].tolist()
+            assert 0 < ny * nz < NG * NG and y0 + ny <= NG and z0 + nz <= NG, rc
     errs = _check(r)
     print("slab", world, errs, "migrated", int(r["migrated"]), "bounds", r["bounds"].tolist())
 
