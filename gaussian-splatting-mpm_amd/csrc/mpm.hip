@@ -1409,6 +1409,8 @@ struct gsmpm_mpm {
   int* mig_boff = nullptr;                   // [nblk][3] their exclusive scan
   int* mig_tot = nullptr;                    // [3] + drift flag copy
   int* mig_host = nullptr;                   // pinned [16]: totals + drift flags + rect handshake
+  int* s_rec = nullptr;                      // [world][8] migration records of every rank (slab_migrate)
+  int* s_rec_host = nullptr;                 // pinned copy
   float* mig_send[2] = {nullptr, nullptr};   // [NMIG][count] payloads
   float* mig_recv[2] = {nullptr, nullptr};
   size_t mig_send_cap[2] = {0, 0}, mig_recv_cap[2] = {0, 0};  // in particles
@@ -2094,6 +2096,8 @@ int gsmpm_mpm_destroy(gsmpm_mpm* h) {
   (void)hipFree(h->mig_boff);
   (void)hipFree(h->mig_tot);
   if (h->mig_host) (void)hipHostFree(h->mig_host);
+  (void)hipFree(h->s_rec);
+  if (h->s_rec_host) (void)hipHostFree(h->s_rec_host);
   if (h->x_host) (void)hipHostFree(h->x_host);
   if (h->s_ev_pack) (void)hipEventDestroy(h->s_ev_pack);
   if (h->s_ev_x) (void)hipEventDestroy(h->s_ev_x);

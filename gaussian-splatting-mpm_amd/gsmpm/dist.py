@@ -20,7 +20,9 @@ on one device (main.py:28); here it is sharded by slab along grid axis 0
   migrate to the neighbour (wave-ballot compaction on the GPU, counts then
   payloads through the transport).  A particle drifting more than ``margin``
   planes between migrations would have scattered outside the exchanged
-  windows; the library detects it and ``step`` raises.
+  windows; the library detects it (and a slab over capacity) and ``step``
+  raises on every rank at the same migration, since every rank's migration
+  record goes to every rank.
 
 ``SlabDomain`` is one rank's view: the engine (``gsmpm.sim.Simulator`` in
 slab mode), the transport, and ``gather`` of per-particle outputs to one rank

@@ -143,7 +143,10 @@ int gsmpm_mpm_slab_set_particles(gsmpm_mpm* h, int32_t n, const float* x, const 
 /* n_substeps substeps of the slab (bc masks as gsmpm_mpm_step), window
  * exchange every substep and particle migration every `interval` substeps
  * through `xp`.  Returns GSMPM_ESTATE if a particle drifted past the margin
- * (its contributions were not exchanged: the state is invalid). */
+ * (its contributions were not exchanged: the state is invalid) or a slab
+ * would exceed its capacity: every rank's migration record goes to every
+ * rank, so all ranks return it at the same migration, with the same message
+ * naming the rank at fault. */
 int gsmpm_mpm_slab_step(gsmpm_mpm* h, float dt, int32_t n_substeps, const uint32_t* bc_active_mask,
                         const gsmpm_transport* xp, void* stream);
 /* current particle count of this rank (changes with migration) */

@@ -6,8 +6,11 @@ split substep, with the same sequence the library runs: per substep P2G
 [b - M, b + M + 2) around each shared bound, the swap through the transport
 (gsmpm.dist.CallbackTransport.exchange, gloo), total = lower rank's partial +
 upper rank's (f32), grid update + G2P (substep_end); every `interval`
-substeps the migration (counts, then payloads; stayers first, then arrivals
-from below, then from above).  gsmpm.dist.SlabDomain drives it exactly as it
+substeps the migration (every rank's record {send to lower, send to upper,
+stayers, error bits, capacity} to every other rank, then the payloads;
+stayers first, then arrivals from below, then from above).  Errors (a drift
+past the margin, a slab over capacity) are checked on the records, so every
+rank raises the same error at the same migration, as the library does.  gsmpm.dist.SlabDomain drives it exactly as it
 drives gsmpm.sim.Simulator, so the CPU tests exercise the domain code
 (partition, chunking, transport, gather) against the single-domain oracle.
 """
@@ -31,6 +34,7 @@ class OracleSlabEngine:
         self.bcs = []  # ("op"|"imp", args) in add order = mask bit order
         self.since = 0
         self.migrated = 0
+        self.err = 0  # bit 0: a particle drifted past the margin (reported at the next migration)
 
     # -- slab setup
     def slab_init(self, rank, world, lo, hi, margin, interval):
@@ -78,7 +82,7 @@ class OracleSlabEngine:
         ia, oa = self._masks(mask)
         b = np.trunc(self.o.x[:, 0] * np.float32(self.inv_dx) - np.float32(0.5)).astype(np.int64)
         if len(b) and ((b < self.lo - self.M) | (b >= self.hi + self.M)).any():
-            raise RuntimeError("a particle drifted past the slab margin")
+            self.err |= 1
         self.o.substep_begin(dt, ia)
         peers, ws = self._peers()
         mine = [self.o.window_sums(self.a[w], self.W) for w in ws]
@@ -102,11 +106,20 @@ class OracleSlabEngine:
                               [self.gid.view(np.float32).reshape(-1, 1)], 1)
         peers, ws = self._peers()
         send = [np.ascontiguousarray(rows[dest == (0 if w == 0 else 2)]) for w in ws]
-        cnt_s = [np.array([len(s)], np.int32) for s in send]
-        cnt_r = [np.zeros(1, np.int32) for _ in send]
         u8 = lambda a: torch.from_numpy(a.view(np.uint8).reshape(-1))
-        xp.exchange(peers, [u8(c) for c in cnt_s], [u8(c) for c in cnt_r])
-        recv = [np.empty((int(c[0]), WIDTH), np.float32) for c in cnt_r]
+        recs = np.zeros((self.world, 8), np.int32)
+        recs[self.rank, :5] = [(dest == 0).sum(), (dest == 2).sum(), (dest == 1).sum(), self.err, self.cap]
+        others = [r for r in range(self.world) if r != self.rank]
+        xp.exchange(others, [u8(recs[self.rank].copy()) for _ in others], [u8(recs[r]) for r in others])
+        for r in range(self.world):
+            if recs[r, 3] & 1:
+                raise RuntimeError(f"rank {r}: a particle drifted past the slab margin")
+            n_new = recs[r, 2] + (recs[r - 1, 1] if r > 0 else 0) + (recs[r + 1, 0] if r < self.world - 1 else 0)
+            if n_new > recs[r, 4]:
+                raise RuntimeError(f"rank {r}: {n_new} particles after the migration, in a slab of capacity "
+                                   f"{recs[r, 4]}")
+        cnt_r = [recs[self.rank + (-1 if w == 0 else 1), 1 if w == 0 else 0] for w in ws]
+        recv = [np.empty((int(c), WIDTH), np.float32) for c in cnt_r]
         xp.exchange(peers, [u8(s) for s in send], [u8(r) for r in recv])
         got = {0: np.zeros((0, WIDTH), np.float32), 2: np.zeros((0, WIDTH), np.float32)}
         for w, r in zip(ws, recv):

@@ -59,7 +59,13 @@ def reference(x, v, cov, vol, steps=STEPS):
     return ref
 
 
-def _cpu_worker(rank, world, port, out, control):
+def top_rank_start_count(x, world):
+    """Particles the top slab starts with: as its capacity, the first arrivals overflow it."""
+    from gsmpm.dist import owner_of, slab_bounds
+    return int((owner_of(x, slab_bounds(x, NG, EXT, world, 2), NG, EXT) == world - 1).sum())
+
+
+def _cpu_worker(rank, world, port, out, control, full_top=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -71,12 +77,22 @@ def _cpu_worker(rank, world, port, out, control):
             wbytes = 6 * NG * NG * 16
             xp.exchange = lambda peers, s, r, f=xp.exchange: [t.zero_() for t in r] \
                 if s and s[0].numel() == wbytes else f(peers, s, r)
+        cap = top_rank_start_count(x, world) if full_top and rank == world - 1 else None
         dom = SlabDomain(x, cov, vol, v=v, rank=rank, world=world, transport=xp, n_grid=NG, grid_extent=EXT,
-                         margin=2, interval=10, device="cpu", engine_factory=OracleSlabEngine,
+                         margin=2, interval=10, capacity=cap, device="cpu", engine_factory=OracleSlabEngine,
                          jelly_quirk=False, **KW)
         dom.add_fixed_cube(*FIXED)
         dom.add_plane_collider([0, 0, 0.4], [0, 0, 1])
         n0 = dom.n
+        if full_top:  # every rank must raise, at the same migration, with the same message
+            try:
+                dom.step(DT, [0b11] * STEPS)
+                msg = "no error"
+            except RuntimeError as e:
+                msg = str(e)
+            with open(os.path.join(out, f"err{rank}.txt"), "w") as f:
+                f.write(f"{dom.engine.since}|{msg}")
+            return
         dom.step(DT, [0b11] * STEPS)
         got = {k: dom.gather_field(k) for k in ("x", "v", "C", "F_trial")}
         mig = torch.tensor([dom.engine.migrated], dtype=torch.int64)
@@ -91,6 +107,10 @@ def _cpu_worker(rank, world, port, out, control):
 def _run(world, tmp_path, control=False):
     mp.spawn(_cpu_worker, args=(world, free_port(), str(tmp_path), control), nprocs=world, join=True)
     return np.load(os.path.join(tmp_path, "res.npz"))
+
+
+def read_errors(tmp_path, world):
+    return [open(os.path.join(tmp_path, f"err{r}.txt")).read() for r in range(world)]
 
 
 def test_slab_bounds_and_owner():
@@ -124,3 +144,18 @@ def test_slab_without_exchange_is_wrong(tmp_path):
     r = _run(2, tmp_path, control=True)
     ref = reference(x, v, cov, vol)
     assert rel_err(r["v"], ref.v) > 1e-2
+
+
+def test_slab_error_stops_every_rank(tmp_path):
+    """The top slab is created full (capacity = its starting count): the first
+    particles that migrate into it overflow it.  Every rank -- not only the
+    top one and its neighbour -- raises the same error at the same migration
+    (the records of every rank are exchanged), so none is left blocked in an
+    exchange with a rank that stopped."""
+    world = 4
+    mp.spawn(_cpu_worker, args=(world, free_port(), str(tmp_path), False, True), nprocs=world, join=True)
+    errs = read_errors(tmp_path, world)
+    assert len(set(errs)) == 1, errs
+    since, msg = errs[0].split("|", 1)
+    assert f"rank {world - 1}:" in msg and "capacity" in msg, msg
+    assert int(since) % 10 == 0 and int(since) < STEPS, since

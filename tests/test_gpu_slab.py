@@ -20,12 +20,13 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from conftest import rel_err
-from test_dist_slab import DT, EXT, FIXED, KW, NG, STEPS, TOL, free_port, reference, scene
+from test_dist_slab import (DT, EXT, FIXED, KW, NG, STEPS, TOL, free_port, read_errors, reference, scene,
+                            top_rank_start_count)
 
 pytestmark = pytest.mark.gpu
 
 
-def _gpu_worker(rank, world, port, out, backend, steps):
+def _gpu_worker(rank, world, port, out, backend, steps, full_top=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dev_index = rank if backend == "nccl" else 0
     torch.cuda.set_device(dev_index)
@@ -38,10 +39,23 @@ def _gpu_worker(rank, world, port, out, backend, steps):
         from gsmpm.dist import SlabDomain, make_transport
         x, v, cov, vol = scene()
         xp = make_transport(rank, world, device=dev)
+        cap = top_rank_start_count(x, world) if full_top and rank == world - 1 else None
         dom = SlabDomain(x, cov, vol, v=v, rank=rank, world=world, transport=xp, n_grid=NG, grid_extent=EXT,
-                         margin=2, interval=10, device=dev, jelly_fcr=True, **KW)
+                         margin=2, interval=10, capacity=cap, device=dev, jelly_fcr=True, **KW)
         dom.add_fixed_cube(*FIXED)
         dom.add_plane_collider([0, 0, 0.4], [0, 0, 1])
+        if full_top:  # every rank must raise, at the same migration, with the same message
+            from gsmpm._lib import GsmpmError
+            try:
+                dom.step(DT, [0b11] * steps)
+                msg = "no error"
+            except GsmpmError as e:
+                msg = str(e)
+            with open(os.path.join(out, f"err{rank}.txt"), "w") as f:
+                f.write(f"{dom.stats()['migrations']}|{msg}")
+            dom.engine.close()
+            xp.close()
+            return
         for s in range(0, steps, 50):  # several calls: chunks continue across calls
             dom.step(DT, [0b11] * min(50, steps - s))
         got = {k: dom.gather_field(k) for k in ("x", "v", "C", "F_trial")}
@@ -115,3 +129,17 @@ def test_slab_refuses_thin_slab_and_plain_step(dev):
         sim.step(DT, [1])  # a slab steps through gsmpm_mpm_slab_step only
     with pytest.raises(GsmpmError):
         sim.slab_step(DT, [1], None)  # rank 0 of 2 has a neighbour: no transport, no step
+
+
+def test_gpu_slab_error_stops_every_rank(dev, tmp_path):
+    """As tests/test_dist_slab.py::test_slab_error_stops_every_rank, on the
+    library: the top slab of 4 is created full, the first arrivals overflow
+    it, and all 4 ranks raise the same error after the same migration count
+    (gsmpm_mpm_slab_step exchanges every rank's migration record)."""
+    world = 4
+    mp.spawn(_gpu_worker, args=(world, free_port(), str(tmp_path), "gloo", STEPS, True), nprocs=world, join=True)
+    errs = read_errors(tmp_path, world)
+    assert len(set(errs)) == 1, errs
+    migs, msg = errs[0].split("|", 1)
+    assert f"rank {world - 1}:" in msg and "capacity" in msg, msg
+    assert int(migs) < STEPS // 10, migs
