@@ -217,6 +217,9 @@ __device__ __forceinline__ bool in_grid(const float (&x)[3], const GridDims& g) 
 // `bin` (uniform): re-bin the particles by their new x into `bo`.
 // Particle storage is in bin order (permuted at every binning), so chunk w's
 // particles are storage rows [first, first + cnt).
+#ifndef GSMPM_STORE_VC
+#define GSMPM_STORE_VC 0  // 1: every G2P stores v and C (A/B)
+#endif
 template <int MAT, int MODE>
 __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTiles tl, ChunkIn ck, Touch tc, BinOutF bo,
                                                int bin, int use_box, const float4* __restrict__ gvel,
@@ -341,15 +344,18 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
         }
         float Fn[3][3];
         f_trial(gvd, F, dt, Fn);
+        // v and C: stored by the last launch of a step only.  The P2G half
+        // takes them from registers, and the next launch's G2P recomputes
+        // both from the grid, so a G2P + P2G launch's copies are never read.
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-          ps.st(PV + d, p, v[d]);
+          if (!P2G || GSMPM_STORE_VC) ps.st(PV + d, p, v[d]);
           x[d] = x[d] + dt * v[d];
           ps.st(PX + d, p, x[d]);
         }
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
-          ps.st(PC + i, p, C[i / 3][i % 3]);
+          if (!P2G || GSMPM_STORE_VC) ps.st(PC + i, p, C[i / 3][i % 3]);
           F[i / 3][i % 3] = Fn[i / 3][i % 3];
         }
         // F_trial is stored here unless the return map below replaces it

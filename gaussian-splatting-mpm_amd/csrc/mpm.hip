@@ -875,6 +875,7 @@ struct BinPermute {
   int np;
   const int* osrc;
   int* odst;
+  int skip_vc;  // v and C are dead (a re-binning between G2P + P2G launches, fused.h): not moved
 };
 __global__ __launch_bounds__(256) void k_finish_bins(Tiles tl, const int* __restrict__ count, ChunkOut co, int n,
                                                      const int* __restrict__ ptile, const int* __restrict__ pslot,
@@ -951,11 +952,14 @@ __global__ __launch_bounds__(256) void k_finish_bins(Tiles tl, const int* __rest
     const int d = s_off[pt] + psl;
     if (bp.dst) {
       float v[NPLANES];
+      const bool skip = bp.skip_vc != 0;
 #pragma unroll
-      for (int q = 0; q < NPLANES; ++q) v[q] = bp.src[(size_t)q * bp.np + p];
+      for (int q = 0; q < NPLANES; ++q)
+        if (!(skip && q >= PV && q < PF)) v[q] = bp.src[(size_t)q * bp.np + p];
       const int o = bp.osrc[p];
 #pragma unroll
-      for (int q = 0; q < NPLANES; ++q) bp.dst[(size_t)q * bp.np + d] = v[q];
+      for (int q = 0; q < NPLANES; ++q)
+        if (!(skip && q >= PV && q < PF)) bp.dst[(size_t)q * bp.np + d] = v[q];
       bp.odst[d] = o;
     } else {
       list[d] = p;
@@ -1507,9 +1511,9 @@ static int finish_binning_f(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_
 // launch on the fused path (k_finish_bins moves the particles), else the
 // list kernels followed by k_permute
 static int permute_to_bins(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t* ev);
-static int rebin_permute_f(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t* ev = nullptr) {
+static int rebin_permute_f(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t* ev = nullptr, bool vc_live = true) {
   if (bins_fused(ftiles_flat(h)) && h->fuse_permute) {
-    const BinPermute bp{h->planes, h->planes_alt, h->np, h->orig, h->orig_alt};
+    const BinPermute bp{h->planes, h->planes_alt, h->np, h->orig, h->orig_alt, (vc_live || GSMPM_STORE_VC) ? 0 : 1};
     int rc = finish_bins_on(h, ftiles_flat(h), h->fcount[c], chunk_out_f(h, c), h->flist[c], st, ev, bp);
     if (rc) return rc;
     if (ev) {  // the permute's timing pair: nothing left to time
@@ -1707,7 +1711,7 @@ static int launch_substeps_f(gsmpm_mpm* h, float dt, int nsub, const uint32_t* b
     if (mode & 2) wp = bp;
     boxed = (mode & 2) && !bin;
     if (bin) {
-      rc = rebin_permute_f(h, bp ^ 1, st, e8 ? e8 + 4 : nullptr);
+      rc = rebin_permute_f(h, bp ^ 1, st, e8 ? e8 + 4 : nullptr, /*vc_live=*/mode != 3);
       if (rc) return rc;
       bp ^= 1;
       zeroed = false;
