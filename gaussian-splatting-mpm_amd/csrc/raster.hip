@@ -44,6 +44,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
 
 #include <chrono>
 #include <cstdlib>
@@ -492,10 +493,14 @@ __global__ __launch_bounds__(256) void k_ids(int K, const unsigned* __restrict__
 // list in (depth, Gaussian index) order -- the list upstream's 64-bit
 // (tile << 32 | depth bits) sort produces, with 4-byte keys and 12 bits of
 // radix instead of 32 + 12.
-__global__ __launch_bounds__(256) void k_tiles_by_rank(int P, const unsigned* __restrict__ order,
-                                                       const unsigned* __restrict__ tiles, unsigned* __restrict__ tr) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r < P) tr[r] = tiles[order[r]];
+// tiles touched by the Gaussian of depth rank r: the depth-order scan's input
+struct TilesOfRank {
+  const unsigned* tiles;
+  __host__ __device__ unsigned operator()(unsigned g) const { return tiles[g]; }
+};
+inline rocprim::transform_iterator<const unsigned*, TilesOfRank, unsigned> ranked_tiles(const unsigned* order,
+                                                                                        const unsigned* tiles) {
+  return rocprim::transform_iterator<const unsigned*, TilesOfRank, unsigned>(order, TilesOfRank{tiles});
 }
 // Depth-ordered emission, one lane per pair (a lane per Gaussian would
 // serialise the ~1600 stores of the frame's largest Gaussians): the pair's
@@ -1091,12 +1096,13 @@ struct gsmpm_raster {
   void* sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
   unsigned* ids_sorted = nullptr;  // Gaussian id per sorted pair (vals_sorted holds emission indices)
-  unsigned *dorder = nullptr, *dsorted = nullptr, *tr = nullptr, *offr = nullptr;  // [capP] depth order, ranked tiles/offsets
+  unsigned *dorder = nullptr, *dsorted = nullptr, *offr = nullptr;  // [capP] depth order, depth-order tile offsets
   void* dsort_tmp = nullptr;
   unsigned* hist = nullptr;  // [2 * capH] tile-major chunk histogram, then its exclusive scan
   size_t capH = 0;
   size_t dsort_tmp_bytes = 0;
   bool slots_pending = false;
+  bool offsets_pending = false;  // depth-ordered forward: the index-order tile scan (offsets) is left to the backward
   bool emit_culled = false;  // the tile lists omit culled pairs: their records must read zero  // vals_sorted still to be derived (depth-ordered path)
   float4* rec = nullptr;           // backward pair records, 3 x float4 per pair
   size_t capRec = 0;
@@ -1144,7 +1150,7 @@ int gsmpm_raster_destroy(gsmpm_raster* r) {
   for (void* p : {(void*)r->radii_tmp, (void*)r->depth, (void*)r->xy, (void*)r->conic, (void*)r->rgb, (void*)r->tiles,
                   (void*)r->offsets, r->scan_tmp, (void*)r->keys, (void*)r->keys_sorted, (void*)r->vals,
                   (void*)r->vals_sorted, r->sort_tmp, (void*)r->ranges, (void*)r->ids_sorted, (void*)r->rec,
-                  (void*)r->final_T, (void*)r->n_contrib, (void*)r->dorder, (void*)r->dsorted, (void*)r->tr, (void*)r->offr, r->dsort_tmp, (void*)r->hist})
+                  (void*)r->final_T, (void*)r->n_contrib, (void*)r->dorder, (void*)r->dsorted, (void*)r->offr, r->dsort_tmp, (void*)r->hist})
     if (p) (void)hipFree(p);
   if (r->h_count) (void)hipHostFree(r->h_count);
   if (r->count_ev) (void)hipEventDestroy(r->count_ev);
@@ -1204,7 +1210,6 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     if ((rc = grow((void**)&r->offsets, cap * sizeof(unsigned)))) return rc;
     if ((rc = grow((void**)&r->dorder, cap * sizeof(unsigned)))) return rc;
     if ((rc = grow((void**)&r->dsorted, cap * sizeof(unsigned)))) return rc;
-    if ((rc = grow((void**)&r->tr, cap * sizeof(unsigned)))) return rc;
     if ((rc = grow((void**)&r->offr, cap * sizeof(unsigned)))) return rc;
     size_t bytes = 0;
     GSMPM_HIP(rocprim::radix_sort_pairs(nullptr, bytes, reinterpret_cast<unsigned*>(r->depth), r->dsorted,
@@ -1214,6 +1219,10 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     r->dsort_tmp_bytes = bytes;
     bytes = 0;
     GSMPM_HIP(rocprim::inclusive_scan(nullptr, bytes, r->tiles, r->offsets, cap, rocprim::plus<unsigned>(), st));
+    size_t gbytes = 0;
+    GSMPM_HIP(rocprim::inclusive_scan(nullptr, gbytes, ranked_tiles(r->dorder, r->tiles), r->offr, cap,
+                                      rocprim::plus<unsigned>(), st));
+    bytes = std::max(bytes, gbytes);
     if ((rc = grow(&r->scan_tmp, bytes))) return rc;
     r->scan_tmp_bytes = bytes;
     r->capP = cap;
@@ -1241,6 +1250,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
   const char* rm = std::getenv("GSMPM_RASTER_RENDER_MODE");
   const int render_mode = rm ? std::atoi(rm) & 1 : 0;
   r->slots_pending = false;
+  r->offsets_pending = false;
   r->emit_culled = false;
   const unsigned* tkeys = nullptr;  // sorted tile keys with sub-tile masks (chunked path)
   unsigned K = 0;
@@ -1249,7 +1259,13 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
                        r->rgb, r->tiles);
     GSMPM_LAUNCH_CHECK();
     size_t bytes = r->scan_tmp_bytes;
-    GSMPM_HIP(rocprim::inclusive_scan(r->scan_tmp, bytes, r->tiles, r->offsets, (size_t)P, rocprim::plus<unsigned>(), st));
+    // the index-order scan (offsets) feeds only the backward's record slots
+    // and the upstream-keyed path: a depth-ordered forward takes K from the
+    // depth-order scan and leaves offsets to gsmpm_raster_backward (one scan
+    // and its look-back init launch less per frame)
+    r->offsets_pending = depth_ordered;
+    if (!depth_ordered)
+      GSMPM_HIP(rocprim::inclusive_scan(r->scan_tmp, bytes, r->tiles, r->offsets, (size_t)P, rocprim::plus<unsigned>(), st));
     if (depth_ordered) {
       // the depth order depends on P only: it runs before the count read-back,
       // queued behind whatever the stream is still doing
@@ -1257,11 +1273,10 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       GSMPM_HIP(rocprim::radix_sort_pairs(r->dsort_tmp, bytes, reinterpret_cast<unsigned*>(r->depth),
                                                         r->dsorted, rocprim::counting_iterator<unsigned>(0u),
                                                         r->dorder, (size_t)P, 0, 32, st));
-      hipLaunchKernelGGL(k_tiles_by_rank, dim3(div_up(P, 256)), dim3(256), 0, st, P, (const unsigned*)r->dorder,
-                         (const unsigned*)r->tiles, r->tr);
-      GSMPM_LAUNCH_CHECK();
+      // the scan reads tiles[dorder[r]] itself (no separate gather launch)
       bytes = r->scan_tmp_bytes;
-      GSMPM_HIP(rocprim::inclusive_scan(r->scan_tmp, bytes, r->tr, r->offr, (size_t)P, rocprim::plus<unsigned>(), st));
+      GSMPM_HIP(rocprim::inclusive_scan(r->scan_tmp, bytes, ranked_tiles(r->dorder, r->tiles), r->offr, (size_t)P,
+                                        rocprim::plus<unsigned>(), st));
     }
     // K straight into pinned, coherent host memory by a one-lane kernel, and a
     // spin on it: no copy-engine packet and no sleeping stream sync between
@@ -1275,7 +1290,8 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
                   "gsmpm_raster_forward: the pair count is read on the host; the stream must not be capturing");
     volatile unsigned* hc = r->h_count;
     *hc = kNoCount;
-    hipLaunchKernelGGL(k_publish_count, dim3(1), dim3(1), 0, st, (const unsigned*)(r->offsets + (P - 1)), r->h_count);
+    hipLaunchKernelGGL(k_publish_count, dim3(1), dim3(1), 0, st,
+                       (const unsigned*)((depth_ordered ? r->offr : r->offsets) + (P - 1)), r->h_count);
     GSMPM_LAUNCH_CHECK();
     GSMPM_HIP(hipEventRecord(r->count_ev, st));
     for (unsigned polls = 1; *hc == kNoCount; ++polls) {
@@ -1418,6 +1434,12 @@ int gsmpm_raster_backward(gsmpm_raster* r, const gsmpm_raster_args* in, const in
     int rc;
     if ((rc = grow((void**)&r->rec, (K + K / 4 + 1024) * 3 * sizeof(float4)))) return rc;
     r->capRec = K + K / 4 + 1024;
+  }
+  if (r->offsets_pending) {  // the forward's tiles are still in r->tiles
+    size_t bytes = r->scan_tmp_bytes;
+    GSMPM_HIP(rocprim::inclusive_scan(r->scan_tmp, bytes, r->tiles, r->offsets, (size_t)in->P,
+                                      rocprim::plus<unsigned>(), st));
+    r->offsets_pending = false;
   }
   if (K > 0 && r->slots_pending) {
     hipLaunchKernelGGL(k_slots, dim3(div_up(K, 256)), dim3(256), 0, st, (int)K,
