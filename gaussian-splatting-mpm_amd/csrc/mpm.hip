@@ -45,6 +45,11 @@
 
 namespace gsmpm {
 
+#ifndef GSMPM_REBIN_SF
+#define GSMPM_REBIN_SF 15
+#endif
+constexpr int kRebinStressFree = GSMPM_REBIN_SF;  // default re-binning interval, stress-free materials
+constexpr int kRebinStress = 10;                  // ... stress-bearing ones
 constexpr int kChunk = 256;  // particles per work chunk (one per lane of a 256-lane workgroup)
 
 // Workgroup timeline stamps (diagnostics): [kernel][wg][start, end] in
@@ -1385,7 +1390,7 @@ struct gsmpm_mpm {
   int* orig_alt = nullptr;                //   storage into bin order, alternating planes / planes_alt
   int fbpar = 0;                          // parity of the bins the next k_fused reads
   int fep = 0;                            // escape flag the next P2G raises
-  int rebin_interval = 10;                // substeps between re-binnings (fused pipeline)
+  int rebin_interval = 10;                // substeps between re-binnings (fused pipeline; set by material at create)
   std::map<std::vector<uint32_t>, hipGraphExec_t> graphs;
   std::map<std::vector<uint32_t>, int> graph_box_parity;
   struct FState {
@@ -1931,6 +1936,10 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
   h->mc.pvisc = (float)prm->plastic_viscosity;
   h->mat_kernel = prm->material;
   if (prm->material == 0 && (prm->flags & GSMPM_FLAG_JELLY_FCR)) h->mat_kernel = 4;
+  // re-binning interval: stress-free jelly every kRebinStressFree substeps; a
+  // stress-bearing material's plastic flow amplifies the change of summation
+  // order a longer interval brings (metal F_trial 1.22e-4 at 15)
+  h->rebin_interval = h->mat_kernel == 0 ? kRebinStressFree : kRebinStress;
   const size_t nn = (size_t)h->g.ng * h->g.ng * h->g.ng;
   auto fail = [&](hipError_t e, const char* what) {
     set_error(std::string(what) + ": " + hipGetErrorString(e));
