@@ -46,7 +46,7 @@
 namespace gsmpm {
 
 #ifndef GSMPM_REBIN_SF
-#define GSMPM_REBIN_SF 15
+#define GSMPM_REBIN_SF 20
 #endif
 constexpr int kRebinStressFree = GSMPM_REBIN_SF;  // default re-binning interval, stress-free materials
 constexpr int kRebinStress = 10;                  // ... stress-bearing ones
@@ -1699,12 +1699,24 @@ static int launch_substeps_f(gsmpm_mpm* h, float dt, int nsub, const uint32_t* b
                              hipEvent_t* ev = nullptr, float* kernel_ms = nullptr,
                              const gsmpm_transport* xp = nullptr) {
   const int R = std::max(1, h->rebin_interval);
+  // m re-binnings, evenly spread (spacing <= R), the last at the end.  Each one
+  // flips the bins parity and the particle buffer, which key the captured
+  // graphs, so outside slabs m is made even: an odd m alternates two graphs
+  // per BC-mask sequence from call to call (a capture inside a timed frame).
+  // Slabs re-bin every R substeps, in step with their migrations.
+  int m = std::max(1, (nsub + R - 1) / R);
+  if (!h->slab && (m & 1) && m < nsub) ++m;
+  auto bin_at = [&](int s) {
+    if (s == nsub) return true;
+    if (s <= 0) return false;
+    return h->slab ? s % R == 0 : (long)s * m / nsub > (long)(s - 1) * m / nsub;
+  };
   int wp = bp;
   bool zeroed = false;  // counts / flags of parity bp ^ 1 zeroed by a grid launch since the last binning
   bool boxed = false;   // the last k_fused launch did P2G on the bins parity bp
   for (int s = 0; s <= nsub; ++s) {
     const int mode = s == 0 ? 2 : (s == nsub ? 1 : 3);
-    const bool bin = s == nsub || (s > 0 && s % R == 0);
+    const bool bin = bin_at(s);
     const uint32_t mask = s < nsub ? (bc ? bc[s] : 0xffffffffu) : 0u;
     hipEvent_t* e8 = ev ? ev + 8 * s : nullptr;
     if (bin && !zeroed) {
@@ -1722,7 +1734,7 @@ static int launch_substeps_f(gsmpm_mpm* h, float dt, int nsub, const uint32_t* b
       zeroed = false;
     }
     if (s < nsub) {
-      const bool next_bin = s + 1 == nsub || (s + 1) % R == 0;
+      const bool next_bin = bin_at(s + 1);
       int *zc = nullptr, *zf = nullptr;
       if (next_bin && wp == bp) {  // this grid launch does not read parity bp ^ 1
         zc = h->fcount[bp ^ 1];
@@ -1738,7 +1750,7 @@ static int launch_substeps_f(gsmpm_mpm* h, float dt, int nsub, const uint32_t* b
   if (ev) {
     GSMPM_HIP(hipStreamSynchronize(st));
     for (int s = 0; s <= nsub; ++s) {
-      const bool bin = s == nsub || (s > 0 && s % R == 0);
+      const bool bin = bin_at(s);
       for (int k = 0; k < 4; ++k) {
         if ((k == 1 && s == nsub) || (k >= 2 && !bin)) continue;
         float ms = 0.f;
