@@ -60,7 +60,40 @@ def parse():
     ap.add_argument("--dp", action="store_true",
                     help="N > 1: independent scenes per rank (no exchange) instead of the default slab sharding")
     ap.add_argument("--rebin", type=int, default=0, help="fused pipeline: substeps between re-binnings (0: library default)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch check only: start the ranks, form the process group, print the JSON line's "
+                         "rank bookkeeping (n_gpus, parallelism) with value null; no GPU work")
     return ap.parse_args()
+
+
+def free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """--gpus N > 1 without a launcher around us: start N rank processes with
+    torch.distributed.run (one per GPU, rendezvous on 127.0.0.1) and return
+    their exit code.  Runs before anything touches the GPU in this process,
+    and starts the ranks as a child (never exec)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def resolve_world(args):
+    """(rank, world, local_rank) of this process, checked against --gpus: the
+    rank count comes from the flag, and a launcher that started a different
+    number of ranks is an error -- never a silent one-rank run."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were started")
+    return int(os.environ.get("RANK", "0")), world, int(os.environ.get("LOCAL_RANK", "0"))
 
 
 # models/bicycle/cameras.json record 0 of the reference (intrinsics only: main.py's
@@ -336,14 +369,40 @@ def config_e(dev, iters=5):
             "particle_substeps_per_s_fwd_bwd": 2 * bf.NSUB * n / (ms * 1e-3)}
 
 
-def main():
-    args = parse()
+def dry_run(args, rank, world):
+    """--dry-run: the launch bookkeeping of the real run on the CPU (gloo), so
+    tests can check that --gpus N starts N ranks that agree on N."""
     import torch
     import torch.distributed as dist
+    if world > 1:
+        dist.init_process_group("gloo")
+        t = torch.ones(1)
+        dist.all_reduce(t)
+        ranks = int(t.item())
+    else:
+        ranks = 1
+    slab = world > 1 and not args.dp
+    out = {"metric": METRIC, "value": None, "unit": "particle-substeps/s", "n_gpus": ranks, "dry_run": True,
+           "scaling": "strong" if slab else "weak",
+           "config": {"parallelism": (f"slab{world}" if slab else f"dp{world} independent scenes") if world > 1
+                      else "single"}}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+def main():
+    args = parse()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
+    rank, world, local = resolve_world(args)
+    if args.dry_run:
+        return dry_run(args, rank, world)
+    import torch
+    import torch.distributed as dist
     # GSMPM_DIST_BACKEND=gloo (+ GSMPM_SHARE_GPU=1: every rank on cuda:0) is for
     # rehearsing the multi-rank path on a one-GPU box; the driver uses RCCL.
     backend = os.environ.get("GSMPM_DIST_BACKEND", "nccl")

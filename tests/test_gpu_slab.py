@@ -26,9 +26,24 @@ from test_dist_slab import (DT, EXT, FIXED, KW, NG, STEPS, TOL, free_port, read_
 pytestmark = pytest.mark.gpu
 
 
+def shared_gpu_rccl_env(rank):
+    """RCCL refuses two ranks on one device ("Duplicate GPU detected": same
+    host hash and bus id).  A distinct NCCL_HOSTID per rank makes every rank
+    a host of its own, so the communicator forms over RCCL's socket transport
+    on the loopback interface: the library's RCCL sequence -- grouped
+    ncclSend/ncclRecv, captured into the chunk graphs -- then runs with every
+    rank on cuda:0.  Only the wire differs from xGMI P2P."""
+    return {"NCCL_HOSTID": f"gsmpm-slab-rank{rank}", "NCCL_SOCKET_IFNAME": "lo", "NCCL_IB_DISABLE": "1"}
+
+
 def _gpu_worker(rank, world, port, out, backend, steps, full_top=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dev_index = rank if backend == "nccl" else 0
+    if backend == "nccl-shared":
+        os.environ.update(shared_gpu_rccl_env(rank))
+        backend = "nccl"
+        dev_index = 0
+    else:
+        dev_index = rank if backend == "nccl" else 0
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
     if backend == "nccl":
@@ -106,6 +121,18 @@ def test_gpu_slabs_match_single_domain_oracle(dev, tmp_path, world):
             assert 0 < ny * nz < NG * NG and y0 + ny <= NG and z0 + nz <= NG, rc
     errs = _check(r)
     print("slab", world, errs, "migrated", int(r["migrated"]), "bounds", r["bounds"].tolist())
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gpu_slabs_rccl_shared_gpu(dev, tmp_path, world):
+    """The RCCL transport -- the path bench.py --gpus N runs -- with every rank
+    on cuda:0 (shared_gpu_rccl_env): chunks of 10 substeps replay as captured
+    graphs holding the window exchanges, and migrations change every slab's
+    particle count between replays of the same graph key."""
+    r = _run(world, tmp_path, backend="nccl-shared")
+    assert int(r["migrated"]) > 50
+    errs = _check(r)
+    print("rccl shared gpu", world, errs, "migrated", int(r["migrated"]))
 
 
 @pytest.mark.skipif(torch.cuda.device_count() < 2, reason="RCCL needs one GPU per rank")
