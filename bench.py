@@ -171,6 +171,30 @@ def make_sim(scene, dev, use_graph=True, slab=None):
     return sim, specs
 
 
+def algorithmic_bytes_live(n, live_nodes, material):
+    """The same split with the grid counted as the nodes the kernels own: the
+    touched tiles' nodes (live_nodes = touched tiles x 448 of the fused
+    pipeline's 8x8x7 tiles) instead of the dense n^3 the reference sweeps --
+    the bytes a sparse implementation must move at least, so the fraction it
+    gives is a bandwidth fraction (<= 1)."""
+    plastic = 8 * n if material in ("metal",) else 0
+    return {"k_fused": 208 * n + 28 * live_nodes + plastic, "k_grid_f": 28 * live_nodes}
+
+
+def source_sha():
+    """Hash of the kernel sources (csrc/*.hip, *.h, *.inc): a committed PMC
+    traffic figure is only reported while the kernels it was measured on are
+    the ones built."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    for f in sorted(glob.glob(os.path.join(PKG, "csrc", "*.hip")) + glob.glob(os.path.join(PKG, "csrc", "*.h")) +
+                    glob.glob(os.path.join(PKG, "csrc", "*.inc"))):
+        with open(f, "rb") as fh:
+            h.update(os.path.basename(f).encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
 def algorithmic_bytes(n, n_grid, material):
     """Per-launch algorithmic bytes: SURVEY.md §8(d)'s per-substep figure
     B_sub = 208 N + 56 n^3 (+ 8 N for plastic materials), split over the kernel
@@ -188,19 +212,41 @@ def algorithmic_bytes(n, n_grid, material):
 
 
 def measured_traffic(kernel, workload):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
-    (profiles/traffic.json, written by tools/traffic.py from separate
-    FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950 note in
-    MI355X_MICROARCH.md) when it was measured on this same workload, else None."""
-    path = os.path.join(ROOT, "profiles", "traffic.json")
-    try:
-        with open(path) as f:
-            t = json.load(f)
-        if t.get("workload") != workload:
-            return None
-        return t["kernels"][kernel]["bytes_per_launch"]
-    except (OSError, KeyError, ValueError):
-        return None
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
+    summaries (profiles/traffic*.json, written by tools/traffic.py from
+    separate FETCH_SIZE / WRITE_SIZE passes, FETCH_SIZE doubled per the gfx950
+    note in MI355X_MICROARCH.md) measured on this same workload AND on the
+    kernel sources built now (source_sha), else None."""
+    import glob
+    sha = source_sha()
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "traffic*.json"))):
+        try:
+            with open(path) as f:
+                t = json.load(f)
+            if t.get("workload") == workload and t.get("source_sha") == sha:
+                return t["kernels"][kernel]["bytes_per_launch"]
+        except (OSError, KeyError, ValueError):
+            continue
+    return None
+
+
+def kernel_roofline(n, n_grid, material, live_nodes, us_per_launch, workload):
+    """Per-kernel roofline figures of the fused pipeline: the SURVEY 8(d) dense
+    bytes (as the reference sweeps its grid), the live-node bytes, and the
+    PMC-measured HBM traffic when it matches the workload and sources."""
+    dense = algorithmic_bytes(n, n_grid, material)
+    live = algorithmic_bytes_live(n, live_nodes, material)
+    out = {}
+    for k, us in us_per_launch.items():
+        if k not in live or not us:
+            continue
+        t = us * 1e-6
+        tr = measured_traffic(k, workload)
+        out[k] = {"us_per_launch": round(us, 2),
+                  "dense_bytes": dense[k], "frac_dense": round(dense[k] / t / 1e9 / HBM_PEAK_GBS, 4),
+                  "live_bytes": live[k], "frac_sparse": round(live[k] / t / 1e9 / HBM_PEAK_GBS, 4),
+                  "traffic": tr, "traffic_frac": None if tr is None else round(tr / t / 1e9 / HBM_PEAK_GBS, 4)}
+    return out
 
 
 def cpu_baseline(scene, args, budget_s):
@@ -236,11 +282,36 @@ def cpu_baseline(scene, args, budget_s):
         el = time.perf_counter() - t0
         if el > budget_s or n_done >= 2000:
             break
-    return {"value": n_done * x.shape[0] / el, "unit": "particle-substeps/s", "cores": threads, "kind": "port",
+    sub_s = n_done / el
+    # the frame's render on the CPU restatement of the rasterizer (oracle/raster_oracle.c, serial), so the
+    # baseline times the same work as the GPU value: steps_per_frame substeps + one 800x800 SH3 render
+    render_s = None
+    if not args.no_render:
+        g, mask, cam = scene["g"], scene["mask"], scene["cam"]
+        c = scene["c"].reshape(-1).cpu().numpy().astype(np.float32)
+        means = (c + (g.get_xyz[mask].cpu().numpy() - np.float32(1.0))).astype(np.float32)  # main.py:139-146 (F7)
+        covs = g.get_covariance()[mask].cpu().numpy()
+        opa = g.get_opacity[mask].reshape(-1).cpu().numpy()
+        shs = g.get_features[mask].cpu().numpy()
+        t0 = time.perf_counter()
+        O.raster_forward(means, opa, cam.view_mat.cpu().numpy(), cam.full_proj_mat.cpu().numpy(),
+                         np.asarray(cam.cam_center.cpu().numpy(), np.float32), np.zeros(3, np.float32),
+                         cam.width, cam.height, math.tan(cam.FovX * 0.5), math.tan(cam.FovY * 0.5), shs=shs,
+                         sh_degree=3, cov3D_precomp=covs)
+        render_s = time.perf_counter() - t0
+    spf = sa.steps_per_frame
+    frame_s = spf / sub_s + (render_s or 0.0)
+    return {"value": x.shape[0] * spf / frame_s, "unit": "particle-substeps/s", "cores": threads, "kind": "port",
             "sample": f"first {n_done} lego substeps of the same workload ({x.shape[0]} particles, {sa.n_grid}^3, "
                       f"same BCs), C restatement oracle/mpm_oracle.c, OpenMP ({threads} threads) -O3 -ffast-math "
-                      f"-march=x86-64-v3, {el:.1f}s",
-            "substeps_per_s": n_done / el}
+                      f"-march=x86-64-v3, {el:.1f}s"
+                      + ("" if render_s is None else
+                         f"; plus one {cam.width}x{cam.height} SH3 render of the scene on oracle/raster_oracle.c "
+                         f"(serial, 1 thread), {render_s:.2f}s")
+                      + f"; value = particles x {spf} / (the frame's {spf} substeps at the measured rate + the "
+                        "render): the same work per frame as the GPU value",
+            "substeps_per_s": sub_s, "sim_only_particle_substeps_per_s": x.shape[0] * sub_s,
+            "render_s_per_frame": render_s}
 
 
 def other_configs(args, dev, frames=3, rank=0, world=1, xp=None, sync=None):
@@ -257,7 +328,9 @@ def other_configs(args, dev, frames=3, rank=0, world=1, xp=None, sync=None):
     slab = xp is not None
     sync = sync or torch.cuda.synchronize
     res = {}
-    for key, cfg, mat, n, ng in (("C_lego_fracture_metal", "lego-fracture.json", "metal", 100_000, 128),
+    # B': the real lego's Gaussian count (models/lego/point_cloud/iteration_7000, 240,549: SURVEY F6)
+    for key, cfg, mat, n, ng in (("B_prime_lego_240549", "lego.json", None, 240_549, 128),
+                                 ("C_lego_fracture_metal", "lego-fracture.json", "metal", 100_000, 128),
                                  ("D_bicycle", "bicycle.json", None, 1_000_000, 256)):
         a = copy.copy(args)
         a.config, a.material, a.particles, a.n_grid = cfg, mat, n, ng
@@ -289,6 +362,12 @@ def other_configs(args, dev, frames=3, rank=0, world=1, xp=None, sync=None):
             prof = sim.profile(dt, masks)
             r["k_fused_us_per_launch"] = round(prof[0] / (spf + 1) * 1e3, 2)
             r["k_grid_f_us_per_launch"] = round(prof[1] / spf * 1e3, 2)
+            live = sim.debug_stats()["touched_tiles"] * 448
+            r["live_nodes"] = live
+            r["roofline"] = kernel_roofline(
+                nsim, sa.n_grid, sa.material, live,
+                {"k_fused": r["k_fused_us_per_launch"], "k_grid_f": r["k_grid_f_us_per_launch"]},
+                {"config": cfg, "particles": n, "n_grid": ng, "material": sa.material})
         else:
             st = sim.stats()
             r["rank0_slab_planes"] = [st["lo"], st["hi"]]
@@ -403,11 +482,13 @@ def main():
         return dry_run(args, rank, world)
     import torch
     import torch.distributed as dist
-    # GSMPM_DIST_BACKEND=gloo (+ GSMPM_SHARE_GPU=1: every rank on cuda:0) is for
-    # rehearsing the multi-rank path on a one-GPU box; the driver uses RCCL.
+    # GSMPM_SHARE_GPU=1 (every rank on cuda:0; RCCL, or GSMPM_DIST_BACKEND=gloo)
+    # rehearses the multi-rank path on a one-GPU box; the driver uses RCCL.
     backend = os.environ.get("GSMPM_DIST_BACKEND", "nccl")
     if os.environ.get("GSMPM_SHARE_GPU") == "1":
         local = 0
+        if backend == "nccl":  # RCCL accepts ranks on one device as separate "hosts" (socket transport)
+            os.environ.update(NCCL_HOSTID=f"gsmpm-bench-rank{rank}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -602,6 +683,7 @@ def main():
         frame_s = frame_prof[dom] * 1e-3
         ach = abytes[dom] * spf / frame_s / 1e9  # one substep's algorithmic bytes per substep
         avg_launch_s = frame_s / nl[dom]
+        lbytes = algorithmic_bytes_live(n_local, live, sa.material).get(dom) if fused else None
         traffic = measured_traffic(dom, {"config": args.config, "particles": args.particles, "n_grid": sa.n_grid,
                                          "material": sa.material})
         out["kernels_ms_per_launch"] = {k: round(frame_prof[k] / nl[k], 5) for k in frame_prof if k in nl}
@@ -617,7 +699,18 @@ def main():
                                     "achieved = spf x bytes / the kernel's summed packet-stamped time over one "
                                     "eager frame (= rocprofv3 avg x launches)",
                            "pipeline": sim.pipeline,
-                           "live_nodes": live}
+                           "live_nodes": live,
+                           # the same kernel time over the live-node bytes (208 N + 28 x touched-tile
+                           # nodes for k_fused): the bandwidth fraction of what the kernel must move
+                           "live_bytes_per_substep": lbytes,
+                           "achieved_sparse": None if lbytes is None else round(lbytes * spf / frame_s / 1e9, 1),
+                           "frac_sparse": None if lbytes is None else
+                           round(lbytes * spf / frame_s / 1e9 / HBM_PEAK_GBS, 4),
+                           "traffic_source_sha": source_sha()}
+        out["kernels_roofline"] = kernel_roofline(
+            n_local, sa.n_grid, sa.material, live,
+            {k: frame_prof[k] / nl[k] * 1e3 for k in ("k_fused", "k_grid_f") if k in frame_prof},
+            {"config": args.config, "particles": args.particles, "n_grid": sa.n_grid, "material": sa.material})
     if not args.no_extra_configs:
         oc = other_configs(args, dev, rank=rank, world=world, xp=xp, sync=barrier) if slab else \
             (other_configs(args, dev) if world == 1 else None)
@@ -631,9 +724,10 @@ def main():
         out["config"]["rank0_window_rects"] = sim.engine.slab_rects()
     if rank == 0:
         print(json.dumps(out), flush=True)
-    # the slab transport's RCCL communicator is left to process exit: captured
-    # chunk graphs still reference it (ncclCommDestroy behind a live graph
-    # that used the communicator blocked in tools/probe/rccl_graph_probe.cpp)
+    if slab:  # the simulator's captured graphs hold RCCL work: destroy them before the communicator
+        sim.engine.close()
+        barrier()
+        xp.close()
     if world > 1:
         dist.destroy_process_group()
 

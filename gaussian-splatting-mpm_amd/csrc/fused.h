@@ -705,7 +705,7 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
 // bin every particle by its current x (set_particles / resort / set x)
 __global__ __launch_bounds__(256) void k_bin_all_f(Particles ps, GridDims g, BinOutF bo) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p < ps.n) {
+  if (p < ps.count()) {
     float x[3];
 #pragma unroll
     for (int d = 0; d < 3; ++d) x[d] = ps.ld(PX + d, p);

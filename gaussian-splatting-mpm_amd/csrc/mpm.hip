@@ -883,11 +883,13 @@ struct BinPermute {
   int skip_vc;  // v and C are dead (a re-binning between G2P + P2G launches, fused.h): not moved
 };
 __global__ __launch_bounds__(256) void k_finish_bins(Tiles tl, const int* __restrict__ count, ChunkOut co, int n,
-                                                     const int* __restrict__ ptile, const int* __restrict__ pslot,
-                                                     int* __restrict__ list, BinPermute bp) {
+                                                     const int* __restrict__ nlive, const int* __restrict__ ptile,
+                                                     const int* __restrict__ pslot, int* __restrict__ list,
+                                                     BinPermute bp) {
   __shared__ int s_off[kFuseTiles];  // count | touched << 31, then list offsets
   __shared__ int s_aux[kFuseTiles];  // first chunk (low 16 bits) | touched-list rank (high 16 bits)
   const int E = tl.ntiles + 1;
+  if (nlive) n = *nlive;  // a slab: the live count, on a capacity-sized grid
   stamp(2, 0);
   // this lane's particle bin, requested first (independent of the scan)
   const int p = blockIdx.x * 256 + threadIdx.x;
@@ -1063,10 +1065,11 @@ __global__ __launch_bounds__(1024) void k_scan_tiles(Tiles tl, const int* __rest
   }
 }
 
-__global__ __launch_bounds__(256) void k_scatter(int n, const int* __restrict__ ptile, const int* __restrict__ pslot,
-                                                 const int* __restrict__ cstart, int* __restrict__ list) {
+__global__ __launch_bounds__(256) void k_scatter(int n, const int* __restrict__ nlive, const int* __restrict__ ptile,
+                                                 const int* __restrict__ pslot, const int* __restrict__ cstart,
+                                                 int* __restrict__ list) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= n) return;
+  if (p >= (nlive ? *nlive : n)) return;
   list[cstart[ptile[p]] + pslot[p]] = p;
 }
 
@@ -1239,11 +1242,11 @@ __global__ __launch_bounds__(256) void k_morton(Particles ps, float inv_dx, uint
 
 // dst[plane][i] = src[plane][perm[i]] for every hot plane (blockIdx.y =
 // plane), and the same for the orig map (blockIdx.y = NPLANES)
-__global__ __launch_bounds__(256) void k_permute(const float* __restrict__ src, float* __restrict__ dst, int n, int np,
-                                                 const int* __restrict__ perm, const int* __restrict__ osrc,
-                                                 int* __restrict__ odst) {
+__global__ __launch_bounds__(256) void k_permute(const float* __restrict__ src, float* __restrict__ dst, int n,
+                                                 const int* __restrict__ nlive, int np, const int* __restrict__ perm,
+                                                 const int* __restrict__ osrc, int* __restrict__ odst) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i >= (nlive ? *nlive : n)) return;
   if (blockIdx.y == NPLANES) {
     odst[i] = osrc[perm[i]];
     return;
@@ -1399,35 +1402,46 @@ struct gsmpm_mpm {
     float* planes_alt;
     int* orig;
     int* orig_alt;
+    // slabs: migrations swap these too, and count on the host
+    float* cold;
+    float* cold_alt;
+    int* gid;
+    int* gid_alt;
+    long since, migrations;
   };
   std::map<std::vector<uint32_t>, FState> graph_fstate;  // fused-pipeline state after the graph
   // ---- multi-GPU slab (slab.h, slab_host.inc): n varies with migration, np is the capacity ----
+  // A step call runs on the device end to end (one captured graph with the
+  // RCCL transport): migrations keep the live count in d_n and raise sticky
+  // flags; the host learns n, the errors and the boxes from one record
+  // exchange at the end of the call (slab_sync).
   bool slab = false;
   int s_lo = 0, s_hi = 0, s_margin = 2, s_interval = 10, s_rank = 0, s_world = 1;
   int s_has[2] = {0, 0};
   SlabWin sw{};                              // windows + this rank's partial buffers
   float4* s_recv[2] = {nullptr, nullptr};    // the neighbours' partials
-  int* s_drift = nullptr;                    // [2]: a particle passed the margin (k_fused); a window node
-                                             // outside its rect got mass (k_grid_f)
-  int* s_rect_dev = nullptr;                 // [12]: this rank's particle yz box, the neighbours' (rect handshake)
-  bool s_rect_set = false;                   // the windows' rects have been agreed once
+  int* d_n = nullptr;                        // [1] live particle count (device)
+  int* s_drift = nullptr;                    // [kSlabFlags] sticky device flags (slab.h SlabFlag): drift past the
+                                             // margin (k_fused), window mass outside the rect (k_grid_f),
+                                             // send / capacity overflow and statistics (k_mig_*)
+  bool s_synced = false;                     // the records have been exchanged since the particles were set
+  bool s_rect_set = false;                   // the windows' rects have been agreed once (they never shrink after)
   int* gid = nullptr;                        // [np] global particle ids, caller order
   int* gid_alt = nullptr;
   float* cold_alt = nullptr;
   int* mig_bcnt = nullptr;                   // [nblk][3] per-block destination counts
   int* mig_boff = nullptr;                   // [nblk][3] their exclusive scan
-  int* mig_tot = nullptr;                    // [3] + drift flag copy
-  int* mig_host = nullptr;                   // pinned [16]: totals + drift flags + rect handshake
-  int* s_rec = nullptr;                      // [world][8] migration records of every rank (slab_migrate)
+  int* mig_tot = nullptr;                    // [3] leavers to lower, stayers, leavers to upper
+  int* s_rec = nullptr;                      // [world][kRecInts] every rank's record (slab_sync)
   int* s_rec_host = nullptr;                 // pinned copy
-  float* mig_send[2] = {nullptr, nullptr};   // [NMIG][count] payloads
+  float* mig_send[2] = {nullptr, nullptr};   // fixed-size payloads: header + [NMIG][mig_cap]
   float* mig_recv[2] = {nullptr, nullptr};
-  size_t mig_send_cap[2] = {0, 0}, mig_recv_cap[2] = {0, 0};  // in particles
+  int mig_cap = 0;                           // leavers one migration may send one way (all ranks agree)
   hipStream_t s_comm = nullptr;              // RCCL exchanges run here, overlapping the interior grid update
   hipEvent_t s_ev_pack = nullptr, s_ev_x = nullptr;
   long s_migrations = 0, s_migrated = 0;     // counters (gsmpm_mpm_slab_stats)
   long s_since = 0;                          // substeps since the last migration
-  bool s_graph = true;                       // capture RCCL chunks in hipGraphs (GSMPM_SLAB_GRAPH=0: eager)
+  bool s_graph = true;                       // capture RCCL step calls in hipGraphs (GSMPM_SLAB_GRAPH=0: eager)
   float* x_host = nullptr;                   // CALLBACK transport: pinned staging of the exchanged buffers
   size_t x_host_cap = 0;
 };
@@ -1436,7 +1450,13 @@ namespace gsmpm {
 static thread_local std::string g_err;
 void set_error(const std::string& m) { g_err = m; }
 
-static Particles particles_of(gsmpm_mpm* h) { return Particles{h->planes, h->n, h->np, h->cold}; }
+static Particles particles_of(gsmpm_mpm* h) {
+  return Particles{h->planes, h->n, h->np, h->cold, h->slab ? h->d_n : nullptr};
+}
+// rows a per-particle launch covers: the live count, or a slab's capacity
+// (its kernels read the live count from the device, ps.count())
+static int live_rows(const gsmpm_mpm* h) { return h->slab ? h->np : h->n; }
+static const int* nlive_of(const gsmpm_mpm* h) { return h->slab ? h->d_n : nullptr; }
 
 static ChunkIn chunk_in(gsmpm_mpm* h, int c) {
   return ChunkIn{h->count[c], h->cbase[c], h->chunk[c], h->nchunk[c], h->list[c], h->touched[c]};
@@ -1492,16 +1512,16 @@ static bool bins_fused(const Tiles& tl) { return tl.ntiles + 1 <= kFuseTiles && 
 static int finish_bins_on(gsmpm_mpm* h, const Tiles& tl, const int* count, const ChunkOut& co, int* list,
                           hipStream_t st, const hipEvent_t* ev, const BinPermute& bp = BinPermute{}) {
   if (bins_fused(tl)) {
-    launch(ev, k_finish_bins, dim3(std::max(1, div_up(h->n, 256))), dim3(256), st, tl, count, co, h->n, (const int*)h->ptile,
-           (const int*)h->pslot, list, bp);
+    launch(ev, k_finish_bins, dim3(std::max(1, div_up(live_rows(h), 256))), dim3(256), st, tl, count, co, h->n,
+           nlive_of(h), (const int*)h->ptile, (const int*)h->pslot, list, bp);
   } else {
     const hipEvent_t e0[2] = {ev ? ev[0] : nullptr, nullptr}, e1[2] = {nullptr, ev ? ev[1] : nullptr};
     const int nblk = div_up(tl.ntiles + 1, 1024);
     launch(ev ? e0 : nullptr, k_scan_partials, dim3(nblk), dim3(1024), st, tl, count, (const int*)co.tflag,
            h->scan_part);
     launch(nullptr, k_scan_tiles, dim3(nblk), dim3(1024), st, tl, count, co, (const int4*)h->scan_part);
-    launch(ev ? e1 : nullptr, k_scatter, dim3(std::max(1, div_up(h->n, 256))), dim3(256), st, h->n, (const int*)h->ptile,
-           (const int*)h->pslot, (const int*)co.cstart, list);
+    launch(ev ? e1 : nullptr, k_scatter, dim3(std::max(1, div_up(live_rows(h), 256))), dim3(256), st, h->n,
+           nlive_of(h), (const int*)h->ptile, (const int*)h->pslot, (const int*)co.cstart, list);
   }
   GSMPM_LAUNCH_CHECK();
   return GSMPM_OK;
@@ -1536,8 +1556,9 @@ static int rebin_permute_f(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t
 // Storage into the bin order of parity c (list[c]: storage rows grouped by
 // tile): planes / orig gathered into the other buffer, which becomes current.
 static int permute_to_bins(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t* ev) {
-  launch(ev, k_permute, dim3(std::max(1, div_up(h->n, 256)), NPLANES + 1), dim3(256), st, (const float*)h->planes, h->planes_alt,
-         h->n, h->np, (const int*)h->flist[c], (const int*)h->orig, h->orig_alt);
+  launch(ev, k_permute, dim3(std::max(1, div_up(live_rows(h), 256)), NPLANES + 1), dim3(256), st,
+         (const float*)h->planes, h->planes_alt, h->n, nlive_of(h), h->np, (const int*)h->flist[c],
+         (const int*)h->orig, h->orig_alt);
   GSMPM_LAUNCH_CHECK();
   std::swap(h->planes, h->planes_alt);
   std::swap(h->orig, h->orig_alt);
@@ -1551,7 +1572,8 @@ static int rebin_f(gsmpm_mpm* h, hipStream_t st) {
   GSMPM_HIP(hipMemsetAsync(h->fcount[c], 0, sizeof(int) * (h->ftl.ntiles + 1), st));
   GSMPM_HIP(hipMemsetAsync(h->ftflag[c], 0, sizeof(int) * h->ftl.ntiles, st));
   GSMPM_HIP(hipMemsetAsync(h->fnchunk[c], 0, sizeof(int) * 2, st));
-  hipLaunchKernelGGL(k_bin_all_f, dim3(std::max(1, div_up(h->n, 256))), dim3(256), 0, st, particles_of(h), h->g, bin_out_f(h, c));
+  hipLaunchKernelGGL(k_bin_all_f, dim3(std::max(1, div_up(live_rows(h), 256))), dim3(256), 0, st, particles_of(h), h->g,
+                     bin_out_f(h, c));
   GSMPM_LAUNCH_CHECK();
   return rebin_permute_f(h, c, st);
 }
@@ -1833,8 +1855,8 @@ static int resort(gsmpm_mpm* h, hipStream_t st) {
   GSMPM_HIP(rocprim::radix_sort_pairs(h->sort_tmp, bytes, h->sort_keys, h->sort_keys + np, h->sort_idx,
                                       h->sort_idx + np, (size_t)n, 0, 30, st));
   const int* perm = h->sort_idx + np;
-  hipLaunchKernelGGL(k_permute, dim3(div_up(n, 256), NPLANES + 1), dim3(256), 0, st, h->planes, h->planes_tmp, n, np,
-                     perm, (const int*)h->orig, h->orig_tmp);
+  hipLaunchKernelGGL(k_permute, dim3(div_up(n, 256), NPLANES + 1), dim3(256), 0, st, h->planes, h->planes_tmp, n,
+                     (const int*)nullptr, np, perm, (const int*)h->orig, h->orig_tmp);
   GSMPM_LAUNCH_CHECK();
   // copy back so pointers baked into cached graphs stay valid
   GSMPM_HIP(hipMemcpyAsync(h->planes, h->planes_tmp, sizeof(float) * (size_t)NPLANES * np, hipMemcpyDeviceToDevice, st));
@@ -1846,15 +1868,36 @@ static int resort(gsmpm_mpm* h, hipStream_t st) {
 }  // namespace gsmpm
 
 namespace gsmpm {
+static int slab_body(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc, hipStream_t st,
+                     const gsmpm_transport* xp);  // slab_host.inc
+
+static gsmpm_mpm::FState fstate_of(const gsmpm_mpm* h, int bp, int ep) {
+  return gsmpm_mpm::FState{bp,      ep,          h->planes, h->planes_alt, h->orig, h->orig_alt, h->cold,
+                           h->cold_alt, h->gid, h->gid_alt, h->s_since, h->s_migrations};
+}
+static void set_fstate(gsmpm_mpm* h, const gsmpm_mpm::FState& f) {
+  h->planes = f.planes;
+  h->planes_alt = f.planes_alt;
+  h->orig = f.orig;
+  h->orig_alt = f.orig_alt;
+  h->cold = f.cold;
+  h->cold_alt = f.cold_alt;
+  h->gid = f.gid;
+  h->gid_alt = f.gid_alt;
+  h->s_since = f.since;
+  h->s_migrations = f.migrations;
+}
+
 // nsub substeps through a cached hipGraph: captured once per (dt, BC masks,
 // bins / escape / buffer parities, transport) key and replayed.  A slab with
-// the RCCL transport captures its window exchanges too (grouped
-// ncclSend/ncclRecv on the comm stream, joined into the capture by events).
+// the RCCL transport captures its whole step call: the window exchanges
+// (grouped ncclSend/ncclRecv on the comm stream, joined into the capture by
+// events) and the migrations between chunks, whose counts stay on the device.
 static int graph_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc, hipStream_t st,
                           const gsmpm_transport* xp) {
   const bool fz = use_fused(h);
   std::vector<uint32_t> key;
-  key.reserve(nsub + 9);
+  key.reserve(nsub + 14);
   uint32_t dtb;
   std::memcpy(&dtb, &dt, 4);
   key.push_back(dtb);
@@ -1866,24 +1909,38 @@ static int graph_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc, 
   key.push_back((uint32_t)h->rebin_interval);
   key.push_back(h->planes_alt && h->planes > h->planes_alt ? 1u : 0u);  // which particle buffer is current
   key.push_back(xp ? (uint32_t)(((uintptr_t)xp->comm >> 4) ^ (uint32_t)xp->kind) : 0u);
+  if (h->slab) {  // where the migrations fall, and the buffers they swap (rects / capacity changes drop graphs)
+    key.push_back((uint32_t)(h->s_since % h->s_interval));
+    key.push_back(h->cold_alt && h->cold > h->cold_alt ? 1u : 0u);
+    key.push_back(h->gid_alt && h->gid > h->gid_alt ? 1u : 0u);
+    key.push_back((uint32_t)h->mig_cap);
+  }
   for (int s = 0; s < nsub; ++s) key.push_back(bc ? bc[s] : 0xffffffffu);
   auto it = h->graphs.find(key);
   if (it == h->graphs.end()) {
     if (h->graphs.size() >= 16) drop_graphs(h);
     hipGraph_t graph;
     int parity = h->cur_box, bp = h->fbpar, ep = h->fep;
-    const gsmpm_mpm::FState start{bp, ep, h->planes, h->planes_alt, h->orig, h->orig_alt};
+    const gsmpm_mpm::FState start = fstate_of(h, bp, ep);
     GSMPM_HIP(hipStreamBeginCapture(h->cap, hipStreamCaptureModeRelaxed));
-    int rc = fz ? launch_substeps_f(h, dt, nsub, bc, h->cap, bp, ep, nullptr, nullptr, xp)
-                : launch_substeps(h, dt, nsub, bc, h->cap, parity);
+    int rc;
+    if (h->slab) {
+      rc = slab_body(h, dt, nsub, bc, h->cap, xp);
+      bp = h->fbpar;
+      ep = h->fep;
+      h->fbpar = start.bpar;
+      h->fep = start.ep;
+    } else {
+      rc = fz ? launch_substeps_f(h, dt, nsub, bc, h->cap, bp, ep, nullptr, nullptr, xp)
+              : launch_substeps(h, dt, nsub, bc, h->cap, parity);
+    }
     hipError_t e = hipStreamEndCapture(h->cap, &graph);
     // capture swapped the particle buffers on the host: keep the end state for
     // the key and start the replay below from the key's state
-    const gsmpm_mpm::FState end{bp, ep, h->planes, h->planes_alt, h->orig, h->orig_alt};
-    h->planes = start.planes;
-    h->planes_alt = start.planes_alt;
-    h->orig = start.orig;
-    h->orig_alt = start.orig_alt;
+    gsmpm_mpm::FState end = fstate_of(h, bp, ep);
+    end.since -= start.since;  // the counters advance by the graph's own substeps / migrations
+    end.migrations -= start.migrations;
+    set_fstate(h, start);
     if (rc) {
       if (e == hipSuccess) (void)hipGraphDestroy(graph);
       return rc;
@@ -1908,10 +1965,10 @@ static int graph_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc, 
   const gsmpm_mpm::FState& fs = h->graph_fstate[key];
   h->fbpar = fs.bpar;
   h->fep = fs.ep;
-  h->planes = fs.planes;
-  h->planes_alt = fs.planes_alt;
-  h->orig = fs.orig;
-  h->orig_alt = fs.orig_alt;
+  const long since = h->s_since, migrations = h->s_migrations;
+  set_fstate(h, fs);
+  h->s_since = since + fs.since;
+  h->s_migrations = migrations + fs.migrations;
   return GSMPM_OK;
 }
 }  // namespace gsmpm
@@ -2113,14 +2170,13 @@ int gsmpm_mpm_destroy(gsmpm_mpm* h) {
     (void)hipFree(h->mig_recv[w]);
   }
   (void)hipFree(h->s_drift);
-  (void)hipFree(h->s_rect_dev);
+  (void)hipFree(h->d_n);
   (void)hipFree(h->gid);
   (void)hipFree(h->gid_alt);
   (void)hipFree(h->cold_alt);
   (void)hipFree(h->mig_bcnt);
   (void)hipFree(h->mig_boff);
   (void)hipFree(h->mig_tot);
-  if (h->mig_host) (void)hipHostFree(h->mig_host);
   (void)hipFree(h->s_rec);
   if (h->s_rec_host) (void)hipHostFree(h->s_rec_host);
   if (h->x_host) (void)hipHostFree(h->x_host);

@@ -62,7 +62,11 @@ struct BcTable {
 struct Particles {
   float* P;
   int n, np;
-  float* cold;  // [NCOLD][np], caller order
+  float* cold;          // [NCOLD][np], caller order
+  const int* nlive;     // slab: the live count on the device (migration changes it inside a captured frame), else null
+  // particles live now: kernels of a slab's step read it from the device and
+  // run on a capacity-sized grid (the host learns n at the end of the step)
+  __device__ __forceinline__ int count() const { return nlive ? *nlive : n; }
   // Plane access through a buffer resource: SGPR descriptor + SGPR plane
   // offset + ONE 32-bit VGPR lane offset for all hot planes (a flat access
   // holds a 64-bit VGPR address per plane, which costs the transfer kernels

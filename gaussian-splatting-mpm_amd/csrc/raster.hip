@@ -469,8 +469,10 @@ __global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges,
     out[pix] = C0 + T * bg[0];
     out[HW + pix] = C1 + T * bg[1];
     out[2 * HW + pix] = C2 + T * bg[2];
-    final_T[pix] = T;
-    n_contrib[pix] = last;
+    if (final_T) {  // the backward's per-pixel state; a forward-only context skips it
+      final_T[pix] = T;
+      n_contrib[pix] = last;
+    }
   }
 }
 
@@ -1118,6 +1120,8 @@ struct gsmpm_raster {
   // the forward the state belongs to
   int P = -1, W = 0, H = 0, gx = 0, gy = 0;
   unsigned K = 0;
+  bool forward_only = false;  // gsmpm_raster_set_forward_only: no per-pixel state for a backward
+  bool has_pixel_state = false;
 };
 
 static int grow(void** p, size_t bytes) {
@@ -1397,7 +1401,9 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
   }
   if (!ranges_written && K == 0) GSMPM_HIP(hipMemsetAsync(r->ranges, 0, ntiles * sizeof(uint2), st));
   hipLaunchKernelGGL(k_render, dim3(2 * a.grid_x, 2 * a.grid_y), dim3(64), 0, st, r->ranges, r->ids_sorted, a.W, a.H,
-                     a.grid_x, r->xy, r->conic, r->rgb, in->bg, out_color, r->final_T, r->n_contrib, tkeys, render_mode);
+                     a.grid_x, r->xy, r->conic, r->rgb, in->bg, out_color, r->forward_only ? nullptr : r->final_T,
+                     r->forward_only ? nullptr : r->n_contrib, tkeys, render_mode);
+  r->has_pixel_state = !r->forward_only;
   GSMPM_LAUNCH_CHECK();
   if (num_rendered) *num_rendered = (int32_t)K;
   r->P = P;
@@ -1416,6 +1422,8 @@ int gsmpm_raster_backward(gsmpm_raster* r, const gsmpm_raster_args* in, const in
                 "gsmpm_raster_backward: null argument");
   GSMPM_REQUIRE(r->P == in->P && r->W == in->W && r->H == in->H,
                 "gsmpm_raster_backward: the context holds no forward of these sizes (one context per differentiable forward)");
+  GSMPM_REQUIRE(r->has_pixel_state || in->P == 0,
+                "gsmpm_raster_backward: the context's forward was forward-only (gsmpm_raster_set_forward_only)");
   GSMPM_REQUIRE(!in->shs || dL_dsh, "gsmpm_raster_backward: shs given but no dL_dsh output");
   GSMPM_REQUIRE(!in->scales || (dL_dscales && dL_drotations), "gsmpm_raster_backward: scales given but no outputs");
   hipStream_t st = (hipStream_t)stream;
@@ -1463,6 +1471,12 @@ int gsmpm_raster_backward(gsmpm_raster* r, const gsmpm_raster_args* in, const in
   hipLaunchKernelGGL(k_preprocess_bwd, dim3(div_up(a.P, 256)), dim3(256), 0, st, a, radii, r->offsets, r->rgb,
                      r->rec, o);
   GSMPM_LAUNCH_CHECK();
+  return GSMPM_OK;
+}
+
+int gsmpm_raster_set_forward_only(gsmpm_raster* r, int32_t on) {
+  GSMPM_REQUIRE(r, "gsmpm_raster_set_forward_only: null context");
+  r->forward_only = on != 0;
   return GSMPM_OK;
 }
 

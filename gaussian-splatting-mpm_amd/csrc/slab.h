@@ -62,16 +62,70 @@ __global__ __launch_bounds__(256) void k_win_update(GridDims g, SlabWin sw, cons
   }
 }
 
-// yz box of the particles' base nodes (trunc(x * inv_dx - 0.5), utils.py:95)
-// -> out4 {min y, max y, min z, max z} (initialised to INT_MAX / INT_MIN).
-__global__ __launch_bounds__(256) void k_slab_bbox(Particles ps, float inv_dx, int* __restrict__ out4) {
+// ------------------------------------------------------------ slab record --
+// Every slab's state after a step call, exchanged with every rank (one round,
+// 64 bytes a peer) so all ranks see the same errors, counts and boxes.
+enum SlabRec : int {
+  RF_FLAGS = 0,   // bit 0 drift past the margin, 1 window mass outside the rect, 3 over capacity
+  RF_N = 1,       // live particles
+  RF_NWANT = 2,   // the most particles a migration tried to hold (capacity overflow)
+  RF_SENDMAX = 3, // the most leavers one migration sent one way (send capacity)
+  RF_MIGRATED = 4,
+  RF_YLO = 5, RF_YHI = 6, RF_ZLO = 7, RF_ZHI = 8,  // yz box of the particles' base nodes
+  RF_VY = 9, RF_VZ = 10,                            // max |v_y|, |v_z| (f32 bits)
+  RF_BAND_LO = 11, RF_BAND_HI = 12,                 // particles within `margin` planes of the lower / upper bound
+  RF_DEFERRED = 13,                                 // leavers kept for a later migration (payload full)
+  kRecInts = 16
+};
+// Device flags of a slab (s_flags): sticky until the handle is reset.
+enum SlabFlag : int {
+  SF_DRIFT = 0, SF_OOB = 1, SF_DEFERRED = 2, SF_NWANT_OVER = 3, SF_SENDMAX = 4, SF_MIGRATED = 5, kSlabFlags = 8
+};
+
+struct MigGeom {
+  float inv_dx;
+  int lo, hi;      // owned planes
+  int has_lo, has_hi;
+};
+
+__global__ void k_rec_init(const int* __restrict__ flags, const int* __restrict__ nlive, int* __restrict__ rec) {
+  if (threadIdx.x != 0) return;
+  rec[RF_FLAGS] = (flags[SF_DRIFT] ? 1 : 0) | (flags[SF_OOB] ? 2 : 0) | (flags[SF_NWANT_OVER] ? 8 : 0);
+  rec[RF_N] = *nlive;
+  rec[RF_NWANT] = flags[SF_NWANT_OVER];
+  rec[RF_SENDMAX] = flags[SF_SENDMAX];
+  rec[RF_MIGRATED] = flags[SF_MIGRATED];
+  rec[RF_YLO] = INT_MAX;
+  rec[RF_YHI] = INT_MIN;
+  rec[RF_ZLO] = INT_MAX;
+  rec[RF_ZHI] = INT_MIN;
+  rec[RF_VY] = 0;
+  rec[RF_VZ] = 0;
+  rec[RF_BAND_LO] = 0;
+  rec[RF_BAND_HI] = 0;
+  rec[RF_DEFERRED] = flags[SF_DEFERRED];
+  for (int i = RF_DEFERRED + 1; i < kRecInts; ++i) rec[i] = 0;
+}
+
+// yz box of the particles' base nodes (trunc(x * inv_dx - 0.5), utils.py:95),
+// max |v_y|, |v_z| and the particles within `margin` planes of each bound (the
+// most that can leave by the next migration) -> rec (after k_rec_init).
+__global__ __launch_bounds__(256) void k_slab_record(Particles ps, MigGeom mg, int margin, int* __restrict__ rec) {
   int v[4] = {INT_MAX, INT_MIN, INT_MAX, INT_MIN};
-  for (int p = blockIdx.x * 256 + threadIdx.x; p < ps.n; p += gridDim.x * 256) {
-    const int by = (int)(ps.ld(PX + 1, p) * inv_dx - 0.5f), bz = (int)(ps.ld(PX + 2, p) * inv_dx - 0.5f);
+  float vy = 0.f, vz = 0.f;
+  int blo = 0, bhi = 0;
+  const int n = ps.count();
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < n; p += gridDim.x * 256) {
+    const int bx = (int)(ps.ld(PX, p) * mg.inv_dx - 0.5f);
+    const int by = (int)(ps.ld(PX + 1, p) * mg.inv_dx - 0.5f), bz = (int)(ps.ld(PX + 2, p) * mg.inv_dx - 0.5f);
     v[0] = min(v[0], by);
     v[1] = max(v[1], by);
     v[2] = min(v[2], bz);
     v[3] = max(v[3], bz);
+    vy = fmaxf(vy, fabsf(ps.ld(PV + 1, p)));
+    vz = fmaxf(vz, fabsf(ps.ld(PV + 2, p)));
+    blo += (bx < mg.lo + margin) ? 1 : 0;
+    bhi += (bx >= mg.hi - margin) ? 1 : 0;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -79,22 +133,38 @@ __global__ __launch_bounds__(256) void k_slab_bbox(Particles ps, float inv_dx, i
     v[1] = max(v[1], __shfl_xor(v[1], o));
     v[2] = min(v[2], __shfl_xor(v[2], o));
     v[3] = max(v[3], __shfl_xor(v[3], o));
+    vy = fmaxf(vy, __shfl_xor(vy, o));
+    vz = fmaxf(vz, __shfl_xor(vz, o));
+    blo += __shfl_xor(blo, o);
+    bhi += __shfl_xor(bhi, o);
   }
-  if ((threadIdx.x & 63) == 0 && v[0] <= v[1]) {
-    atomicMin(out4 + 0, v[0]);
-    atomicMax(out4 + 1, v[1]);
-    atomicMin(out4 + 2, v[2]);
-    atomicMax(out4 + 3, v[3]);
+  if ((threadIdx.x & 63) == 0) {
+    if (v[0] <= v[1]) {
+      atomicMin(rec + RF_YLO, v[0]);
+      atomicMax(rec + RF_YHI, v[1]);
+      atomicMin(rec + RF_ZLO, v[2]);
+      atomicMax(rec + RF_ZHI, v[3]);
+    }
+    // non-negative floats order as their bit patterns (NaN: all bits set, wins)
+    atomicMax(rec + RF_VY, __float_as_int(vy));
+    atomicMax(rec + RF_VZ, __float_as_int(vz));
+    if (blo) atomicAdd(rec + RF_BAND_LO, blo);
+    if (bhi) atomicAdd(rec + RF_BAND_HI, bhi);
   }
 }
 
 // ------------------------------------------------------------- migration --
+// Runs on the device between two chunks of substeps, inside the captured
+// frame: the counts never visit the host.  The payload to each neighbour has
+// a FIXED size (RCCL send/recv sizes are baked into the graph): a header of
+// kMigHdr ints (the leaver count first) and [NMIG][cap] floats.  Leavers
+// beyond `cap` stay for a later migration (SF_DEFERRED): ownership does not
+// change the physics while a particle stays within the margin, which k_fused
+// checks, and the host grows `cap` after the call.
+constexpr int kMigHdr = 16;
+__host__ __device__ constexpr size_t mig_payload_floats(int cap) { return (size_t)kMigHdr + (size_t)NMIG * cap; }
+
 // Destination of a particle: 0 the lower neighbour, 1 stay, 2 the upper one.
-struct MigGeom {
-  float inv_dx;
-  int lo, hi;      // owned planes
-  int has_lo, has_hi;
-};
 __device__ __forceinline__ int mig_dest(const MigGeom& mg, float x0) {
   const int b = (int)(x0 * mg.inv_dx - 0.5f);  // utils.py:95 (trunc), as every kernel computes it
   if (mg.has_lo && b < mg.lo) return 0;
@@ -102,11 +172,12 @@ __device__ __forceinline__ int mig_dest(const MigGeom& mg, float x0) {
   return 1;
 }
 
-// Per-block counts of the three destinations (wave ballots), blocks of 256.
+// Per-block counts of the three destinations (wave ballots), blocks of 256
+// over the capacity (rows past the live count count nowhere).
 __global__ __launch_bounds__(256) void k_mig_count(Particles ps, MigGeom mg, int* __restrict__ bcnt) {
   __shared__ int s_c[4][3];
   const int p = blockIdx.x * 256 + threadIdx.x;
-  const int d = p < ps.n ? mig_dest(mg, ps.ld(PX, p)) : -1;
+  const int d = p < ps.count() ? mig_dest(mg, ps.ld(PX, p)) : -1;
   const int wv = threadIdx.x >> 6;
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
@@ -121,9 +192,16 @@ __global__ __launch_bounds__(256) void k_mig_count(Particles ps, MigGeom mg, int
 }
 
 // Exclusive scan of the per-block counts (one workgroup of 1024; nblk is a
-// few thousand at most): boff[b][c] and the totals tot[c].
+// few thousand at most): boff[b][c] and the totals tot = {leavers down,
+// stayers, leavers up, rows kept (stayers + deferred leavers)}; then the send
+// headers and the statistics flags.
+struct MigSend {
+  float* buf[2];  // lower / upper payloads (null: no neighbour)
+  int cap;
+  int* flags;     // s_flags
+};
 __global__ __launch_bounds__(1024) void k_mig_scan(int nblk, const int* __restrict__ bcnt, int* __restrict__ boff,
-                                                   int* __restrict__ tot) {
+                                                   int* __restrict__ tot, MigSend ms) {
   __shared__ int s_w[16][3];
   __shared__ int s_carry[3];
   if (threadIdx.x < 3) s_carry[threadIdx.x] = 0;
@@ -160,26 +238,38 @@ __global__ __launch_bounds__(1024) void k_mig_scan(int nblk, const int* __restri
     }
     __syncthreads();
   }
-  if (threadIdx.x < 3) tot[threadIdx.x] = s_carry[threadIdx.x];
+  if (threadIdx.x == 0) {
+    const int c_lo = s_carry[0], n_stay = s_carry[1], c_hi = s_carry[2];
+    const int d_lo = max(0, c_lo - ms.cap), d_hi = max(0, c_hi - ms.cap);
+    tot[0] = c_lo;
+    tot[1] = n_stay;
+    tot[2] = c_hi;
+    tot[3] = n_stay + d_lo + d_hi;
+    if (ms.buf[0]) reinterpret_cast<int*>(ms.buf[0])[0] = c_lo - d_lo;
+    if (ms.buf[1]) reinterpret_cast<int*>(ms.buf[1])[0] = c_hi - d_hi;
+    atomicMax(ms.flags + SF_SENDMAX, max(c_lo, c_hi));
+    if (d_lo + d_hi) atomicAdd(ms.flags + SF_DEFERRED, d_lo + d_hi);
+    atomicAdd(ms.flags + SF_MIGRATED, c_lo - d_lo + c_hi - d_hi);
+  }
 }
 
 // Stable scatter: stayers to rows [0, n_stay) of the new storage (hot planes,
 // and the cold planes / global id read through orig, which become caller
-// order = the new storage order); leavers to their send buffer, SoA
-// [NMIG][count] (hot planes, cold planes, id as float bits).
+// order = the new storage order), deferred leavers after them; leavers to
+// their payload, SoA [NMIG][cap] after the header (hot planes, cold planes,
+// id as float bits).
 struct MigOut {
   float* planes;   // new hot planes [NPLANES][np]
   float* cold;     // new cold planes [NCOLD][np]
   int* gid;        // new global ids [np]
-  float* send[2];  // lower / upper payloads
 };
 __global__ __launch_bounds__(256) void k_mig_scatter(Particles ps, const int* __restrict__ orig,
                                                      const int* __restrict__ gid, MigGeom mg,
                                                      const int* __restrict__ boff, const int* __restrict__ tot,
-                                                     MigOut mo) {
+                                                     MigOut mo, MigSend ms) {
   __shared__ int s_c[4][3];
   const int p = blockIdx.x * 256 + threadIdx.x;
-  const int d = p < ps.n ? mig_dest(mg, ps.ld(PX, p)) : -1;
+  int d = p < ps.count() ? mig_dest(mg, ps.ld(PX, p)) : -1;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   int rank_in_wave = 0;
 #pragma unroll
@@ -193,31 +283,62 @@ __global__ __launch_bounds__(256) void k_mig_scatter(Particles ps, const int* __
   int row = boff[(size_t)blockIdx.x * 3 + d] + rank_in_wave;
   for (int w = 0; w < wv; ++w) row += s_c[w][d];
   const int src = orig[p];  // caller row of the cold planes / id
+  if (d != 1 && row >= ms.cap) {  // payload full: stays, after the stayers
+    row = tot[1] + (d == 0 ? 0 : max(0, tot[0] - ms.cap)) + row - ms.cap;
+    d = 1;
+  }
   if (d == 1) {
     for (int q = 0; q < NPLANES; ++q) mo.planes[(size_t)q * ps.np + row] = ps.ld(q, p);
     for (int q = 0; q < NCOLD; ++q) mo.cold[(size_t)q * ps.np + row] = ps.ldc(q, src);
     mo.gid[row] = gid[src];
   } else {
-    float* out = mo.send[d >> 1];
-    const size_t cnt = (size_t)tot[d];
-    for (int q = 0; q < NPLANES; ++q) out[(size_t)q * cnt + row] = ps.ld(q, p);
-    for (int q = 0; q < NCOLD; ++q) out[(size_t)(NPLANES + q) * cnt + row] = ps.ldc(q, src);
-    out[(size_t)(NPLANES + NCOLD) * cnt + row] = __int_as_float(gid[src]);
+    float* out = ms.buf[d >> 1] + kMigHdr;
+    const size_t cap = (size_t)ms.cap;
+    for (int q = 0; q < NPLANES; ++q) out[(size_t)q * cap + row] = ps.ld(q, p);
+    for (int q = 0; q < NCOLD; ++q) out[(size_t)(NPLANES + q) * cap + row] = ps.ldc(q, src);
+    out[(size_t)(NPLANES + NCOLD) * cap + row] = __int_as_float(gid[src]);
   }
 }
 
-// Arrivals: payload rows -> storage rows [row0, row0 + cnt) (hot + cold + id).
-__global__ __launch_bounds__(256) void k_mig_unpack(const float* __restrict__ in, int cnt, int row0, float* planes,
+// Arrivals: payload rows -> storage rows after the kept rows (blockIdx.y =
+// the side: the lower neighbour's first), hot + cold + id; rows past the capacity
+// raise SF_NWANT_OVER and are dropped (the state is invalid).
+struct MigRecv {
+  const float* buf[2];  // null: no neighbour on that side
+  int cap;
+};
+__device__ __forceinline__ int mig_arrivals(const MigRecv& mr, int w) {
+  return mr.buf[w] ? reinterpret_cast<const int*>(mr.buf[w])[0] : 0;
+}
+__global__ __launch_bounds__(256) void k_mig_unpack(MigRecv mr, const int* __restrict__ tot, float* planes,
                                                     float* cold, int* gid, int np) {
+  const int w = blockIdx.y;
+  const int cnt = mig_arrivals(mr, w);
   const int r = blockIdx.x * 256 + threadIdx.x;
   if (r >= cnt) return;
-  const size_t c = (size_t)cnt;
-  for (int q = 0; q < NPLANES; ++q) planes[(size_t)q * np + row0 + r] = in[(size_t)q * c + r];
-  for (int q = 0; q < NCOLD; ++q) cold[(size_t)q * np + row0 + r] = in[(size_t)(NPLANES + q) * c + r];
-  gid[row0 + r] = __float_as_int(in[(size_t)(NPLANES + NCOLD) * c + r]);
+  const int row = tot[3] + (w ? mig_arrivals(mr, 0) : 0) + r;
+  if (row >= np) return;
+  const float* in = mr.buf[w] + kMigHdr;
+  const size_t c = (size_t)mr.cap;
+  for (int q = 0; q < NPLANES; ++q) planes[(size_t)q * np + row] = in[(size_t)q * c + r];
+  for (int q = 0; q < NCOLD; ++q) cold[(size_t)q * np + row] = in[(size_t)(NPLANES + q) * c + r];
+  gid[row] = __float_as_int(in[(size_t)(NPLANES + NCOLD) * c + r]);
 }
 
-__global__ __launch_bounds__(256) void k_iota(int* __restrict__ a, int n) {
+// The new live count (kept rows + arrivals, capped at the capacity), and the
+// caller order := the new storage order.
+__global__ __launch_bounds__(256) void k_mig_finish(MigRecv mr, const int* __restrict__ tot, int np, int* __restrict__ nlive,
+                                                    int* __restrict__ orig, int* __restrict__ flags) {
+  const int want = tot[3] + mig_arrivals(mr, 0) + mig_arrivals(mr, 1);
+  const int n = min(want, np);
   const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n) a[i] = i;
+  if (i == 0) {
+    *nlive = n;
+    if (want > np) atomicMax(flags + SF_NWANT_OVER, want);
+  }
+  if (i < n) orig[i] = i;
+}
+
+__global__ void k_set_int(int* __restrict__ p, int v) {
+  if (threadIdx.x == 0) *p = v;
 }

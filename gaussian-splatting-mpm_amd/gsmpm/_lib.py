@@ -139,6 +139,7 @@ _SIGS = {
     "gsmpm_raster_backward": (ctypes.c_int, [c_void_p, ctypes.POINTER(RasterArgs), c_void_p, c_void_p] +
                               [c_void_p] * 8 + [c_void_p]),
     "gsmpm_raster_mark_visible": (ctypes.c_int, [c_void_p, ctypes.c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "gsmpm_raster_set_forward_only": (ctypes.c_int, [c_void_p, ctypes.c_int32]),
 }
 
 # slab transports (include/gsmpm.h)

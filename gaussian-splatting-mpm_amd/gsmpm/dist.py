@@ -162,10 +162,11 @@ class SlabDomain:
 
     def __init__(self, x_grid, cov6, vol, *, rank: int, world: int, transport, n_grid: int, grid_extent: float = 2.0,
                  margin: int = 2, interval: int = 10, capacity: int | None = None, v=None, device=None,
-                 engine_factory=None, **sim_kwargs):
+                 engine_factory=None, group=None, **sim_kwargs):
         from .sim import Simulator
         engine_factory = engine_factory or Simulator
         self.rank, self.world, self.transport = int(rank), int(world), transport
+        self.group = group  # the process group of the slab ranks (None: the default group)
         self.n_grid, self.grid_extent = int(n_grid), float(grid_extent)
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         self.margin, self.interval = int(margin), int(interval)
@@ -215,31 +216,35 @@ class SlabDomain:
     # outputs in global order on one rank
     def gather(self, rows: torch.Tensor, dst: int = 0):
         """Per-particle rows of this rank ([n, w] in the engine's row order)
-        -> on rank `dst` the [n_total, w] tensor in global particle order
-        (None elsewhere).  all_gather of count-padded blocks + global ids."""
-        gid = self.engine.get_gid().to(torch.int64)
-        rows = rows.reshape(gid.numel(), -1).to(torch.float32)
+        -> on rank `dst` (a rank of the slab group) the [n_total, w] tensor in
+        global particle order (None elsewhere).  One max-reduce of the counts,
+        then a gather to `dst` of count-padded blocks whose last column is the
+        global id as int32 bits (a block's unused rows carry id -1)."""
+        gid = self.engine.get_gid()
+        n = gid.numel()
+        rows = rows.reshape(n, -1).to(torch.float32)
         w = rows.shape[1]
-        on_dev = dist.get_backend() == "nccl"
+        on_dev = dist.get_backend(self.group) == "nccl"
         dev = self.device if on_dev else torch.device("cpu")
-        cnt = torch.tensor([gid.numel()], dtype=torch.int64, device=dev)
-        cnts = [torch.zeros_like(cnt) for _ in range(self.world)]
-        dist.all_gather(cnts, cnt)
-        nmax = int(max(int(c.item()) for c in cnts))
-        blk = torch.zeros((nmax, w + 1), dtype=torch.float32, device=dev)
-        blk[: gid.numel(), :w] = rows.to(dev)
-        blk[: gid.numel(), w] = gid.to(dev).to(torch.float32)  # exact below 2^24 particles
-        assert self.n_total < (1 << 24)
-        parts = [torch.empty_like(blk) for _ in range(self.world)]
-        dist.all_gather(parts, blk)
-        if self.rank != dst:
+        nmax = torch.tensor([n], dtype=torch.int64, device=dev)
+        dist.all_reduce(nmax, op=dist.ReduceOp.MAX, group=self.group)
+        nmax = int(nmax.item())
+        blk = torch.empty((nmax, w + 1), dtype=torch.float32, device=dev)
+        blk[:n, :w] = rows.to(dev)
+        ids = blk[:, w:].view(torch.int32)  # the id column, reinterpreted: exact for any count
+        ids.fill_(-1)
+        ids[:n, 0] = gid.to(dev)
+        me = dist.get_rank(self.group) if self.group is not None else self.rank
+        g_dst = dist.get_global_rank(self.group, dst) if self.group is not None else dst
+        parts = [torch.empty_like(blk) for _ in range(self.world)] if me == dst else None
+        dist.gather(blk, parts, dst=g_dst, group=self.group)
+        if me != dst:
             return None
+        allb = torch.cat(parts).to(self.device)
+        idx = allb[:, w:].contiguous().view(torch.int32).reshape(-1).to(torch.int64)
+        keep = idx >= 0
         out = torch.empty((self.n_total, w), dtype=torch.float32, device=self.device)
-        for c, p in zip(cnts, parts):
-            k = int(c.item())
-            if k:
-                p = p[:k].to(self.device)
-                out[p[:, w].to(torch.int64)] = p[:, :w]
+        out[idx[keep]] = allb[keep, :w]
         return out
 
     def gather_field(self, name: str, dst: int = 0):

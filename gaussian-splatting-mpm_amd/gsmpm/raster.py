@@ -12,10 +12,13 @@ _CTX = {}
 
 
 def _context(device_index: int):
+    """The shared per-device context of forwards without a backward (main.py's
+    frames): forward-only, so no per-pixel backward state is written."""
     h = _CTX.get(device_index)
     if h is None:
         h = ctypes.c_void_p()
         check(LIB.gsmpm_raster_create(ctypes.byref(h)), "gsmpm_raster_create")
+        check(LIB.gsmpm_raster_set_forward_only(h, 1), "gsmpm_raster_set_forward_only")
         _CTX[device_index] = h
     return h
 

@@ -378,6 +378,12 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* a, float* out
 int gsmpm_raster_backward(gsmpm_raster* r, const gsmpm_raster_args* a, const int32_t* radii, const float* dL_dcolor,
                           float* dL_dmeans2D, float* dL_dcolors, float* dL_dopacity, float* dL_dmeans3D,
                           float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drotations, void* stream);
+/* Forward-only context (on != 0): gsmpm_raster_forward skips the per-pixel
+ * state (final T, last contributor: 8 B a pixel) that only a backward reads,
+ * and gsmpm_raster_backward on it fails.  Used for main.py's frames
+ * (main.py:148-157 never differentiates); autograd forwards use contexts
+ * with it off (the default). */
+int gsmpm_raster_set_forward_only(gsmpm_raster* r, int32_t on);
 /* GaussianRasterizer.markVisible -> _C.mark_visible: visible[P] (u8) = view z > 0.2 */
 int gsmpm_raster_mark_visible(const float* means3D, int32_t P, const float* viewmatrix, const float* projmatrix,
                               uint8_t* visible, void* stream);

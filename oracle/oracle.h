@@ -115,6 +115,11 @@ typedef struct {
 /* Returns num_rendered; out_color is (3,H,W), out_radii (P). */
 int or_forward(const or_args* a, float* out_color, int32_t* out_radii,
                float* out_depth /*P, may be null*/, int32_t* out_tiles_touched /*P, may be null*/);
+/* or_forward on the tiles [crop4[0], crop4[2]) x [crop4[1], crop4[3]) only
+ * (pixels elsewhere untouched); radii, depth, tiles_touched and the returned
+ * num_rendered are the whole frame's. */
+long or_forward_crop(const or_args* a, float* out_color, int32_t* out_radii, float* out_depth, int32_t* out_tt,
+                     const int* crop4);
 /* Backward of the same forward for dL/d(out_color) [3,H,W].  Outputs (P rows):
  * dL_dmeans2D [P,3] (NDC, z = 0), dL_dcolors [P,3], dL_dopacity [P],
  * dL_dmeans3D [P,3], dL_dcov3D [P,6], dL_dsh [P,M,3] (if shs), dL_dscales [P,3]

@@ -155,9 +155,16 @@ static void fs_free(fstate* f) {
   free(f->rs); free(f->re); free(f->kv); free(f->final_T); free(f->n_contrib);
 }
 
-static void forward_core(const or_args* a, fstate* f, float* out_color) {
+/* crop (test infrastructure for large frames): only the pairs of tiles
+ * [c[0], c[2]) x [c[1], c[3]) are emitted, sorted and blended -- the same
+ * per-tile lists as the full frame (a tile's list is its own pairs in
+ * (depth, index) order); preprocess, radii, tiles_touched and K stay global.
+ * NULL: the whole frame. */
+static void forward_core(const or_args* a, fstate* f, float* out_color, const int* crop) {
   const int P = a->P, W = a->W, H = a->H;
   const int gx = (W + BX - 1) / BX, gy = (H + BY - 1) / BY;
+  const int cx0 = crop ? mxi(0, crop[0]) : 0, cy0 = crop ? mxi(0, crop[1]) : 0;
+  const int cx1 = crop ? mni(gx, crop[2]) : gx, cy1 = crop ? mni(gy, crop[3]) : gy;
   const float fx = W / (2.0f * a->tanfovx), fy = H / (2.0f * a->tanfovy);
   f->P = P; f->W = W; f->H = H; f->gx = gx; f->gy = gy; f->fx = fx; f->fy = fy;
   float* xy = f->xy = (float*)calloc((size_t)P * 2 + 2, sizeof(float));
@@ -206,9 +213,17 @@ static void forward_core(const or_args* a, fstate* f, float* out_color) {
     con[i * 4] = conic[0]; con[i * 4 + 1] = conic[1]; con[i * 4 + 2] = conic[2]; con[i * 4 + 3] = a->opacities[i];
     tt[i] = (rmax[1] - rmin[1]) * (rmax[0] - rmin[0]);
   }
-  long K = 0;
-  for (int i = 0; i < P; ++i) K += tt[i];
-  kv_t* kv = f->kv = (kv_t*)malloc(sizeof(kv_t) * (size_t)(K + 1));
+  long K = 0, Kc = 0;
+  for (int i = 0; i < P; ++i) {
+    K += tt[i];
+    if (out_radii[i] <= 0 || !crop) continue;
+    int rmin[2], rmax[2];
+    get_rect(xy + i * 2, out_radii[i], gx, gy, rmin, rmax);
+    const long wx = mni(rmax[0], cx1) - mxi(rmin[0], cx0), wy = mni(rmax[1], cy1) - mxi(rmin[1], cy0);
+    if (wx > 0 && wy > 0) Kc += wx * wy;
+  }
+  if (!crop) Kc = K;
+  kv_t* kv = f->kv = (kv_t*)malloc(sizeof(kv_t) * (size_t)(Kc + 1));
   f->K = K;
   long off = 0;
   for (int i = 0; i < P; ++i) {
@@ -217,24 +232,24 @@ static void forward_core(const or_args* a, fstate* f, float* out_color) {
     get_rect(xy + i * 2, out_radii[i], gx, gy, rmin, rmax);
     uint32_t dbits;
     memcpy(&dbits, &depth[i], 4);
-    for (int y = rmin[1]; y < rmax[1]; ++y)
-      for (int x = rmin[0]; x < rmax[0]; ++x) {
+    for (int y = mxi(rmin[1], cy0); y < mni(rmax[1], cy1); ++y)
+      for (int x = mxi(rmin[0], cx0); x < mni(rmax[0], cx1); ++x) {
         kv[off].key = ((uint64_t)(uint32_t)(y * gx + x) << 32) | dbits;
         kv[off].val = (uint32_t)i;
         ++off;
       }
   }
-  qsort(kv, (size_t)K, sizeof(kv_t), kv_cmp);
+  qsort(kv, (size_t)Kc, sizeof(kv_t), kv_cmp);
   int ntiles = gx * gy;
   int32_t* rs = f->rs = (int32_t*)calloc((size_t)ntiles, sizeof(int32_t));
   int32_t* re = f->re = (int32_t*)calloc((size_t)ntiles, sizeof(int32_t));
-  for (long k = 0; k < K; ++k) {
+  for (long k = 0; k < Kc; ++k) {
     int t = (int)(kv[k].key >> 32);
     if (k == 0 || (int)(kv[k - 1].key >> 32) != t) rs[t] = (int32_t)k;
-    if (k == K - 1 || (int)(kv[k + 1].key >> 32) != t) re[t] = (int32_t)(k + 1);
+    if (k == Kc - 1 || (int)(kv[k + 1].key >> 32) != t) re[t] = (int32_t)(k + 1);
   }
-  for (int ty = 0; ty < gy; ++ty)
-    for (int tx = 0; tx < gx; ++tx) {
+  for (int ty = cy0; ty < cy1; ++ty)
+    for (int tx = cx0; tx < cx1; ++tx) {
       int t = ty * gx + tx;
       for (int py = ty * BY; py < ty * BY + BY && py < H; ++py)
         for (int px = tx * BX; px < tx * BX + BX && px < W; ++px) {
@@ -266,12 +281,17 @@ static void forward_core(const or_args* a, fstate* f, float* out_color) {
 }
 
 int or_forward(const or_args* a, float* out_color, int32_t* out_radii, float* out_depth, int32_t* out_tt) {
+  return or_forward_crop(a, out_color, out_radii, out_depth, out_tt, NULL);
+}
+
+long or_forward_crop(const or_args* a, float* out_color, int32_t* out_radii, float* out_depth, int32_t* out_tt,
+                     const int* crop4) {
   fstate f;
-  forward_core(a, &f, out_color);
+  forward_core(a, &f, out_color, crop4);
   memcpy(out_radii, f.radii, sizeof(int32_t) * a->P);
   if (out_depth) memcpy(out_depth, f.depth, sizeof(float) * a->P);
   if (out_tt) memcpy(out_tt, f.tt, sizeof(int32_t) * a->P);
-  const int K = (int)f.K;
+  const long K = f.K;
   fs_free(&f);
   return K;
 }
@@ -397,7 +417,7 @@ void or_backward(const or_args* a, const float* dL_dpix, float* dL_dmeans2D, flo
                  float* dL_dmeans3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscales, float* dL_drot) {
   const int P = a->P, W = a->W, H = a->H;
   fstate f;
-  forward_core(a, &f, NULL);
+  forward_core(a, &f, NULL, NULL);
   float* dconic = (float*)calloc((size_t)P * 3 + 3, sizeof(float));
   memset(dL_dmeans2D, 0, sizeof(float) * 3 * P);
   memset(dL_dcolors, 0, sizeof(float) * 3 * P);

@@ -5,9 +5,11 @@ transport, host-staged): the library's native sequence runs -- k_grid_f's
 window pass, the exchange, the interior pass, k_win_update, and every 10
 substeps the k_mig_* migration -- 200 substeps of a scene drifting along the
 slab axis, gathered in global order and compared with the single-domain CPU
-oracle (the same scene as tests/test_dist_slab.py).  The RCCL transport
-differs only in moving the same buffers with ncclSend/ncclRecv; its test needs
-two GPUs (RCCL refuses two ranks on one device) and is skipped otherwise.
+oracle (the same scene as tests/test_dist_slab.py).  The RCCL transport --
+what bench.py --gpus N runs: each step call captured whole, window exchanges
+and device-side migrations included -- runs with 2 and 3 ranks on cuda:0
+too, each rank given an NCCL_HOSTID of its own (shared_gpu_rccl_env) so RCCL
+accepts them on one device over its socket transport.
 """
 from __future__ import annotations
 
@@ -36,8 +38,9 @@ def shared_gpu_rccl_env(rank):
     return {"NCCL_HOSTID": f"gsmpm-slab-rank{rank}", "NCCL_SOCKET_IFNAME": "lo", "NCCL_IB_DISABLE": "1"}
 
 
-def _gpu_worker(rank, world, port, out, backend, steps, full_top=False):
+def _gpu_worker(rank, world, port, out, backend, steps, full_top=False, env=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(env or {})
     if backend == "nccl-shared":
         os.environ.update(shared_gpu_rccl_env(rank))
         backend = "nccl"
@@ -92,8 +95,9 @@ def _gpu_worker(rank, world, port, out, backend, steps, full_top=False):
         dist.destroy_process_group()
 
 
-def _run(world, tmp_path, backend="gloo", steps=STEPS):
-    mp.spawn(_gpu_worker, args=(world, free_port(), str(tmp_path), backend, steps), nprocs=world, join=True)
+def _run(world, tmp_path, backend="gloo", steps=STEPS, env=None):
+    mp.spawn(_gpu_worker, args=(world, free_port(), str(tmp_path), backend, steps, False, env), nprocs=world,
+             join=True)
     return np.load(os.path.join(tmp_path, "res.npz"))
 
 
@@ -135,6 +139,17 @@ def test_gpu_slabs_rccl_shared_gpu(dev, tmp_path, world):
     print("rccl shared gpu", world, errs, "migrated", int(r["migrated"]))
 
 
+@pytest.mark.parametrize("backend", ["gloo", "nccl-shared"])
+def test_gpu_slabs_deferred_migration(dev, tmp_path, backend):
+    """Migration payloads of 4 particles (GSMPM_SLAB_MIG_CAP): most leavers
+    cannot be sent at their first migration and stay with their old slab for
+    a later one -- ownership must not change the physics."""
+    r = _run(3, tmp_path, backend=backend, env={"GSMPM_SLAB_MIG_CAP": "4"})
+    assert int(r["migrated"]) > 50
+    errs = _check(r)
+    print("deferred", backend, errs, "migrated", int(r["migrated"]))
+
+
 @pytest.mark.skipif(torch.cuda.device_count() < 2, reason="RCCL needs one GPU per rank")
 def test_gpu_slabs_rccl_two_gpus(dev, tmp_path):
     r = _run(2, tmp_path, backend="nccl")
@@ -164,9 +179,10 @@ def test_gpu_slab_error_stops_every_rank(dev, tmp_path):
     it, and all 4 ranks raise the same error after the same migration count
     (gsmpm_mpm_slab_step exchanges every rank's migration record)."""
     world = 4
-    mp.spawn(_gpu_worker, args=(world, free_port(), str(tmp_path), "gloo", STEPS, True), nprocs=world, join=True)
+    mp.spawn(_gpu_worker, args=(world, free_port(), str(tmp_path), "gloo", STEPS, True, None), nprocs=world,
+             join=True)
     errs = read_errors(tmp_path, world)
     assert len(set(errs)) == 1, errs
     migs, msg = errs[0].split("|", 1)
     assert f"rank {world - 1}:" in msg and "capacity" in msg, msg
-    assert int(migs) < STEPS // 10, migs
+    assert int(migs) <= STEPS // 10, migs  # errors surface at the end of the step call, on every rank

@@ -45,7 +45,10 @@ def main():
         fb, wb = 2 * 1024 * f.get(k, 0.0), 1024 * w.get(k, 0.0)
         res[k] = {"fetch_bytes": fb, "write_bytes": wb, "bytes_per_launch": fb + wb,
                   "fetch_size_kib_raw": f.get(k), "write_size_kib_raw": w.get(k)}
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    import bench  # source_sha: the kernel sources these counters were measured on
     doc = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes (tools/pmc.sh)",
+           "source_sha": bench.source_sha(),
            "correction": "FETCH_SIZE x2 (gfx950), KiB -> bytes",
            # tools/pmc_probe.py's workload (bench.py only uses these numbers for the same one)
            "workload": {"config": os.environ.get("CONFIG", "lego.json"), "particles": int(os.environ.get("N", 100000)),
