@@ -1414,7 +1414,7 @@ struct gsmpm_mpm {
   // A step call runs on the device end to end (one captured graph with the
   // RCCL transport): migrations keep the live count in d_n and raise sticky
   // flags; the host learns n, the errors and the boxes from one record
-  // exchange at the end of the call (slab_sync).
+  // exchange at the end of the call (slab_records / slab_check).
   bool slab = false;
   int s_lo = 0, s_hi = 0, s_margin = 2, s_interval = 10, s_rank = 0, s_world = 1;
   int s_has[2] = {0, 0};
@@ -1432,13 +1432,15 @@ struct gsmpm_mpm {
   int* mig_bcnt = nullptr;                   // [nblk][3] per-block destination counts
   int* mig_boff = nullptr;                   // [nblk][3] their exclusive scan
   int* mig_tot = nullptr;                    // [3] leavers to lower, stayers, leavers to upper
-  int* s_rec = nullptr;                      // [world][kRecInts] every rank's record (slab_sync)
+  int* s_rec = nullptr;                      // [world][kRecInts] every rank's record (slab_records)
   int* s_rec_host = nullptr;                 // pinned copy
   float* mig_send[2] = {nullptr, nullptr};   // fixed-size payloads: header + [NMIG][mig_cap]
   float* mig_recv[2] = {nullptr, nullptr};
   int mig_cap = 0;                           // leavers one migration may send one way (all ranks agree)
   hipStream_t s_comm = nullptr;              // RCCL exchanges run here, overlapping the interior grid update
   hipEvent_t s_ev_pack = nullptr, s_ev_x = nullptr;
+  hipEvent_t s_ev_join = nullptr;            // the event the last exchange's join waits on
+  bool capturing = false;                    // a graph capture of this handle is open (graph_substeps)
   long s_migrations = 0, s_migrated = 0;     // counters (gsmpm_mpm_slab_stats)
   long s_since = 0;                          // substeps since the last migration
   bool s_graph = true;                       // capture RCCL step calls in hipGraphs (GSMPM_SLAB_GRAPH=0: eager)
@@ -1893,6 +1895,11 @@ static void set_fstate(gsmpm_mpm* h, const gsmpm_mpm::FState& f) {
 // the RCCL transport captures its whole step call: the window exchanges
 // (grouped ncclSend/ncclRecv on the comm stream, joined into the capture by
 // events) and the migrations between chunks, whose counts stay on the device.
+// GSMPM_GRAPH_TRACE=1: one stderr line per stage of a capture / replay (diagnostics)
+static void gtrace(const char* what) {
+  static const bool on = std::getenv("GSMPM_GRAPH_TRACE") && std::getenv("GSMPM_GRAPH_TRACE")[0] == '1';
+  if (on) std::fprintf(stderr, "[gsmpm graph] %s\n", what), std::fflush(stderr);
+}
 static int graph_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc, hipStream_t st,
                           const gsmpm_transport* xp) {
   const bool fz = use_fused(h);
@@ -1922,10 +1929,13 @@ static int graph_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc, 
     hipGraph_t graph;
     int parity = h->cur_box, bp = h->fbpar, ep = h->fep;
     const gsmpm_mpm::FState start = fstate_of(h, bp, ep);
+    gtrace("begin capture");
     GSMPM_HIP(hipStreamBeginCapture(h->cap, hipStreamCaptureModeRelaxed));
+    h->capturing = true;
     int rc;
     if (h->slab) {
       rc = slab_body(h, dt, nsub, bc, h->cap, xp);
+      gtrace("slab body captured");
       bp = h->fbpar;
       ep = h->fep;
       h->fbpar = start.bpar;
@@ -1934,7 +1944,9 @@ static int graph_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc, 
       rc = fz ? launch_substeps_f(h, dt, nsub, bc, h->cap, bp, ep, nullptr, nullptr, xp)
               : launch_substeps(h, dt, nsub, bc, h->cap, parity);
     }
+    h->capturing = false;
     hipError_t e = hipStreamEndCapture(h->cap, &graph);
+    gtrace(e == hipSuccess ? "end capture ok" : "end capture FAILED");
     // capture swapped the particle buffers on the host: keep the end state for
     // the key and start the replay below from the key's state
     gsmpm_mpm::FState end = fstate_of(h, bp, ep);
@@ -1951,6 +1963,7 @@ static int graph_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc, 
     }
     hipGraphExec_t exec;
     e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    gtrace(e == hipSuccess ? "instantiated" : "instantiate FAILED");
     (void)hipGraphDestroy(graph);
     if (e != hipSuccess) {
       set_error(std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
@@ -1960,7 +1973,9 @@ static int graph_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc, 
     h->graph_box_parity[key] = parity;
     h->graph_fstate[key] = end;
   }
+  gtrace("launch");
   GSMPM_HIP(hipGraphLaunch(it->second, st));
+  gtrace("launched");
   h->cur_box = h->graph_box_parity[key];
   const gsmpm_mpm::FState& fs = h->graph_fstate[key];
   h->fbpar = fs.bpar;

@@ -476,6 +476,141 @@ __global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges,
   }
 }
 
+// k_render4: the same blend, one 256-lane workgroup per tile, wave q = the
+// tile's 8x8 quarter q.  Each batch of kBatch list entries is read ONCE per
+// tile: lane t loads entry j0 + t's id and sub-tile mask and, if any quarter
+// wants it, gathers its xy / conic / rgb into LDS (k_render's four quarter
+// workgroups each read the whole list and gather their own reachers, up to
+// 4x the bytes).  Each wave then compacts its quarter's survivors, in list
+// order, as indices into the staged batch and blends them exactly as
+// k_render does (same arithmetic, same order: bit-identical pixels, final T
+// and last contributor).  Staging is double-buffered: one barrier a batch,
+// and the next batch's gathers are in flight while this one blends.  The
+// workgroup stops when all 256 pixels are done.
+constexpr int kStage = kBatch + kU;  // + kU all-zero slots: the padding of a wave's last group of kU
+__global__ __launch_bounds__(256) void k_render4(const uint2* __restrict__ ranges, const unsigned* __restrict__ list,
+                                                 int W, int H, int gx, const float2* __restrict__ xy,
+                                                 const float4* __restrict__ conic_o, const float4* __restrict__ rgbo,
+                                                 const float* __restrict__ bg, float* __restrict__ out,
+                                                 float* __restrict__ final_T, int* __restrict__ n_contrib,
+                                                 const unsigned* __restrict__ tkeys, int mode) {
+  __shared__ float2 s_xy[2][kStage];
+  __shared__ float4 s_co[2][kStage];
+  __shared__ float4 s_rgb[2][kStage];  // .w: the entry's tile-list index (as int bits)
+  __shared__ unsigned char s_m[2][kBatch];
+  __shared__ unsigned short s_idx[4][kBatch + kU];
+  const int t = threadIdx.x, lane = t & 63, q = t >> 6;
+  const int x0 = blockIdx.x * kBX + (q & 1) * kSub, y0 = blockIdx.y * kBY + (q >> 1) * kSub;
+  const int px = x0 + (lane & (kSub - 1)), py = y0 + (lane / kSub);
+  const bool inside = px < W && py < H;
+  const uint2 range = ranges[blockIdx.y * gx + blockIdx.x];
+  const int n = (int)(range.y - range.x);
+  const unsigned* lst = list + range.x;
+  const unsigned* tk = tkeys ? tkeys + range.x : nullptr;
+  const float pfx = (float)px, pfy = (float)py, fx0 = (float)x0, fy0 = (float)y0;
+  float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f;
+  int last = 0;
+  bool done = !inside;
+  if (t < kU)
+    for (int b = 0; b < 2; ++b) {
+      s_xy[b][kBatch + t] = make_float2(0.f, 0.f);
+      s_co[b][kBatch + t] = make_float4(0.f, 0.f, 0.f, 0.f);
+      s_rgb[b][kBatch + t] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  // lane t's entry of the current batch (gathered) and of the next (id, mask)
+  float2 g_xy = make_float2(0.f, 0.f);
+  float4 g_co = make_float4(0.f, 0.f, 0.f, 0.f), g_rgb = g_co;
+  unsigned g_m = 0, n_id = 0, n_m = 0;
+  auto mask_of = [&](int j) -> unsigned { return tk ? (tk[j] >> kMaskShift) & 0xfu : 0xfu; };
+  if (t < n) {
+    g_m = mask_of(t);
+    if (g_m) {
+      const unsigned id = lst[t];
+      g_xy = xy[id];
+      g_co = conic_o[id];
+      g_rgb = rgbo[id];
+    }
+  }
+  if (kBatch + t < n) {
+    n_id = lst[kBatch + t];
+    n_m = mask_of(kBatch + t);
+  }
+  int buf = 0;
+  for (int j0 = 0; j0 < n; j0 += kBatch, buf ^= 1) {
+    s_xy[buf][t] = g_xy;
+    s_co[buf][t] = g_co;
+    s_rgb[buf][t] = make_float4(g_rgb.x, g_rgb.y, g_rgb.z, __int_as_float(j0 + t));
+    s_m[buf][t] = (unsigned char)(j0 + t < n ? g_m : 0u);
+    if (__syncthreads_count(!done) == 0) break;
+    // the next batch's gather and the one after's ids fly while this one blends
+    g_m = j0 + kBatch + t < n ? n_m : 0u;
+    if (g_m) {
+      g_xy = xy[n_id];
+      g_co = conic_o[n_id];
+      g_rgb = rgbo[n_id];
+    }
+    if (j0 + 2 * kBatch + t < n) {
+      n_id = lst[j0 + 2 * kBatch + t];
+      n_m = mask_of(j0 + 2 * kBatch + t);
+    }
+    // this quarter's survivors of the staged batch, in list order
+    int cnt = 0;
+#pragma unroll
+    for (int r = 0; r < kBatch / 64; ++r) {
+      const int e = r * 64 + lane;
+      bool keep = (s_m[buf][e] >> q) & 1u;
+      if (keep && !tk && !(mode & 1)) keep = reaches_subtile(s_xy[buf][e], s_co[buf][e], fx0, fy0);
+      const unsigned long long m = __ballot(keep);
+      const int pos =
+          cnt + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+      if (keep) s_idx[q][pos] = (unsigned short)e;
+      cnt += __popcll(m);
+    }
+    if (lane < ((cnt + kU - 1) & ~(kU - 1)) - cnt) s_idx[q][cnt + lane] = (unsigned short)(kBatch + lane);
+    __syncthreads();  // s_idx: written by the wave's lanes, read across lanes (a wave-scope fence is not enough here)
+    for (int b = 0; b < cnt; b += kU) {
+      if (__all(done)) break;
+      float al[kU];
+      float4 c[kU];
+#pragma unroll
+      for (int k = 0; k < kU; ++k) {
+        const int e = s_idx[q][b + k];
+        const float2 g = s_xy[buf][e];
+        const float4 co = s_co[buf][e];
+        c[k] = s_rgb[buf][e];
+        const float dx = g.x - pfx, dy = g.y - pfy;
+        const float power = __builtin_fmaf(-0.5f, __builtin_fmaf(co.x * dx, dx, co.z * dy * dy), -co.y * dx * dy);
+        const float alpha = fminf(0.99f, co.w * __builtin_amdgcn_exp2f(power * 1.4426950408889634f));
+        al[k] = (power > 0.0f || alpha < 1.0f / 255.0f) ? 0.f : alpha;
+      }
+#pragma unroll
+      for (int k = 0; k < kU; ++k) {
+        const float a = done ? 0.f : al[k];
+        const float test_T = T * (1 - a);
+        const bool stop = a != 0.f && test_T < 0.0001f;
+        done = done || stop;
+        const bool take = a != 0.f && !stop;
+        const float aT = take ? a * T : 0.f;
+        C0 = __builtin_fmaf(c[k].x, aT, C0);
+        C1 = __builtin_fmaf(c[k].y, aT, C1);
+        C2 = __builtin_fmaf(c[k].z, aT, C2);
+        T = take ? test_T : T;
+        last = take ? __float_as_int(c[k].w) + 1 : last;
+      }
+    }
+  }
+  if (inside) {
+    const size_t pix = (size_t)py * W + px, HW = (size_t)H * W;
+    out[pix] = C0 + T * bg[0];
+    out[HW + pix] = C1 + T * bg[1];
+    out[2 * HW + pix] = C2 + T * bg[2];
+    if (final_T) {
+      final_T[pix] = T;
+      n_contrib[pix] = last;
+    }
+  }
+}
+
 constexpr unsigned kNoCount = 0xffffffffu;
 __global__ void k_publish_count(const unsigned* __restrict__ src, unsigned* dst) {
   __hip_atomic_store(dst, *src, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1400,9 +1535,17 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     }
   }
   if (!ranges_written && K == 0) GSMPM_HIP(hipMemsetAsync(r->ranges, 0, ntiles * sizeof(uint2), st));
-  hipLaunchKernelGGL(k_render, dim3(2 * a.grid_x, 2 * a.grid_y), dim3(64), 0, st, r->ranges, r->ids_sorted, a.W, a.H,
-                     a.grid_x, r->xy, r->conic, r->rgb, in->bg, out_color, r->forward_only ? nullptr : r->final_T,
-                     r->forward_only ? nullptr : r->n_contrib, tkeys, render_mode);
+  // GSMPM_RASTER_QUARTERS=1: the earlier one-workgroup-per-quarter k_render (A/B; bit-identical output)
+  const char* rq = std::getenv("GSMPM_RASTER_QUARTERS");
+  if (rq && rq[0] == '1')
+    hipLaunchKernelGGL(k_render, dim3(2 * a.grid_x, 2 * a.grid_y), dim3(64), 0, st, r->ranges, r->ids_sorted, a.W,
+                       a.H, a.grid_x, r->xy, r->conic, r->rgb, in->bg, out_color,
+                       r->forward_only ? nullptr : r->final_T, r->forward_only ? nullptr : r->n_contrib, tkeys,
+                       render_mode);
+  else
+    hipLaunchKernelGGL(k_render4, dim3(a.grid_x, a.grid_y), dim3(256), 0, st, r->ranges, r->ids_sorted, a.W, a.H,
+                       a.grid_x, r->xy, r->conic, r->rgb, in->bg, out_color, r->forward_only ? nullptr : r->final_T,
+                       r->forward_only ? nullptr : r->n_contrib, tkeys, render_mode);
   r->has_pixel_state = !r->forward_only;
   GSMPM_LAUNCH_CHECK();
   if (num_rendered) *num_rendered = (int32_t)K;

@@ -14,11 +14,12 @@ import faulthandler
 import os
 import sys
 
-faulthandler.enable()
+SEGV = None
 if os.environ.get("SEGV_TRACE"):  # native backtrace of a crash (tools/probe/segv_trace.c)
     import ctypes
-    ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "segv_trace.so"))
-    faulthandler.disable()
+    SEGV = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "segv_trace.so"))
+else:
+    faulthandler.enable()
 ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..")
 sys.path[:0] = [os.path.join(ROOT, "gaussian-splatting-mpm_amd"), os.path.join(ROOT, "tests"),
                 os.path.join(ROOT, "oracle")]
@@ -66,6 +67,8 @@ if last >= 3:
         if stage > last:
             break
         os.environ["GSMPM_SLAB_GRAPH"] = graph
+        if SEGV is not None:
+            SEGV.segv_trace_reinstall()
         dom = SlabDomain(x, cov, vol, v=v, rank=rank, world=world, transport=xp, n_grid=NG, grid_extent=EXT,
                          margin=2, interval=10, device=dev, jelly_fcr=True, **KW)
         dom.add_fixed_cube(*FIXED)

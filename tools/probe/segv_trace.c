@@ -21,4 +21,7 @@ __attribute__((constructor)) static void install(void) {
   signal(SIGABRT, on_fault);
 }
 
+/* again, after the runtimes loaded by then installed handlers of their own */
+void segv_trace_reinstall(void) { install(); }
+
 int segv_trace_installed(void) { return 1; }
