@@ -75,6 +75,7 @@ enum SlabRec : int {
   RF_VY = 9, RF_VZ = 10,                            // max |v_y|, |v_z| (f32 bits)
   RF_BAND_LO = 11, RF_BAND_HI = 12,                 // particles within `margin` planes of the lower / upper bound
   RF_DEFERRED = 13,                                 // leavers kept for a later migration (payload full)
+  RF_CAP = 14,                                      // the slab's particle capacity
   kRecInts = 16
 };
 // Device flags of a slab (s_flags): sticky until the handle is reset.
@@ -88,7 +89,8 @@ struct MigGeom {
   int has_lo, has_hi;
 };
 
-__global__ void k_rec_init(const int* __restrict__ flags, const int* __restrict__ nlive, int* __restrict__ rec) {
+__global__ void k_rec_init(const int* __restrict__ flags, const int* __restrict__ nlive, int capacity,
+                           int* __restrict__ rec) {
   if (threadIdx.x != 0) return;
   rec[RF_FLAGS] = (flags[SF_DRIFT] ? 1 : 0) | (flags[SF_OOB] ? 2 : 0) | (flags[SF_NWANT_OVER] ? 8 : 0);
   rec[RF_N] = *nlive;
@@ -104,7 +106,8 @@ __global__ void k_rec_init(const int* __restrict__ flags, const int* __restrict_
   rec[RF_BAND_LO] = 0;
   rec[RF_BAND_HI] = 0;
   rec[RF_DEFERRED] = flags[SF_DEFERRED];
-  for (int i = RF_DEFERRED + 1; i < kRecInts; ++i) rec[i] = 0;
+  rec[RF_CAP] = capacity;
+  for (int i = RF_CAP + 1; i < kRecInts; ++i) rec[i] = 0;
 }
 
 // yz box of the particles' base nodes (trunc(x * inv_dx - 0.5), utils.py:95),
@@ -311,13 +314,13 @@ __device__ __forceinline__ int mig_arrivals(const MigRecv& mr, int w) {
   return mr.buf[w] ? reinterpret_cast<const int*>(mr.buf[w])[0] : 0;
 }
 __global__ __launch_bounds__(256) void k_mig_unpack(MigRecv mr, const int* __restrict__ tot, float* planes,
-                                                    float* cold, int* gid, int np) {
+                                                    float* cold, int* gid, int np, int capacity) {
   const int w = blockIdx.y;
   const int cnt = mig_arrivals(mr, w);
   const int r = blockIdx.x * 256 + threadIdx.x;
   if (r >= cnt) return;
   const int row = tot[3] + (w ? mig_arrivals(mr, 0) : 0) + r;
-  if (row >= np) return;
+  if (row >= capacity) return;
   const float* in = mr.buf[w] + kMigHdr;
   const size_t c = (size_t)mr.cap;
   for (int q = 0; q < NPLANES; ++q) planes[(size_t)q * np + row] = in[(size_t)q * c + r];
@@ -325,16 +328,18 @@ __global__ __launch_bounds__(256) void k_mig_unpack(MigRecv mr, const int* __res
   gid[row] = __float_as_int(in[(size_t)(NPLANES + NCOLD) * c + r]);
 }
 
-// The new live count (kept rows + arrivals, capped at the capacity), and the
-// caller order := the new storage order.
-__global__ __launch_bounds__(256) void k_mig_finish(MigRecv mr, const int* __restrict__ tot, int np, int* __restrict__ nlive,
-                                                    int* __restrict__ orig, int* __restrict__ flags) {
+// The new live count (kept rows + arrivals, capped at the slab's capacity:
+// the chunk tables are sized for it), and the caller order := the new
+// storage order.
+__global__ __launch_bounds__(256) void k_mig_finish(MigRecv mr, const int* __restrict__ tot, int capacity,
+                                                    int* __restrict__ nlive, int* __restrict__ orig,
+                                                    int* __restrict__ flags) {
   const int want = tot[3] + mig_arrivals(mr, 0) + mig_arrivals(mr, 1);
-  const int n = min(want, np);
+  const int n = min(want, capacity);
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i == 0) {
     *nlive = n;
-    if (want > np) atomicMax(flags + SF_NWANT_OVER, want);
+    if (want > capacity) atomicMax(flags + SF_NWANT_OVER, want);
   }
   if (i < n) orig[i] = i;
 }

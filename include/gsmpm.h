@@ -142,19 +142,23 @@ int gsmpm_mpm_slab_set_particles(gsmpm_mpm* h, int32_t n, const float* x, const 
                                  const float* v_or_null, const int32_t* gid, void* stream);
 /* n_substeps substeps of the slab (bc masks as gsmpm_mpm_step), window
  * exchange every substep and particle migration every `interval` substeps
- * through `xp`.  Returns GSMPM_ESTATE if a particle drifted past the margin
- * (its contributions were not exchanged: the state is invalid) or a slab
- * would exceed its capacity: every rank's migration record goes to every
- * rank, so all ranks return it at the same migration, with the same message
- * naming the rank at fault. */
+ * through `xp`, all on the device (with RCCL one captured graph per call:
+ * counts never visit the host inside the call).  Migration payloads have a
+ * fixed capacity, grown between calls; leavers beyond it stay for a later
+ * migration.  Returns GSMPM_ESTATE if a particle drifted past the margin or a
+ * window node outside the exchanged rect got mass (contributions were not
+ * exchanged: the state is invalid) or a slab would exceed its capacity: every
+ * rank's record goes to every rank at the end of the call, so all ranks return
+ * it from the same call, with the same message naming the rank at fault. */
 int gsmpm_mpm_slab_step(gsmpm_mpm* h, float dt, int32_t n_substeps, const uint32_t* bc_active_mask,
                         const gsmpm_transport* xp, void* stream);
 /* current particle count of this rank (changes with migration) */
 int gsmpm_mpm_count(gsmpm_mpm* h);
 /* global ids of this rank's particles, in the order gsmpm_mpm_get returns rows */
 int gsmpm_mpm_get_gid(gsmpm_mpm* h, int32_t* out, void* stream);
-/* {migrations, particles migrated (sent), lo, hi, margin, interval, window planes, capacity} */
-int gsmpm_mpm_slab_stats(gsmpm_mpm* h, int64_t out8[8]);
+/* {migrations, particles migrated (sent), lo, hi, margin, interval, window planes, capacity,
+ *  leavers deferred (payload full), migration payload capacity} */
+int gsmpm_mpm_slab_stats(gsmpm_mpm* h, int64_t out10[10]);
 /* The yz rect of each window that the exchange moves, agreed by the two ranks of
  * the bound at every migration: {y0, ny, z0, nz} of the lower window, then of the
  * upper one (ny = nz = 0: nothing to exchange; before the first slab_step, the

@@ -235,3 +235,38 @@ def test_num_rendered_and_radii_exact(dev, P, W, H, tiles):
     assert K == oK, (K, oK)
     assert np.array_equal(radii.cpu().numpy(), orad)
     assert np.abs(color.cpu().numpy() - oc).max() < 1e-3
+
+
+@pytest.mark.parametrize("scene,onesweep", [("dense", "0"), ("sparse", "0"), ("sparse", "1")])
+def test_tile_shared_render_matches_quarter_render(dev, monkeypatch, scene, onesweep):
+    """k_render4 (one workgroup per tile, each list entry read and gathered once
+    for the four quarter waves) against the one-workgroup-per-quarter k_render
+    (GSMPM_RASTER_QUARTERS=1): pixels and, through the backward, final T and
+    last contributor are bit-identical -- with sub-tile masks (chunked sort)
+    and without (onesweep: the quarter test on the gathered conic)."""
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    if scene == "dense":
+        P, W, H = 8000, 100, 72
+        means, c6, opa, shs = _dense_scene(P, P, 0.03, 0.5)
+    else:
+        P, W, H = 3000, 256, 192
+        means, c6, opa, shs = _scene(P, seed=9)
+    view, full, campos, tx, ty = _camera(W, H, 0.9)
+    rng = np.random.default_rng(2)
+    wgt = torch.from_numpy(rng.normal(0, 1, (3, H, W)).astype(np.float32)).to(dev)
+    t = lambda a, g=False: torch.from_numpy(np.ascontiguousarray(a)).to(dev).requires_grad_(g)
+    st = GaussianRasterizationSettings(image_height=H, image_width=W, tanfovx=tx, tanfovy=ty,
+                                       bg=t(np.full(3, 0.25, np.float32)), scale_modifier=1.0, viewmatrix=t(view),
+                                       projmatrix=t(full), sh_degree=3, campos=t(campos), prefiltered=False,
+                                       debug=False)
+    monkeypatch.setenv("GSMPM_RASTER_ONESWEEP", onesweep)
+    out = {}
+    for quarters in ("1", "0"):
+        monkeypatch.setenv("GSMPM_RASTER_QUARTERS", quarters)
+        m3, o1, s1, cv = t(means, True), t(opa, True), t(shs, True), t(c6, True)
+        img, _ = GaussianRasterizer(st)(means3D=m3, means2D=None, opacities=o1, shs=s1, cov3D_precomp=cv)
+        (img * wgt).sum().backward()
+        out[quarters] = [x.detach().cpu().numpy() for x in (img, m3.grad, o1.grad, s1.grad, cv.grad)]
+    for a, b in zip(out["0"], out["1"]):
+        assert np.array_equal(a, b)

@@ -81,12 +81,14 @@ def _gpu_worker(rank, world, port, out, backend, steps, full_top=False, env=None
         got["cov"] = dom.gather_field("cov")
         st = dom.stats()
         rects = np.array(dom.engine.slab_rects(), np.int64).reshape(-1)
-        mig = torch.tensor([st["migrated"]], dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
+        mig = torch.tensor([st["migrated"], st.get("deferred", 0)], dtype=torch.int64,
+                           device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(mig)
         rect_all = [None] * world
         dist.all_gather_object(rect_all, rects.tolist())
         if rank == 0:
-            np.savez(os.path.join(out, "res.npz"), migrated=int(mig.item()), bounds=np.array(dom.bounds),
+            np.savez(os.path.join(out, "res.npz"), migrated=int(mig[0].item()), deferred=int(mig[1].item()),
+                     bounds=np.array(dom.bounds),
                      rects=np.array(rect_all, np.int64),
                      **{k: g.cpu().numpy() for k, g in got.items()})
         dom.engine.close()  # its graphs before the communicator
@@ -141,11 +143,12 @@ def test_gpu_slabs_rccl_shared_gpu(dev, tmp_path, world):
 
 @pytest.mark.parametrize("backend", ["gloo", "nccl-shared"])
 def test_gpu_slabs_deferred_migration(dev, tmp_path, backend):
-    """Migration payloads of 4 particles (GSMPM_SLAB_MIG_CAP): most leavers
-    cannot be sent at their first migration and stay with their old slab for
-    a later one -- ownership must not change the physics."""
-    r = _run(3, tmp_path, backend=backend, env={"GSMPM_SLAB_MIG_CAP": "4"})
-    assert int(r["migrated"]) > 50
+    """Migration payloads of 2 particles in the first step call
+    (GSMPM_SLAB_MIG_CAP; the library grows them after): most leavers cannot
+    be sent at their first migration and stay with their old slab for a later
+    one -- ownership must not change the physics."""
+    r = _run(3, tmp_path, backend=backend, env={"GSMPM_SLAB_MIG_CAP": "2"})
+    assert int(r["migrated"]) > 50 and int(r["deferred"]) > 0, (int(r["migrated"]), int(r["deferred"]))
     errs = _check(r)
     print("deferred", backend, errs, "migrated", int(r["migrated"]))
 
