@@ -18,14 +18,17 @@ namespace gsmpm {
 
 // FAST: reciprocal square roots and square roots by the hardware
 // instructions (v_rsq_f32 / v_sqrt_f32, ~1 ulp) instead of the correctly
-// rounded sequences (27 / 18 VALU each, 25 per SVD).  Sifakis' algorithm is
-// written around an approximate rsqrt, and Taichi builds it with fast math.
-// Where a result depends on the SVD basis itself (foam's element-wise
-// U * diag * V^T, SURVEY F13: for F ~ I the basis is ill-defined and one ulp
-// picks another) the correctly rounded form is used, as in the oracle.
-// GSMPM_SVD_FAST=0 at build time: correctly rounded everywhere.
+// rounded sequences (27 / 18 VALU each, 25 per SVD).  Off by default (round
+// 3): at the BASELINE sizes the ~1 ulp per SVD put the plastic materials ~10x
+// further from the oracle than the oracle is from itself under a reordered
+// P2G sum (metal, 100k / 128^3, substep 100: F_trial 1.2e-4 with it, 1.7e-5
+// without, reorder spread 1.5e-5; sand v 2.3e-3 vs 4.3e-4 vs 4.4e-4;
+// tests/test_gpu_parity_long.py), for 2.3 us of k_fused<metal>.  Where a
+// result depends on the SVD basis itself (foam's element-wise U * diag * V^T,
+// SURVEY F13) the correctly rounded form is used regardless.
+// GSMPM_SVD_FAST=1 at build time: the hardware instructions (A/B).
 #ifndef GSMPM_SVD_FAST
-#define GSMPM_SVD_FAST 1
+#define GSMPM_SVD_FAST 0
 #endif
 template <bool FAST>
 __device__ __forceinline__ float svd_rsqrt(float x) {
