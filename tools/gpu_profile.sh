@@ -1,8 +1,9 @@
-# One GPU call: bench line, rocprofv3 kernel stats of the bench, PMC passes.
+# One GPU call: bench line, rocprofv3 kernel stats of the bench, PMC passes
+# for config B (lego, tools/pmc.sh) and config D (bicycle, tools/pmc_D.sh).
 # Raw traces are pruned at the end so gpurun_out/ stays small (only the
 # summaries travel back).  Usage: bash tools/gpu_profile.sh <tag>
 set -e
-TAG=${1:-r02}
+TAG=${1:-r03}
 O=gpurun_out/$TAG
 mkdir -p $O
 timeout -k 10 400 python3 bench.py > $O/bench.log 2>&1
@@ -14,5 +15,6 @@ rm -rf $O/prof
 if [ "${PMC:-1}" = "1" ]; then
   bash tools/pmc.sh $O/pmc > $O/pmc.log 2>&1
   for d in p1 p2 p3 p4; do rm -rf $O/pmc/$d; done
+  bash tools/pmc_D.sh $O/pmcD > $O/pmcD.log 2>&1
 fi
 echo ok
