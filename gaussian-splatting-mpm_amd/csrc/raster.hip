@@ -567,7 +567,12 @@ __global__ __launch_bounds__(256) void k_render4(const uint2* __restrict__ range
       cnt += __popcll(m);
     }
     if (lane < ((cnt + kU - 1) & ~(kU - 1)) - cnt) s_idx[q][cnt + lane] = (unsigned short)(kBatch + lane);
-    __syncthreads();  // s_idx: written by the wave's lanes, read across lanes (a wave-scope fence is not enough here)
+#ifdef GSMPM_RENDER4_BARRIER
+    __syncthreads();
+#else
+    // s_idx is this wave's own: its LDS writes complete (in order) before its reads
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#endif
     for (int b = 0; b < cnt; b += kU) {
       if (__all(done)) break;
       float al[kU];
@@ -1535,9 +1540,12 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     }
   }
   if (!ranges_written && K == 0) GSMPM_HIP(hipMemsetAsync(r->ranges, 0, ntiles * sizeof(uint2), st));
-  // GSMPM_RASTER_QUARTERS=1: the earlier one-workgroup-per-quarter k_render (A/B; bit-identical output)
-  const char* rq = std::getenv("GSMPM_RASTER_QUARTERS");
-  if (rq && rq[0] == '1')
+  // GSMPM_RASTER_TILE_SHARED=1: k_render4 (one workgroup per tile; bit-identical output).  It
+  // moves 35 % fewer bytes (lego frame: 41.3 vs 63.6 MB per launch, PMC) but renders in
+  // 0.30-0.33 ms against 0.26-0.27 ms (tools/ab_render.sh, 3 pairs): the blend is bound by
+  // the heaviest tiles' serial walk, and a tile's four quarters now wait for each other
+  const char* ts = std::getenv("GSMPM_RASTER_TILE_SHARED");
+  if (!(ts && ts[0] == '1'))
     hipLaunchKernelGGL(k_render, dim3(2 * a.grid_x, 2 * a.grid_y), dim3(64), 0, st, r->ranges, r->ids_sorted, a.W,
                        a.H, a.grid_x, r->xy, r->conic, r->rgb, in->bg, out_color,
                        r->forward_only ? nullptr : r->final_T, r->forward_only ? nullptr : r->n_contrib, tkeys,

@@ -241,7 +241,7 @@ def test_num_rendered_and_radii_exact(dev, P, W, H, tiles):
 def test_tile_shared_render_matches_quarter_render(dev, monkeypatch, scene, onesweep):
     """k_render4 (one workgroup per tile, each list entry read and gathered once
     for the four quarter waves) against the one-workgroup-per-quarter k_render
-    (GSMPM_RASTER_QUARTERS=1): pixels and, through the backward, final T and
+    (the default; k_render4 with GSMPM_RASTER_TILE_SHARED=1): pixels and, through the backward, final T and
     last contributor are bit-identical -- with sub-tile masks (chunked sort)
     and without (onesweep: the quarter test on the gathered conic)."""
     import torch
@@ -263,7 +263,7 @@ def test_tile_shared_render_matches_quarter_render(dev, monkeypatch, scene, ones
     monkeypatch.setenv("GSMPM_RASTER_ONESWEEP", onesweep)
     out = {}
     for quarters in ("1", "0"):
-        monkeypatch.setenv("GSMPM_RASTER_QUARTERS", quarters)
+        monkeypatch.setenv("GSMPM_RASTER_TILE_SHARED", "0" if quarters == "1" else "1")
         m3, o1, s1, cv = t(means, True), t(opa, True), t(shs, True), t(c6, True)
         img, _ = GaussianRasterizer(st)(means3D=m3, means2D=None, opacities=o1, shs=s1, cov3D_precomp=cv)
         (img * wgt).sum().backward()
