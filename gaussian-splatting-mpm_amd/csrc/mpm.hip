@@ -1443,6 +1443,7 @@ struct gsmpm_mpm {
   bool capturing = false;                    // a graph capture of this handle is open (graph_substeps)
   long s_migrations = 0, s_migrated = 0;     // counters (gsmpm_mpm_slab_stats)
   long s_deferred = 0;
+  long s_host_syncs = 0, s_calls = 0;        // host syncs inside gsmpm_mpm_slab_step, step calls
   long s_since = 0;                          // substeps since the last migration
   bool s_graph = true;                       // capture RCCL step calls in hipGraphs (GSMPM_SLAB_GRAPH=0: eager)
   float* x_host = nullptr;                   // CALLBACK transport: pinned staging of the exchanged buffers

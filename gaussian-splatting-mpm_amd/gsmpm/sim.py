@@ -138,10 +138,10 @@ class Simulator:
         return out
 
     def slab_stats(self):
-        b = (ctypes.c_int64 * 10)()
+        b = (ctypes.c_int64 * 12)()
         check(LIB.gsmpm_mpm_slab_stats(self._h, b), "gsmpm_mpm_slab_stats")
         keys = ("migrations", "migrated", "lo", "hi", "margin", "interval", "window_planes", "capacity", "deferred",
-                "payload_capacity")
+                "payload_capacity", "host_syncs", "step_calls")
         return dict(zip(keys, [int(v) for v in b]))
 
     def slab_rects(self):

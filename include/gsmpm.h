@@ -157,8 +157,10 @@ int gsmpm_mpm_count(gsmpm_mpm* h);
 /* global ids of this rank's particles, in the order gsmpm_mpm_get returns rows */
 int gsmpm_mpm_get_gid(gsmpm_mpm* h, int32_t* out, void* stream);
 /* {migrations, particles migrated (sent), lo, hi, margin, interval, window planes, capacity,
- *  leavers deferred (payload full), migration payload capacity} */
-int gsmpm_mpm_slab_stats(gsmpm_mpm* h, int64_t out10[10]);
+ *  leavers deferred (payload full), migration payload capacity, host syncs inside
+ *  gsmpm_mpm_slab_step (one per call, plus one on the first call after set_particles),
+ *  step calls} */
+int gsmpm_mpm_slab_stats(gsmpm_mpm* h, int64_t out12[12]);
 /* The yz rect of each window that the exchange moves, agreed by the two ranks of
  * the bound at every migration: {y0, ny, z0, nz} of the lower window, then of the
  * upper one (ny = nz = 0: nothing to exchange; before the first slab_step, the

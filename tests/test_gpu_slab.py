@@ -189,3 +189,74 @@ def test_gpu_slab_error_stops_every_rank(dev, tmp_path):
     migs, msg = errs[0].split("|", 1)
     assert f"rank {world - 1}:" in msg and "capacity" in msg, msg
     assert int(migs) <= STEPS // 10, migs  # errors surface at the end of the step call, on every rank
+
+
+def _bicycle_worker(rank, world, port, out, steps, calls):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(shared_gpu_rccl_env(rank))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    try:
+        from gsmpm.dist import SlabDomain, make_transport
+        from scenarios import lego_problem
+        prob = lego_problem(1_000_000, 256, config="bicycle.json")
+        cfg = prob["cfg"]
+        v = np.tile(np.array(BICYCLE_V0, np.float32), (len(prob["x"]), 1))
+        xp = make_transport(rank, world, device=dev)
+        dom = SlabDomain(prob["x"], prob["cov"], prob["vol"], v=v, rank=rank, world=world, transport=xp,
+                         n_grid=256, grid_extent=cfg["grid_extent"], margin=2, interval=10, device=dev,
+                         material=cfg["material"], E=cfg["E"], nu=cfg["nu"], density=cfg["density"],
+                         gravity=cfg["gravity"])
+        dom.add_plane_collider([0, 0, 0.4], [0, 0, 1])  # main.py:276 (bicycle.json has no BC list)
+        per = steps // calls
+        for _ in range(calls):
+            dom.step(cfg["substep_dt"], [1] * per)
+        got = {k: dom.gather_field(k) for k in ("x", "F_trial")}
+        dom.postprocess()
+        got["cov"] = dom.gather_field("cov")
+        st = dom.stats()
+        tot = torch.tensor([st["migrated"], st["host_syncs"], st["step_calls"]], dtype=torch.int64, device=dev)
+        dist.all_reduce(tot)
+        if rank == 0:
+            np.savez(os.path.join(out, "bicycle.npz"), migrated=int(tot[0]), host_syncs=int(tot[1]),
+                     calls=int(tot[2]), bounds=np.array(dom.bounds), **{k: g.cpu().numpy() for k, g in got.items()})
+        dom.engine.close()
+        xp.close()
+    finally:
+        dist.destroy_process_group()
+
+
+BICYCLE_V0 = (2.0, 0.0, 0.0)  # +x drift (grid units / s) so particles cross the slab plane and migrate
+
+
+def test_gpu_slabs_bicycle_two_ranks_rccl(dev, tmp_path):
+    """configs[3]'s workload through the slab path: bicycle.json, 1M Gaussians
+    in [0.05, 0.95]^3, 256^3, two RCCL slab ranks (sharing cuda:0), 50
+    substeps in 5 step calls with a migration every 10 substeps (an initial
+    +x drift makes ~1% of the particles cross the slab plane), against the
+    single-domain OpenMP oracle: x, F_trial, cov within 1e-4.  Each step call
+    is one captured graph with the counts kept on the device: the library
+    syncs the host once per call (the record check), +1 on the first call."""
+    import oracle as O
+    from scenarios import lego_problem
+    steps, calls, world = 50, 5, 2
+    mp.spawn(_bicycle_worker, args=(world, free_port(), str(tmp_path), steps, calls), nprocs=world, join=True)
+    r = np.load(os.path.join(tmp_path, "bicycle.npz"))
+    assert int(r["migrated"]) > 1000, int(r["migrated"])
+    assert int(r["calls"]) == world * calls
+    assert int(r["host_syncs"]) == world * (calls + 1), (int(r["host_syncs"]), world * (calls + 1))
+    prob = lego_problem(1_000_000, 256, config="bicycle.json")
+    cfg = prob["cfg"]
+    v = np.tile(np.array(BICYCLE_V0, np.float32), (len(prob["x"]), 1))
+    ref = O.OracleMPM(prob["x"], prob["cov"], prob["vol"], v=v, n_grid=256, grid_extent=cfg["grid_extent"],
+                      material=cfg["material"], E=cfg["E"], nu=cfg["nu"], density=cfg["density"],
+                      gravity=cfg["gravity"], threaded=True)
+    ref.add_collider([0.0, 0.0, 0.4], [0.0, 0.0, 1.0], 0.0)
+    for _ in range(steps):
+        ref.substep(cfg["substep_dt"], [], [1])
+    ref.postprocess()
+    errs = {"x": rel_err(r["x"], ref.x), "F_trial": rel_err(r["F_trial"], ref.F_trial), "cov": rel_err(r["cov"], ref.cov)}
+    print("bicycle slab2", errs, "migrated", int(r["migrated"]), "bounds", r["bounds"].tolist())
+    for k, e in errs.items():
+        assert e < 1e-4, (k, e, errs)
