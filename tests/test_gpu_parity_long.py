@@ -74,14 +74,14 @@ def _field_errs(got, exp, inv_dx):
     return e
 
 
-def _horizon(prob, material, checkpoints, dev, spread=True):
+def _horizon(prob, material, checkpoints, dev, spread=True, runs=None):
     """Run the drop-in simulator, the oracle and (spread=True) SPREAD_RUNS
     oracles on permuted particle orders in lockstep; the error curves at
     `checkpoints` (the spread: the largest error of the permuted runs)."""
     from gpu_helpers import dropin_sim
     ref, imps, ops = build_oracle_sim(prob, material=material, threaded=True)
     alts = []
-    for k in range(SPREAD_RUNS if spread else 0):
+    for k in range((runs or SPREAD_RUNS) if spread else 0):
         pprob, inv = _permuted(prob, seed=11 + k)
         alts.append((build_oracle_sim(pprob, material=material, threaded=True), inv))
     s, _ = dropin_sim(prob, dev, **({"material": material} if material else {}))
@@ -133,15 +133,18 @@ def _bound(bound, rec, key, curve=None):
 def test_config_B_ten_frames(dev):
     """lego.json, 100k, 128^3, 1,000 substeps (10 frames): x, F_trial, cov and R
     within 1e-4 of the field's max at every checkpoint; v, C within the
-    documented bounds of test_gpu_mpm.py; per-element x within 1e-3."""
+    documented bounds of test_gpu_mpm.py; per-element x within 1e-3; the
+    per-element covariance error (floored at 1e-3 of the max) reported beside
+    a reordered oracle's and held to twice it."""
     prob = lego_problem(100_000, 128)
-    curve, post = _horizon(prob, None, (1, 100, 250, 500, 1000), dev, spread=False)
+    curve, post = _horizon(prob, None, (1, 100, 250, 500, 1000), dev, runs=1)
     for c, rec in curve.items():
         g = rec["gpu"]
         assert g["x"] < TOL and g["F_trial"] < TOL, (c, g)
         assert g["v"] < 2e-3 and g["C"] < 5e-3, (c, g)
         assert g["x_elem"] < 1e-3, (c, g)
     assert post["gpu"]["cov"] < TOL and post["gpu"]["R"] < TOL, post
+    assert post["gpu"]["cov_elem"] < _bound(TOL, post, "cov_elem"), post
     _dump("long_config_B_1000", {"config": "lego.json", "N": 100_000, "n_grid": 128, "curve": curve, "post": post})
 
 
