@@ -731,17 +731,21 @@ __global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int 
     v[i] = e < K ? vals[e] : kNoEntry;
   }
   BRS().sort(k, v, s_sort, 0, bits);
+  // sorted position sp = thread * kSortI + i lives at s_key[(sp % kSortI) * kSortT + sp / kSortI]:
+  // a wave's 64 stores (or loads) of one i hit 64 consecutive words -- the plain
+  // sp layout strided them by kSortI words, 8 lanes per bank
+  auto slot = [](int sp) { return (sp % kSortI) * kSortT + sp / kSortI; };
   unsigned t[kSortI];
 #pragma unroll
   for (int i = 0; i < kSortI; ++i) {
     t[i] = sort_tile(k[i], lowmask, ntiles);
-    s_key[threadIdx.x * kSortI + i] = t[i];
+    s_key[i * kSortT + threadIdx.x] = t[i];
   }
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < kSortI; ++i) {
     const int sp = threadIdx.x * kSortI + i;
-    if (v[i] != kNoEntry && (sp == 0 || s_key[sp - 1] != t[i])) s_start[t[i]] = sp;
+    if (v[i] != kNoEntry && (sp == 0 || s_key[slot(sp - 1)] != t[i])) s_start[t[i]] = sp;
   }
   __syncthreads();
 #pragma unroll
