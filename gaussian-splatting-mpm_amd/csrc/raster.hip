@@ -78,6 +78,8 @@ struct RasterDev {
   const float *viewmatrix, *projmatrix, *campos, *bg;
   float tanfovx, tanfovy, focal_x, focal_y;
   int grid_x, grid_y;
+  int tight;  // bin each Gaussian into the tiles its alpha >= 1/255 box reaches (k_preprocess)
+  int sh_vec4;  // M == 16 and shs 16-byte aligned: a Gaussian's 48 SH floats as 12 dwordx4 loads
 };
 
 __device__ __forceinline__ void xform4x3(const float* p, const float* m, float o[3]) {
@@ -93,6 +95,17 @@ __device__ __forceinline__ void get_rect(float px, float py, int r, int gx, int 
   rmin[1] = min(gy, max(0, (int)((py - r) / kBY)));
   rmax[0] = min(gx, max(0, (int)((px + r + kBX - 1) / kBX)));
   rmax[1] = min(gy, max(0, (int)((py + r + kBY - 1) / kBY)));
+}
+
+// a Gaussian's binning rect [x0, x1) x [y0, y1) in tiles, 16 bits each (k_preprocess writes it)
+__device__ __forceinline__ uint2 pack_rect(int x0, int y0, int x1, int y1) {
+  return make_uint2((unsigned)x0 | ((unsigned)y0 << 16), (unsigned)x1 | ((unsigned)y1 << 16));
+}
+__device__ __forceinline__ void unpack_rect(uint2 r, int rmin[2], int rmax[2]) {
+  rmin[0] = (int)(r.x & 0xffffu);
+  rmin[1] = (int)(r.x >> 16);
+  rmax[0] = (int)(r.y & 0xffffu);
+  rmax[1] = (int)(r.y >> 16);
 }
 
 // computeCov3D: Sigma = R diag(s*mod)^2 R^T, R from the (unnormalised) quaternion (r,x,y,z)
@@ -154,13 +167,30 @@ __device__ __forceinline__ void cov2d(const float* mean, const RasterDev& a, con
   out[2] = cc + 0.3f;
 }
 
+// VEC4: the Gaussian's 48 coefficients arrive as 12 16-byte loads into
+// registers (one lane's 192 B are contiguous; 48 scalar loads made every load
+// instruction touch 64 cache lines); the arithmetic is the same either way
+template <bool VEC4>
 __device__ __forceinline__ void sh_rgb(const RasterDev& a, int idx, const float* pos, float rgb[3], unsigned& clamp) {
   float dir[3] = {pos[0] - a.campos[0], pos[1] - a.campos[1], pos[2] - a.campos[2]};
   const float len = sqrtf(dir[0] * dir[0] + dir[1] * dir[1] + dir[2] * dir[2]);
   dir[0] /= len;
   dir[1] /= len;
   dir[2] /= len;
-  const float* sh = a.shs + (size_t)idx * a.M * 3;
+  const float* shg = a.shs + (size_t)idx * a.M * 3;
+  float shv[VEC4 ? 48 : 1];
+  if constexpr (VEC4) {
+    const float4* s4 = reinterpret_cast<const float4*>(shg);
+#pragma unroll
+    for (int q = 0; q < 12; ++q) {
+      const float4 v = s4[q];
+      shv[4 * q] = v.x;
+      shv[4 * q + 1] = v.y;
+      shv[4 * q + 2] = v.z;
+      shv[4 * q + 3] = v.w;
+    }
+  }
+  const float* sh = VEC4 ? shv : shg;
   const float x = dir[0], y = dir[1], z = dir[2];
   const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
 #pragma unroll
@@ -187,13 +217,78 @@ __device__ __forceinline__ void sh_rgb(const RasterDev& a, int idx, const float*
   }
 }
 
+constexpr int kSub = 8;  // pixel sub-tile side: one wave of pixels
+
+// can alpha = o exp(power) reach 1/255 at a pixel centre of the sub-tile
+// [x0, x0 + 7] x [y0, y0 + 7]?  Conservative; NaNs keep the Gaussian.  The
+// Gaussian-only part (the ellipse's half extents) is factored out so the
+// emission computes it once per Gaussian, not once per (tile, quarter).
+struct Reach {
+  float ex, ey;  // half extents of the alpha >= 1/255 ellipse's box, + 1 px
+  int mode;      // 0: test the box, 1: reaches nothing (o < 1/255), 2: keep (degenerate conic)
+};
+__device__ __forceinline__ Reach reach_of(float4 co) {
+  Reach r{0.f, 0.f, 0};
+  if (co.w * 255.0f < 0.999f) {  // o < 1/255: alpha < 1/255 everywhere
+    r.mode = 1;
+    return r;
+  }
+  const float det = co.x * co.z - co.y * co.y;
+  if (!(det > 0.0f)) {
+    r.mode = 2;
+    return r;
+  }
+  const float k = fmaxf(2.0f * __logf(255.0f * co.w), 0.0f) * 1.02f + 0.02f;
+  r.ex = sqrtf(k * co.z / det) + 1.0f;
+  r.ey = sqrtf(k * co.x / det) + 1.0f;
+  return r;
+}
+__device__ __forceinline__ bool reaches_box(const Reach& r, float2 g, float x0, float y0) {
+  if (r.mode) return r.mode == 2;
+  return !(g.x + r.ex < x0 || g.x - r.ex > x0 + (kSub - 1) || g.y + r.ey < y0 || g.y - r.ey > y0 + (kSub - 1));
+}
+__device__ __forceinline__ bool reaches_subtile(float2 g, float4 co, float x0, float y0) {
+  return reaches_box(reach_of(co), g, x0, y0);
+}
+
+// Tight binning (RasterDev::tight).  A (Gaussian, tile) pair whose four
+// sub-tiles the Gaussian's alpha-reach box misses is one upstream's blend
+// skips at every pixel of the tile.  The box is axis-aligned, so the tiles it
+// reaches within the 3-sigma rect are themselves a rect: the sub-tile columns
+// c (pixels [8c, 8c + 7]) that reaches_box passes are those with
+// !(lo > 8c + 7) (true from some c on) and !(hi < 8c) (true up to some c),
+// an interval, and likewise for rows.  k_preprocess bins the Gaussian into
+// that rect only, with reaches_box's own comparisons on the same floats, so
+// every emitted pair reaches at least one sub-tile and no pair that reaches
+// one is lost: the tile lists are the culled lists k_render walks, and K
+// shrinks before the sort.  num_rendered stays upstream's 3-sigma count.
+// [first, last] sub-cells of [c0, c1) the box [lo, hi] reaches (first > last: none)
+__device__ __forceinline__ void reach_cells(float lo, float hi, int c0, int c1, int& first, int& last) {
+  int a = c0, b = c1;
+  while (a < b) {  // first c with !(lo > 8c + 7)
+    const int m = (a + b) >> 1;
+    if (!(lo > (float)(m * kSub) + (kSub - 1))) b = m;
+    else a = m + 1;
+  }
+  first = a;
+  a = c0;
+  b = c1;
+  while (a < b) {  // first c with hi < 8c
+    const int m = (a + b) >> 1;
+    if (hi < (float)(m * kSub)) b = m;
+    else a = m + 1;
+  }
+  last = a - 1;
+}
+
 __global__ __launch_bounds__(256) void k_preprocess(RasterDev a, int* __restrict__ radii, float* __restrict__ depth,
                                                     float2* __restrict__ xy, float4* __restrict__ conic_o,
-                                                    float4* __restrict__ rgbo, unsigned* __restrict__ tiles) {
+                                                    float4* __restrict__ rgbo, unsigned long long* __restrict__ tiles,
+                                                    uint2* __restrict__ rect) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= a.P) return;
   radii[idx] = 0;
-  tiles[idx] = 0;
+  tiles[idx] = 0;  // (3-sigma tile count << 32) | binned tile count
   const float* p = a.means3D + (size_t)idx * 3;
   float pv[3];
   xform4x3(p, a.viewmatrix, pv);
@@ -232,25 +327,46 @@ __global__ __launch_bounds__(256) void k_preprocess(RasterDev a, int* __restrict
     rgb[1] = a.colors_precomp[(size_t)idx * 3 + 1];
     rgb[2] = a.colors_precomp[(size_t)idx * 3 + 2];
   } else {
-    sh_rgb(a, idx, p, rgb, clamp);
+    if (a.sh_vec4) sh_rgb<true>(a, idx, p, rgb, clamp);
+    else sh_rgb<false>(a, idx, p, rgb, clamp);
   }
   depth[idx] = pv[2];
   radii[idx] = rad;
   xy[idx] = make_float2(px, py);
-  conic_o[idx] = make_float4(cv[2] * di, -cv[1] * di, cv[0] * di, a.opacities[idx]);
+  const float4 co = make_float4(cv[2] * di, -cv[1] * di, cv[0] * di, a.opacities[idx]);
+  conic_o[idx] = co;
   rgbo[idx] = make_float4(rgb[0], rgb[1], rgb[2], __uint_as_float(clamp));  // .w: SH clamp bits
-  tiles[idx] = (unsigned)((rmax[1] - rmin[1]) * (rmax[0] - rmin[0]));
+  const unsigned full = (unsigned)((rmax[1] - rmin[1]) * (rmax[0] - rmin[0]));
+  int t0[2] = {rmin[0], rmin[1]}, t1[2] = {rmax[0], rmax[1]};
+  if (a.tight) {
+    const Reach rc = reach_of(co);
+    if (rc.mode == 1) {
+      t1[0] = t0[0];
+    } else if (rc.mode == 0) {
+      const float lo[2] = {px - rc.ex, py - rc.ey}, hi[2] = {px + rc.ex, py + rc.ey};
+#pragma unroll
+      for (int d = 0; d < 2; ++d) {
+        int first, last;
+        reach_cells(lo[d], hi[d], 2 * rmin[d], 2 * rmax[d], first, last);
+        t0[d] = first >> 1;
+        t1[d] = first > last ? t0[d] : (last >> 1) + 1;
+      }
+    }
+  }
+  rect[idx] = pack_rect(t0[0], t0[1], t1[0], t1[1]);
+  tiles[idx] = ((unsigned long long)full << 32) | (unsigned)((t1[0] - t0[0]) * (t1[1] - t0[1]));
 }
 
-__global__ __launch_bounds__(256) void k_duplicate(int P, const float2* __restrict__ xy, const float* __restrict__ depth,
-                                                   const unsigned* __restrict__ offsets, const int* __restrict__ radii,
-                                                   int gx, int gy, unsigned long long* __restrict__ keys,
+__global__ __launch_bounds__(256) void k_duplicate(int P, const uint2* __restrict__ rect, const float* __restrict__ depth,
+                                                   const unsigned long long* __restrict__ offsets,
+                                                   const int* __restrict__ radii, int gx,
+                                                   unsigned long long* __restrict__ keys,
                                                    unsigned* __restrict__ vals) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= P || radii[idx] <= 0) return;
-  unsigned off = idx == 0 ? 0u : offsets[idx - 1];
+  unsigned off = idx == 0 ? 0u : (unsigned)offsets[idx - 1];
   int rmin[2], rmax[2];
-  get_rect(xy[idx].x, xy[idx].y, radii[idx], gx, gy, rmin, rmax);
+  unpack_rect(rect[idx], rmin, rmax);
   const unsigned dbits = __float_as_uint(depth[idx]);
   for (int y = rmin[1]; y < rmax[1]; ++y)
     for (int x = rmin[0]; x < rmax[0]; ++x) {
@@ -299,41 +415,9 @@ __global__ __launch_bounds__(256) void k_ranges(int L, const unsigned long long*
 // evaluated independently (their LDS reads and exp2s pipeline) and then folded
 // in order, branch-free.
 constexpr int kU = 8;
-constexpr int kSub = 8;          // pixel sub-tile side: one wave of pixels
 constexpr int kQ = 4;            // list entries per lane per batch
 constexpr int kBatch = 64 * kQ;  // entries staged per batch
 
-// can alpha = o exp(power) reach 1/255 at a pixel centre of the sub-tile
-// [x0, x0 + 7] x [y0, y0 + 7]?  Conservative; NaNs keep the Gaussian.  The
-// Gaussian-only part (the ellipse's half extents) is factored out so the
-// emission computes it once per Gaussian, not once per (tile, quarter).
-struct Reach {
-  float ex, ey;  // half extents of the alpha >= 1/255 ellipse's box, + 1 px
-  int mode;      // 0: test the box, 1: reaches nothing (o < 1/255), 2: keep (degenerate conic)
-};
-__device__ __forceinline__ Reach reach_of(float4 co) {
-  Reach r{0.f, 0.f, 0};
-  if (co.w * 255.0f < 0.999f) {  // o < 1/255: alpha < 1/255 everywhere
-    r.mode = 1;
-    return r;
-  }
-  const float det = co.x * co.z - co.y * co.y;
-  if (!(det > 0.0f)) {
-    r.mode = 2;
-    return r;
-  }
-  const float k = fmaxf(2.0f * __logf(255.0f * co.w), 0.0f) * 1.02f + 0.02f;
-  r.ex = sqrtf(k * co.z / det) + 1.0f;
-  r.ey = sqrtf(k * co.x / det) + 1.0f;
-  return r;
-}
-__device__ __forceinline__ bool reaches_box(const Reach& r, float2 g, float x0, float y0) {
-  if (r.mode) return r.mode == 2;
-  return !(g.x + r.ex < x0 || g.x - r.ex > x0 + (kSub - 1) || g.y + r.ey < y0 || g.y - r.ey > y0 + (kSub - 1));
-}
-__device__ __forceinline__ bool reaches_subtile(float2 g, float4 co, float x0, float y0) {
-  return reaches_box(reach_of(co), g, x0, y0);
-}
 
 // Tile keys of the depth-ordered path carry, above the tile index, a mask of
 // the tile's four 8x8 sub-tiles the Gaussian can reach (alpha >= 1/255 there,
@@ -617,8 +701,11 @@ __global__ __launch_bounds__(256) void k_render4(const uint2* __restrict__ range
 }
 
 constexpr unsigned kNoCount = 0xffffffffu;
-__global__ void k_publish_count(const unsigned* __restrict__ src, unsigned* dst) {
-  __hip_atomic_store(dst, *src, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+// dst[1] = the 3-sigma pair count (num_rendered), then dst[0] = the binned count K (the host spins on it)
+__global__ void k_publish_count(const unsigned long long* __restrict__ src, unsigned* dst) {
+  const unsigned long long v = *src;
+  __hip_atomic_store(dst + 1, (unsigned)(v >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(dst, (unsigned)v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // sorted emission index -> Gaussian id (the sort carries emission indices)
@@ -636,36 +723,45 @@ __global__ __launch_bounds__(256) void k_ids(int K, const unsigned* __restrict__
 // (tile << 32 | depth bits) sort produces, with 4-byte keys and 12 bits of
 // radix instead of 32 + 12.
 // tiles touched by the Gaussian of depth rank r: the depth-order scan's input
+// (both counts of k_preprocess's tiles word: their scan's last entry holds K and num_rendered)
 struct TilesOfRank {
-  const unsigned* tiles;
-  __host__ __device__ unsigned operator()(unsigned g) const { return tiles[g]; }
+  const unsigned long long* tiles;
+  __host__ __device__ unsigned long long operator()(unsigned g) const { return tiles[g]; }
 };
-inline rocprim::transform_iterator<const unsigned*, TilesOfRank, unsigned> ranked_tiles(const unsigned* order,
-                                                                                        const unsigned* tiles) {
-  return rocprim::transform_iterator<const unsigned*, TilesOfRank, unsigned>(order, TilesOfRank{tiles});
+inline rocprim::transform_iterator<const unsigned*, TilesOfRank, unsigned long long> ranked_tiles(
+    const unsigned* order, const unsigned long long* tiles) {
+  return rocprim::transform_iterator<const unsigned*, TilesOfRank, unsigned long long>(order, TilesOfRank{tiles});
+}
+// the binned count alone (the index-order offsets of the record slots)
+struct BinnedTiles {
+  __host__ __device__ unsigned operator()(unsigned long long t) const { return (unsigned)t; }
+};
+inline rocprim::transform_iterator<const unsigned long long*, BinnedTiles, unsigned> binned_tiles(
+    const unsigned long long* tiles) {
+  return rocprim::transform_iterator<const unsigned long long*, BinnedTiles, unsigned>(tiles, BinnedTiles{});
 }
 // Depth-ordered emission, one lane per pair (a lane per Gaussian would
 // serialise the ~1600 stores of the frame's largest Gaussians): the pair's
 // Gaussian is found by binary search over the depth-order offsets, and the
 // pair lands at its depth-order offset + its index in the Gaussian's rect.
 __global__ __launch_bounds__(256) void k_emit_pairs(int K, int P, const unsigned* __restrict__ order,
-                                                    const unsigned* __restrict__ offr, const float2* __restrict__ xy,
-                                                    const float4* __restrict__ conic_o,
-                                                    const int* __restrict__ radii, int gx, int gy, int cull,
+                                                    const unsigned long long* __restrict__ offr,
+                                                    const float2* __restrict__ xy, const float4* __restrict__ conic_o,
+                                                    const uint2* __restrict__ rect, int gx, int cull,
                                                     unsigned* __restrict__ keys, unsigned* __restrict__ ids) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= K) return;
   int lo = 0, hi = P - 1;  // first r with offr[r] > e (offr: inclusive scan)
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
-    if (offr[mid] > (unsigned)e) hi = mid;
+    if ((unsigned)offr[mid] > (unsigned)e) hi = mid;
     else lo = mid + 1;
   }
   const unsigned g = order[lo];
-  const unsigned local = (unsigned)e - (lo ? offr[lo - 1] : 0u);
+  const unsigned local = (unsigned)e - (lo ? (unsigned)offr[lo - 1] : 0u);
   const float2 gp = xy[g];
   int rmin[2], rmax[2];
-  get_rect(gp.x, gp.y, radii[g], gx, gy, rmin, rmax);
+  unpack_rect(rect[g], rmin, rmax);
   const unsigned w = (unsigned)(rmax[0] - rmin[0]);
   const int x = rmin[0] + (int)(local % w), y = rmin[1] + (int)(local / w);
   unsigned m = 0xfu;
@@ -678,6 +774,97 @@ __global__ __launch_bounds__(256) void k_emit_pairs(int K, int P, const unsigned
   }
   keys[e] = m ? ((unsigned)(y * gx + x) | (m << kMaskShift)) : kCulledKey;
   ids[e] = g;
+}
+// Balanced depth-ordered emission (the default; k_emit_pairs above stays for
+// GSMPM_RASTER_EMIT_LANE=1).  k_emit_pairs' per-lane binary search is a
+// ~20-deep chain of dependent global loads at 1M Gaussians: bicycle's 39M
+// pairs took 546 us, memory-wait bound (SQ_WAIT_ANY 75 %).  Here a workgroup
+// owns `items` x 256 consecutive pairs [e0, e1):
+//   - the Gaussians r0 / r1 of its first and last pair come from a
+//     cooperative 256-ary search over the depth-order offsets (one load per
+//     lane per round, three rounds at 1M Gaussians);
+//   - the Gaussians [r0, r1] are staged in LDS, kEmitG at a time: offsets,
+//     id, tile rect and (culling) the alpha-reach box, one coalesced round
+//     of loads per Gaussian instead of one per pair;
+//   - each pair of the staged span finds its Gaussian by a binary search in
+//     LDS (from the lane's previous one) and is emitted from LDS alone.
+// Same pairs, same positions, same keys as k_emit_pairs.
+constexpr int kEmitT = 256, kEmitMaxI = 16, kEmitG = 1024;
+// first r in [lo, hi) with offr[r] > e, hi if none; uniform over the workgroup
+__device__ __forceinline__ int wg_upper_bound(const unsigned long long* __restrict__ offr, int lo, int hi, unsigned e) {
+  while (hi > lo) {
+    const int step = (hi - lo + kEmitT - 1) / kEmitT;
+    const int pos = lo + (int)threadIdx.x * step;
+    const int c = __syncthreads_count(pos < hi && (unsigned)offr[pos] <= e);  // samples <= e: a prefix of the samples
+    if (c == 0) return lo;
+    lo += (c - 1) * step + 1;
+    hi = min(hi, lo - 1 + step);  // the first sample > e (if any) bounds the answer
+  }
+  return lo;
+}
+__global__ __launch_bounds__(kEmitT) void k_emit_wg(int K, int P, int items, const unsigned* __restrict__ order,
+                                                    const unsigned long long* __restrict__ offr,
+                                                    const float2* __restrict__ xy, const float4* __restrict__ conic_o,
+                                                    const uint2* __restrict__ rect, int gx, int cull,
+                                                    unsigned* __restrict__ keys, unsigned* __restrict__ ids) {
+  __shared__ unsigned s_off[kEmitG + 1];  // [i]: first pair of staged Gaussian i, [i + 1]: one past its last
+  __shared__ unsigned s_g[kEmitG];        // Gaussian id
+  __shared__ uint2 s_rect[kEmitG];        // (x0 | y0 << 16, rect width) in tiles
+  __shared__ float4 s_box[kEmitG];        // alpha-reach box (x lo, x hi, y lo, y hi) in pixels (culling)
+  const int e0 = blockIdx.x * kEmitT * items, e1 = min(K, e0 + kEmitT * items);
+  const int r0 = wg_upper_bound(offr, 0, P, (unsigned)e0);
+  const int r1 = wg_upper_bound(offr, r0, P, (unsigned)(e1 - 1));
+  int rs = r0;        // first Gaussian of the span to stage
+  unsigned pa = e0;   // first pair not yet emitted
+  while (true) {      // uniform: spans of <= kEmitG Gaussians
+    const int ns = min(kEmitG, r1 + 1 - rs);
+    __syncthreads();  // the previous span's readers are done
+    if (threadIdx.x == 0) s_off[0] = rs ? (unsigned)offr[rs - 1] : 0u;
+    for (int i = threadIdx.x; i < ns; i += kEmitT) {
+      const unsigned g = order[rs + i];
+      s_off[i + 1] = (unsigned)offr[rs + i];
+      s_g[i] = g;
+      const uint2 rr = rect[g];
+      s_rect[i] = make_uint2(rr.x, (unsigned)max((int)(rr.y & 0xffffu) - (int)(rr.x & 0xffffu), 1));
+      if (cull) {
+        const float2 gp = xy[g];  // reaches_box's comparisons on the same sums (mode 1: empty box, mode 2: everything)
+        const Reach rc = reach_of(conic_o[g]);
+        const float inf = __builtin_inff();
+        s_box[i] = rc.mode == 1   ? make_float4(inf, -inf, inf, -inf)
+                   : rc.mode == 2 ? make_float4(-inf, inf, -inf, inf)
+                                  : make_float4(gp.x - rc.ex, gp.x + rc.ex, gp.y - rc.ey, gp.y + rc.ey);
+      }
+    }
+    __syncthreads();
+    const unsigned pb = min((unsigned)e1, s_off[ns]);
+    int lo = 0;
+    for (unsigned e = pa + threadIdx.x; e < pb; e += kEmitT) {
+      int hi = ns - 1;  // first i with s_off[i + 1] > e (exists: e < s_off[ns])
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (s_off[mid + 1] > e) hi = mid;
+        else lo = mid + 1;
+      }
+      const uint2 rw = s_rect[lo];
+      const unsigned local = e - s_off[lo];
+      const int x = (int)(rw.x & 0xffffu) + (int)(local % rw.y), y = (int)(rw.x >> 16) + (int)(local / rw.y);
+      unsigned m = 0xfu;
+      if (cull) {
+        const float4 bx = s_box[lo];
+        m = 0u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float x0 = (float)(x * kBX + (q & 1) * kSub), y0 = (float)(y * kBY + (q >> 1) * kSub);
+          if (!(bx.y < x0 || bx.x > x0 + (kSub - 1) || bx.w < y0 || bx.z > y0 + (kSub - 1))) m |= 1u << q;
+        }
+      }
+      keys[e] = m ? ((unsigned)(y * gx + x) | (m << kMaskShift)) : kCulledKey;
+      ids[e] = s_g[lo];
+    }
+    pa = pb;
+    rs += ns;
+    if (pa >= (unsigned)e1) break;
+  }
 }
 // Stable tile sort of the depth-ordered emission list for <= kMaxTiles tiles
 // (replaces the two onesweep passes: 2 kernels + a scan instead of ~8
@@ -765,33 +952,35 @@ __global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int 
 // Gaussian-index emission order (k_preprocess_bwd sums each Gaussian's
 // contiguous slots without atomics)
 __global__ __launch_bounds__(256) void k_slots(int K, const unsigned* __restrict__ tile_sorted,
-                                               const unsigned* __restrict__ ids, const float2* __restrict__ xy,
-                                               const int* __restrict__ radii, const unsigned* __restrict__ offsets,
-                                               int gx, int gy, unsigned* __restrict__ pos) {
+                                               const unsigned* __restrict__ ids, const uint2* __restrict__ rect,
+                                               const unsigned* __restrict__ offsets, int gx, int gy,
+                                               unsigned* __restrict__ pos) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= K) return;
   const unsigned id = ids[k], tile = tile_sorted[k] & kTileField;
   if (tile >= (unsigned)(gx * gy)) return;  // a culled pair (in no tile list)
   int rmin[2], rmax[2];
-  get_rect(xy[id].x, xy[id].y, radii[id], gx, gy, rmin, rmax);
+  unpack_rect(rect[id], rmin, rmax);
   const int tx = (int)(tile % (unsigned)gx), ty = (int)(tile / (unsigned)gx);
   pos[k] = (id == 0 ? 0u : offsets[id - 1]) + (unsigned)((ty - rmin[1]) * (rmax[0] - rmin[0]) + (tx - rmin[0]));
 }
-__global__ __launch_bounds__(256) void k_ranges32(int L, const unsigned* __restrict__ keys, int rb,
+// keys of tile >= ntiles (culled pairs, sorted last) are in no range
+__global__ __launch_bounds__(256) void k_ranges32(int L, const unsigned* __restrict__ keys, int rb, unsigned ntiles,
                                                   uint2* __restrict__ ranges) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= L) return;
   const unsigned cur = (keys[idx] & kTileField) >> rb;
+  const bool live = cur < ntiles;
   if (idx == 0) {
-    ranges[cur].x = 0;
+    if (live) ranges[cur].x = 0;
   } else {
     const unsigned prev = (keys[idx - 1] & kTileField) >> rb;
     if (cur != prev) {
-      ranges[prev].y = idx;
-      ranges[cur].x = idx;
+      if (prev < ntiles) ranges[prev].y = idx;
+      if (live) ranges[cur].x = idx;
     }
   }
-  if (idx == L - 1) ranges[cur].y = L;
+  if (idx == L - 1 && live) ranges[cur].y = L;
 }
 
 // ------------------------------------------------------------- backward --
@@ -1231,7 +1420,8 @@ struct gsmpm_raster {
   float2* xy = nullptr;
   float4* conic = nullptr;
   float4* rgb = nullptr;
-  unsigned* tiles = nullptr;
+  unsigned long long* tiles = nullptr;  // (3-sigma tile count << 32) | binned tile count
+  uint2* rect = nullptr;                // binned tile rect (pack_rect)
   unsigned* offsets = nullptr;
   void* scan_tmp = nullptr;
   size_t scan_tmp_bytes = 0;
@@ -1242,7 +1432,8 @@ struct gsmpm_raster {
   void* sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
   unsigned* ids_sorted = nullptr;  // Gaussian id per sorted pair (vals_sorted holds emission indices)
-  unsigned *dorder = nullptr, *dsorted = nullptr, *offr = nullptr;  // [capP] depth order, depth-order tile offsets
+  unsigned *dorder = nullptr, *dsorted = nullptr;  // [capP] depth order
+  unsigned long long* offr = nullptr;  // [capP] inclusive scan of tiles in depth order (index order: upstream keys)
   void* dsort_tmp = nullptr;
   unsigned* hist = nullptr;  // [2 * capH] tile-major chunk histogram, then its exclusive scan
   size_t capH = 0;
@@ -1255,7 +1446,7 @@ struct gsmpm_raster {
   // tile ranges
   size_t capT = 0;
   uint2* ranges = nullptr;
-  unsigned* h_count = nullptr;  // pinned, mapped + coherent (the device writes K into it)
+  unsigned* h_count = nullptr;  // [2] pinned, mapped + coherent (the device writes K, num_rendered into it)
   hipEvent_t count_ev = nullptr;  // recorded after k_publish_count: surfaces a fault while the host spins
   // per pixel (backward)
   size_t capPix = 0;
@@ -1280,7 +1471,7 @@ extern "C" {
 int gsmpm_raster_create(gsmpm_raster** out) {
   GSMPM_REQUIRE(out, "gsmpm_raster_create: null argument");
   auto* r = new gsmpm_raster();
-  hipError_t e = hipHostMalloc((void**)&r->h_count, sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent);
+  hipError_t e = hipHostMalloc((void**)&r->h_count, 2 * sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&r->count_ev, hipEventDisableTiming);
   if (e != hipSuccess) {
     if (r->h_count) (void)hipHostFree(r->h_count);
@@ -1295,7 +1486,7 @@ int gsmpm_raster_create(gsmpm_raster** out) {
 
 int gsmpm_raster_destroy(gsmpm_raster* r) {
   if (!r) return GSMPM_OK;
-  for (void* p : {(void*)r->radii_tmp, (void*)r->depth, (void*)r->xy, (void*)r->conic, (void*)r->rgb, (void*)r->tiles,
+  for (void* p : {(void*)r->radii_tmp, (void*)r->depth, (void*)r->xy, (void*)r->conic, (void*)r->rgb, (void*)r->tiles, (void*)r->rect,
                   (void*)r->offsets, r->scan_tmp, (void*)r->keys, (void*)r->keys_sorted, (void*)r->vals,
                   (void*)r->vals_sorted, r->sort_tmp, (void*)r->ranges, (void*)r->ids_sorted, (void*)r->rec,
                   (void*)r->final_T, (void*)r->n_contrib, (void*)r->dorder, (void*)r->dsorted, (void*)r->offr, r->dsort_tmp, (void*)r->hist})
@@ -1354,11 +1545,12 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     if ((rc = grow((void**)&r->xy, cap * sizeof(float2)))) return rc;
     if ((rc = grow((void**)&r->conic, cap * sizeof(float4)))) return rc;
     if ((rc = grow((void**)&r->rgb, cap * sizeof(float4)))) return rc;
-    if ((rc = grow((void**)&r->tiles, cap * sizeof(unsigned)))) return rc;
+    if ((rc = grow((void**)&r->tiles, cap * sizeof(unsigned long long)))) return rc;
+    if ((rc = grow((void**)&r->rect, cap * sizeof(uint2)))) return rc;
     if ((rc = grow((void**)&r->offsets, cap * sizeof(unsigned)))) return rc;
     if ((rc = grow((void**)&r->dorder, cap * sizeof(unsigned)))) return rc;
     if ((rc = grow((void**)&r->dsorted, cap * sizeof(unsigned)))) return rc;
-    if ((rc = grow((void**)&r->offr, cap * sizeof(unsigned)))) return rc;
+    if ((rc = grow((void**)&r->offr, cap * sizeof(unsigned long long)))) return rc;
     size_t bytes = 0;
     GSMPM_HIP(rocprim::radix_sort_pairs(nullptr, bytes, reinterpret_cast<unsigned*>(r->depth), r->dsorted,
                                                       rocprim::counting_iterator<unsigned>(0u), r->dorder, cap, 0, 32,
@@ -1366,11 +1558,14 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     if ((rc = grow(&r->dsort_tmp, bytes))) return rc;
     r->dsort_tmp_bytes = bytes;
     bytes = 0;
-    GSMPM_HIP(rocprim::inclusive_scan(nullptr, bytes, r->tiles, r->offsets, cap, rocprim::plus<unsigned>(), st));
-    size_t gbytes = 0;
-    GSMPM_HIP(rocprim::inclusive_scan(nullptr, gbytes, ranked_tiles(r->dorder, r->tiles), r->offr, cap,
+    GSMPM_HIP(rocprim::inclusive_scan(nullptr, bytes, binned_tiles(r->tiles), r->offsets, cap,
                                       rocprim::plus<unsigned>(), st));
-    bytes = std::max(bytes, gbytes);
+    size_t gbytes = 0, ibytes = 0;
+    GSMPM_HIP(rocprim::inclusive_scan(nullptr, gbytes, ranked_tiles(r->dorder, r->tiles), r->offr, cap,
+                                      rocprim::plus<unsigned long long>(), st));
+    GSMPM_HIP(rocprim::inclusive_scan(nullptr, ibytes, r->tiles, r->offr, cap, rocprim::plus<unsigned long long>(),
+                                      st));
+    bytes = std::max(bytes, std::max(gbytes, ibytes));
     if ((rc = grow(&r->scan_tmp, bytes))) return rc;
     r->scan_tmp_bytes = bytes;
     r->capP = cap;
@@ -1397,23 +1592,26 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
   // check that culling changes no pixel, final T or last contributor)
   const char* rm = std::getenv("GSMPM_RASTER_RENDER_MODE");
   const int render_mode = rm ? std::atoi(rm) & 1 : 0;
+  a.tight = !(render_mode & 1);
+  a.sh_vec4 = in->shs && in->M == 16 && ((uintptr_t)in->shs & 15u) == 0;
   r->slots_pending = false;
   r->offsets_pending = false;
   r->emit_culled = false;
   const unsigned* tkeys = nullptr;  // sorted tile keys with sub-tile masks (chunked path)
-  unsigned K = 0;
+  unsigned K = 0, K_full = 0;  // binned pairs, upstream's 3-sigma pairs (num_rendered)
   if (P > 0) {
     hipLaunchKernelGGL(k_preprocess, dim3(div_up(P, 256)), dim3(256), 0, st, a, out_radii, r->depth, r->xy, r->conic,
-                       r->rgb, r->tiles);
+                       r->rgb, r->tiles, r->rect);
     GSMPM_LAUNCH_CHECK();
     size_t bytes = r->scan_tmp_bytes;
     // the index-order scan (offsets) feeds only the backward's record slots
     // and the upstream-keyed path: a depth-ordered forward takes K from the
     // depth-order scan and leaves offsets to gsmpm_raster_backward (one scan
     // and its look-back init launch less per frame)
-    r->offsets_pending = depth_ordered;
-    if (!depth_ordered)
-      GSMPM_HIP(rocprim::inclusive_scan(r->scan_tmp, bytes, r->tiles, r->offsets, (size_t)P, rocprim::plus<unsigned>(), st));
+    r->offsets_pending = true;
+    if (!depth_ordered)  // upstream keys: the index-order scan of both counts (k_duplicate's offsets, K)
+      GSMPM_HIP(rocprim::inclusive_scan(r->scan_tmp, bytes, r->tiles, r->offr, (size_t)P,
+                                        rocprim::plus<unsigned long long>(), st));
     if (depth_ordered) {
       // the depth order depends on P only: it runs before the count read-back,
       // queued behind whatever the stream is still doing
@@ -1424,7 +1622,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       // the scan reads tiles[dorder[r]] itself (no separate gather launch)
       bytes = r->scan_tmp_bytes;
       GSMPM_HIP(rocprim::inclusive_scan(r->scan_tmp, bytes, ranked_tiles(r->dorder, r->tiles), r->offr, (size_t)P,
-                                        rocprim::plus<unsigned>(), st));
+                                        rocprim::plus<unsigned long long>(), st));
     }
     // K straight into pinned, coherent host memory by a one-lane kernel, and a
     // spin on it: no copy-engine packet and no sleeping stream sync between
@@ -1438,8 +1636,9 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
                   "gsmpm_raster_forward: the pair count is read on the host; the stream must not be capturing");
     volatile unsigned* hc = r->h_count;
     *hc = kNoCount;
-    hipLaunchKernelGGL(k_publish_count, dim3(1), dim3(1), 0, st,
-                       (const unsigned*)((depth_ordered ? r->offr : r->offsets) + (P - 1)), r->h_count);
+    hc[1] = kNoCount;
+    hipLaunchKernelGGL(k_publish_count, dim3(1), dim3(1), 0, st, (const unsigned long long*)(r->offr + (P - 1)),
+                       r->h_count);
     GSMPM_LAUNCH_CHECK();
     GSMPM_HIP(hipEventRecord(r->count_ev, st));
     for (unsigned polls = 1; *hc == kNoCount; ++polls) {
@@ -1450,8 +1649,9 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       }
       __builtin_ia32_pause();
     }
-    K = *hc;
-    GSMPM_REQUIRE(K != kNoCount, "gsmpm_raster_forward: the pair count never arrived");
+    K = hc[0];
+    K_full = hc[1];
+    GSMPM_REQUIRE(K != kNoCount && K_full != kNoCount, "gsmpm_raster_forward: the pair count never arrived");
   }
   if (K > 0) {
     if (K > r->capK) {
@@ -1498,10 +1698,18 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       }
       // sub-tile masks and emission culling ride on the chunked sort (its
       // virtual culled tile); the onesweep fallback keeps every pair
-      const int cull = chunked && !(render_mode & 1);
-      hipLaunchKernelGGL(k_emit_pairs, dim3(div_up(K, 256)), dim3(256), 0, st, (int)K, P, (const unsigned*)r->dorder,
-                         (const unsigned*)r->offr, (const float2*)r->xy, (const float4*)r->conic,
-                         (const int*)out_radii, a.grid_x, a.grid_y, cull, tile_keys, r->vals);
+      const int cull = !(render_mode & 1);
+      const char* el = std::getenv("GSMPM_RASTER_EMIT_LANE");
+      if (el && el[0] == '1') {
+        hipLaunchKernelGGL(k_emit_pairs, dim3(div_up(K, 256)), dim3(256), 0, st, (int)K, P, (const unsigned*)r->dorder,
+                           (const unsigned long long*)r->offr, (const float2*)r->xy, (const float4*)r->conic,
+                           (const uint2*)r->rect, a.grid_x, cull, tile_keys, r->vals);
+      } else {  // >= ~1024 workgroups, up to kEmitMaxI pairs per lane
+        const int items = std::min(kEmitMaxI, std::max(1, div_up((long)K, (long)kEmitT * 1024)));
+        hipLaunchKernelGGL(k_emit_wg, dim3(div_up((long)K, (long)kEmitT * items)), dim3(kEmitT), 0, st, (int)K, P, items,
+                           (const unsigned*)r->dorder, (const unsigned long long*)r->offr, (const float2*)r->xy,
+                           (const float4*)r->conic, (const uint2*)r->rect, a.grid_x, cull, tile_keys, r->vals);
+      }
       GSMPM_LAUNCH_CHECK();
       size_t bytes = r->sort_tmp_bytes;
       if (chunked) {
@@ -1523,13 +1731,15 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
                                                           r->ids_sorted, (size_t)K, 0, bits, st));
         GSMPM_HIP(hipMemsetAsync(r->ranges, 0, ntiles * sizeof(uint2), st));
         hipLaunchKernelGGL(k_ranges32, dim3(div_up(K, 256)), dim3(256), 0, st, (int)K, (const unsigned*)tile_sorted,
-                           0, r->ranges);
+                           0, (unsigned)ntiles, r->ranges);
         GSMPM_LAUNCH_CHECK();
+        tkeys = tile_sorted;
+        r->emit_culled = cull != 0;
       }
       r->slots_pending = true;
     } else {
-    hipLaunchKernelGGL(k_duplicate, dim3(div_up(P, 256)), dim3(256), 0, st, P, r->xy, r->depth, r->offsets, out_radii,
-                       a.grid_x, a.grid_y, r->keys, r->vals);
+    hipLaunchKernelGGL(k_duplicate, dim3(div_up(P, 256)), dim3(256), 0, st, P, (const uint2*)r->rect, r->depth,
+                       (const unsigned long long*)r->offr, out_radii, a.grid_x, r->keys, r->vals);
     GSMPM_LAUNCH_CHECK();
     size_t bytes = r->sort_tmp_bytes;
     // values = emission indices (a Gaussian's pairs are contiguous in emission order: the
@@ -1560,7 +1770,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
                        r->forward_only ? nullptr : r->n_contrib, tkeys, render_mode);
   r->has_pixel_state = !r->forward_only;
   GSMPM_LAUNCH_CHECK();
-  if (num_rendered) *num_rendered = (int32_t)K;
+  if (num_rendered) *num_rendered = (int32_t)K_full;
   r->P = P;
   r->W = a.W;
   r->H = a.H;
@@ -1592,6 +1802,7 @@ int gsmpm_raster_backward(gsmpm_raster* r, const gsmpm_raster_args* in, const in
   a.focal_x = in->W / (2.0f * in->tanfovx);
   a.focal_y = in->H / (2.0f * in->tanfovy);
   a.grid_x = r->gx; a.grid_y = r->gy;
+  a.tight = 0; a.sh_vec4 = 0;  // forward-only fields
   const size_t K = r->K;
   if (K > r->capRec) {
     int rc;
@@ -1600,14 +1811,14 @@ int gsmpm_raster_backward(gsmpm_raster* r, const gsmpm_raster_args* in, const in
   }
   if (r->offsets_pending) {  // the forward's tiles are still in r->tiles
     size_t bytes = r->scan_tmp_bytes;
-    GSMPM_HIP(rocprim::inclusive_scan(r->scan_tmp, bytes, r->tiles, r->offsets, (size_t)in->P,
+    GSMPM_HIP(rocprim::inclusive_scan(r->scan_tmp, bytes, binned_tiles(r->tiles), r->offsets, (size_t)in->P,
                                       rocprim::plus<unsigned>(), st));
     r->offsets_pending = false;
   }
   if (K > 0 && r->slots_pending) {
     hipLaunchKernelGGL(k_slots, dim3(div_up(K, 256)), dim3(256), 0, st, (int)K,
                        (const unsigned*)reinterpret_cast<unsigned*>(r->keys_sorted), (const unsigned*)r->ids_sorted,
-                       (const float2*)r->xy, radii, (const unsigned*)r->offsets, r->gx, r->gy, r->vals_sorted);
+                       (const uint2*)r->rect, (const unsigned*)r->offsets, r->gx, r->gy, r->vals_sorted);
     GSMPM_LAUNCH_CHECK();
     r->slots_pending = false;
   }
