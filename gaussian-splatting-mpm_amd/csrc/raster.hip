@@ -780,29 +780,31 @@ __global__ __launch_bounds__(256) void k_emit_pairs(int K, int P, const unsigned
 // ~20-deep chain of dependent global loads at 1M Gaussians: bicycle's 39M
 // pairs took 546 us, memory-wait bound (SQ_WAIT_ANY 75 %).  Here a workgroup
 // owns `items` x 256 consecutive pairs [e0, e1):
-//   - the Gaussians r0 / r1 of its first and last pair come from a
-//     cooperative 256-ary search over the depth-order offsets (one load per
-//     lane per round, three rounds at 1M Gaussians);
+//   - the Gaussians r0 / r1 of its first and last pair come from
+//     k_emit_starts (the Gaussian holding each workgroup's first pair,
+//     written by that Gaussian's lane; a cooperative 256-ary search per
+//     workgroup cost six dependent round trips before any work started);
 //   - the Gaussians [r0, r1] are staged in LDS, kEmitG at a time: offsets,
 //     id, tile rect and (culling) the alpha-reach box, one coalesced round
 //     of loads per Gaussian instead of one per pair;
 //   - each pair of the staged span finds its Gaussian by a binary search in
 //     LDS (from the lane's previous one) and is emitted from LDS alone.
 // Same pairs, same positions, same keys as k_emit_pairs.
-constexpr int kEmitT = 256, kEmitMaxI = 16, kEmitG = 1024;
-// first r in [lo, hi) with offr[r] > e, hi if none; uniform over the workgroup
-__device__ __forceinline__ int wg_upper_bound(const unsigned long long* __restrict__ offr, int lo, int hi, unsigned e) {
-  while (hi > lo) {
-    const int step = (hi - lo + kEmitT - 1) / kEmitT;
-    const int pos = lo + (int)threadIdx.x * step;
-    const int c = __syncthreads_count(pos < hi && (unsigned)offr[pos] <= e);  // samples <= e: a prefix of the samples
-    if (c == 0) return lo;
-    lo += (c - 1) * step + 1;
-    hi = min(hi, lo - 1 + step);  // the first sample > e (if any) bounds the answer
-  }
-  return lo;
+#ifndef GSMPM_EMIT_G
+#define GSMPM_EMIT_G 512  // 16 KB of staging: 8 workgroups per CU (1024: 4 per CU, bicycle k_emit_wg 133 vs 114 us)
+#endif
+constexpr int kEmitT = 256, kEmitMaxI = 16, kEmitG = GSMPM_EMIT_G;
+// starts[b] = the depth rank of the Gaussian holding pair b * E (E = pairs per
+// emission workgroup): each boundary lies in exactly one non-empty Gaussian
+__global__ __launch_bounds__(256) void k_emit_starts(int P, const unsigned long long* __restrict__ offr, unsigned E,
+                                                     unsigned* __restrict__ starts) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= P) return;
+  const unsigned s = r ? (unsigned)offr[r - 1] : 0u, t = (unsigned)offr[r];
+  for (unsigned b = (s + E - 1) / E; b * E < t; ++b) starts[b] = (unsigned)r;
 }
-__global__ __launch_bounds__(kEmitT) void k_emit_wg(int K, int P, int items, const unsigned* __restrict__ order,
+__global__ __launch_bounds__(kEmitT) void k_emit_wg(int K, int P, int items, const unsigned* __restrict__ starts,
+                                                    const unsigned* __restrict__ order,
                                                     const unsigned long long* __restrict__ offr,
                                                     const float2* __restrict__ xy, const float4* __restrict__ conic_o,
                                                     const uint2* __restrict__ rect, int gx, int cull,
@@ -812,8 +814,8 @@ __global__ __launch_bounds__(kEmitT) void k_emit_wg(int K, int P, int items, con
   __shared__ uint2 s_rect[kEmitG];        // (x0 | y0 << 16, rect width) in tiles
   __shared__ float4 s_box[kEmitG];        // alpha-reach box (x lo, x hi, y lo, y hi) in pixels (culling)
   const int e0 = blockIdx.x * kEmitT * items, e1 = min(K, e0 + kEmitT * items);
-  const int r0 = wg_upper_bound(offr, 0, P, (unsigned)e0);
-  const int r1 = wg_upper_bound(offr, r0, P, (unsigned)(e1 - 1));
+  const int r0 = (int)starts[blockIdx.x];
+  const int r1 = e1 < K ? (int)starts[blockIdx.x + 1] : P - 1;  // may stage one Gaussian past pair e1 - 1
   int rs = r0;        // first Gaussian of the span to stage
   unsigned pa = e0;   // first pair not yet emitted
   while (true) {      // uniform: spans of <= kEmitG Gaussians
@@ -1432,6 +1434,7 @@ struct gsmpm_raster {
   void* sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
   unsigned* ids_sorted = nullptr;  // Gaussian id per sorted pair (vals_sorted holds emission indices)
+  unsigned* estart = nullptr;      // [capK / kEmitT + 2] k_emit_starts
   unsigned *dorder = nullptr, *dsorted = nullptr;  // [capP] depth order
   unsigned long long* offr = nullptr;  // [capP] inclusive scan of tiles in depth order (index order: upstream keys)
   void* dsort_tmp = nullptr;
@@ -1488,7 +1491,7 @@ int gsmpm_raster_destroy(gsmpm_raster* r) {
   if (!r) return GSMPM_OK;
   for (void* p : {(void*)r->radii_tmp, (void*)r->depth, (void*)r->xy, (void*)r->conic, (void*)r->rgb, (void*)r->tiles, (void*)r->rect,
                   (void*)r->offsets, r->scan_tmp, (void*)r->keys, (void*)r->keys_sorted, (void*)r->vals,
-                  (void*)r->vals_sorted, r->sort_tmp, (void*)r->ranges, (void*)r->ids_sorted, (void*)r->rec,
+                  (void*)r->vals_sorted, r->sort_tmp, (void*)r->ranges, (void*)r->ids_sorted, (void*)r->estart, (void*)r->rec,
                   (void*)r->final_T, (void*)r->n_contrib, (void*)r->dorder, (void*)r->dsorted, (void*)r->offr, r->dsort_tmp, (void*)r->hist})
     if (p) (void)hipFree(p);
   if (r->h_count) (void)hipHostFree(r->h_count);
@@ -1662,6 +1665,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       if ((rc = grow((void**)&r->vals, cap * 4))) return rc;
       if ((rc = grow((void**)&r->vals_sorted, cap * 4))) return rc;
       if ((rc = grow((void**)&r->ids_sorted, cap * 4))) return rc;
+      if ((rc = grow((void**)&r->estart, (cap / kEmitT + 2) * 4))) return rc;
       size_t bytes = 0;
       GSMPM_HIP(rocprim::radix_sort_pairs(nullptr, bytes, r->keys, r->keys_sorted, rocprim::counting_iterator<unsigned>(0u),
                                           r->vals_sorted, cap, 0, 64, st));
@@ -1706,7 +1710,11 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
                            (const uint2*)r->rect, a.grid_x, cull, tile_keys, r->vals);
       } else {  // >= ~1024 workgroups, up to kEmitMaxI pairs per lane
         const int items = std::min(kEmitMaxI, std::max(1, div_up((long)K, (long)kEmitT * 1024)));
-        hipLaunchKernelGGL(k_emit_wg, dim3(div_up((long)K, (long)kEmitT * items)), dim3(kEmitT), 0, st, (int)K, P, items,
+        const int nwg = div_up((long)K, (long)kEmitT * items);
+        hipLaunchKernelGGL(k_emit_starts, dim3(div_up(P, 256)), dim3(256), 0, st, P, (const unsigned long long*)r->offr,
+                           (unsigned)(kEmitT * items), r->estart);
+        GSMPM_LAUNCH_CHECK();
+        hipLaunchKernelGGL(k_emit_wg, dim3(nwg), dim3(kEmitT), 0, st, (int)K, P, items, (const unsigned*)r->estart,
                            (const unsigned*)r->dorder, (const unsigned long long*)r->offr, (const float2*)r->xy,
                            (const float4*)r->conic, (const uint2*)r->rect, a.grid_x, cull, tile_keys, r->vals);
       }
