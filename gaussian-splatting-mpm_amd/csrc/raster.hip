@@ -1457,7 +1457,7 @@ struct gsmpm_raster {
   int* n_contrib = nullptr;
   // the forward the state belongs to
   int P = -1, W = 0, H = 0, gx = 0, gy = 0;
-  unsigned K = 0;
+  unsigned K = 0, K_full = 0;  // binned pairs, num_rendered
   bool forward_only = false;  // gsmpm_raster_set_forward_only: no per-pixel state for a backward
   bool has_pixel_state = false;
 };
@@ -1785,6 +1785,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
   r->gx = a.grid_x;
   r->gy = a.grid_y;
   r->K = K;
+  r->K_full = K_full;
   return GSMPM_OK;
 }
 
@@ -1845,6 +1846,13 @@ int gsmpm_raster_backward(gsmpm_raster* r, const gsmpm_raster_args* in, const in
   hipLaunchKernelGGL(k_preprocess_bwd, dim3(div_up(a.P, 256)), dim3(256), 0, st, a, radii, r->offsets, r->rgb,
                      r->rec, o);
   GSMPM_LAUNCH_CHECK();
+  return GSMPM_OK;
+}
+
+int gsmpm_raster_pair_counts(const gsmpm_raster* r, uint32_t* binned, uint32_t* rendered) {
+  GSMPM_REQUIRE(r, "gsmpm_raster_pair_counts: null context");
+  if (binned) *binned = r->K;
+  if (rendered) *rendered = r->K_full;
   return GSMPM_OK;
 }
 

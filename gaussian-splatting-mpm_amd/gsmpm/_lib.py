@@ -140,6 +140,7 @@ _SIGS = {
                               [c_void_p] * 8 + [c_void_p]),
     "gsmpm_raster_mark_visible": (ctypes.c_int, [c_void_p, ctypes.c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gsmpm_raster_set_forward_only": (ctypes.c_int, [c_void_p, ctypes.c_int32]),
+    "gsmpm_raster_pair_counts": (ctypes.c_int, [c_void_p, c_void_p, c_void_p]),
 }
 
 # slab transports (include/gsmpm.h)

@@ -23,6 +23,15 @@ def _context(device_index: int):
     return h
 
 
+def pair_counts(device_index: int = 0):
+    """(binned pairs, num_rendered) of the shared context's last forward on
+    the device (diagnostics: the tight binning's pair count vs the 3-sigma one)."""
+    b, n = ctypes.c_uint32(), ctypes.c_uint32()
+    check(LIB.gsmpm_raster_pair_counts(_context(device_index), ctypes.byref(b), ctypes.byref(n)),
+          "gsmpm_raster_pair_counts")
+    return int(b.value), int(n.value)
+
+
 class RasterContext:
     """A dedicated gsmpm_raster context: holds one forward's binning and
     per-pixel state until its backward (upstream keeps geom/binning/image

@@ -390,6 +390,11 @@ int gsmpm_raster_backward(gsmpm_raster* r, const gsmpm_raster_args* a, const int
  * (main.py:148-157 never differentiates); autograd forwards use contexts
  * with it off (the default). */
 int gsmpm_raster_set_forward_only(gsmpm_raster* r, int32_t on);
+/* Diagnostics of the context's last forward: *binned = the (Gaussian, tile)
+ * pairs actually sorted and listed (each Gaussian binned into the tiles its
+ * alpha >= 1/255 box reaches, a subset of the 3-sigma rect), *rendered = its
+ * num_rendered (upstream's 3-sigma pair count).  Either pointer may be null. */
+int gsmpm_raster_pair_counts(const gsmpm_raster* r, uint32_t* binned, uint32_t* rendered);
 /* GaussianRasterizer.markVisible -> _C.mark_visible: visible[P] (u8) = view z > 0.2 */
 int gsmpm_raster_mark_visible(const float* means3D, int32_t P, const float* viewmatrix, const float* projmatrix,
                               uint8_t* visible, void* stream);

@@ -178,14 +178,19 @@ def test_segmented_blend_vs_oracle(dev, P, W, H, lo, hi):
     assert err.max() < 1e-3, (err.max(), (err > 1e-3).sum())
 
 
-@pytest.mark.parametrize("scene", ["dense", "sparse"])
-def test_subtile_culling_changes_nothing(dev, monkeypatch, scene):
-    """k_render's sub-tile culling only drops Gaussians upstream's loop skips
-    (alpha < 1/255 at every pixel of the sub-tile): pixels, final T and last
-    contributor -- hence the backward's gradients -- are bit-identical with
-    culling off (GSMPM_RASTER_RENDER_MODE=1)."""
+@pytest.mark.parametrize("scene,path", [("dense", "chunked"), ("sparse", "chunked"), ("sparse", "onesweep"),
+                                        ("dense", "wide")])
+def test_subtile_culling_changes_nothing(dev, monkeypatch, scene, path):
+    """k_render's sub-tile culling and the tight binning (each Gaussian binned
+    into the tiles its alpha-reach box meets) only drop Gaussians upstream's
+    loop skips (alpha < 1/255 at every pixel of the sub-tile): pixels, final T
+    and last contributor -- hence the backward's gradients -- are bit-identical
+    with both off (GSMPM_RASTER_RENDER_MODE=1, 3-sigma rects), on the chunked
+    tile sort, the onesweep sort and upstream's 64-bit keys."""
     import torch
     from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    monkeypatch.setenv("GSMPM_RASTER_ONESWEEP", "1" if path == "onesweep" else "0")
+    monkeypatch.setenv("GSMPM_RASTER_WIDE_KEYS", "1" if path == "wide" else "0")
     if scene == "dense":
         P, W, H = 8000, 100, 72
         means, c6, opa, shs = _dense_scene(P, P, 0.03, 0.5)
@@ -235,6 +240,30 @@ def test_num_rendered_and_radii_exact(dev, P, W, H, tiles):
     assert K == oK, (K, oK)
     assert np.array_equal(radii.cpu().numpy(), orad)
     assert np.abs(color.cpu().numpy() - oc).max() < 1e-3
+
+
+@pytest.mark.parametrize("P,W,H", [(20000, 1024, 1024), (6000, 272, 3856)])
+def test_tight_binning_pair_counts(dev, monkeypatch, P, W, H):
+    """The tight binning sorts fewer pairs than upstream's 3-sigma count (which
+    num_rendered keeps), and exactly that count with it off (render mode 1)."""
+    import torch
+    from gsmpm import raster
+    means, c6, opa, shs = _scene(P, seed=P + W)
+    view, full, campos, tx, ty = _camera(W, H, 0.9)
+    bgv = np.zeros(3, np.float32)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    counts = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("GSMPM_RASTER_RENDER_MODE", mode)
+        K, _, _ = raster.forward(t(means), t(opa), t(view), t(full), t(campos), t(bgv), H, W, tx, ty,
+                                 sh_degree=3, shs=t(shs), cov3D_precomp=t(c6))
+        binned, rendered = raster.pair_counts(dev.index or 0)
+        assert rendered == K
+        counts[mode] = (binned, K)
+    (b0, k0), (b1, k1) = counts["0"], counts["1"]
+    assert k0 == k1 and b1 == k1, counts
+    assert 0 < b0 < k0, counts
+    print("binned / 3-sigma pairs", b0, k0, round(b0 / k0, 3))
 
 
 @pytest.mark.parametrize("scene,onesweep", [("dense", "0"), ("sparse", "0"), ("sparse", "1")])

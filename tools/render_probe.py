@@ -49,4 +49,5 @@ t0 = time.perf_counter()
 for _ in range(reps):
     K = fwd()[0]
 torch.cuda.synchronize()
-print(f"render {1e3 * (time.perf_counter() - t0) / reps:.4f} ms/frame, K {K}")
+binned, _ = raster.pair_counts(dev.index or 0)
+print(f"render {1e3 * (time.perf_counter() - t0) / reps:.4f} ms/frame, K {K}, binned {binned}")
