@@ -950,6 +950,70 @@ __global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int 
       ranges[tt] = make_uint2(Hs[(size_t)tt * nch], Hs[(size_t)(tt + 1) * nch]);
 }
 
+// Above kMaxTiles tiles: the same chunked counting sort, LSD over 8-bit
+// digits of the tile index (two passes up to 65,535 tiles, three above).  A
+// pass keeps 256 histogram entries per 2,048-pair chunk (the one-pass form's
+// entry per (tile, chunk) would be ~1e9 entries at the bicycle's 63,860 tiles
+// and 30M pairs), scans them digit-major, and scatters each chunk's stably
+// block-sorted pairs to their digit runs: no look-back chain.  Culled keys
+// (tile field all ones) carry digit 255 in every pass, so they sort after
+// every real tile (ntiles <= 256^passes - 1).
+__global__ __launch_bounds__(kSortT) void k_digit_hist(int K, int nch, int shift, const unsigned* __restrict__ keys,
+                                                       unsigned* __restrict__ H) {
+  __shared__ unsigned s_h[256];
+  s_h[threadIdx.x] = 0;
+  __syncthreads();
+  const int c = blockIdx.x;
+#pragma unroll
+  for (int i = 0; i < kSortI; ++i) {
+    const int e = c * kChunk + i * kSortT + threadIdx.x;
+    if (e < K) atomicAdd(&s_h[(keys[e] >> shift) & 255u], 1u);
+  }
+  __syncthreads();
+  H[(size_t)threadIdx.x * nch + c] = s_h[threadIdx.x];
+}
+__global__ __launch_bounds__(kSortT) void k_digit_scatter(int K, int nch, int shift, const unsigned* __restrict__ keys,
+                                                          const unsigned* __restrict__ vals,
+                                                          const unsigned* __restrict__ Hs,
+                                                          unsigned* __restrict__ keys_out,
+                                                          unsigned* __restrict__ vals_out) {
+  using BRS = rocprim::block_radix_sort<unsigned, kSortT, kSortI, unsigned>;
+  __shared__ typename BRS::storage_type s_sort;
+  __shared__ unsigned s_key[kChunk];
+  __shared__ int s_start[256];
+  const int c = blockIdx.x;
+  unsigned k[kSortI], v[kSortI];
+#pragma unroll
+  for (int i = 0; i < kSortI; ++i) {
+    const int e = c * kChunk + threadIdx.x * kSortI + i;  // blocked: the sort is stable in this order
+    k[i] = e < K ? keys[e] : 0xffffffffu;
+    v[i] = e < K ? vals[e] : kNoEntry;
+  }
+  BRS().sort(k, v, s_sort, shift, shift + 8);  // the chunk's tail (digit 255) sorts last
+  auto slot = [](int sp) { return (sp % kSortI) * kSortT + sp / kSortI; };  // as k_tile_scatter
+  unsigned d[kSortI];
+#pragma unroll
+  for (int i = 0; i < kSortI; ++i) {
+    d[i] = (k[i] >> shift) & 255u;
+    s_key[i * kSortT + threadIdx.x] = d[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kSortI; ++i) {
+    const int sp = threadIdx.x * kSortI + i;
+    if (v[i] != kNoEntry && (sp == 0 || s_key[slot(sp - 1)] != d[i])) s_start[d[i]] = sp;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kSortI; ++i) {
+    if (v[i] == kNoEntry) continue;
+    const int sp = threadIdx.x * kSortI + i;
+    const unsigned pos = Hs[(size_t)d[i] * nch + c] + (unsigned)(sp - s_start[d[i]]);
+    keys_out[pos] = k[i];
+    vals_out[pos] = v[i];
+  }
+}
+
 // backward only: sorted pair -> its record slot, the pair's index in
 // Gaussian-index emission order (k_preprocess_bwd sums each Gaussian's
 // contiguous slots without atomics)
@@ -1677,12 +1741,28 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     if (depth_ordered) {
       unsigned* tile_keys = reinterpret_cast<unsigned*>(r->keys);
       unsigned* tile_sorted = reinterpret_cast<unsigned*>(r->keys_sorted);
-      // the chunked counting sort needs the tile histogram in LDS; GSMPM_RASTER_ONESWEEP=1 forces rocPRIM
+      // the chunked counting sort needs the tile histogram in LDS; above kMaxTiles
+      // tiles rocPRIM onesweep (GSMPM_RASTER_ONESWEEP=1 forces it everywhere).
+      // GSMPM_RASTER_DIGIT_SORT=1: the LSD digit form of the chunked sort above
+      // kMaxTiles instead (bit-identical; bicycle render 2.09 against 1.30 ms)
       const char* os = std::getenv("GSMPM_RASTER_ONESWEEP");
-      const bool chunked = ntiles <= (size_t)kMaxTiles && !(os && os[0] == '1');
+      const char* ds = std::getenv("GSMPM_RASTER_DIGIT_SORT");
+      const bool force_onesweep = os && os[0] == '1';
+      const bool chunked = ntiles <= (size_t)kMaxTiles && !force_onesweep;
+      const bool digits = !chunked && !force_onesweep && ds && ds[0] == '1';
+      const int passes = (bits + 7) / 8;  // ntiles <= 256^passes - 1: the all-ones tile field stays the culled one
       const int nch = (int)div_up(K, kChunk);
       size_t need = 0;
-      if (chunked) {
+      if (digits) {
+        const size_t nh = 256 * (size_t)nch;
+        if (nh > r->capH) {
+          int rc;
+          if ((rc = grow((void**)&r->hist, 2 * (nh + nh / 4 + 1024) * sizeof(unsigned)))) return rc;
+          r->capH = nh + nh / 4 + 1024;
+        }
+        GSMPM_HIP(rocprim::exclusive_scan(nullptr, need, r->hist, r->hist + r->capH, 0u, nh, rocprim::plus<unsigned>(),
+                                          st));
+      } else if (chunked) {
         const size_t nh = (ntiles + 1) * (size_t)nch;
         if (nh > r->capH) {
           int rc;
@@ -1700,8 +1780,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
         if ((rc = grow(&r->sort_tmp, need))) return rc;
         r->sort_tmp_bytes = need;
       }
-      // sub-tile masks and emission culling ride on the chunked sort (its
-      // virtual culled tile); the onesweep fallback keeps every pair
+      // sub-tile masks in the keys' top bits (every sort orders the tile bits only)
       const int cull = !(render_mode & 1);
       const char* el = std::getenv("GSMPM_RASTER_EMIT_LANE");
       if (el && el[0] == '1') {
@@ -1735,8 +1814,30 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
         r->emit_culled = cull != 0;
         ranges_written = true;
       } else {
-        GSMPM_HIP(rocprim::radix_sort_pairs<OnesweepSort>(r->sort_tmp, bytes, tile_keys, tile_sorted, r->vals,
-                                                          r->ids_sorted, (size_t)K, 0, bits, st));
+        if (digits) {  // passes alternate between the final buffers and spare ones, ending in the final
+          const size_t nh = 256 * (size_t)nch;
+          unsigned* Hs = r->hist + r->capH;
+          unsigned* alt_k = tile_keys + r->capK;  // the upper half of the 8-byte key buffer
+          unsigned* alt_v = r->vals_sorted;       // (the backward's slots; free in the forward)
+          const unsigned *sk = tile_keys, *sv = r->vals;
+          for (int p = 0; p < passes; ++p) {
+            const bool fin = (passes - 1 - p) % 2 == 0;
+            unsigned* dk = fin ? tile_sorted : alt_k;
+            unsigned* dv = fin ? r->ids_sorted : alt_v;
+            hipLaunchKernelGGL(k_digit_hist, dim3(nch), dim3(kSortT), 0, st, (int)K, nch, 8 * p, sk, r->hist);
+            GSMPM_LAUNCH_CHECK();
+            bytes = r->sort_tmp_bytes;
+            GSMPM_HIP(rocprim::exclusive_scan(r->sort_tmp, bytes, r->hist, Hs, 0u, nh, rocprim::plus<unsigned>(), st));
+            hipLaunchKernelGGL(k_digit_scatter, dim3(nch), dim3(kSortT), 0, st, (int)K, nch, 8 * p, sk, sv,
+                               (const unsigned*)Hs, dk, dv);
+            GSMPM_LAUNCH_CHECK();
+            sk = dk;
+            sv = dv;
+          }
+        } else {
+          GSMPM_HIP(rocprim::radix_sort_pairs<OnesweepSort>(r->sort_tmp, bytes, tile_keys, tile_sorted, r->vals,
+                                                            r->ids_sorted, (size_t)K, 0, bits, st));
+        }
         GSMPM_HIP(hipMemsetAsync(r->ranges, 0, ntiles * sizeof(uint2), st));
         hipLaunchKernelGGL(k_ranges32, dim3(div_up(K, 256)), dim3(256), 0, st, (int)K, (const unsigned*)tile_sorted,
                            0, (unsigned)ntiles, r->ranges);

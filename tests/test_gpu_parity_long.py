@@ -188,7 +188,8 @@ def test_sand_foam_full_size(dev, material):
                                         "n_grid": 128, "curve": curve, "post": post})
 
 
-def test_lego_impulse_window_at_substep_8001(dev):
+@pytest.mark.parametrize("lift", [False, True])
+def test_lego_impulse_window_at_substep_8001(dev, lift):
     """The lego impulse (configs/lego.json:42-47: start 0.8 s, 10 substeps)
     fires on substeps 8001-8010 of the float64 host clock.  The
     drop-in simulator runs 7,990 substeps at full size; the oracle is seeded
@@ -196,7 +197,14 @@ def test_lego_impulse_window_at_substep_8001(dev):
     the next 30 substeps with BC activity decided by their own clocks: x and
     F_trial within 1e-4, v / C within their bounds at substeps 8000 (before),
     8010 (end of the impulse) and 8020; an oracle without the impulse is far
-    from both (the window was crossed at the same substeps)."""
+    from both (the window was crossed at the same substeps).
+
+    The synthetic lego (the PLY is an LFS pointer) has fallen below the
+    impulse box by 0.8 s, so at its own state the kick is vacuous on both
+    sides.  lift=True moves the substep-7990 cloud (set through the drop-in's
+    particle_xyz, on the simulator and the oracle alike) so its centroid sits
+    at the box centre: thousands of particles then take the kick, which must
+    be visible against the no-impulse control and matched."""
     from gpu_helpers import dropin_sim
     from gsmpm.bc import substep_masks  # noqa: F401  (the drop-in's scheduler is what runs)
     prob = lego_problem(100_000, 128)
@@ -207,6 +215,13 @@ def test_lego_impulse_window_at_substep_8001(dev):
     t0 = s.time
     st = _state(s)
     inv_dx = prob["n_grid"] / prob["cfg"]["grid_extent"]
+    if lift:
+        import torch
+        box = [b for b in prob["cfg"]["boundary_conditions"] if b["type"] == "impulse"][0]
+        shift = np.asarray(box["center"], np.float32) - st["x"].mean(0).astype(np.float32)
+        st["x"] = (st["x"] + shift).astype(np.float32)
+        s.mpm_state.particle_xyz.from_torch(torch.from_numpy(st["x"]).to(dev))
+        assert np.array_equal(_state(s)["x"], st["x"])
 
     def seeded(with_impulse):
         ref, imps, ops = build_oracle_sim(prob, threaded=True)
@@ -250,7 +265,11 @@ def test_lego_impulse_window_at_substep_8001(dev):
                 assert ctrl > 100 * max(g["v"], 1e-6), (c, ctrl, g)
             else:  # the synthetic lego has fallen out of the box by 0.8 s: a vacuous kick on both sides
                 assert ctrl == 0.0, (c, ctrl)
-    _dump("lego_impulse_8001", {"config": "lego.json", "N": 100_000, "n_grid": 128, "start": 7990, "curve": rec})
+    if lift:
+        assert in_box > 1000, in_box
+    _dump("lego_impulse_8001" + ("_lifted" if lift else ""),
+          {"config": "lego.json", "N": 100_000, "n_grid": 128, "start": 7990, "lifted_to_box_centre": lift,
+           "curve": rec})
 
 
 # the scene's footprint at this camera spans tiles x ~125-175, y ~80-134: the centre, two

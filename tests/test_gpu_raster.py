@@ -242,6 +242,37 @@ def test_num_rendered_and_radii_exact(dev, P, W, H, tiles):
     assert np.abs(color.cpu().numpy() - oc).max() < 1e-3
 
 
+@pytest.mark.parametrize("P,W,H,tiles", [(6000, 272, 3856, 4097), (20000, 1600, 1200, 7500),
+                                         (20000, 4200, 4200, 69169)])
+def test_digit_tile_sort_matches_onesweep(dev, monkeypatch, P, W, H, tiles):
+    """Above 4,096 tiles, the chunked LSD digit sort (GSMPM_RASTER_DIGIT_SORT=1:
+    two 8-bit passes; three above 65,535 tiles) against rocPRIM onesweep (the
+    default there): pixels, final T, last contributor and every gradient equal
+    bit for bit -- both are stable sorts of the same depth-ordered emission."""
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    assert ((W + 15) // 16) * ((H + 15) // 16) == tiles
+    means, c6, opa, shs = _scene(P, seed=P + W)
+    view, full, campos, tx, ty = _camera(W, H, 0.9)
+    rng = np.random.default_rng(3)
+    wgt = torch.from_numpy(rng.normal(0, 1, (3, H, W)).astype(np.float32)).to(dev)
+    t = lambda a, g=False: torch.from_numpy(np.ascontiguousarray(a)).to(dev).requires_grad_(g)
+    st = GaussianRasterizationSettings(image_height=H, image_width=W, tanfovx=tx, tanfovy=ty,
+                                       bg=t(np.full(3, 0.25, np.float32)), scale_modifier=1.0, viewmatrix=t(view),
+                                       projmatrix=t(full), sh_degree=3, campos=t(campos), prefiltered=False,
+                                       debug=False)
+    out = {}
+    for os_ in ("1", "0"):
+        monkeypatch.setenv("GSMPM_RASTER_DIGIT_SORT", "0" if os_ == "1" else "1")
+        m3, o1, s1, cv = t(means, True), t(opa, True), t(shs, True), t(c6, True)
+        img, radii = GaussianRasterizer(st)(means3D=m3, means2D=None, opacities=o1, shs=s1, cov3D_precomp=cv)
+        (img * wgt).sum().backward()
+        out[os_] = [x.detach().cpu().numpy() for x in (img, radii, m3.grad, o1.grad, s1.grad, cv.grad)]
+    assert (out["0"][1] > 0).sum() > P // 4
+    for a, b in zip(out["0"], out["1"]):
+        assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("P,W,H", [(20000, 1024, 1024), (6000, 272, 3856)])
 def test_tight_binning_pair_counts(dev, monkeypatch, P, W, H):
     """The tight binning sorts fewer pairs than upstream's 3-sigma count (which
