@@ -886,6 +886,19 @@ __device__ __forceinline__ unsigned sort_tile(unsigned key, unsigned lowmask, in
   const unsigned t = key & lowmask;
   return t < (unsigned)ntiles ? t : (unsigned)ntiles;
 }
+// a block sort's blocked result (thread t holds sorted positions t * kSortI + i)
+// to LDS in sorted order: two 16-byte stores of keys and of values per thread
+__device__ __forceinline__ void sorted_to_lds(const unsigned (&k)[kSortI], const unsigned (&v)[kSortI],
+                                              unsigned* s_k, unsigned* s_v) {
+  static_assert(kSortI == 8, "two uint4 per thread");
+  uint4* dk = reinterpret_cast<uint4*>(s_k + threadIdx.x * kSortI);
+  uint4* dv = reinterpret_cast<uint4*>(s_v + threadIdx.x * kSortI);
+  dk[0] = make_uint4(k[0], k[1], k[2], k[3]);
+  dk[1] = make_uint4(k[4], k[5], k[6], k[7]);
+  dv[0] = make_uint4(v[0], v[1], v[2], v[3]);
+  dv[1] = make_uint4(v[4], v[5], v[6], v[7]);
+  __syncthreads();
+}
 __global__ __launch_bounds__(kSortT) void k_tile_hist(int K, int ntiles, int nch, int bits,
                                                       const unsigned* __restrict__ keys, unsigned* __restrict__ H) {
   __shared__ unsigned s_h[kMaxTiles + 1];
@@ -908,7 +921,7 @@ __global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int 
                                                          uint2* __restrict__ ranges) {
   using BRS = rocprim::block_radix_sort<unsigned, kSortT, kSortI, unsigned>;
   __shared__ typename BRS::storage_type s_sort;
-  __shared__ unsigned s_key[kChunk];
+  __shared__ unsigned s_k[kChunk], s_v[kChunk];
   __shared__ int s_start[kMaxTiles + 1];
   const int c = blockIdx.x;
   const unsigned lowmask = (1u << bits) - 1u;  // >= ntiles
@@ -920,30 +933,25 @@ __global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int 
     v[i] = e < K ? vals[e] : kNoEntry;
   }
   BRS().sort(k, v, s_sort, 0, bits);
-  // sorted position sp = thread * kSortI + i lives at s_key[(sp % kSortI) * kSortT + sp / kSortI]:
-  // a wave's 64 stores (or loads) of one i hit 64 consecutive words -- the plain
-  // sp layout strided them by kSortI words, 8 lanes per bank
-  auto slot = [](int sp) { return (sp % kSortI) * kSortT + sp / kSortI; };
-  unsigned t[kSortI];
+  sorted_to_lds(k, v, s_k, s_v);
+  // sorted position sp is read striped (sp = i * kSortT + lane): a run's pairs
+  // go out as coalesced stores (the blocked order wrote 64 lanes 32 B apart)
 #pragma unroll
   for (int i = 0; i < kSortI; ++i) {
-    t[i] = sort_tile(k[i], lowmask, ntiles);
-    s_key[i * kSortT + threadIdx.x] = t[i];
+    const int sp = i * kSortT + threadIdx.x;
+    const unsigned t = sort_tile(s_k[sp], lowmask, ntiles);
+    if (s_v[sp] != kNoEntry && (sp == 0 || sort_tile(s_k[sp - 1], lowmask, ntiles) != t)) s_start[t] = sp;
   }
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < kSortI; ++i) {
-    const int sp = threadIdx.x * kSortI + i;
-    if (v[i] != kNoEntry && (sp == 0 || s_key[slot(sp - 1)] != t[i])) s_start[t[i]] = sp;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < kSortI; ++i) {
-    if (v[i] == kNoEntry) continue;
-    const int sp = threadIdx.x * kSortI + i;
-    const unsigned pos = Hs[(size_t)t[i] * nch + c] + (unsigned)(sp - s_start[t[i]]);
-    keys_out[pos] = k[i];
-    vals_out[pos] = v[i];
+    const int sp = i * kSortT + threadIdx.x;
+    const unsigned vv = s_v[sp];
+    if (vv == kNoEntry) continue;
+    const unsigned kk = s_k[sp], t = sort_tile(kk, lowmask, ntiles);
+    const unsigned pos = Hs[(size_t)t * nch + c] + (unsigned)(sp - s_start[t]);
+    keys_out[pos] = kk;
+    vals_out[pos] = vv;
   }
   if (c == 0)
     for (int tt = threadIdx.x; tt < ntiles; tt += kSortT)
@@ -979,7 +987,7 @@ __global__ __launch_bounds__(kSortT) void k_digit_scatter(int K, int nch, int sh
                                                           unsigned* __restrict__ vals_out) {
   using BRS = rocprim::block_radix_sort<unsigned, kSortT, kSortI, unsigned>;
   __shared__ typename BRS::storage_type s_sort;
-  __shared__ unsigned s_key[kChunk];
+  __shared__ unsigned s_k[kChunk], s_v[kChunk];
   __shared__ int s_start[256];
   const int c = blockIdx.x;
   unsigned k[kSortI], v[kSortI];
@@ -990,27 +998,23 @@ __global__ __launch_bounds__(kSortT) void k_digit_scatter(int K, int nch, int sh
     v[i] = e < K ? vals[e] : kNoEntry;
   }
   BRS().sort(k, v, s_sort, shift, shift + 8);  // the chunk's tail (digit 255) sorts last
-  auto slot = [](int sp) { return (sp % kSortI) * kSortT + sp / kSortI; };  // as k_tile_scatter
-  unsigned d[kSortI];
+  sorted_to_lds(k, v, s_k, s_v);
 #pragma unroll
-  for (int i = 0; i < kSortI; ++i) {
-    d[i] = (k[i] >> shift) & 255u;
-    s_key[i * kSortT + threadIdx.x] = d[i];
+  for (int i = 0; i < kSortI; ++i) {  // striped, as k_tile_scatter
+    const int sp = i * kSortT + threadIdx.x;
+    const unsigned d = (s_k[sp] >> shift) & 255u;
+    if (s_v[sp] != kNoEntry && (sp == 0 || ((s_k[sp - 1] >> shift) & 255u) != d)) s_start[d] = sp;
   }
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < kSortI; ++i) {
-    const int sp = threadIdx.x * kSortI + i;
-    if (v[i] != kNoEntry && (sp == 0 || s_key[slot(sp - 1)] != d[i])) s_start[d[i]] = sp;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < kSortI; ++i) {
-    if (v[i] == kNoEntry) continue;
-    const int sp = threadIdx.x * kSortI + i;
-    const unsigned pos = Hs[(size_t)d[i] * nch + c] + (unsigned)(sp - s_start[d[i]]);
-    keys_out[pos] = k[i];
-    vals_out[pos] = v[i];
+    const int sp = i * kSortT + threadIdx.x;
+    const unsigned vv = s_v[sp];
+    if (vv == kNoEntry) continue;
+    const unsigned kk = s_k[sp], d = (kk >> shift) & 255u;
+    const unsigned pos = Hs[(size_t)d * nch + c] + (unsigned)(sp - s_start[d]);
+    keys_out[pos] = kk;
+    vals_out[pos] = vv;
   }
 }
 
