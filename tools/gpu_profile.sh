@@ -16,5 +16,6 @@ if [ "${PMC:-1}" = "1" ]; then
   bash tools/pmc.sh $O/pmc > $O/pmc.log 2>&1
   for d in p1 p2 p3 p4; do rm -rf $O/pmc/$d; done
   bash tools/pmc_D.sh $O/pmcD > $O/pmcD.log 2>&1
+  if [ "${PMC_RENDER:-0}" = "1" ]; then bash tools/pmc_render_D.sh $O/pmc_render_D > $O/pmc_render_D.log 2>&1; fi
 fi
 echo ok
