@@ -74,7 +74,8 @@ def lib(threaded=False):
     """Load (building if needed) liboracle.so, with threaded=True the OpenMP
     build liboracle_omp.so (checker of the BASELINE-size parity runs), or with
     threaded="fast" liboracle_fast.so (OpenMP, -O3 -ffast-math, AVX2/FMA:
-    bench.py's timed CPU baseline only)."""
+    bench.py's timed CPU baseline, and in the long-horizon parity tests one
+    member of the spread of valid reference outputs -- never the checker)."""
     name = "liboracle_fast.so" if threaded == "fast" else ("liboracle_omp.so" if threaded else "liboracle.so")
     if name not in _LIBS:
         path = os.path.join(_HERE, name)

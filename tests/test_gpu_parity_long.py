@@ -60,6 +60,10 @@ def _oracle_fields(ref, inv=None):
     return {k: (v[inv] if inv is not None else v) for k, v in f.items()}
 
 
+def _rows(a, inv):
+    return a if inv is None else a[inv]
+
+
 def _permuted(prob, seed=11):
     p = np.random.default_rng(seed).permutation(len(prob["x"]))
     q = dict(prob)
@@ -75,15 +79,21 @@ def _field_errs(got, exp, inv_dx):
 
 
 def _horizon(prob, material, checkpoints, dev, spread=True, runs=None):
-    """Run the drop-in simulator, the oracle and (spread=True) SPREAD_RUNS
-    oracles on permuted particle orders in lockstep; the error curves at
-    `checkpoints` (the spread: the largest error of the permuted runs)."""
+    """Run the drop-in simulator, the oracle and (spread=True) the reference's
+    other valid outputs in lockstep: SPREAD_RUNS oracles on permuted particle
+    orders (the reference's P2G atomics sum in no fixed order) and the
+    fast-math build of the same restatement (main.py:28 runs ti.init with
+    Taichi's default fast_math=True, so contraction and reassociation are the
+    reference's own freedom); the error curves at `checkpoints` (the spread:
+    the largest error of those runs against the IEEE oracle)."""
     from gpu_helpers import dropin_sim
     ref, imps, ops = build_oracle_sim(prob, material=material, threaded=True)
     alts = []
     for k in range((runs or SPREAD_RUNS) if spread else 0):
         pprob, inv = _permuted(prob, seed=11 + k)
         alts.append((build_oracle_sim(pprob, material=material, threaded=True), inv))
+    if spread:
+        alts.append((build_oracle_sim(prob, material=material, threaded="fast"), None))
     s, _ = dropin_sim(prob, dev, **({"material": material} if material else {}))
     dt = prob["cfg"]["substep_dt"]
     inv_dx = prob["n_grid"] / prob["cfg"]["grid_extent"]
@@ -116,8 +126,8 @@ def _horizon(prob, material, checkpoints, dev, spread=True, runs=None):
     post = {"gpu": {"cov": rel_err(cov, ref.cov), "cov_elem": rel_err_elem(cov, ref.cov), "R": rel_err(R, ref.R)}}
     for (alt, _, _), inv in alts:
         alt.postprocess()
-        e = {"cov": rel_err(alt.cov[inv], ref.cov), "cov_elem": rel_err_elem(alt.cov[inv], ref.cov),
-             "R": rel_err(alt.R[inv], ref.R)}
+        e = {"cov": rel_err(_rows(alt.cov, inv), ref.cov), "cov_elem": rel_err_elem(_rows(alt.cov, inv), ref.cov),
+             "R": rel_err(_rows(alt.R, inv), ref.R)}
         post["spread"] = {k: max(v, post.get("spread", {}).get(k, 0.0)) for k, v in e.items()}
     return curve, post
 
@@ -135,7 +145,7 @@ def test_config_B_ten_frames(dev):
     within 1e-4 of the field's max at every checkpoint; v, C within the
     documented bounds of test_gpu_mpm.py; per-element x within 1e-3; the
     per-element covariance error (floored at 1e-3 of the max) reported beside
-    a reordered oracle's and held to twice it."""
+    the spread of a reordered and a fast-math oracle and held to twice it."""
     prob = lego_problem(100_000, 128)
     curve, post = _horizon(prob, None, (1, 100, 250, 500, 1000), dev, runs=1)
     for c, rec in curve.items():
@@ -150,8 +160,9 @@ def test_config_B_ten_frames(dev):
 
 def test_config_C_metal_five_frames(dev):
     """lego-fracture.json --material metal, 100k, 128^3, 500 substeps (5 frames)
-    against the oracle, with the oracle-vs-permuted-oracle spread: x within
-    1e-4 throughout; F_trial, cov, yield, v, C within max(bound, 4 x spread)."""
+    against the oracle, with the spread of the reference's valid variants
+    (permuted orders, fast math): x within 1e-4 throughout; F_trial, cov,
+    yield, v, C within max(bound, 2 x spread)."""
     prob = lego_problem(100_000, 128, config="lego-fracture.json")
     curve, post = _horizon(prob, "metal", (100, 200, 300, 500), dev)
     for c, rec in curve.items():
