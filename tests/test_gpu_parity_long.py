@@ -91,16 +91,16 @@ def _horizon(prob, material, checkpoints, dev, spread=True, runs=None):
     alts = []
     for k in range((runs or SPREAD_RUNS) if spread else 0):
         pprob, inv = _permuted(prob, seed=11 + k)
-        alts.append((build_oracle_sim(pprob, material=material, threaded=True), inv))
-    if spread:
-        alts.append((build_oracle_sim(prob, material=material, threaded="fast"), None))
+        alts.append((build_oracle_sim(pprob, material=material, threaded=True), inv, f"permuted{k}"))
+    if spread:  # a member whose state goes non-finite (fast math on foam) is no valid output: excluded
+        alts.append((build_oracle_sim(prob, material=material, threaded="fast"), None, "fast_math"))
     s, _ = dropin_sim(prob, dev, **({"material": material} if material else {}))
     dt = prob["cfg"]["substep_dt"]
     inv_dx = prob["n_grid"] / prob["cfg"]["grid_extent"]
     curve, done, t = {}, 0, 0.0
     for c in checkpoints:
         t1 = oracle_run(ref, imps, ops, dt, c - done, t0=t)
-        for (alt, aimps, aops), _ in alts:
+        for (alt, aimps, aops), _, _ in alts:
             oracle_run(alt, aimps, aops, dt, c - done, t0=t)
         for _ in range(c - done):
             s.p2g2p(dt)
@@ -110,24 +110,30 @@ def _horizon(prob, material, checkpoints, dev, spread=True, runs=None):
         rec = {"gpu": _field_errs(_state(s), exp, inv_dx)}
         if material in ("metal",):
             rec["gpu"]["yield"] = rel_err(s.mpm_model.yield_stress.to_torch().cpu().numpy(), exp["yield"])
-        for (alt, _, _), inv in alts:
+        for (alt, _, _), inv, label in alts:
             a = _oracle_fields(alt, inv)
             e = _field_errs(a, exp, inv_dx)
             if material in ("metal",):
                 e["yield"] = rel_err(a["yield"], exp["yield"])
+            if not all(np.isfinite(v) for v in e.values()):
+                rec.setdefault("excluded", []).append(label)
+                continue
             rec["spread"] = {k: max(v, rec.get("spread", {}).get(k, 0.0)) for k, v in e.items()}
         curve[c] = rec
         print(f"substep {c}", {k: f"{v:.2e}" for k, v in rec["gpu"].items()},
-              "spread", {k: f"{v:.2e}" for k, v in rec.get("spread", {}).items()})
+              "spread", {k: f"{v:.2e}" for k, v in rec.get("spread", {}).items()}, "excluded", rec.get("excluded"))
     s.postprocess()
     ref.postprocess()
     cov = s.mpm_state.particle_cov.to_torch().cpu().numpy().reshape(-1, 6)
     R = s.mpm_state.particle_R.to_torch().cpu().numpy().reshape(-1, 9)
     post = {"gpu": {"cov": rel_err(cov, ref.cov), "cov_elem": rel_err_elem(cov, ref.cov), "R": rel_err(R, ref.R)}}
-    for (alt, _, _), inv in alts:
+    for (alt, _, _), inv, label in alts:
         alt.postprocess()
         e = {"cov": rel_err(_rows(alt.cov, inv), ref.cov), "cov_elem": rel_err_elem(_rows(alt.cov, inv), ref.cov),
              "R": rel_err(_rows(alt.R, inv), ref.R)}
+        if not all(np.isfinite(v) for v in e.values()):
+            post.setdefault("excluded", []).append(label)
+            continue
         post["spread"] = {k: max(v, post.get("spread", {}).get(k, 0.0)) for k, v in e.items()}
     return curve, post
 
