@@ -426,20 +426,41 @@ constexpr int kBatch = 64 * kQ;  // entries staged per batch
 // pixel of the tile).  num_rendered stays upstream's rect count.
 constexpr unsigned kMaskShift = 28, kTileField = (1u << kMaskShift) - 1u, kCulledKey = kTileField;
 constexpr unsigned kNoEntry = 0xffffffffu;  // id of a chunk-tail slot past K
+// Quarter of the workgroup (its 8x8 pixels: column bx, row by in quarters).
+// xcd: the four quarters of a tile take linear workgroup ids 32 g + 8 h + x8
+// (h: the quarter), so they share id mod 8 -- one XCD (workgroup j runs on
+// XCD j mod 8), one L2: the tile's list, its gathered Gaussians and its
+// 16-pixel output rows are fetched and merged there once, not in four L2s
+// (the row-major grid put a tile's two left/right quarters on two XCDs,
+// each writing back half-filled 64-byte lines).  Else the 2-D grid's order.
+__device__ __forceinline__ bool render_quarter(int xcd, int gx, int ntiles, int& bx, int& by) {
+  if (!xcd) {
+    bx = blockIdx.x;
+    by = blockIdx.y;
+    return true;
+  }
+  const int L = blockIdx.x, x8 = L & 7, h = (L >> 3) & 3, tile = (L >> 5) * 8 + x8;
+  if (tile >= ntiles) return false;
+  bx = 2 * (tile % gx) + (h & 1);
+  by = 2 * (tile / gx) + (h >> 1);
+  return true;
+}
 __global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges, const unsigned* __restrict__ list,
                                                int W, int H, int gx, const float2* __restrict__ xy,
                                                const float4* __restrict__ conic_o, const float4* __restrict__ rgbo,
                                                const float* __restrict__ bg, float* __restrict__ out,
                                                float* __restrict__ final_T, int* __restrict__ n_contrib,
-                                               const unsigned* __restrict__ tkeys, int mode) {
+                                               const unsigned* __restrict__ tkeys, int mode, int xcd, int ntiles) {
   __shared__ float2 s_xy[kBatch];
   __shared__ float4 s_co[kBatch];
   __shared__ float4 s_rgb[kBatch];  // .w: the entry's tile-list index (as int bits)
+  int bx, by;
+  if (!render_quarter(xcd, gx, ntiles, bx, by)) return;  // workgroup-uniform
   const int lane = threadIdx.x;
-  const int x0 = blockIdx.x * kSub, y0 = blockIdx.y * kSub;
+  const int x0 = bx * kSub, y0 = by * kSub;
   const int px = x0 + (lane & (kSub - 1)), py = y0 + (lane / kSub);
   const bool inside = px < W && py < H;
-  const uint2 range = ranges[(blockIdx.y >> 1) * gx + (blockIdx.x >> 1)];
+  const uint2 range = ranges[(by >> 1) * gx + (bx >> 1)];
   const int n = (int)(range.y - range.x);
   const unsigned* lst = list + range.x;
   const float pfx = (float)px, pfy = (float)py, fx0 = (float)x0, fy0 = (float)y0;
@@ -451,7 +472,7 @@ __global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges,
   // whether it reaches this quarter: the gather of one that does not is
   // skipped; without, the quarter test runs on the gathered conic
   const unsigned* tk = tkeys ? tkeys + range.x : nullptr;
-  const unsigned qbit = 1u << (kMaskShift + (((blockIdx.y & 1) << 1) | (blockIdx.x & 1)));
+  const unsigned qbit = 1u << (kMaskShift + (((by & 1) << 1) | (bx & 1)));
   float2 g_xy[kQ];
   float4 g_co[kQ], g_rgb[kQ];
   unsigned nid[kQ];
@@ -1872,11 +1893,14 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
   // 0.30-0.33 ms against 0.26-0.27 ms (tools/ab_render.sh, 3 pairs): the blend is bound by
   // the heaviest tiles' serial walk, and a tile's four quarters now wait for each other
   const char* ts = std::getenv("GSMPM_RASTER_TILE_SHARED");
+  // GSMPM_RASTER_XCD=0: the row-major 2-D grid of quarters instead of the XCD-grouped one
+  const char* xe = std::getenv("GSMPM_RASTER_XCD");
+  const int xcd = !(xe && xe[0] == '0');
+  const dim3 rgrid = xcd ? dim3((unsigned)(32 * div_up((long)ntiles, 8))) : dim3(2 * a.grid_x, 2 * a.grid_y);
   if (!(ts && ts[0] == '1'))
-    hipLaunchKernelGGL(k_render, dim3(2 * a.grid_x, 2 * a.grid_y), dim3(64), 0, st, r->ranges, r->ids_sorted, a.W,
-                       a.H, a.grid_x, r->xy, r->conic, r->rgb, in->bg, out_color,
-                       r->forward_only ? nullptr : r->final_T, r->forward_only ? nullptr : r->n_contrib, tkeys,
-                       render_mode);
+    hipLaunchKernelGGL(k_render, rgrid, dim3(64), 0, st, r->ranges, r->ids_sorted, a.W, a.H, a.grid_x, r->xy, r->conic,
+                       r->rgb, in->bg, out_color, r->forward_only ? nullptr : r->final_T,
+                       r->forward_only ? nullptr : r->n_contrib, tkeys, render_mode, xcd, (int)ntiles);
   else
     hipLaunchKernelGGL(k_render4, dim3(a.grid_x, a.grid_y), dim3(256), 0, st, r->ranges, r->ids_sorted, a.W, a.H,
                        a.grid_x, r->xy, r->conic, r->rgb, in->bg, out_color, r->forward_only ? nullptr : r->final_T,
