@@ -637,6 +637,16 @@ __device__ __forceinline__ void node_extra(const float4* __restrict__ slots, con
 #endif
 constexpr int kGridParts = GSMPM_GRID_PARTS;  // workgroups per touched tile
 constexpr int kGridT = kFTN / kGridParts;     // lanes per grid workgroup
+// Nodes that received no mass at all keep whatever v_out they held: the next
+// G2P gathers only the stencils of particles whose P2G built this grid, and a
+// stencil node of such a particle has mass (the fixed-point sums are exact, so
+// only a contribution below 2^-51 of its chunk's largest can round to zero,
+// and that weight then multiplies the stale value instead of 0: < 1e-15
+// relative).  A node of mass in (0, 1e-15] still stores 0 (utils.py:177-183).
+#ifndef GSMPM_GRID_SKIP0
+#define GSMPM_GRID_SKIP0 0
+#endif
+constexpr bool kGridSkip0 = GSMPM_GRID_SKIP0 != 0;
 __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_grid_f(GridDims g, FTiles tl, ChunkIn ck, const int* __restrict__ tbox,
                                                     const float4* __restrict__ slots, float4* __restrict__ gacc,
                                                     float4* __restrict__ gvel, const BcTable* __restrict__ bct,
@@ -694,7 +704,7 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
       if (sww >= 0 && !inrect && a.w != 0.f) *sw.oob = 1;
       if (inrect)  // a window node: this rank's partial, totalled after the exchange (k_win_update)
         sw.part[sww][((size_t)(i - sw.a[sww]) * sw.ny[sww] + (j - sw.y0[sww])) * sw.nz[sww] + (k - sw.z0[sww])] = a;
-      else
+      else if (!kGridSkip0 || a.w != 0.f)
         gvel[idx] = node_update(a, i, j, k, g, gs, bct);
     }
     if (wt == (int)blockIdx.x) stamp(3, 4);

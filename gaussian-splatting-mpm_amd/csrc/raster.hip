@@ -433,13 +433,13 @@ constexpr unsigned kNoEntry = 0xffffffffu;  // id of a chunk-tail slot past K
 // 16-pixel output rows are fetched and merged there once, not in four L2s
 // (the row-major grid put a tile's two left/right quarters on two XCDs,
 // each writing back half-filled 64-byte lines).  Else the 2-D grid's order.
-__device__ __forceinline__ bool render_quarter(int xcd, int gx, int ntiles, int& bx, int& by) {
+__device__ __forceinline__ bool render_quarter(int xcd, int gx, int ntiles, int L, int& bx, int& by) {
   if (!xcd) {
     bx = blockIdx.x;
     by = blockIdx.y;
     return true;
   }
-  const int L = blockIdx.x, x8 = L & 7, h = (L >> 3) & 3, tile = (L >> 5) * 8 + x8;
+  const int x8 = L & 7, h = (L >> 3) & 3, tile = (L >> 5) * 8 + x8;
   if (tile >= ntiles) return false;
   bx = 2 * (tile % gx) + (h & 1);
   by = 2 * (tile / gx) + (h >> 1);
@@ -450,12 +450,16 @@ __global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges,
                                                const float4* __restrict__ conic_o, const float4* __restrict__ rgbo,
                                                const float* __restrict__ bg, float* __restrict__ out,
                                                float* __restrict__ final_T, int* __restrict__ n_contrib,
-                                               const unsigned* __restrict__ tkeys, int mode, int xcd, int ntiles) {
+                                               const unsigned* __restrict__ tkeys, int mode, int xcd, int ntiles,
+                                               int nq) {
   __shared__ float2 s_xy[kBatch];
   __shared__ float4 s_co[kBatch];
   __shared__ float4 s_rgb[kBatch];  // .w: the entry's tile-list index (as int bits)
+  // one quarter per workgroup, or (a grid of fewer workgroups, a multiple of 8
+  // so a quarter keeps its XCD) quarters L, L + grid, ...
+  for (int L = blockIdx.x; L < nq; L += gridDim.x) {
   int bx, by;
-  if (!render_quarter(xcd, gx, ntiles, bx, by)) return;  // workgroup-uniform
+  if (!render_quarter(xcd, gx, ntiles, L, bx, by)) continue;  // workgroup-uniform
   const int lane = threadIdx.x;
   const int x0 = bx * kSub, y0 = by * kSub;
   const int px = x0 + (lane & (kSub - 1)), py = y0 + (lane / kSub);
@@ -578,6 +582,7 @@ __global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges,
       final_T[pix] = T;
       n_contrib[pix] = last;
     }
+  }
   }
 }
 
@@ -1915,11 +1920,16 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
   // GSMPM_RASTER_XCD=0: the row-major 2-D grid of quarters instead of the XCD-grouped one
   const char* xe = std::getenv("GSMPM_RASTER_XCD");
   const int xcd = !(xe && xe[0] == '0');
-  const dim3 rgrid = xcd ? dim3((unsigned)(32 * div_up((long)ntiles, 8))) : dim3(2 * a.grid_x, 2 * a.grid_y);
+  const int nq = xcd ? (int)(32 * div_up((long)ntiles, 8)) : 2 * a.grid_x;  // the 2-D grid: one pass per workgroup
+  dim3 rgrid = xcd ? dim3((unsigned)nq) : dim3(2 * a.grid_x, 2 * a.grid_y);
+  // GSMPM_RASTER_RENDER_WGS=N (a multiple of 8): k_render as N workgroups looping over the quarters
+  // (A/B: a render overlapping the simulator holds fewer of the CU slots its one-round launches need)
+  if (const char* rw = std::getenv("GSMPM_RASTER_RENDER_WGS"))
+    if (xcd && std::atoi(rw) >= 8) rgrid = dim3((unsigned)std::min(nq, std::atoi(rw) & ~7));
   if (!(ts && ts[0] == '1'))
     hipLaunchKernelGGL(k_render, rgrid, dim3(64), 0, st, r->ranges, r->ids_sorted, a.W, a.H, a.grid_x, r->xy, r->conic,
                        r->rgb, in->bg, out_color, r->forward_only ? nullptr : r->final_T,
-                       r->forward_only ? nullptr : r->n_contrib, tkeys, render_mode, xcd, (int)ntiles);
+                       r->forward_only ? nullptr : r->n_contrib, tkeys, render_mode, xcd, (int)ntiles, nq);
   else
     hipLaunchKernelGGL(k_render4, dim3(a.grid_x, a.grid_y), dim3(256), 0, st, r->ranges, r->ids_sorted, a.W, a.H,
                        a.grid_x, r->xy, r->conic, r->rgb, in->bg, out_color, r->forward_only ? nullptr : r->final_T,
