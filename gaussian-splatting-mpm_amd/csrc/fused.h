@@ -643,8 +643,10 @@ constexpr int kGridT = kFTN / kGridParts;     // lanes per grid workgroup
 // only a contribution below 2^-51 of its chunk's largest can round to zero,
 // and that weight then multiplies the stale value instead of 0: < 1e-15
 // relative).  A node of mass in (0, 1e-15] still stores 0 (utils.py:177-183).
+// About half the touched tiles' nodes are massless on the lego frame; A/B
+// (tools/ab_skip0.sh, 3 interleaved pairs): sim 3.136 -> 3.116 ms/frame.
 #ifndef GSMPM_GRID_SKIP0
-#define GSMPM_GRID_SKIP0 0
+#define GSMPM_GRID_SKIP0 1
 #endif
 constexpr bool kGridSkip0 = GSMPM_GRID_SKIP0 != 0;
 __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_grid_f(GridDims g, FTiles tl, ChunkIn ck, const int* __restrict__ tbox,
