@@ -61,8 +61,33 @@ constexpr int kBX = 16, kBY = 16, kBlock = kBX * kBY;
 // launches instead of one per 8-bit digit; measured 0.05 ms/frame slower on the
 // bench's ~500k pairs).  The 100k-key depth sort keeps the default: there the
 // merge path is the faster one (onesweep's look-back chain dominates).
+// GSMPM_OS_BLOCK / GSMPM_OS_ITEMS (A/B builds): an explicit onesweep block config instead of rocPRIM's
+// default for the arch (gfx950 has no tuned entry and takes the generic 256 x 16, 8-bit digits).
+#ifndef GSMPM_OS_BLOCK
+#define GSMPM_OS_BLOCK 0
+#endif
+#ifndef GSMPM_OS_ITEMS
+#define GSMPM_OS_ITEMS 16
+#endif
+#if GSMPM_OS_BLOCK > 0
+using OnesweepSort = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<GSMPM_OS_BLOCK, GSMPM_OS_ITEMS>,
+                                        rocprim::kernel_config<GSMPM_OS_BLOCK, GSMPM_OS_ITEMS>, 8,
+                                        rocprim::block_radix_rank_algorithm::match>,
+    0>;
+#else
 using OnesweepSort = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
                                                 rocprim::default_config, 0>;
+#endif
+// The depth sort takes onesweep from this many Gaussians on (GSMPM_DEPTH_OS_MIN; below it rocPRIM's
+// default block sort + merge passes, which win at lego's 100k keys); 0 = never.  Bicycle (1M): render
+// 1.256 -> 1.241 ms (3 interleaved rounds, tools/ab_render_os.sh; explicit 512 / 1024 x 16 onesweep
+// blocks for the tile sort measured 1.256 / 1.260 ms, so the tile sort keeps rocPRIM's default)
+#ifndef GSMPM_DEPTH_OS_MIN
+#define GSMPM_DEPTH_OS_MIN 262144
+#endif
+constexpr size_t kDepthOnesweepMin = GSMPM_DEPTH_OS_MIN;
 
 __constant__ float kSH_C0 = 0.28209479177387814f;
 __constant__ float kSH_C1 = 0.4886025119029199f;
@@ -1667,10 +1692,15 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     if ((rc = grow((void**)&r->dorder, cap * sizeof(unsigned)))) return rc;
     if ((rc = grow((void**)&r->dsorted, cap * sizeof(unsigned)))) return rc;
     if ((rc = grow((void**)&r->offr, cap * sizeof(unsigned long long)))) return rc;
-    size_t bytes = 0;
+    size_t bytes = 0, obytes = 0;
     GSMPM_HIP(rocprim::radix_sort_pairs(nullptr, bytes, reinterpret_cast<unsigned*>(r->depth), r->dsorted,
                                                       rocprim::counting_iterator<unsigned>(0u), r->dorder, cap, 0, 32,
                                                       st));
+    if (kDepthOnesweepMin > 0 && cap >= kDepthOnesweepMin)
+      GSMPM_HIP(rocprim::radix_sort_pairs<OnesweepSort>(nullptr, obytes, reinterpret_cast<unsigned*>(r->depth),
+                                                        r->dsorted, rocprim::counting_iterator<unsigned>(0u),
+                                                        r->dorder, cap, 0, 32, st));
+    bytes = std::max(bytes, obytes);
     if ((rc = grow(&r->dsort_tmp, bytes))) return rc;
     r->dsort_tmp_bytes = bytes;
     bytes = 0;
@@ -1732,9 +1762,14 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       // the depth order depends on P only: it runs before the count read-back,
       // queued behind whatever the stream is still doing
       bytes = r->dsort_tmp_bytes;
-      GSMPM_HIP(rocprim::radix_sort_pairs(r->dsort_tmp, bytes, reinterpret_cast<unsigned*>(r->depth),
-                                                        r->dsorted, rocprim::counting_iterator<unsigned>(0u),
-                                                        r->dorder, (size_t)P, 0, 32, st));
+      if (kDepthOnesweepMin > 0 && (size_t)P >= kDepthOnesweepMin)
+        GSMPM_HIP(rocprim::radix_sort_pairs<OnesweepSort>(r->dsort_tmp, bytes, reinterpret_cast<unsigned*>(r->depth),
+                                                          r->dsorted, rocprim::counting_iterator<unsigned>(0u),
+                                                          r->dorder, (size_t)P, 0, 32, st));
+      else
+        GSMPM_HIP(rocprim::radix_sort_pairs(r->dsort_tmp, bytes, reinterpret_cast<unsigned*>(r->depth),
+                                            r->dsorted, rocprim::counting_iterator<unsigned>(0u), r->dorder,
+                                            (size_t)P, 0, 32, st));
       // the scan reads tiles[dorder[r]] itself (no separate gather launch)
       bytes = r->scan_tmp_bytes;
       GSMPM_HIP(rocprim::inclusive_scan(r->scan_tmp, bytes, ranked_tiles(r->dorder, r->tiles), r->offr, (size_t)P,
