@@ -808,7 +808,7 @@ __global__ __launch_bounds__(256) void k_emit_pairs(int K, int P, const unsigned
     if ((unsigned)offr[mid] > (unsigned)e) hi = mid;
     else lo = mid + 1;
   }
-  const unsigned g = order[lo];
+  const unsigned g = order ? order[lo] : (unsigned)lo;
   const unsigned local = (unsigned)e - (lo ? (unsigned)offr[lo - 1] : 0u);
   const float2 gp = xy[g];
   int rmin[2], rmax[2];
@@ -874,7 +874,7 @@ __global__ __launch_bounds__(kEmitT) void k_emit_wg(int K, int P, int items, con
     __syncthreads();  // the previous span's readers are done
     if (threadIdx.x == 0) s_off[0] = rs ? (unsigned)offr[rs - 1] : 0u;
     for (int i = threadIdx.x; i < ns; i += kEmitT) {
-      const unsigned g = order[rs + i];
+      const unsigned g = order ? order[rs + i] : (unsigned)(rs + i);  // null: Gaussian-index order
       s_off[i + 1] = (unsigned)offr[rs + i];
       s_g[i] = g;
       const uint2 rr = rect[g];
@@ -969,8 +969,9 @@ __global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int 
                                                          const unsigned* __restrict__ vals,
                                                          const unsigned* __restrict__ Hs,
                                                          unsigned* __restrict__ keys_out, unsigned* __restrict__ vals_out,
-                                                         uint2* __restrict__ ranges) {
+                                                         uint2* __restrict__ ranges, int* __restrict__ dsort_counts) {
   using BRS = rocprim::block_radix_sort<unsigned, kSortT, kSortI, unsigned>;
+  if (dsort_counts && blockIdx.x == 0 && threadIdx.x < 2) dsort_counts[threadIdx.x] = 0;  // k_tile_dsort's lists
   __shared__ typename BRS::storage_type s_sort;
   __shared__ unsigned s_k[kChunk], s_v[kChunk];
   __shared__ int s_start[kMaxTiles + 1];
@@ -1007,6 +1008,105 @@ __global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int 
   if (c == 0)
     for (int tt = threadIdx.x; tt < ntiles; tt += kSortT)
       ranges[tt] = make_uint2(Hs[(size_t)tt * nch], Hs[(size_t)(tt + 1) * nch]);
+}
+
+// Per-tile depth order (the chunked path's default, GSMPM_RASTER_TILE_DSORT).
+// Pairs are emitted in Gaussian-index order and the stable tile sort keeps it,
+// so each tile's list comes out in index order; sorting each list by the
+// composite (depth bits << 32 | position) -- unique, and position order is
+// index order -- gives exactly the (depth, index) order a global stable depth
+// sort of the Gaussians followed by emission in that order produced, without
+// the global sort (rocPRIM's block sort + merge passes over all P depths).
+// Lists of <= CAP entries are sorted in LDS by a bitonic network (tiles with
+// (lo, CAP] entries: two launches, a small and a large LDS class); longer ones
+// by k_tile_dsort_rank.  Depths are > 0.2 (k_preprocess culls nearer ones), so
+// their bits order as the floats do.
+// tl: [0] tiles listed for the large class, [1] for k_tile_dsort_rank, then
+// the two lists of ntiles entries each (k_tile_scatter's chunk 0 zeroes the
+// counts).  The small class walks every tile and lists the longer ones; the
+// large class walks its list and lists the longer ones for the rank kernel.
+template <int CAP, bool LISTED>
+__global__ __launch_bounds__(256) void k_tile_dsort(const uint2* __restrict__ ranges, int ntiles,
+                                                    const float* __restrict__ depth, unsigned* __restrict__ keys,
+                                                    unsigned* __restrict__ ids, int* __restrict__ tl) {
+  __shared__ unsigned long long s_c[CAP];
+  __shared__ unsigned s_id[CAP], s_key[CAP];
+  const int nt = LISTED ? tl[0] : ntiles;
+  for (int w = blockIdx.x; w < nt; w += gridDim.x) {
+    const int t = LISTED ? tl[2 + w] : w;
+    const uint2 rg = ranges[t];
+    const int n = (int)(rg.y - rg.x);
+    if (n > CAP) {  // workgroup-uniform: the next class
+      if (threadIdx.x == 0) {
+        const int i = atomicAdd(&tl[LISTED ? 1 : 0], 1);
+        tl[2 + (LISTED ? ntiles : 0) + i] = t;
+      }
+      continue;
+    }
+    if (n <= 1) continue;
+    int m = 2;
+    while (m < n) m <<= 1;
+    __syncthreads();  // the previous tile's readers are done
+    for (int j = threadIdx.x; j < m; j += 256) {
+      if (j < n) {
+        const unsigned id = ids[rg.x + j];
+        s_id[j] = id;
+        s_key[j] = keys[rg.x + j];
+        s_c[j] = ((unsigned long long)__float_as_uint(depth[id]) << 32) | (unsigned)j;
+      } else {
+        s_c[j] = ~0ull;
+      }
+    }
+    __syncthreads();
+    for (int k = 2; k <= m; k <<= 1)
+      for (int h = k >> 1; h > 0; h >>= 1) {
+        for (int i = threadIdx.x; i < m; i += 256) {
+          const int ix = i ^ h;
+          if (ix > i) {
+            const unsigned long long a = s_c[i], b = s_c[ix];
+            if ((a > b) == ((i & k) == 0)) {
+              s_c[i] = b;
+              s_c[ix] = a;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    for (int j = threadIdx.x; j < n; j += 256) {
+      const unsigned p = (unsigned)s_c[j];
+      ids[rg.x + j] = s_id[p];
+      keys[rg.x + j] = s_key[p];
+    }
+  }
+}
+// Lists longer than the large LDS class (rare): each entry's rank among its
+// tile's composites, counted against the whole list (O(n^2) per tile), into
+// scratch, then copied back.
+constexpr int kDsortSmall = 1024, kDsortLarge = 8192;
+__global__ __launch_bounds__(256) void k_tile_dsort_rank(const uint2* __restrict__ ranges, int ntiles,
+                                                         const float* __restrict__ depth,
+                                                         unsigned* __restrict__ keys, unsigned* __restrict__ ids,
+                                                         const int* __restrict__ tl, unsigned* __restrict__ scr_keys,
+                                                         unsigned* __restrict__ scr_ids) {
+  for (int w = blockIdx.x; w < tl[1]; w += gridDim.x) {
+    const int t = tl[2 + ntiles + w];
+    const uint2 rg = ranges[t];
+    const int n = (int)(rg.y - rg.x);
+    for (int j = threadIdx.x; j < n; j += 256) {
+      const unsigned long long cj = ((unsigned long long)__float_as_uint(depth[ids[rg.x + j]]) << 32) | (unsigned)j;
+      int r = 0;
+      for (int i = 0; i < n; ++i)
+        r += (((unsigned long long)__float_as_uint(depth[ids[rg.x + i]]) << 32) | (unsigned)i) < cj;
+      scr_ids[rg.x + r] = ids[rg.x + j];
+      scr_keys[rg.x + r] = keys[rg.x + j];
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < n; j += 256) {
+      ids[rg.x + j] = scr_ids[rg.x + j];
+      keys[rg.x + j] = scr_keys[rg.x + j];
+    }
+    __syncthreads();
+  }
 }
 
 // Above kMaxTiles tiles: the same chunked counting sort, LSD over 8-bit
@@ -1587,6 +1687,7 @@ struct gsmpm_raster {
   // tile ranges
   size_t capT = 0;
   uint2* ranges = nullptr;
+  int* dsort_tl = nullptr;  // [2 + 2 * capT] k_tile_dsort's size-class lists
   unsigned* h_count = nullptr;  // [2] pinned, mapped + coherent (the device writes K, num_rendered into it)
   hipEvent_t count_ev = nullptr;  // recorded after k_publish_count: surfaces a fault while the host spins
   // per pixel (backward)
@@ -1630,7 +1731,8 @@ int gsmpm_raster_destroy(gsmpm_raster* r) {
   for (void* p : {(void*)r->radii_tmp, (void*)r->depth, (void*)r->xy, (void*)r->conic, (void*)r->rgb, (void*)r->tiles, (void*)r->rect,
                   (void*)r->offsets, r->scan_tmp, (void*)r->keys, (void*)r->keys_sorted, (void*)r->vals,
                   (void*)r->vals_sorted, r->sort_tmp, (void*)r->ranges, (void*)r->ids_sorted, (void*)r->estart, (void*)r->rec,
-                  (void*)r->final_T, (void*)r->n_contrib, (void*)r->dorder, (void*)r->dsorted, (void*)r->offr, r->dsort_tmp, (void*)r->hist})
+                  (void*)r->final_T, (void*)r->n_contrib, (void*)r->dorder, (void*)r->dsorted, (void*)r->offr, r->dsort_tmp, (void*)r->hist,
+                  (void*)r->dsort_tl})
     if (p) (void)hipFree(p);
   if (r->h_count) (void)hipHostFree(r->h_count);
   if (r->count_ev) (void)hipEventDestroy(r->count_ev);
@@ -1719,6 +1821,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
   if (ntiles > r->capT) {
     int rc;
     if ((rc = grow((void**)&r->ranges, ntiles * sizeof(uint2)))) return rc;
+    if ((rc = grow((void**)&r->dsort_tl, (2 + 2 * ntiles) * sizeof(int)))) return rc;
     r->capT = ntiles;
   }
   // tile ranges: the chunked tile sort writes every tile's; the other paths
@@ -1739,6 +1842,15 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
   const char* rm = std::getenv("GSMPM_RASTER_RENDER_MODE");
   const int render_mode = rm ? std::atoi(rm) & 1 : 0;
   a.tight = !(render_mode & 1);
+  // the chunked tile sort (<= kMaxTiles tiles; GSMPM_RASTER_ONESWEEP=1 forces rocPRIM onesweep everywhere)
+  const char* os = std::getenv("GSMPM_RASTER_ONESWEEP");
+  const bool force_onesweep = os && os[0] == '1';
+  const bool chunked = ntiles <= (size_t)kMaxTiles && !force_onesweep;
+  // GSMPM_RASTER_TILE_DSORT=1 (chunked path): depth order per tile after the tile sort (k_tile_dsort)
+  // instead of the global depth sort before the emission.  Bit-identical (the raster, golden, e2e and
+  // config tests pass with it) but slower: lego render alone 0.311 vs 0.194 ms (3 rounds), so off
+  const char* td = std::getenv("GSMPM_RASTER_TILE_DSORT");
+  const bool tile_dsort = depth_ordered && chunked && td && td[0] == '1';
   a.sh_vec4 = in->shs && in->M == 16 && ((uintptr_t)in->shs & 15u) == 0;
   r->slots_pending = false;
   r->offsets_pending = false;
@@ -1755,10 +1867,10 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     // depth-order scan and leaves offsets to gsmpm_raster_backward (one scan
     // and its look-back init launch less per frame)
     r->offsets_pending = true;
-    if (!depth_ordered)  // upstream keys: the index-order scan of both counts (k_duplicate's offsets, K)
+    if (!depth_ordered || tile_dsort)  // the index-order scan of both counts (emission offsets, K)
       GSMPM_HIP(rocprim::inclusive_scan(r->scan_tmp, bytes, r->tiles, r->offr, (size_t)P,
                                         rocprim::plus<unsigned long long>(), st));
-    if (depth_ordered) {
+    if (depth_ordered && !tile_dsort) {
       // the depth order depends on P only: it runs before the count read-back,
       // queued behind whatever the stream is still doing
       bytes = r->dsort_tmp_bytes;
@@ -1829,10 +1941,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       // tiles rocPRIM onesweep (GSMPM_RASTER_ONESWEEP=1 forces it everywhere).
       // GSMPM_RASTER_DIGIT_SORT=1: the LSD digit form of the chunked sort above
       // kMaxTiles instead (bit-identical; bicycle render 2.09 against 1.30 ms)
-      const char* os = std::getenv("GSMPM_RASTER_ONESWEEP");
       const char* ds = std::getenv("GSMPM_RASTER_DIGIT_SORT");
-      const bool force_onesweep = os && os[0] == '1';
-      const bool chunked = ntiles <= (size_t)kMaxTiles && !force_onesweep;
       const bool digits = !chunked && !force_onesweep && ds && ds[0] == '1';
       const int passes = (bits + 7) / 8;  // ntiles <= 256^passes - 1: the all-ones tile field stays the culled one
       const int nch = (int)div_up(K, kChunk);
@@ -1868,7 +1977,8 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       const int cull = !(render_mode & 1);
       const char* el = std::getenv("GSMPM_RASTER_EMIT_LANE");
       if (el && el[0] == '1') {
-        hipLaunchKernelGGL(k_emit_pairs, dim3(div_up(K, 256)), dim3(256), 0, st, (int)K, P, (const unsigned*)r->dorder,
+        hipLaunchKernelGGL(k_emit_pairs, dim3(div_up(K, 256)), dim3(256), 0, st, (int)K, P,
+                           tile_dsort ? nullptr : (const unsigned*)r->dorder,
                            (const unsigned long long*)r->offr, (const float2*)r->xy, (const float4*)r->conic,
                            (const uint2*)r->rect, a.grid_x, cull, tile_keys, r->vals);
       } else {  // >= ~1024 workgroups, up to kEmitMaxI pairs per lane
@@ -1878,7 +1988,8 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
                            (unsigned)(kEmitT * items), r->estart);
         GSMPM_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_emit_wg, dim3(nwg), dim3(kEmitT), 0, st, (int)K, P, items, (const unsigned*)r->estart,
-                           (const unsigned*)r->dorder, (const unsigned long long*)r->offr, (const float2*)r->xy,
+                           tile_dsort ? nullptr : (const unsigned*)r->dorder, (const unsigned long long*)r->offr,
+                           (const float2*)r->xy,
                            (const float4*)r->conic, (const uint2*)r->rect, a.grid_x, cull, tile_keys, r->vals);
       }
       GSMPM_LAUNCH_CHECK();
@@ -1892,8 +2003,19 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
         GSMPM_HIP(rocprim::exclusive_scan(r->sort_tmp, bytes, r->hist, Hs, 0u, nh, rocprim::plus<unsigned>(), st));
         hipLaunchKernelGGL(k_tile_scatter, dim3(nch), dim3(kSortT), 0, st, (int)K, (int)ntiles, nch, bits,
                            (const unsigned*)tile_keys, (const unsigned*)r->vals, (const unsigned*)Hs, tile_sorted,
-                           r->ids_sorted, r->ranges);
+                           r->ids_sorted, r->ranges, tile_dsort ? r->dsort_tl : nullptr);
         GSMPM_LAUNCH_CHECK();
+        if (tile_dsort) {  // depth order within each tile's list (the emission keys are dead: scratch)
+          hipLaunchKernelGGL((k_tile_dsort<kDsortSmall, false>), dim3((unsigned)ntiles), dim3(256), 0, st,
+                             (const uint2*)r->ranges, (int)ntiles, (const float*)r->depth, tile_sorted, r->ids_sorted,
+                             r->dsort_tl);
+          hipLaunchKernelGGL((k_tile_dsort<kDsortLarge, true>), dim3(256), dim3(256), 0, st, (const uint2*)r->ranges,
+                             (int)ntiles, (const float*)r->depth, tile_sorted, r->ids_sorted, r->dsort_tl);
+          hipLaunchKernelGGL(k_tile_dsort_rank, dim3(64), dim3(256), 0, st, (const uint2*)r->ranges, (int)ntiles,
+                             (const float*)r->depth, tile_sorted, r->ids_sorted, (const int*)r->dsort_tl,
+                             tile_keys, tile_keys + r->capK);
+          GSMPM_LAUNCH_CHECK();
+        }
         tkeys = tile_sorted;
         r->emit_culled = cull != 0;
         ranges_written = true;
