@@ -127,9 +127,11 @@ def test_narrow_keys_match_upstream_keys(dev, monkeypatch, W, H):
                                        projmatrix=t(full), sh_degree=3, campos=t(campos), prefiltered=False,
                                        debug=False)
     outs = []
-    for wide, onesweep in (("1", "0"), ("0", "0"), ("0", "1")):
+    # (wide keys, onesweep, per-tile depth sort: GSMPM_RASTER_TILE_DSORT, chunked path only)
+    for wide, onesweep, tds in (("1", "0", "0"), ("0", "0", "0"), ("0", "1", "0"), ("0", "0", "1")):
         monkeypatch.setenv("GSMPM_RASTER_WIDE_KEYS", wide)
         monkeypatch.setenv("GSMPM_RASTER_ONESWEEP", onesweep)
+        monkeypatch.setenv("GSMPM_RASTER_TILE_DSORT", tds)
         m, s, o, c = (t(a).requires_grad_(True) for a in (means, shs, opa, c6))
         color, radii = GaussianRasterizer(st)(means3D=m, means2D=None, opacities=o, shs=s, cov3D_precomp=c)
         (color * torch.linspace(0.5, 1.5, color.numel(), device=dev).reshape(color.shape)).sum().backward()
@@ -137,6 +139,36 @@ def test_narrow_keys_match_upstream_keys(dev, monkeypatch, W, H):
     for other in outs[1:]:
         for a, b in zip(outs[0], other):
             assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("P", [3000, 12000])
+def test_tile_depth_sort_size_classes(dev, monkeypatch, P):
+    """GSMPM_RASTER_TILE_DSORT=1 on lists of every size class: a 48 x 48 image
+    (9 tiles) under P Gaussians puts 1,024 < n <= 8,192 (P = 3000) and n > 8,192
+    (P = 12000: the rank fallback) entries in a tile; images, radii and every
+    input gradient equal the global depth sort's bitwise, depth ties included."""
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    W = H = 48
+    means, c6, opa, shs = _scene(P, seed=5)
+    means[:, :2] *= 0.15  # all in front of the small image
+    means[1::5, 2] = means[::5, 2][: len(means[1::5])]  # depth ties
+    view, full, campos, tx, ty = _camera(W, H, 0.9)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    st = GaussianRasterizationSettings(image_height=H, image_width=W, tanfovx=tx, tanfovy=ty,
+                                       bg=t(np.zeros(3, np.float32)), scale_modifier=1.0, viewmatrix=t(view),
+                                       projmatrix=t(full), sh_degree=3, campos=t(campos), prefiltered=False,
+                                       debug=False)
+    outs = []
+    for tds in ("0", "1"):
+        monkeypatch.setenv("GSMPM_RASTER_TILE_DSORT", tds)
+        m, s, o, c = (t(a).requires_grad_(True) for a in (means, shs, opa, c6))
+        color, radii = GaussianRasterizer(st)(means3D=m, means2D=None, opacities=o, shs=s, cov3D_precomp=c)
+        (color * torch.linspace(0.5, 1.5, color.numel(), device=dev).reshape(color.shape)).sum().backward()
+        outs.append([x.detach().cpu().numpy() for x in (color, radii, m.grad, s.grad, o.grad, c.grad)])
+    assert (outs[0][1] > 0).sum() > 0.9 * P
+    for a, b in zip(outs[0], outs[1]):
+        assert np.array_equal(a, b)
 
 
 def _dense_scene(P, seed, lo, hi):
