@@ -628,16 +628,28 @@ def main():
     barrier()
     sim_ms = e0.elapsed_time(e1)
     state["t"] = t_after
-    render_ms = None
+    render_ms = render_host_ms = None
     if not args.no_render and rank == 0 and world == 1:
+        # on the stream the timed frames rendered on, after one warm-up render
+        # there; device time between hipEvents recorded on that stream around 5
+        # renders (each holds its host read-back of the pair count), and beside
+        # it the host wall time of the same 5 calls
         means_r, covs_r = sim.world_outputs(w_scale, w_center, render_space=True)
         torch.cuda.synchronize()
-        r0 = time.perf_counter()
-        for _ in range(5):
+        with torch.cuda.stream(render_stream):
             raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg, cam.height, cam.width,
                            tanx, tany, sh_degree=3, shs=feats, cov3D_precomp=covs_r)
-        torch.cuda.synchronize()
-        render_ms = (time.perf_counter() - r0) / 5 * 1e3
+            torch.cuda.synchronize()
+            r_ev0, r_ev1 = ev(), ev()
+            r0 = time.perf_counter()
+            r_ev0.record(render_stream)
+            for _ in range(5):
+                raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg, cam.height,
+                               cam.width, tanx, tany, sh_degree=3, shs=feats, cov3D_precomp=covs_r)
+            r_ev1.record(render_stream)
+            torch.cuda.synchronize()
+            render_host_ms = (time.perf_counter() - r0) / 5 * 1e3
+        render_ms = r_ev0.elapsed_time(r_ev1) / 5
     kern = frame_prof = None
     if world == 1:
         fused = sim.pipeline == "fused"
@@ -684,6 +696,7 @@ def main():
         "sim_ms_per_frame": sim_ms,
         "sim_substeps_per_s": spf / (sim_ms / 1e3),
         "render_ms_per_frame": render_ms,
+        "render_host_ms_per_frame": render_host_ms,
         "num_rendered": state["K"],
     }
     if kern is not None:

@@ -220,6 +220,14 @@ __device__ __forceinline__ bool in_grid(const float (&x)[3], const GridDims& g) 
 #ifndef GSMPM_STORE_VC
 #define GSMPM_STORE_VC 0  // 1: every G2P stores v and C (A/B)
 #endif
+// GSMPM_ZERO_BOX=1: the P2G half zeroes only its chunk's store box of the LDS
+// window (the nodes its stencils reach: ~57 % of the 1,584 on the lego
+// frame), once the box is known, with one more workgroup barrier, instead
+// of the whole window before it (A/B)
+#ifndef GSMPM_ZERO_BOX
+#define GSMPM_ZERO_BOX 0
+#endif
+constexpr bool kZeroBox = GSMPM_ZERO_BOX != 0;
 template <int MAT, int MODE>
 __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTiles tl, ChunkIn ck, Touch tc, BinOutF bo,
                                                int bin, int use_box, const float4* __restrict__ gvel,
@@ -394,7 +402,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
       if (w == (int)blockIdx.x) stamp(SK, 3);
     }
     if constexpr (P2G) {
-      if (!outside) {  // 16-byte stores: half the LDS write instructions of u64 ones
+      if (!outside && !kZeroBox) {  // 16-byte stores: half the LDS write instructions of u64 ones
         uint4* z = reinterpret_cast<uint4*>(s_acc);
         for (int e = k; e < kFWin * 2; e += 256) z[e] = make_uint4(0u, 0u, 0u, 0u);
       }
@@ -498,6 +506,21 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
         tc.tbox[t] = (cr.w & 8) ? kFullBox : box;  // tiles with several chunks: whole windows
       }
       if (cr.w & 8) box = kFullBox;
+      if constexpr (kZeroBox) {  // only the nodes the scatter can reach and the store reads
+        int lo[3], hi[3];
+        box_unpack(box, lo, hi);
+        const int n1 = hi[1] - lo[1] + 1, n2 = hi[2] - lo[2] + 1, n12 = n1 * n2;
+        const int nvol = (hi[0] - lo[0] + 1) * n12;
+        const float r12 = 1.0f / (float)n12, r2 = 1.0f / (float)n2;
+        for (int qn = k; qn < nvol; qn += 256) {
+          const int a = (int)(((float)qn + 0.5f) * r12), rem = qn - a * n12;
+          const int bq = (int)(((float)rem + 0.5f) * r2), c = rem - bq * n2;
+          const int node = ((lo[0] + a) * kFW1 + lo[1] + bq) * kFW2 + lo[2] + c;
+#pragma unroll
+          for (int ch = 0; ch < 4; ++ch) s_acc[ch * kFWin + node] = 0ull;
+        }
+        __syncthreads();  // zeroing before the adds
+      }
       int ebits;
       frexpf(bmax, &ebits);
       const int S = bmax > 0.f ? 50 - ebits : 0;  // see k_p2g
@@ -639,10 +662,15 @@ constexpr int kGridParts = GSMPM_GRID_PARTS;  // workgroups per touched tile
 constexpr int kGridT = kFTN / kGridParts;     // lanes per grid workgroup
 // Nodes that received no mass at all keep whatever v_out they held: the next
 // G2P gathers only the stencils of particles whose P2G built this grid, and a
-// stencil node of such a particle has mass (the fixed-point sums are exact, so
-// only a contribution below 2^-51 of its chunk's largest can round to zero,
-// and that weight then multiplies the stale value instead of 0: < 1e-15
-// relative).  A node of mass in (0, 1e-15] still stores 0 (utils.py:177-183).
+// stencil node of such a particle has mass -- except in one case: the
+// fixed-point sums are exact, so a node's mass rounds to zero only when every
+// contribution to it is below 2^-51 of its chunk's largest, i.e. a particle
+// lighter than 2^-51 of the heaviest in its chunk.  That particle's G2P weight
+// at the node is still O(0.1-0.75), so its gathered velocity picks up the
+// node's stale v_out (any finite O(1) value) where the reference's reset grid
+// gives 0 (utils.py:177-183).  The scenes here have particle masses within a
+// few orders of magnitude of each other; GSMPM_GRID_SKIP0=0 restores the
+// store of every node.  A node of mass in (0, 1e-15] still stores 0.
 // About half the touched tiles' nodes are massless on the lego frame; A/B
 // (tools/ab_skip0.sh, 3 interleaved pairs): sim 3.136 -> 3.116 ms/frame.
 #ifndef GSMPM_GRID_SKIP0

@@ -76,6 +76,7 @@ enum SlabRec : int {
   RF_BAND_LO = 11, RF_BAND_HI = 12,                 // particles within `margin` planes of the lower / upper bound
   RF_DEFERRED = 13,                                 // leavers kept for a later migration (payload full)
   RF_CAP = 14,                                      // the slab's particle capacity
+  RF_MMIN = 15,                                     // min particle mass (f32 bits; INT_MAX: no particle)
   kRecInts = 16
 };
 // Device flags of a slab (s_flags): sticky until the handle is reset.
@@ -107,7 +108,8 @@ __global__ void k_rec_init(const int* __restrict__ flags, const int* __restrict_
   rec[RF_BAND_HI] = 0;
   rec[RF_DEFERRED] = flags[SF_DEFERRED];
   rec[RF_CAP] = capacity;
-  for (int i = RF_CAP + 1; i < kRecInts; ++i) rec[i] = 0;
+  rec[RF_MMIN] = INT_MAX;
+  for (int i = RF_MMIN + 1; i < kRecInts; ++i) rec[i] = 0;
 }
 
 // yz box of the particles' base nodes (trunc(x * inv_dx - 0.5), utils.py:95),
@@ -115,7 +117,7 @@ __global__ void k_rec_init(const int* __restrict__ flags, const int* __restrict_
 // most that can leave by the next migration) -> rec (after k_rec_init).
 __global__ __launch_bounds__(256) void k_slab_record(Particles ps, MigGeom mg, int margin, int* __restrict__ rec) {
   int v[4] = {INT_MAX, INT_MIN, INT_MAX, INT_MIN};
-  float vy = 0.f, vz = 0.f;
+  float vy = 0.f, vz = 0.f, mmin = __int_as_float(INT_MAX);  // INT_MAX bits: a NaN above every finite mass
   int blo = 0, bhi = 0;
   const int n = ps.count();
   for (int p = blockIdx.x * 256 + threadIdx.x; p < n; p += gridDim.x * 256) {
@@ -127,6 +129,7 @@ __global__ __launch_bounds__(256) void k_slab_record(Particles ps, MigGeom mg, i
     v[3] = max(v[3], bz);
     vy = fmaxf(vy, fabsf(ps.ld(PV + 1, p)));
     vz = fmaxf(vz, fabsf(ps.ld(PV + 2, p)));
+    mmin = __int_as_float(min(__float_as_int(mmin), __float_as_int(ps.ld(PMASS, p))));
     blo += (bx < mg.lo + margin) ? 1 : 0;
     bhi += (bx >= mg.hi - margin) ? 1 : 0;
   }
@@ -138,6 +141,7 @@ __global__ __launch_bounds__(256) void k_slab_record(Particles ps, MigGeom mg, i
     v[3] = max(v[3], __shfl_xor(v[3], o));
     vy = fmaxf(vy, __shfl_xor(vy, o));
     vz = fmaxf(vz, __shfl_xor(vz, o));
+    mmin = __int_as_float(min(__float_as_int(mmin), __float_as_int(__shfl_xor(mmin, o))));
     blo += __shfl_xor(blo, o);
     bhi += __shfl_xor(bhi, o);
   }
@@ -151,6 +155,7 @@ __global__ __launch_bounds__(256) void k_slab_record(Particles ps, MigGeom mg, i
     // non-negative floats order as their bit patterns (NaN: all bits set, wins)
     atomicMax(rec + RF_VY, __float_as_int(vy));
     atomicMax(rec + RF_VZ, __float_as_int(vz));
+    atomicMin(rec + RF_MMIN, __float_as_int(mmin));  // masses are positive: bit order is value order
     if (blo) atomicAdd(rec + RF_BAND_LO, blo);
     if (bhi) atomicAdd(rec + RF_BAND_HI, bhi);
   }

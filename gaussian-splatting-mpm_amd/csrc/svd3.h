@@ -27,17 +27,34 @@ namespace gsmpm {
 // result depends on the SVD basis itself (foam's element-wise U * diag * V^T,
 // SURVEY F13) the correctly rounded form is used regardless.
 // GSMPM_SVD_FAST=1 at build time: the hardware instructions (A/B).
+// GSMPM_SVD_FAST=2: the hardware rsqrt refined by one Newton-Raphson step
+// (y (3 - x y^2) / 2, ~0.5 ulp) and sqrt as x * rsqrt plus one Heron
+// correction: 6 / 8 VALU instead of 27 / 18, not bit-identical to the oracle's
+// 1 / sqrtf (A/B against the long-horizon spread).
 #ifndef GSMPM_SVD_FAST
 #define GSMPM_SVD_FAST 0
 #endif
+__device__ __forceinline__ float svd_rsqrt_nr(float x) {
+  const float y0 = __builtin_amdgcn_rsqf(x);
+  const float y = y0 * fmaf(-0.5f * x, y0 * y0, 1.5f);
+  return x > 0.0f ? y : y0;  // 0 -> inf as 1 / sqrtf(0) (the Newton step would give NaN)
+}
+__device__ __forceinline__ float svd_sqrt_nr(float x) {
+  const float y = svd_rsqrt_nr(x);
+  const float s = x * y;
+  const float r = fmaf(0.5f * y, fmaf(-s, s, x), s);
+  return x > 0.0f ? r : sqrtf(x);  // 0 -> 0, negative -> NaN
+}
 template <bool FAST>
 __device__ __forceinline__ float svd_rsqrt(float x) {
-  if constexpr (FAST && GSMPM_SVD_FAST) return __builtin_amdgcn_rsqf(x);
+  if constexpr (FAST && GSMPM_SVD_FAST == 1) return __builtin_amdgcn_rsqf(x);
+  if constexpr (FAST && GSMPM_SVD_FAST == 2) return svd_rsqrt_nr(x);
   return 1.0f / sqrtf(x);
 }
 template <bool FAST>
 __device__ __forceinline__ float svd_sqrt(float x) {
-  if constexpr (FAST && GSMPM_SVD_FAST) return __builtin_amdgcn_sqrtf(x);
+  if constexpr (FAST && GSMPM_SVD_FAST == 1) return __builtin_amdgcn_sqrtf(x);
+  if constexpr (FAST && GSMPM_SVD_FAST == 2) return svd_sqrt_nr(x);
   return sqrtf(x);
 }
 

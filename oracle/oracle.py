@@ -271,10 +271,13 @@ class OracleMPM:
 
 def raster_forward(means3D, opacities, viewmatrix, projmatrix, campos, bg, W, H, tanfovx, tanfovy,
                    shs=None, sh_degree=3, colors_precomp=None, cov3D_precomp=None, scales=None, rotations=None,
-                   scale_modifier=1.0, crop_tiles=None):
+                   scale_modifier=1.0, crop_tiles=None, threaded=False):
     """Returns (color (3,H,W), radii (P,), num_rendered, depth, tiles_touched).
     crop_tiles=(tx0, ty0, tx1, ty1): blend only those 16x16 tiles (the rest of
-    color stays 0); radii / num_rendered / depth / tiles_touched are global."""
+    color stays 0); radii / num_rendered / depth / tiles_touched are global.
+    threaded=True: the OpenMP build (per-tile sorts and blends in parallel,
+    the same arithmetic and lists: a full bicycle frame in seconds);
+    threaded="fast": the -O3 -ffast-math build (bench.py's CPU baseline)."""
     c = lambda a: None if a is None else np.ascontiguousarray(np.asarray(a, np.float32))
     means3D = c(means3D).reshape(-1, 3)
     P = means3D.shape[0]
@@ -296,11 +299,12 @@ def raster_forward(means3D, opacities, viewmatrix, projmatrix, campos, bg, W, H,
     radii = np.zeros(P, np.int32)
     depth = np.zeros(P, np.float32)
     tt = np.zeros(P, np.int32)
+    L = lib(threaded)
     if crop_tiles is None:
-        K = lib().or_forward(ctypes.byref(a), _p(color), _p(radii), _p(depth), _p(tt))
+        K = int(L.or_forward_crop(ctypes.byref(a), _p(color), _p(radii), _p(depth), _p(tt), None))
     else:
         crop = np.ascontiguousarray(np.asarray(crop_tiles, np.int32).reshape(4))
-        K = int(lib().or_forward_crop(ctypes.byref(a), _p(color), _p(radii), _p(depth), _p(tt), _p(crop)))
+        K = int(L.or_forward_crop(ctypes.byref(a), _p(color), _p(radii), _p(depth), _p(tt), _p(crop)))
     return color, radii, K, depth, tt
 
 

@@ -225,7 +225,29 @@ static void forward_core(const or_args* a, fstate* f, float* out_color, const in
   if (!crop) Kc = K;
   kv_t* kv = f->kv = (kv_t*)malloc(sizeof(kv_t) * (size_t)(Kc + 1));
   f->K = K;
-  long off = 0;
+  /* The sorted pair list of upstream's stable radix sort on (tile << 32 |
+   * depth bits), built tile by tile: count each tile's pairs, place every
+   * Gaussian's pairs into its tiles' runs in index order, then sort each run
+   * by (depth bits, index) -- the same order as one global sort on (key,
+   * emission index), since a Gaussian's pairs in one tile are one pair.  The
+   * per-tile runs sort independently (OpenMP build: in parallel; the serial
+   * checker gives the same array). */
+  int ntiles = gx * gy;
+  int32_t* rs = f->rs = (int32_t*)calloc((size_t)ntiles, sizeof(int32_t));
+  int32_t* re = f->re = (int32_t*)calloc((size_t)ntiles, sizeof(int32_t));
+  long* tcur = (long*)calloc((size_t)ntiles + 1, sizeof(long));
+  for (int i = 0; i < P; ++i) {
+    if (out_radii[i] <= 0) continue;
+    int rmin[2], rmax[2];
+    get_rect(xy + i * 2, out_radii[i], gx, gy, rmin, rmax);
+    for (int y = mxi(rmin[1], cy0); y < mni(rmax[1], cy1); ++y)
+      for (int x = mxi(rmin[0], cx0); x < mni(rmax[0], cx1); ++x) tcur[y * gx + x + 1] += 1;
+  }
+  for (int t = 0; t < ntiles; ++t) {
+    tcur[t + 1] += tcur[t];
+    rs[t] = (int32_t)tcur[t];
+    re[t] = (int32_t)tcur[t + 1];
+  }
   for (int i = 0; i < P; ++i) {
     if (out_radii[i] <= 0) continue;
     int rmin[2], rmax[2];
@@ -234,20 +256,16 @@ static void forward_core(const or_args* a, fstate* f, float* out_color, const in
     memcpy(&dbits, &depth[i], 4);
     for (int y = mxi(rmin[1], cy0); y < mni(rmax[1], cy1); ++y)
       for (int x = mxi(rmin[0], cx0); x < mni(rmax[0], cx1); ++x) {
-        kv[off].key = ((uint64_t)(uint32_t)(y * gx + x) << 32) | dbits;
-        kv[off].val = (uint32_t)i;
-        ++off;
+        const long o = tcur[y * gx + x]++;
+        kv[o].key = ((uint64_t)(uint32_t)(y * gx + x) << 32) | dbits;
+        kv[o].val = (uint32_t)i;
       }
   }
-  qsort(kv, (size_t)Kc, sizeof(kv_t), kv_cmp);
-  int ntiles = gx * gy;
-  int32_t* rs = f->rs = (int32_t*)calloc((size_t)ntiles, sizeof(int32_t));
-  int32_t* re = f->re = (int32_t*)calloc((size_t)ntiles, sizeof(int32_t));
-  for (long k = 0; k < Kc; ++k) {
-    int t = (int)(kv[k].key >> 32);
-    if (k == 0 || (int)(kv[k - 1].key >> 32) != t) rs[t] = (int32_t)k;
-    if (k == Kc - 1 || (int)(kv[k + 1].key >> 32) != t) re[t] = (int32_t)(k + 1);
-  }
+  free(tcur);
+#pragma omp parallel for schedule(dynamic, 16)
+  for (int t = 0; t < ntiles; ++t)
+    if (re[t] - rs[t] > 1) qsort(kv + rs[t], (size_t)(re[t] - rs[t]), sizeof(kv_t), kv_cmp);
+#pragma omp parallel for collapse(2) schedule(dynamic, 4)
   for (int ty = cy0; ty < cy1; ++ty)
     for (int tx = cx0; tx < cx1; ++tx) {
       int t = ty * gx + tx;

@@ -96,13 +96,27 @@ def _run_curve(s, ref, imps, ops, dt, checkpoints, extra=None, stress=False):
     return curve
 
 
-def _post(s, ref):
+def rel_err_elem(a, b, floor=1e-3):
+    """max_i |a_i - b_i| / max(|b_i|, floor * max|b|): relative per element, so a
+    small Gaussian's covariance cannot hide under the field's largest."""
+    a = np.asarray(a, np.float64).reshape(-1)
+    b = np.asarray(b, np.float64).reshape(-1)
+    scale = np.maximum(np.abs(b), floor * max(np.abs(b).max(), 1e-30))
+    return float((np.abs(a - b) / scale).max())
+
+
+def _post(s, ref, per_element=True):
+    """compute_cov_from_F / compute_R_from_F (mpm_solver/utils.py:376-433): cov and
+    R within 1e-4 of the field's max, and (per_element) every covariance
+    element within 1e-4 of itself (floored at 1e-3 of the max)."""
     s.postprocess()
     ref.postprocess()
     cov = s.mpm_state.particle_cov.to_torch().cpu().numpy().reshape(-1, 6)
     R = s.mpm_state.particle_R.to_torch().cpu().numpy().reshape(-1, 9)
-    e = {"cov": rel_err(cov, ref.cov), "R": rel_err(R, ref.R)}
+    e = {"cov": rel_err(cov, ref.cov), "R": rel_err(R, ref.R), "cov_elem": rel_err_elem(cov, ref.cov)}
     assert e["cov"] < TOL and e["R"] < TOL, e
+    if per_element:
+        assert e["cov_elem"] < TOL, e
     return e
 
 
@@ -221,7 +235,7 @@ def test_config_C_lego_fracture(dev, material):
         y = s.mpm_model.yield_stress.to_torch().cpu().numpy()
         rec["yield"] = rel_err(y, ref.yield_stress)
         assert rec["yield"] < extra["yield"]
-    rec["post"] = _post(s, ref)
+    rec["post"] = _post(s, ref, per_element=material == "jelly")
     _dump(f"config_C_{material}", rec)
 
 

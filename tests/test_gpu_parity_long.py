@@ -10,7 +10,7 @@ short horizons tightly and long horizons statistically").
   full size, both sides starting from the same state at substep 7,990;
 * sand and foam at 100k / 128^3 for 100 substeps;
 * config D's render at the bicycle camera (4946 x 3286, 1M Gaussians), the
-  oracle blending deterministic crops of tiles (K and radii exact globally).
+  whole frame against the OpenMP build of the oracle rasterizer.
 
 Two error measures per field: ``rel_err`` (max abs error / the field's max,
 conftest.py) and ``rel_err_elem`` (per element, |a - b| / max(|b|, 1e-3 x
@@ -33,7 +33,7 @@ import pytest
 
 from conftest import rel_err
 from scenarios import build_oracle_sim, lego_problem, oracle_run
-from test_gpu_configs import TOL, _c_err, _dump, _state
+from test_gpu_configs import TOL, _c_err, _dump, _state, rel_err_elem
 
 pytestmark = pytest.mark.gpu
 
@@ -44,15 +44,6 @@ FIELDS = ("x", "v", "C", "F_trial")
 # camera replaces the pose, main.py:84-106), as data: nothing reads /root/reference on the box
 BICYCLE_CAM0 = {"width": 4946, "height": 3286, "fx": 4649.505977743847, "fy": 4627.300372546341,
                 "position": [0.0, 0.0, 0.0], "rotation": [[1, 0, 0], [0, 1, 0], [0, 0, 1]]}
-
-
-def rel_err_elem(a, b, floor=1e-3):
-    """max_i |a_i - b_i| / max(|b_i|, floor * max|b|): relative per element, so a
-    small Gaussian's covariance cannot hide under the field's largest."""
-    a = np.asarray(a, np.float64).reshape(-1)
-    b = np.asarray(b, np.float64).reshape(-1)
-    scale = np.maximum(np.abs(b), floor * max(np.abs(b).max(), 1e-30))
-    return float((np.abs(a - b) / scale).max())
 
 
 def _oracle_fields(ref, inv=None):
@@ -138,27 +129,37 @@ def _horizon(prob, material, checkpoints, dev, spread=True, runs=None):
     return curve, post
 
 
-def _bound(bound, rec, key, curve=None):
+def _bound(bound, rec, key, curve=None, upto=None):
     """max(bound, SPREAD_FACTOR x spread): the spread of `rec`, or with
-    `curve` the largest spread over the horizon's checkpoints."""
-    recs = list(curve.values()) if curve else [rec]
+    `curve` the running maximum of the spread over the horizon's checkpoints
+    up to and including `upto` (an early checkpoint is never held to a
+    later, larger spread)."""
+    recs = [r for c, r in curve.items() if upto is None or c <= upto] if curve else [rec]
     sp = [r["spread"][key] for r in recs if key in r.get("spread", {})]
     return bound if not sp else max(bound, SPREAD_FACTOR * max(sp))
 
 
+# stress-free runs (jelly as written): v and C against the oracle, about 10x what
+# the kernels measure at substep 1,000 (v 1.6e-5, C 3.3e-5; profiles/r03/parity)
+TOL_V_FREE = 2e-4
+TOL_C_FREE = 2e-4
+
+
 def test_config_B_ten_frames(dev):
     """lego.json, 100k, 128^3, 1,000 substeps (10 frames): x, F_trial, cov and R
-    within 1e-4 of the field's max at every checkpoint; v, C within the
-    documented bounds of test_gpu_mpm.py; per-element x within 1e-3; the
-    per-element covariance error (floored at 1e-3 of the max) reported beside
-    the spread of a reordered and a fast-math oracle and held to twice it."""
+    within 1e-4 of the field's max and x within 1e-4 per element at every
+    checkpoint; v and C within 2e-4 (10x measured); the per-element covariance
+    error after 1,000 substeps (floored at 1e-3 of the max) reported beside
+    the spread of a reordered and a fast-math oracle and held to twice it
+    (north_star's 1e-4 per element holds at substep 100: test_gpu_configs.py
+    test_config_B_lego_full_frame)."""
     prob = lego_problem(100_000, 128)
     curve, post = _horizon(prob, None, (1, 100, 250, 500, 1000), dev, runs=1)
     for c, rec in curve.items():
         g = rec["gpu"]
         assert g["x"] < TOL and g["F_trial"] < TOL, (c, g)
-        assert g["v"] < 2e-3 and g["C"] < 5e-3, (c, g)
-        assert g["x_elem"] < 1e-3, (c, g)
+        assert g["v"] < TOL_V_FREE and g["C"] < TOL_C_FREE, (c, g)
+        assert g["x_elem"] < TOL, (c, g)
     assert post["gpu"]["cov"] < TOL and post["gpu"]["R"] < TOL, post
     assert post["gpu"]["cov_elem"] < _bound(TOL, post, "cov_elem"), post
     _dump("long_config_B_1000", {"config": "lego.json", "N": 100_000, "n_grid": 128, "curve": curve, "post": post})
@@ -173,10 +174,10 @@ def test_config_C_metal_five_frames(dev):
     curve, post = _horizon(prob, "metal", (100, 200, 300, 500), dev)
     for c, rec in curve.items():
         g = rec["gpu"]
-        assert g["x"] < TOL, (c, rec)
-        assert g["F_trial"] < _bound(TOL, rec, "F_trial", curve), (c, rec)
-        assert g["v"] < _bound(2e-3, rec, "v", curve) and g["C"] < _bound(5e-3, rec, "C", curve), (c, rec)
-        assert g["yield"] < _bound(5e-3, rec, "yield", curve), (c, rec)
+        assert g["x"] < TOL and g["x_elem"] < TOL, (c, rec)
+        assert g["F_trial"] < _bound(TOL, rec, "F_trial", curve, c), (c, rec)
+        assert g["v"] < _bound(2e-3, rec, "v", curve, c) and g["C"] < _bound(5e-3, rec, "C", curve, c), (c, rec)
+        assert g["yield"] < _bound(5e-3, rec, "yield", curve, c), (c, rec)
     assert post["gpu"]["cov"] < _bound(TOL, post, "cov") and post["gpu"]["R"] < _bound(TOL, post, "R"), post
     _dump("long_config_C_metal_500", {"config": "lego-fracture.json", "material": "metal", "N": len(prob["x"]),
                                       "n_grid": 128, "curve": curve, "post": post})
@@ -187,22 +188,35 @@ def test_sand_foam_full_size(dev, material):
     """The Drucker-Prager sand return map (constitutive_models.py:105-140) and
     the viscoplastic foam one (216-259, the element-wise product of F13) on
     lego.json's scene at 100k / 128^3, 100 substeps, against the oracle and
-    its permuted-order spread.  Foam at this size is ill-conditioned in the
-    reference itself: F13's U * diag * V^T is not a deformation gradient, and
-    the oracle run on a permuted particle order moves F_trial by O(1) and x by
-    ~1e-3 within 50 substeps -- so foam is held to the spread (GPU within 4x
-    the reference's own nondeterminism) on every field, x included."""
+    its permuted-order spread.  Sand: x within 1e-4 (max and per element),
+    stress-bearing fields within max(bound, 2 x spread).
+
+    Foam: NO PARITY POSSIBLE (the reference is ill-conditioned).  F13's
+    U * diag * V^T is not a deformation gradient, and the oracle itself, run
+    on a permuted particle order (another valid f32 evaluation of the same
+    P2G sums), moves F_trial by O(1) and x by ~1e-3 within 50 substeps: no
+    implementation, the reference's own included, can meet north_star's 1e-4
+    on it.  What this case checks is only consistency: every GPU field,
+    x and R included, within 2x the reference's own nondeterminism.  It is
+    recorded as "parity": "none possible" and not counted as parity."""
     prob = lego_problem(100_000, 128)
     curve, post = _horizon(prob, material, (10, 50, 100), dev)
     foam = material == "foam"
     for c, rec in curve.items():
         g = rec["gpu"]
-        assert g["x"] < (_bound(TOL, rec, "x", curve) if foam else TOL), (c, rec)
-        assert g["F_trial"] < _bound(TOL, rec, "F_trial", curve), (c, rec)
-        assert g["v"] < _bound(2e-3, rec, "v", curve) and g["C"] < _bound(5e-3, rec, "C", curve), (c, rec)
+        if foam:
+            assert g["x"] < _bound(TOL, rec, "x", curve, c), (c, rec)
+        else:
+            assert g["x"] < TOL and g["x_elem"] < TOL, (c, rec)
+        assert g["F_trial"] < _bound(TOL, rec, "F_trial", curve, c), (c, rec)
+        assert g["v"] < _bound(2e-3, rec, "v", curve, c) and g["C"] < _bound(5e-3, rec, "C", curve, c), (c, rec)
     assert post["gpu"]["cov"] < _bound(TOL, post, "cov"), post
+    if foam:
+        assert post["gpu"]["R"] < _bound(TOL, post, "R"), post
     _dump(f"full_size_{material}_100", {"config": "lego.json", "material": material, "N": len(prob["x"]),
-                                        "n_grid": 128, "curve": curve, "post": post})
+                                        "n_grid": 128, "curve": curve, "post": post,
+                                        "parity": "none possible (reference ill-conditioned: the oracle's own "
+                                                  "reordered runs differ by O(1))" if foam else "spread-bounded"})
 
 
 @pytest.mark.parametrize("lift", [False, True])
@@ -272,7 +286,8 @@ def test_lego_impulse_window_at_substep_8001(dev, lift):
         ctrl = rel_err(ref.v, ctl.v)
         rec[c] = {"gpu": g, "oracle_vs_no_impulse_v": ctrl, "in_impulse_box": in_box}
         print(c, {k: f"{v:.2e}" for k, v in g.items()}, "no-impulse v", f"{ctrl:.2e}", "in box", in_box)
-        assert g["x"] < TOL and g["F_trial"] < TOL and g["v"] < 2e-3 and g["C"] < 5e-3, (c, g)
+        assert g["x"] < TOL and g["x_elem"] < TOL and g["F_trial"] < TOL, (c, g)
+        assert g["v"] < TOL_V_FREE and g["C"] < TOL_C_FREE, (c, g)
         if c == 8000:  # particles inside the impulse box when it fires (boundary_conditions.py:41-45, f32)
             bc = imps[0].d
             ctr, half = np.asarray(bc["center"], np.float32), np.asarray(bc["size"], np.float32)
@@ -289,21 +304,19 @@ def test_lego_impulse_window_at_substep_8001(dev, lift):
            "curve": rec})
 
 
-# the scene's footprint at this camera spans tiles x ~125-175, y ~80-134: the centre, two
-# corners of the footprint (partly covered tiles), and the image's partial last tiles
-@pytest.mark.parametrize("crop", [(140, 95, 172, 115), (118, 74, 134, 90), (166, 122, 182, 140),
-                                  (300, 200, 310, 206)])
-def test_config_D_bicycle_render_crops(dev, crop):
+def test_config_D_bicycle_render_full_frame(dev):
     """configs[3]'s render: 1M synthetic Gaussians of the bicycle scene at the
     bicycle camera (models/bicycle/cameras.json record 0: 4946 x 3286,
-    63,860 tiles -- the > 4,096-tile sort path), HIP vs the oracle: num_rendered
-    and every radius exact, pixels of the cropped tiles within 1e-3 but for
-    alpha cut-off flips: a Gaussian whose alpha lands within an ulp of 1/255
-    at a pixel is blended on one side and skipped on the other (the kernel's
-    hardware exp2 vs the oracle's expf -- upstream's __expf would flip such
+    63,860 tiles -- the > 4,096-tile sort path), HIP vs the OpenMP build of
+    the oracle rasterizer over the WHOLE frame (every tile's list built,
+    sorted and blended; oracle/raster_oracle.c, 48.8M pixel values):
+    num_rendered and every radius exact, pixels within 1e-3 but for alpha
+    cut-off flips -- a Gaussian whose alpha lands within an ulp of 1/255 at a
+    pixel is blended on one side and skipped on the other (the kernel's
+    hardware exp2 vs the oracle's expf; upstream's __expf would flip such
     pixels against the oracle too), moving that pixel by at most alpha T rgb
-    <= 1/255 plus the change of T: at most 1e-4 of the pixels may exceed
-    1e-3, none 5e-3."""
+    <= 1/255 plus the change of T: at most 1e-4 of the pixel values may
+    exceed 1e-3, none 5e-3."""
     import oracle as O
     import torch
     import main as drv
@@ -332,19 +345,17 @@ def test_config_D_bicycle_render_crops(dev, crop):
     K, color, radii = raster.forward(t(means), t(opa), t(view), t(full), t(campos), t(bg), cam.height, cam.width,
                                      tx, ty, sh_degree=3, shs=t(shs), cov3D_precomp=t(covs))
     oc, orad, oK, _, _ = O.raster_forward(means, opa, view, full, campos, bg, cam.width, cam.height, tx, ty,
-                                          shs=shs, sh_degree=3, cov3D_precomp=covs, crop_tiles=crop)
+                                          shs=shs, sh_degree=3, cov3D_precomp=covs, threaded=True)
     assert K == oK and K > 10_000_000, (K, oK)
     assert np.array_equal(radii.cpu().numpy(), orad)
-    y0, y1 = crop[1] * 16, min(cam.height, crop[3] * 16)
-    x0, x1 = crop[0] * 16, min(cam.width, crop[2] * 16)
-    got = color[:, y0:y1, x0:x1].cpu().numpy()
-    exp = oc[:, y0:y1, x0:x1]
-    err = np.abs(got - exp)
-    rec = {"crop_tiles": list(crop), "pixels": int(err.size), "num_rendered": int(K),
-           "pixel_max_err": float(err.max()), "pixels_over_1e-3": int((err > 1e-3).sum()),
-           "pixel_mean": float(exp.mean())}
+    got = color.cpu().numpy()
+    err = np.abs(got - oc)
+    covered = oc.max(0) > 0  # pixels some Gaussian reached (the background is black)
+    rec = {"frame": [cam.width, cam.height], "pixel_values": int(err.size), "num_rendered": int(K),
+           "pixels_covered": int(covered.sum()), "pixel_max_err": float(err.max()),
+           "pixel_values_over_1e-3": int((err > 1e-3).sum()), "pixel_values_over_1e-4": int((err > 1e-4).sum()),
+           "pixel_mean": float(oc.mean())}
     print(rec)
-    if crop[0] < 200:
-        assert exp.mean() > 0.01  # the footprint crops hold Gaussians
-    assert rec["pixels_over_1e-3"] <= 1e-4 * err.size and err.max() < 5e-3, rec
-    _dump("D_bicycle_render_crop_" + "_".join(map(str, crop)), rec)
+    assert rec["pixels_covered"] > 0.05 * cam.width * cam.height, rec  # the frame holds the scene
+    assert rec["pixel_values_over_1e-3"] <= 1e-4 * err.size and err.max() < 5e-3, rec
+    _dump("D_bicycle_render_full_frame", rec)

@@ -191,6 +191,63 @@ def test_gpu_slab_error_stops_every_rank(dev, tmp_path):
     assert int(migs) <= STEPS // 10, migs  # errors surface at the end of the step call, on every rank
 
 
+IMPULSE = ([1.0, 1.0, 0.8], [0.4, 0.4, 0.4], [0.0, 300.0, 0.0])  # center, half-size, force (grid units)
+IMP_ON = range(10, 20)  # substeps of the one 100-substep call on which it fires
+
+
+def _impulse_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(shared_gpu_rccl_env(rank))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    try:
+        from gsmpm.dist import SlabDomain, make_transport
+        x, v, cov, vol = scene()
+        xp = make_transport(rank, world, device=dev)
+        dom = SlabDomain(x, cov, vol, v=v, rank=rank, world=world, transport=xp, n_grid=NG, grid_extent=EXT,
+                         margin=2, interval=10, device=dev, jelly_fcr=True, **KW)
+        dom.add_fixed_cube(*FIXED)
+        dom.add_plane_collider([0, 0, 0.4], [0, 0, 1])
+        b = dom.add_impulse(*IMPULSE, DT)
+        dom.step(DT, [0b11 | ((1 << b) if s in IMP_ON else 0) for s in range(100)])
+        got = {k: dom.gather_field(k) for k in ("x", "v", "F_trial")}
+        rects = np.array(dom.engine.slab_rects(), np.int64).reshape(-1)
+        if rank == 0:
+            np.savez(os.path.join(out, "imp.npz"), rects=rects, **{k: g.cpu().numpy() for k, g in got.items()})
+        dom.engine.close()
+        xp.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gpu_slabs_impulse_mid_call(dev, tmp_path):
+    """window rects are agreed once per step call, so velocity an
+    impulse adds DURING the call must be inside the rect's widening.  Two
+    RCCL ranks on cuda:0, ONE call of 100 substeps, an impulse kicking the
+    middle of the scene along +y on substeps 10-19 (boundary_conditions.py:
+    41-45): the kicked particles travel ~10+ cells in y across the window
+    planes before the call ends -- further than the rect's velocity-only
+    widening (interval + 1 = 11 cells) covers.  The call must complete (no
+    GSMPM_ESTATE "outside the exchanged rect") and match the oracle."""
+    import oracle as O
+    world = 2
+    mp.spawn(_impulse_worker, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
+    r = np.load(os.path.join(tmp_path, "imp.npz"))
+    x, v, cov, vol = scene()
+    ref = O.OracleMPM(x, cov, vol, v=v, n_grid=NG, grid_extent=EXT, jelly_quirk=False, **KW)
+    ref.add_fixed_box(*FIXED)
+    ref.add_collider([0, 0, 0.4], [0, 0, 1])
+    ref.add_impulse(*IMPULSE, DT)
+    for s in range(100):
+        ref.substep(DT, imp_active=[1 if s in IMP_ON else 0], op_active=[1, 1])
+    moved_y = float(np.abs(ref.x[:, 1] - x[:, 1]).max() * NG / EXT)
+    assert moved_y > 11, moved_y  # the kick carried particles past the velocity-only widening
+    errs = {k: rel_err(r[k], getattr(ref, k)) for k in ("x", "v", "F_trial")}
+    print("impulse mid-call", errs, "moved cells y", moved_y, "rects", r["rects"].tolist())
+    assert errs["x"] < 1e-4 and errs["F_trial"] < 1e-4 and errs["v"] < TOL["v"], errs
+
+
 def _bicycle_worker(rank, world, port, out, steps, calls):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     os.environ.update(shared_gpu_rccl_env(rank))
@@ -230,22 +287,26 @@ def _bicycle_worker(rank, world, port, out, steps, calls):
 BICYCLE_V0 = (2.0, 0.0, 0.0)  # +x drift (grid units / s) so particles cross the slab plane and migrate
 
 
-def test_gpu_slabs_bicycle_two_ranks_rccl(dev, tmp_path):
+@pytest.mark.parametrize("world", [2, 8])
+def test_gpu_slabs_bicycle_rccl(dev, tmp_path, world):
     """configs[3]'s workload through the slab path: bicycle.json, 1M Gaussians
-    in [0.05, 0.95]^3, 256^3, two RCCL slab ranks (sharing cuda:0), 50
-    substeps in 5 step calls with a migration every 10 substeps (an initial
-    +x drift makes ~1% of the particles cross the slab plane), against the
-    single-domain OpenMP oracle: x, F_trial, cov within 1e-4.  Each step call
-    is one captured graph with the counts kept on the device: the library
-    syncs the host once per call (the record check), +1 on the first call."""
+    in [0.05, 0.95]^3, 256^3, `world` RCCL slab ranks sharing cuda:0 (8: the
+    config's own "shard across 8 MI355X", here 8 processes on one device over
+    RCCL's socket transport), 50 substeps in 5 step calls with a migration
+    every 10 substeps (an initial +x drift makes particles cross every slab
+    plane), against the single-domain OpenMP oracle: x, F_trial, cov within
+    1e-4.  Each step call is one captured graph with the counts kept on the
+    device: the library syncs the host once per call (the record check), +1
+    on the first call, on every rank."""
     import oracle as O
     from scenarios import lego_problem
-    steps, calls, world = 50, 5, 2
+    steps, calls = 50, 5
     mp.spawn(_bicycle_worker, args=(world, free_port(), str(tmp_path), steps, calls), nprocs=world, join=True)
     r = np.load(os.path.join(tmp_path, "bicycle.npz"))
-    assert int(r["migrated"]) > 1000, int(r["migrated"])
+    assert int(r["migrated"]) > 1000 * (world - 1), int(r["migrated"])
     assert int(r["calls"]) == world * calls
     assert int(r["host_syncs"]) == world * (calls + 1), (int(r["host_syncs"]), world * (calls + 1))
+    assert len(r["bounds"]) == world + 1
     prob = lego_problem(1_000_000, 256, config="bicycle.json")
     cfg = prob["cfg"]
     v = np.tile(np.array(BICYCLE_V0, np.float32), (len(prob["x"]), 1))
@@ -257,6 +318,10 @@ def test_gpu_slabs_bicycle_two_ranks_rccl(dev, tmp_path):
         ref.substep(cfg["substep_dt"], [], [1])
     ref.postprocess()
     errs = {"x": rel_err(r["x"], ref.x), "F_trial": rel_err(r["F_trial"], ref.F_trial), "cov": rel_err(r["cov"], ref.cov)}
-    print("bicycle slab2", errs, "migrated", int(r["migrated"]), "bounds", r["bounds"].tolist())
+    rec = {"world": world, "errs": errs, "migrated": int(r["migrated"]), "bounds": r["bounds"].tolist(),
+           "host_syncs": int(r["host_syncs"]), "calls": int(r["calls"])}
+    print(f"bicycle slab{world}", rec)
+    from test_gpu_configs import _dump
+    _dump(f"D_bicycle_slab{world}_rccl", rec)
     for k, e in errs.items():
         assert e < 1e-4, (k, e, errs)
