@@ -306,18 +306,19 @@ __device__ __forceinline__ void reach_cells(float lo, float hi, int c0, int c1, 
   last = a - 1;
 }
 
-__global__ __launch_bounds__(256) void k_preprocess(RasterDev a, int* __restrict__ radii, float* __restrict__ depth,
-                                                    float2* __restrict__ xy, float4* __restrict__ conic_o,
-                                                    float4* __restrict__ rgbo, unsigned long long* __restrict__ tiles,
-                                                    uint2* __restrict__ rect) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= a.P) return;
+#include "dsort.h"
+
+// returns the depth bits of a visible Gaussian (tiles word != 0), else 0
+__device__ __forceinline__ unsigned preprocess_one(const RasterDev& a, int idx, int* __restrict__ radii,
+                                                   float* __restrict__ depth, float2* __restrict__ xy,
+                                                   float4* __restrict__ conic_o, float4* __restrict__ rgbo,
+                                                   unsigned long long* __restrict__ tiles, uint2* __restrict__ rect) {
   radii[idx] = 0;
   tiles[idx] = 0;  // (3-sigma tile count << 32) | binned tile count
   const float* p = a.means3D + (size_t)idx * 3;
   float pv[3];
   xform4x3(p, a.viewmatrix, pv);
-  if (pv[2] <= 0.2f) return;
+  if (pv[2] <= 0.2f) return 0u;
   const float* pm = a.projmatrix;
   const float hx = pm[0] * p[0] + pm[4] * p[1] + pm[8] * p[2] + pm[12];
   const float hy = pm[1] * p[0] + pm[5] * p[1] + pm[9] * p[2] + pm[13];
@@ -335,7 +336,7 @@ __global__ __launch_bounds__(256) void k_preprocess(RasterDev a, int* __restrict
   float cv[3];
   cov2d(p, a, c3, cv);
   const float det = cv[0] * cv[2] - cv[1] * cv[1];
-  if (det == 0.0f) return;
+  if (det == 0.0f) return 0u;
   const float di = 1.f / det;
   const float mid = 0.5f * (cv[0] + cv[2]);
   const float l1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
@@ -344,7 +345,7 @@ __global__ __launch_bounds__(256) void k_preprocess(RasterDev a, int* __restrict
   const float px = ndc2pix(ppx, a.W), py = ndc2pix(ppy, a.H);
   int rmin[2], rmax[2];
   get_rect(px, py, rad, a.grid_x, a.grid_y, rmin, rmax);
-  if ((rmax[0] - rmin[0]) * (rmax[1] - rmin[1]) == 0) return;
+  if ((rmax[0] - rmin[0]) * (rmax[1] - rmin[1]) == 0) return 0u;
   float rgb[3];
   unsigned clamp = 0;
   if (a.colors_precomp) {
@@ -380,6 +381,17 @@ __global__ __launch_bounds__(256) void k_preprocess(RasterDev a, int* __restrict
   }
   rect[idx] = pack_rect(t0[0], t0[1], t1[0], t1[1]);
   tiles[idx] = ((unsigned long long)full << 32) | (unsigned)((t1[0] - t0[0]) * (t1[1] - t0[1]));
+  return __float_as_uint(pv[2]);
+}
+// dst (optional): the depth order's min / max shards (dsort.h)
+__global__ __launch_bounds__(256) void k_preprocess(RasterDev a, int* __restrict__ radii, float* __restrict__ depth,
+                                                    float2* __restrict__ xy, float4* __restrict__ conic_o,
+                                                    float4* __restrict__ rgbo, unsigned long long* __restrict__ tiles,
+                                                    uint2* __restrict__ rect, unsigned* __restrict__ dst) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  unsigned bits = 0u;
+  if (idx < a.P) bits = preprocess_one(a, idx, radii, depth, xy, conic_o, rgbo, tiles, rect);
+  if (dst) ds_minmax(dst, bits != 0u, bits);  // every lane of the wave: a shuffle reduction
 }
 
 __global__ __launch_bounds__(256) void k_duplicate(int P, const uint2* __restrict__ rect, const float* __restrict__ depth,
@@ -752,9 +764,12 @@ __global__ __launch_bounds__(256) void k_render4(const uint2* __restrict__ range
 }
 
 constexpr unsigned kNoCount = 0xffffffffu;
-// dst[1] = the 3-sigma pair count (num_rendered), then dst[0] = the binned count K (the host spins on it)
-__global__ void k_publish_count(const unsigned long long* __restrict__ src, unsigned* dst) {
+// dst[1] = the 3-sigma pair count (num_rendered), dst[2] = the depth order's
+// overflow flag (dsort.h; null: 0), then dst[0] = the binned count K (the host spins on it)
+__global__ void k_publish_count(const unsigned long long* __restrict__ src, const unsigned* __restrict__ over,
+                                unsigned* dst) {
   const unsigned long long v = *src;
+  __hip_atomic_store(dst + 2, over ? *over : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(dst + 1, (unsigned)(v >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(dst, (unsigned)v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -964,10 +979,38 @@ __global__ __launch_bounds__(kSortT) void k_tile_hist(int K, int ntiles, int nch
   __syncthreads();
   for (int t = threadIdx.x; t <= ntiles; t += kSortT) H[(size_t)t * nch + c] = s_h[t];
 }
+// The chunk histograms' positions, without a device-wide scan: a wave per
+// tile row (H is tile-major, [tile][chunk]) writes the row's exclusive prefix
+// (the chunk's offset inside the tile's run) into Hs and the row total into
+// tot[tile]; k_tile_scatter's workgroups each scan the <= 4,097 totals in LDS
+// (redundantly: cheaper than one more launch and a look-back chain).
+__global__ __launch_bounds__(256) void k_tile_rows(int ntiles, int nch, const unsigned* __restrict__ H,
+                                                   unsigned* __restrict__ Hs, unsigned* __restrict__ tot) {
+  const int t = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (t > ntiles) return;  // wave-uniform
+  const unsigned* h = H + (size_t)t * nch;
+  unsigned* o = Hs + (size_t)t * nch;
+  unsigned carry = 0;
+  for (int c0 = 0; c0 < nch; c0 += 64) {
+    const int c = c0 + lane;
+    const unsigned v = c < nch ? h[c] : 0u;
+    unsigned inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const unsigned u = (unsigned)__shfl_up((int)inc, d);
+      if (lane >= d) inc += u;
+    }
+    if (c < nch) o[c] = carry + inc - v;
+    carry += (unsigned)__shfl((int)inc, 63);
+  }
+  if (lane == 0) tot[t] = carry;
+}
+
 __global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int nch, int bits,
                                                          const unsigned* __restrict__ keys,
                                                          const unsigned* __restrict__ vals,
                                                          const unsigned* __restrict__ Hs,
+                                                         const unsigned* __restrict__ tot,
                                                          unsigned* __restrict__ keys_out, unsigned* __restrict__ vals_out,
                                                          uint2* __restrict__ ranges, int* __restrict__ dsort_counts) {
   using BRS = rocprim::block_radix_sort<unsigned, kSortT, kSortI, unsigned>;
@@ -975,7 +1018,29 @@ __global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int 
   __shared__ typename BRS::storage_type s_sort;
   __shared__ unsigned s_k[kChunk], s_v[kChunk];
   __shared__ int s_start[kMaxTiles + 1];
+  __shared__ unsigned s_ts[kMaxTiles + 2];  // exclusive scan of the tile totals: each tile's run start
+  __shared__ unsigned s_part[kSortT];
   const int c = blockIdx.x;
+  {
+    const int per = (ntiles + 1 + kSortT - 1) / kSortT, t0 = threadIdx.x * per;
+    unsigned sum = 0;
+    for (int q = 0; q < per; ++q) sum += t0 + q <= ntiles ? tot[t0 + q] : 0u;
+    s_part[threadIdx.x] = sum;
+    __syncthreads();
+    for (int o = 1; o < kSortT; o <<= 1) {
+      const unsigned u = threadIdx.x >= (unsigned)o ? s_part[threadIdx.x - o] : 0u;
+      __syncthreads();
+      s_part[threadIdx.x] += u;
+      __syncthreads();
+    }
+    unsigned run = s_part[threadIdx.x] - sum;
+    for (int q = 0; q < per; ++q)
+      if (t0 + q <= ntiles) {
+        s_ts[t0 + q] = run;
+        run += tot[t0 + q];
+      }
+    if (threadIdx.x == kSortT - 1) s_ts[ntiles + 1] = run;
+  }
   const unsigned lowmask = (1u << bits) - 1u;  // >= ntiles
   unsigned k[kSortI], v[kSortI];
 #pragma unroll
@@ -1001,13 +1066,12 @@ __global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int 
     const unsigned vv = s_v[sp];
     if (vv == kNoEntry) continue;
     const unsigned kk = s_k[sp], t = sort_tile(kk, lowmask, ntiles);
-    const unsigned pos = Hs[(size_t)t * nch + c] + (unsigned)(sp - s_start[t]);
+    const unsigned pos = s_ts[t] + Hs[(size_t)t * nch + c] + (unsigned)(sp - s_start[t]);
     keys_out[pos] = kk;
     vals_out[pos] = vv;
   }
   if (c == 0)
-    for (int tt = threadIdx.x; tt < ntiles; tt += kSortT)
-      ranges[tt] = make_uint2(Hs[(size_t)tt * nch], Hs[(size_t)(tt + 1) * nch]);
+    for (int tt = threadIdx.x; tt < ntiles; tt += kSortT) ranges[tt] = make_uint2(s_ts[tt], s_ts[tt + 1]);
 }
 
 // Per-tile depth order (chunked path, opt-in with GSMPM_RASTER_TILE_DSORT=1; off by
@@ -1689,7 +1753,14 @@ struct gsmpm_raster {
   size_t capT = 0;
   uint2* ranges = nullptr;
   int* dsort_tl = nullptr;  // [2 + 2 * capT] k_tile_dsort's size-class lists
-  unsigned* h_count = nullptr;  // [2] pinned, mapped + coherent (the device writes K, num_rendered into it)
+  unsigned* h_count = nullptr;  // [4] pinned, mapped + coherent (the device writes K, num_rendered, overflow into it)
+  // the hand-written depth order (dsort.h): state + bucket arrays (fixed size), per-Gaussian runs
+  char* ds_state = nullptr;    // kDsStateBytes, zero when idle
+  unsigned *ds_bbase = nullptr, *ds_bcur = nullptr, *ds_blist = nullptr, *ds_bbig = nullptr;  // [kDsNBMax]
+  unsigned long long* ds_bpre = nullptr;  // [kDsNBMax]
+  unsigned *ds_key = nullptr, *ds_val = nullptr;  // [capP]
+  unsigned* ttot = nullptr;    // [capT + 2] chunked tile sort: tile totals (k_tile_rows)
+  long dsort_fallbacks = 0;    // forwards whose depth order fell back to the library sort
   hipEvent_t count_ev = nullptr;  // recorded after k_publish_count: surfaces a fault while the host spins
   // per pixel (backward)
   size_t capPix = 0;
@@ -1700,7 +1771,34 @@ struct gsmpm_raster {
   unsigned K = 0, K_full = 0;  // binned pairs, num_rendered
   bool forward_only = false;  // gsmpm_raster_set_forward_only: no per-pixel state for a backward
   bool has_pixel_state = false;
+  // caller-owned workspace (gsmpm_raster_forward_ws): every buffer is carved
+  // from it, nothing is allocated; the pair-dependent part is carved once the
+  // pair count is known (ws_carve_pairs), or the call fails with GSMPM_ESPACE
+  char* ws = nullptr;
+  size_t ws_bytes = 0, ws_pre = 0;  // workspace size, bytes of the pair-independent part
+  int64_t pairs_needed = 0;
 };
+
+static DsortBufs dsort_bufs(gsmpm_raster* r) {
+  DsortBufs d;
+  d.st = reinterpret_cast<unsigned*>(r->ds_state);
+  d.bcount = d.st ? d.st + kDsWords : nullptr;
+  d.bsum = d.st ? reinterpret_cast<unsigned long long*>(d.bcount + kDsNBMax) : nullptr;
+  d.bbase = r->ds_bbase;
+  d.bcur = r->ds_bcur;
+  d.bpre = r->ds_bpre;
+  d.blist = r->ds_blist;
+  d.bbig = r->ds_bbig;
+  d.dkey = r->ds_key;
+  d.dval = r->ds_val;
+  return d;
+}
+// buckets of the depth order: a power of two, ~8 visible Gaussians a bucket, in [1024, kDsNBMax]
+static int dsort_buckets(int P) {
+  int nb = 1024;
+  while (nb < kDsNBMax && nb * 8 < P) nb <<= 1;
+  return nb;
+}
 
 static int grow(void** p, size_t bytes) {
   if (*p) (void)hipFree(*p);
@@ -1709,16 +1807,128 @@ static int grow(void** p, size_t bytes) {
   return GSMPM_OK;
 }
 
+// ---- caller-owned workspace ----
+// Layout: the pair-independent buffers (per Gaussian, per tile, the device
+// scan / depth-sort temporaries), then the pair buffers for `pairs` binned
+// pairs (keys, values, emission starts, chunk histograms, the tile-sort
+// temporary: the largest any binning path takes), each 256-B aligned.  A
+// walk over the buffers in a fixed order gives both the size and, with a
+// base, the pointers.
+struct WsWalk {
+  char* base;
+  size_t off = 0;
+  template <class T>
+  void take(T*& p, size_t bytes) {
+    off = (off + 255) & ~size_t(255);
+    if (base) p = reinterpret_cast<T*>(base + off);
+    off += std::max<size_t>(bytes, 16);
+  }
+};
+static int ws_pre_walk(WsWalk& w, gsmpm_raster* r, size_t P, size_t ntiles) {
+  const size_t cap = std::max<size_t>(P, 1);
+  size_t dbytes = 0, obytes = 0, sbytes = 0, gbytes = 0, ibytes = 0;
+  GSMPM_HIP(rocprim::radix_sort_pairs(nullptr, dbytes, reinterpret_cast<unsigned*>(r->depth), r->dsorted,
+                                      rocprim::counting_iterator<unsigned>(0u), r->dorder, cap, 0, 32, hipStream_t(0)));
+  if (kDepthOnesweepMin > 0 && cap >= kDepthOnesweepMin)
+    GSMPM_HIP(rocprim::radix_sort_pairs<OnesweepSort>(nullptr, obytes, reinterpret_cast<unsigned*>(r->depth),
+                                                      r->dsorted, rocprim::counting_iterator<unsigned>(0u), r->dorder,
+                                                      cap, 0, 32, hipStream_t(0)));
+  GSMPM_HIP(rocprim::inclusive_scan(nullptr, sbytes, binned_tiles(r->tiles), r->offsets, cap,
+                                    rocprim::plus<unsigned>(), hipStream_t(0)));
+  GSMPM_HIP(rocprim::inclusive_scan(nullptr, gbytes, ranked_tiles(r->dorder, r->tiles), r->offr, cap,
+                                    rocprim::plus<unsigned long long>(), hipStream_t(0)));
+  GSMPM_HIP(rocprim::inclusive_scan(nullptr, ibytes, r->tiles, r->offr, cap, rocprim::plus<unsigned long long>(),
+                                    hipStream_t(0)));
+  r->dsort_tmp_bytes = std::max(dbytes, obytes);
+  r->scan_tmp_bytes = std::max(sbytes, std::max(gbytes, ibytes));
+  w.take(r->ds_state, kDsStateBytes);  // first, at a fixed offset: zero when idle (the caller zero-fills once)
+  w.take(r->ds_bbase, kDsNBMax * sizeof(unsigned));
+  w.take(r->ds_bcur, kDsNBMax * sizeof(unsigned));
+  w.take(r->ds_blist, kDsNBMax * sizeof(unsigned));
+  w.take(r->ds_bbig, kDsNBMax * sizeof(unsigned));
+  w.take(r->ds_bpre, kDsNBMax * sizeof(unsigned long long));
+  w.take(r->ds_key, cap * sizeof(unsigned));
+  w.take(r->ds_val, cap * sizeof(unsigned));
+  w.take(r->ttot, (ntiles + 2) * sizeof(unsigned));
+  w.take(r->depth, cap * sizeof(float));
+  w.take(r->xy, cap * sizeof(float2));
+  w.take(r->conic, cap * sizeof(float4));
+  w.take(r->rgb, cap * sizeof(float4));
+  w.take(r->tiles, cap * sizeof(unsigned long long));
+  w.take(r->rect, cap * sizeof(uint2));
+  w.take(r->offsets, cap * sizeof(unsigned));
+  w.take(r->dorder, cap * sizeof(unsigned));
+  w.take(r->dsorted, cap * sizeof(unsigned));
+  w.take(r->offr, cap * sizeof(unsigned long long));
+  w.take(r->dsort_tmp, r->dsort_tmp_bytes);
+  w.take(r->scan_tmp, r->scan_tmp_bytes);
+  w.take(r->ranges, ntiles * sizeof(uint2));
+  w.take(r->dsort_tl, (2 + 2 * ntiles) * sizeof(int));
+  r->capP = cap;
+  r->capT = ntiles;
+  return GSMPM_OK;
+}
+static int ws_pairs_walk(WsWalk& w, gsmpm_raster* r, size_t K, size_t ntiles) {
+  const size_t cap = std::max<size_t>(K, 1);
+  const int bits = msb_bits((unsigned)ntiles);
+  const size_t nch = div_up(cap, (size_t)kChunk);
+  const size_t capH = std::max((ntiles + 1) * nch, 256 * nch);
+  size_t b[4] = {0, 0, 0, 0};
+  GSMPM_HIP(rocprim::radix_sort_pairs(nullptr, b[0], r->keys, r->keys_sorted, rocprim::counting_iterator<unsigned>(0u),
+                                      r->vals_sorted, cap, 0, 64, hipStream_t(0)));
+  GSMPM_HIP(rocprim::radix_sort_pairs<OnesweepSort>(nullptr, b[1], reinterpret_cast<unsigned*>(r->keys),
+                                                    reinterpret_cast<unsigned*>(r->keys_sorted), r->vals,
+                                                    r->ids_sorted, cap, 0, bits, hipStream_t(0)));
+  GSMPM_HIP(rocprim::exclusive_scan(nullptr, b[2], r->hist, r->hist + capH, 0u, capH, rocprim::plus<unsigned>(),
+                                    hipStream_t(0)));
+  r->sort_tmp_bytes = std::max(std::max(b[0], b[1]), b[2]);
+  w.take(r->keys, cap * 8);
+  w.take(r->keys_sorted, cap * 8);
+  w.take(r->vals, cap * 4);
+  w.take(r->vals_sorted, cap * 4);
+  w.take(r->ids_sorted, cap * 4);
+  w.take(r->estart, (cap / kEmitT + 2) * 4);
+  w.take(r->hist, 2 * capH * sizeof(unsigned));
+  w.take(r->sort_tmp, r->sort_tmp_bytes);
+  r->capK = cap;
+  r->capH = capH;
+  return GSMPM_OK;
+}
+// carve the pair buffers for K pairs from r's workspace, or GSMPM_ESPACE (pairs_needed = K)
+static int ws_carve_pairs(gsmpm_raster* r, size_t K, size_t ntiles) {
+  WsWalk probe{nullptr, r->ws_pre};
+  gsmpm_raster tmp;
+  int rc = ws_pairs_walk(probe, &tmp, K, ntiles);
+  if (rc) return rc;
+  if (probe.off > r->ws_bytes) {
+    r->pairs_needed = (int64_t)K;
+    set_error("gsmpm_raster_forward_ws: the workspace holds too few pairs for this frame (" + std::to_string(K) +
+              " binned pairs need " + std::to_string(probe.off) + " bytes, the workspace has " +
+              std::to_string(r->ws_bytes) + "); grow it (gsmpm_raster_workspace_size) and call again");
+    return GSMPM_ESPACE;
+  }
+  WsWalk w{r->ws, r->ws_pre};
+  return ws_pairs_walk(w, r, K, ntiles);
+}
+
 extern "C" {
 
 int gsmpm_raster_create(gsmpm_raster** out) {
   GSMPM_REQUIRE(out, "gsmpm_raster_create: null argument");
   auto* r = new gsmpm_raster();
-  hipError_t e = hipHostMalloc((void**)&r->h_count, 2 * sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent);
+  hipError_t e = hipHostMalloc((void**)&r->h_count, 4 * sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent);
   if (e == hipSuccess) e = hipEventCreateWithFlags(&r->count_ev, hipEventDisableTiming);
+  if (e == hipSuccess) e = hipMalloc((void**)&r->ds_state, kDsStateBytes);
+  if (e == hipSuccess) e = hipMemset(r->ds_state, 0, kDsStateBytes);
+  for (unsigned** q : {&r->ds_bbase, &r->ds_bcur, &r->ds_blist, &r->ds_bbig})
+    if (e == hipSuccess) e = hipMalloc((void**)q, kDsNBMax * sizeof(unsigned));
+  if (e == hipSuccess) e = hipMalloc((void**)&r->ds_bpre, kDsNBMax * sizeof(unsigned long long));
   if (e != hipSuccess) {
     if (r->h_count) (void)hipHostFree(r->h_count);
-  if (r->count_ev) (void)hipEventDestroy(r->count_ev);
+    if (r->count_ev) (void)hipEventDestroy(r->count_ev);
+    for (void* q : {(void*)r->ds_state, (void*)r->ds_bbase, (void*)r->ds_bcur, (void*)r->ds_blist, (void*)r->ds_bbig,
+                    (void*)r->ds_bpre})
+      if (q) (void)hipFree(q);
     delete r;
     set_error(std::string("hipHostMalloc: ") + hipGetErrorString(e));
     return GSMPM_EHIP;
@@ -1733,7 +1943,8 @@ int gsmpm_raster_destroy(gsmpm_raster* r) {
                   (void*)r->offsets, r->scan_tmp, (void*)r->keys, (void*)r->keys_sorted, (void*)r->vals,
                   (void*)r->vals_sorted, r->sort_tmp, (void*)r->ranges, (void*)r->ids_sorted, (void*)r->estart, (void*)r->rec,
                   (void*)r->final_T, (void*)r->n_contrib, (void*)r->dorder, (void*)r->dsorted, (void*)r->offr, r->dsort_tmp, (void*)r->hist,
-                  (void*)r->dsort_tl})
+                  (void*)r->dsort_tl, (void*)r->ds_state, (void*)r->ds_bbase, (void*)r->ds_bcur, (void*)r->ds_blist,
+                  (void*)r->ds_bbig, (void*)r->ds_bpre, (void*)r->ds_key, (void*)r->ds_val, (void*)r->ttot})
     if (p) (void)hipFree(p);
   if (r->h_count) (void)hipHostFree(r->h_count);
   if (r->count_ev) (void)hipEventDestroy(r->count_ev);
@@ -1782,7 +1993,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
   a.grid_y = (in->H + kBY - 1) / kBY;
   const int P = in->P;
   const size_t ntiles = (size_t)a.grid_x * a.grid_y;
-  if ((size_t)P > r->capP || r->capP == 0) {
+  if (!r->ws && ((size_t)P > r->capP || r->capP == 0)) {
     const size_t cap = std::max<size_t>(P, 1024);
     int rc;
     if ((rc = grow((void**)&r->depth, cap * sizeof(float)))) return rc;
@@ -1795,6 +2006,8 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     if ((rc = grow((void**)&r->dorder, cap * sizeof(unsigned)))) return rc;
     if ((rc = grow((void**)&r->dsorted, cap * sizeof(unsigned)))) return rc;
     if ((rc = grow((void**)&r->offr, cap * sizeof(unsigned long long)))) return rc;
+    if ((rc = grow((void**)&r->ds_key, cap * sizeof(unsigned)))) return rc;
+    if ((rc = grow((void**)&r->ds_val, cap * sizeof(unsigned)))) return rc;
     size_t bytes = 0, obytes = 0;
     GSMPM_HIP(rocprim::radix_sort_pairs(nullptr, bytes, reinterpret_cast<unsigned*>(r->depth), r->dsorted,
                                                       rocprim::counting_iterator<unsigned>(0u), r->dorder, cap, 0, 32,
@@ -1819,17 +2032,18 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     r->scan_tmp_bytes = bytes;
     r->capP = cap;
   }
-  if (ntiles > r->capT) {
+  if (!r->ws && ntiles > r->capT) {
     int rc;
     if ((rc = grow((void**)&r->ranges, ntiles * sizeof(uint2)))) return rc;
     if ((rc = grow((void**)&r->dsort_tl, (2 + 2 * ntiles) * sizeof(int)))) return rc;
+    if ((rc = grow((void**)&r->ttot, (2 + ntiles) * sizeof(unsigned)))) return rc;
     r->capT = ntiles;
   }
   // tile ranges: the chunked tile sort writes every tile's; the other paths
   // (and K = 0) start from empty ranges
   bool ranges_written = false;
   const size_t npix = (size_t)in->W * in->H;
-  if (npix > r->capPix) {
+  if (!r->ws && npix > r->capPix) {  // a workspace forward is forward-only: no per-pixel state
     int rc;
     if ((rc = grow((void**)&r->final_T, npix * sizeof(float)))) return rc;
     if ((rc = grow((void**)&r->n_contrib, npix * sizeof(int)))) return rc;
@@ -1859,8 +2073,14 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
   const unsigned* tkeys = nullptr;  // sorted tile keys with sub-tile masks (chunked path)
   unsigned K = 0, K_full = 0;  // binned pairs, upstream's 3-sigma pairs (num_rendered)
   if (P > 0) {
+    // GSMPM_RASTER_DSORT=lib: the library's radix sort + scan for the depth order (A/B; also the
+    // fallback when a depth bucket overflows, dsort.h)
+    const char* dl = std::getenv("GSMPM_RASTER_DSORT");
+    const bool lib_dsort = dl && dl[0] == 'l';
+    const bool own_dsort = depth_ordered && !tile_dsort && !lib_dsort;
+    const DsortBufs db = dsort_bufs(r);
     hipLaunchKernelGGL(k_preprocess, dim3(div_up(P, 256)), dim3(256), 0, st, a, out_radii, r->depth, r->xy, r->conic,
-                       r->rgb, r->tiles, r->rect);
+                       r->rgb, r->tiles, r->rect, own_dsort ? db.st : nullptr);
     GSMPM_LAUNCH_CHECK();
     size_t bytes = r->scan_tmp_bytes;
     // the index-order scan (offsets) feeds only the backward's record slots
@@ -1871,22 +2091,39 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     if (!depth_ordered || tile_dsort)  // the index-order scan of both counts (emission offsets, K)
       GSMPM_HIP(rocprim::inclusive_scan(r->scan_tmp, bytes, r->tiles, r->offr, (size_t)P,
                                         rocprim::plus<unsigned long long>(), st));
-    if (depth_ordered && !tile_dsort) {
-      // the depth order depends on P only: it runs before the count read-back,
-      // queued behind whatever the stream is still doing
-      bytes = r->dsort_tmp_bytes;
+    auto lib_depth_order = [&]() -> int {
+      size_t b2 = r->dsort_tmp_bytes;
       if (kDepthOnesweepMin > 0 && (size_t)P >= kDepthOnesweepMin)
-        GSMPM_HIP(rocprim::radix_sort_pairs<OnesweepSort>(r->dsort_tmp, bytes, reinterpret_cast<unsigned*>(r->depth),
+        GSMPM_HIP(rocprim::radix_sort_pairs<OnesweepSort>(r->dsort_tmp, b2, reinterpret_cast<unsigned*>(r->depth),
                                                           r->dsorted, rocprim::counting_iterator<unsigned>(0u),
                                                           r->dorder, (size_t)P, 0, 32, st));
       else
-        GSMPM_HIP(rocprim::radix_sort_pairs(r->dsort_tmp, bytes, reinterpret_cast<unsigned*>(r->depth),
-                                            r->dsorted, rocprim::counting_iterator<unsigned>(0u), r->dorder,
-                                            (size_t)P, 0, 32, st));
+        GSMPM_HIP(rocprim::radix_sort_pairs(r->dsort_tmp, b2, reinterpret_cast<unsigned*>(r->depth), r->dsorted,
+                                            rocprim::counting_iterator<unsigned>(0u), r->dorder, (size_t)P, 0, 32,
+                                            st));
       // the scan reads tiles[dorder[r]] itself (no separate gather launch)
-      bytes = r->scan_tmp_bytes;
-      GSMPM_HIP(rocprim::inclusive_scan(r->scan_tmp, bytes, ranked_tiles(r->dorder, r->tiles), r->offr, (size_t)P,
+      b2 = r->scan_tmp_bytes;
+      GSMPM_HIP(rocprim::inclusive_scan(r->scan_tmp, b2, ranked_tiles(r->dorder, r->tiles), r->offr, (size_t)P,
                                         rocprim::plus<unsigned long long>(), st));
+      return GSMPM_OK;
+    };
+    // the depth order depends on P only: it runs before the count read-back,
+    // queued behind whatever the stream is still doing
+    if (own_dsort) {
+      const int nb = dsort_buckets(P);
+      hipLaunchKernelGGL(k_dsort_hist, dim3(div_up(P, 256)), dim3(256), 0, st, P, nb, (const float*)r->depth,
+                         (const unsigned long long*)r->tiles, db);
+      hipLaunchKernelGGL(k_dsort_scan, dim3(1), dim3(kDsScanT), 0, st, nb, db);
+      hipLaunchKernelGGL(k_dsort_scatter, dim3(div_up(P, 256)), dim3(256), 0, st, P, (const float*)r->depth,
+                         (const unsigned long long*)r->tiles, db, r->dorder, r->offr);
+      hipLaunchKernelGGL(k_dsort_small, dim3((unsigned)std::max(1, std::min(4096, div_up(std::min(nb, P), 16)))),
+                         dim3(256), 0, st, (const unsigned long long*)r->tiles, db, r->dorder, r->offr);
+      hipLaunchKernelGGL(k_dsort_big, dim3(256), dim3(1024), 0, st, (const unsigned long long*)r->tiles, db,
+                         r->dorder, r->offr);
+      GSMPM_LAUNCH_CHECK();
+    } else if (depth_ordered && !tile_dsort) {
+      const int rc = lib_depth_order();
+      if (rc) return rc;
     }
     // K straight into pinned, coherent host memory by a one-lane kernel, and a
     // spin on it: no copy-engine packet and no sleeping stream sync between
@@ -1899,23 +2136,37 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     GSMPM_REQUIRE(cap == hipStreamCaptureStatusNone,
                   "gsmpm_raster_forward: the pair count is read on the host; the stream must not be capturing");
     volatile unsigned* hc = r->h_count;
-    *hc = kNoCount;
-    hc[1] = kNoCount;
-    hipLaunchKernelGGL(k_publish_count, dim3(1), dim3(1), 0, st, (const unsigned long long*)(r->offr + (P - 1)),
-                       r->h_count);
-    GSMPM_LAUNCH_CHECK();
-    GSMPM_HIP(hipEventRecord(r->count_ev, st));
-    for (unsigned polls = 1; *hc == kNoCount; ++polls) {
-      if ((polls & 255) == 0) {
-        const hipError_t q = hipEventQuery(r->count_ev);
-        if (q == hipSuccess) break;  // everything up to the publish finished: K is visible below
-        if (q != hipErrorNotReady) GSMPM_HIP(q);
+    auto publish = [&](const unsigned* over) -> int {
+      *hc = kNoCount;
+      hc[1] = kNoCount;
+      hc[2] = 0;
+      hipLaunchKernelGGL(k_publish_count, dim3(1), dim3(1), 0, st, (const unsigned long long*)(r->offr + (P - 1)),
+                         over, r->h_count);
+      GSMPM_LAUNCH_CHECK();
+      GSMPM_HIP(hipEventRecord(r->count_ev, st));
+      for (unsigned polls = 1; *hc == kNoCount; ++polls) {
+        if ((polls & 255) == 0) {
+          const hipError_t q = hipEventQuery(r->count_ev);
+          if (q == hipSuccess) break;  // everything up to the publish finished: K is visible below
+          if (q != hipErrorNotReady) GSMPM_HIP(q);
+        }
+        __builtin_ia32_pause();
       }
-      __builtin_ia32_pause();
+      return GSMPM_OK;
+    };
+    int rc = publish(own_dsort ? db.st + DS_OVER : nullptr);
+    if (rc) return rc;
+    if (own_dsort && hc[2]) {  // a depth bucket above kDsBig entries: the library sort instead (dsort.h)
+      r->dsort_fallbacks += 1;
+      if ((rc = lib_depth_order()) || (rc = publish(nullptr))) return rc;
     }
     K = hc[0];
     K_full = hc[1];
     GSMPM_REQUIRE(K != kNoCount && K_full != kNoCount, "gsmpm_raster_forward: the pair count never arrived");
+  }
+  if (K > 0 && r->ws) {
+    const int rc = ws_carve_pairs(r, K, ntiles);
+    if (rc) return rc;
   }
   if (K > 0) {
     if (K > r->capK) {
@@ -1963,8 +2214,6 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
           if ((rc = grow((void**)&r->hist, 2 * (nh + nh / 4 + 1024) * sizeof(unsigned)))) return rc;
           r->capH = nh + nh / 4 + 1024;
         }
-        GSMPM_HIP(rocprim::exclusive_scan(nullptr, need, r->hist, r->hist + r->capH, 0u, nh, rocprim::plus<unsigned>(),
-                                          st));
       } else {
         GSMPM_HIP(rocprim::radix_sort_pairs<OnesweepSort>(nullptr, need, tile_keys, tile_sorted, r->vals,
                                                           r->ids_sorted, (size_t)K, 0, bits, st));
@@ -1996,14 +2245,15 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       GSMPM_LAUNCH_CHECK();
       size_t bytes = r->sort_tmp_bytes;
       if (chunked) {
-        const size_t nh = (ntiles + 1) * (size_t)nch;
         unsigned* Hs = r->hist + r->capH;
         hipLaunchKernelGGL(k_tile_hist, dim3(nch), dim3(kSortT), 0, st, (int)K, (int)ntiles, nch, bits,
                            (const unsigned*)tile_keys, r->hist);
         GSMPM_LAUNCH_CHECK();
-        GSMPM_HIP(rocprim::exclusive_scan(r->sort_tmp, bytes, r->hist, Hs, 0u, nh, rocprim::plus<unsigned>(), st));
+        hipLaunchKernelGGL(k_tile_rows, dim3(div_up((long)ntiles + 1, 4)), dim3(256), 0, st, (int)ntiles, nch,
+                           (const unsigned*)r->hist, Hs, r->ttot);
         hipLaunchKernelGGL(k_tile_scatter, dim3(nch), dim3(kSortT), 0, st, (int)K, (int)ntiles, nch, bits,
-                           (const unsigned*)tile_keys, (const unsigned*)r->vals, (const unsigned*)Hs, tile_sorted,
+                           (const unsigned*)tile_keys, (const unsigned*)r->vals, (const unsigned*)Hs,
+                           (const unsigned*)r->ttot, tile_sorted,
                            r->ids_sorted, r->ranges, tile_dsort ? r->dsort_tl : nullptr);
         GSMPM_LAUNCH_CHECK();
         if (tile_dsort) {  // depth order within each tile's list (the emission keys are dead: scratch)
@@ -2176,6 +2426,68 @@ int gsmpm_raster_set_forward_only(gsmpm_raster* r, int32_t on) {
   GSMPM_REQUIRE(r, "gsmpm_raster_set_forward_only: null context");
   r->forward_only = on != 0;
   return GSMPM_OK;
+}
+
+int gsmpm_raster_workspace_size(int32_t P, int32_t H, int32_t W, int64_t pairs, uint64_t* bytes) {
+  GSMPM_REQUIRE(bytes && P >= 0 && H > 0 && W > 0 && pairs >= 0, "gsmpm_raster_workspace_size: bad argument");
+  const size_t ntiles = (size_t)div_up(W, kBX) * (size_t)div_up(H, kBY);
+  gsmpm_raster tmp;
+  WsWalk w{nullptr, 0};
+  int rc = ws_pre_walk(w, &tmp, (size_t)P, ntiles);
+  if (!rc) rc = ws_pairs_walk(w, &tmp, (size_t)pairs, ntiles);
+  if (rc) return rc;
+  *bytes = (uint64_t)w.off;
+  return GSMPM_OK;
+}
+
+// the pinned pair-count word and its event for workspace forwards: one per
+// thread and device (a workspace forward holds no context)
+struct WsCount {
+  unsigned* h = nullptr;
+  hipEvent_t ev = nullptr;
+};
+static int ws_count(WsCount*& out) {
+  static thread_local std::vector<WsCount> per_dev;
+  int dev = 0;
+  GSMPM_HIP(hipGetDevice(&dev));
+  if ((int)per_dev.size() <= dev) per_dev.resize(dev + 1);
+  WsCount& c = per_dev[dev];
+  if (!c.h) {
+    GSMPM_HIP(hipHostMalloc((void**)&c.h, 4 * sizeof(unsigned), hipHostMallocMapped | hipHostMallocCoherent));
+    GSMPM_HIP(hipEventCreateWithFlags(&c.ev, hipEventDisableTiming));
+  }
+  out = &c;
+  return GSMPM_OK;
+}
+
+int gsmpm_raster_forward_ws(const gsmpm_raster_args* a, float* out_color, int32_t* out_radii, int32_t* num_rendered,
+                            void* workspace, uint64_t ws_bytes, int64_t* pairs_needed, void* stream) {
+  GSMPM_REQUIRE(a && workspace && ((uintptr_t)workspace & 255u) == 0,
+                "gsmpm_raster_forward_ws: null argument or workspace not 256-byte aligned");
+  GSMPM_REQUIRE(a->P >= 0 && a->W > 0 && a->H > 0, "gsmpm_raster_forward_ws: bad sizes");
+  if (pairs_needed) *pairs_needed = 0;
+  WsCount* c = nullptr;
+  int rc = ws_count(c);
+  if (rc) return rc;
+  gsmpm_raster r;  // a view of the workspace: nothing in it is allocated or freed
+  r.forward_only = true;
+  r.h_count = c->h;
+  r.count_ev = c->ev;
+  r.ws = reinterpret_cast<char*>(workspace);
+  r.ws_bytes = (size_t)ws_bytes;
+  const size_t ntiles = (size_t)div_up(a->W, kBX) * (size_t)div_up(a->H, kBY);
+  WsWalk w{r.ws, 0};
+  rc = ws_pre_walk(w, &r, (size_t)a->P, ntiles);
+  if (rc) return rc;
+  r.ws_pre = w.off;
+  if (r.ws_pre > r.ws_bytes) {
+    if (pairs_needed) *pairs_needed = 0;
+    set_error("gsmpm_raster_forward_ws: the workspace is smaller than gsmpm_raster_workspace_size(P, H, W, 0)");
+    return GSMPM_ESPACE;
+  }
+  rc = gsmpm_raster_forward(&r, a, out_color, out_radii, num_rendered, stream);
+  if (rc == GSMPM_ESPACE && pairs_needed) *pairs_needed = r.pairs_needed;
+  return rc;
 }
 
 int gsmpm_raster_mark_visible(const float* means3D, int32_t P, const float* vm, const float* pm, uint8_t* vis,

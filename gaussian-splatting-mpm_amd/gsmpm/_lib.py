@@ -141,7 +141,14 @@ _SIGS = {
     "gsmpm_raster_mark_visible": (ctypes.c_int, [c_void_p, ctypes.c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gsmpm_raster_set_forward_only": (ctypes.c_int, [c_void_p, ctypes.c_int32]),
     "gsmpm_raster_pair_counts": (ctypes.c_int, [c_void_p, c_void_p, c_void_p]),
+    "gsmpm_raster_workspace_size": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
+                                                   ctypes.POINTER(ctypes.c_uint64)]),
+    "gsmpm_raster_forward_ws": (ctypes.c_int, [ctypes.POINTER(RasterArgs), c_void_p, c_void_p,
+                                               ctypes.POINTER(ctypes.c_int32), c_void_p, ctypes.c_uint64,
+                                               ctypes.POINTER(ctypes.c_int64), c_void_p]),
 }
+GSMPM_OK, GSMPM_EINVAL, GSMPM_EHIP, GSMPM_ESTATE = 0, -1, -2, -3
+ESPACE = GSMPM_ESPACE = -4  # a caller-owned workspace is too small
 
 # slab transports (include/gsmpm.h)
 XPORT_NONE, XPORT_RCCL, XPORT_CALLBACK = 0, 1, 2

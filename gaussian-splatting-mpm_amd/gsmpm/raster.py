@@ -11,25 +11,76 @@ from ._lib import LIB, check, ptr, stream_of
 _CTX = {}
 
 
-def _context(device_index: int):
-    """The shared per-device context of forwards without a backward (main.py's
-    frames): forward-only, so no per-pixel backward state is written."""
-    h = _CTX.get(device_index)
-    if h is None:
-        h = ctypes.c_void_p()
-        check(LIB.gsmpm_raster_create(ctypes.byref(h)), "gsmpm_raster_create")
-        check(LIB.gsmpm_raster_set_forward_only(h, 1), "gsmpm_raster_set_forward_only")
-        _CTX[device_index] = h
-    return h
+class SharedContext:
+    """A forward-only library-owned context (gsmpm_raster_create): its buffers
+    grow inside the library.  The default forward uses a caller-owned
+    workspace instead (Workspace); this form remains for the diagnostics
+    (pair_counts) and as the C-ABI's context entry point."""
+
+    def __init__(self):
+        self.h = ctypes.c_void_p()
+        check(LIB.gsmpm_raster_create(ctypes.byref(self.h)), "gsmpm_raster_create")
+        check(LIB.gsmpm_raster_set_forward_only(self.h, 1), "gsmpm_raster_set_forward_only")
 
 
-def pair_counts(device_index: int = 0):
-    """(binned pairs, num_rendered) of the shared context's last forward on
-    the device (diagnostics: the tight binning's pair count vs the 3-sigma one)."""
+def shared_context(device_index: int = 0) -> SharedContext:
+    c = _CTX.get(device_index)
+    if c is None:
+        c = _CTX[device_index] = SharedContext()
+    return c
+
+
+def pair_counts(context) -> tuple:
+    """(binned pairs, num_rendered) of `context`'s last forward (diagnostics:
+    the tight binning's pair count vs the 3-sigma one)."""
     b, n = ctypes.c_uint32(), ctypes.c_uint32()
-    check(LIB.gsmpm_raster_pair_counts(_context(device_index), ctypes.byref(b), ctypes.byref(n)),
-          "gsmpm_raster_pair_counts")
+    check(LIB.gsmpm_raster_pair_counts(context.h, ctypes.byref(b), ctypes.byref(n)), "gsmpm_raster_pair_counts")
     return int(b.value), int(n.value)
+
+
+class Workspace:
+    """A caller-owned rasterizer workspace: one torch byte tensor
+    (gsmpm_raster_workspace_size / gsmpm_raster_forward_ws), as upstream's
+    RasterizeGaussiansCUDA keeps its geometry / binning / image buffers in
+    torch byte tensors.  Sized for the last frame's Gaussians, image and
+    binned pairs; when a frame bins more pairs than it holds, the library
+    reports how many (GSMPM_ESPACE) and the forward is repeated once on a
+    workspace grown for 1.25x that many."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.buf = None
+        self.key = None  # (P, H, W, pairs) the buffer is sized for
+
+    def ensure(self, P, H, W, pairs):
+        if self.key is not None and self.key[0] >= P and self.key[1:3] == (H, W) and self.key[3] >= pairs:
+            return
+        if self.key is not None and self.key[1:3] == (H, W):
+            P, pairs = max(P, self.key[0]), max(pairs, self.key[3])
+        nb = ctypes.c_uint64()
+        check(LIB.gsmpm_raster_workspace_size(int(P), int(H), int(W), int(pairs), ctypes.byref(nb)),
+              "gsmpm_raster_workspace_size")
+        self.buf = None  # release before allocating the larger one
+        # zero-filled once: the library keeps its depth-order state zero between forwards (csrc/dsort.h)
+        self.buf = torch.zeros(int(nb.value) + 256, dtype=torch.uint8, device=self.device)
+        self.key = (P, H, W, pairs)
+
+    def ptr(self):
+        a = self.buf.data_ptr()
+        return (a + 255) & ~255  # 256-byte aligned start
+
+    def nbytes(self):
+        return self.buf.numel() - (self.ptr() - self.buf.data_ptr())
+
+
+_WS = {}
+
+
+def workspace(device_index: int = 0) -> Workspace:
+    w = _WS.get(device_index)
+    if w is None:
+        w = _WS[device_index] = Workspace(torch.device("cuda", device_index))
+    return w
 
 
 class RasterContext:
@@ -135,10 +186,11 @@ def backward(context, keep, a, radii, grad_color):
 
 def forward(means3D, opacities, viewmatrix, projmatrix, campos, bg, image_height, image_width, tanfovx, tanfovy,
             sh_degree=0, shs=None, colors_precomp=None, scales=None, rotations=None, cov3D_precomp=None,
-            scale_modifier=1.0, prefiltered=False, context=None, return_args=False):
+            scale_modifier=1.0, prefiltered=False, context=None, return_args=False, ws=None):
     """Returns (num_rendered, color [3,H,W], radii [P] int32) [+ (args, kept tensors)
-    when return_args].  `context` (a RasterContext) keeps this forward's state
-    for `backward`; by default a shared per-device context is used."""
+    when return_args].  `context` (a RasterContext, or a SharedContext) keeps
+    this forward's state (for `backward`, or the diagnostics); by default the
+    forward runs in the device's caller-owned Workspace (or `ws`)."""
     dev = means3D.device
     a, keep = _args(means3D, opacities, viewmatrix, projmatrix, campos, bg, image_height, image_width, tanfovx,
                     tanfovy, sh_degree, shs, colors_precomp, scales, rotations, cov3D_precomp, scale_modifier,
@@ -150,11 +202,23 @@ def forward(means3D, opacities, viewmatrix, projmatrix, campos, bg, image_height
     if P == 0:
         # nothing to splat: the image is the background (upstream behaviour)
         color[:] = keep["bg"].view(3, 1, 1)
-    else:
+    elif context is not None:
         with torch.cuda.device(dev):
-            check(LIB.gsmpm_raster_forward(context.h if context is not None else _context(dev.index or 0),
-                                           ctypes.byref(a), ptr(color), ptr(radii), ctypes.byref(nr),
+            check(LIB.gsmpm_raster_forward(context.h, ctypes.byref(a), ptr(color), ptr(radii), ctypes.byref(nr),
                                            stream_of(dev)), "rasterize_gaussians")
+    else:
+        w = ws if ws is not None else workspace(dev.index or 0)
+        H, W = int(image_height), int(image_width)
+        w.ensure(P, H, W, w.key[3] if w.key else 8 * P + 4096)
+        need = ctypes.c_int64(0)
+        with torch.cuda.device(dev):
+            for attempt in range(2):
+                rc = LIB.gsmpm_raster_forward_ws(ctypes.byref(a), ptr(color), ptr(radii), ctypes.byref(nr), w.ptr(),
+                                                 w.nbytes(), ctypes.byref(need), stream_of(dev))
+                if rc != _lib.ESPACE or attempt == 1:
+                    break
+                w.ensure(P, H, W, int(need.value) + int(need.value) // 4 + 1024)
+            check(rc, "rasterize_gaussians")
     if return_args:
         return int(nr.value), color, radii, a, keep
     return int(nr.value), color, radii

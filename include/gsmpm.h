@@ -22,6 +22,7 @@ extern "C" {
 #define GSMPM_EINVAL -1
 #define GSMPM_EHIP -2
 #define GSMPM_ESTATE -3
+#define GSMPM_ESPACE -4  /* a caller-owned workspace is too small (gsmpm_raster_forward_ws) */
 
 /* ------------------------------------------------------------ common --- */
 const char* gsmpm_last_error(void);
@@ -390,6 +391,25 @@ int gsmpm_raster_backward(gsmpm_raster* r, const gsmpm_raster_args* a, const int
  * (main.py:148-157 never differentiates); autograd forwards use contexts
  * with it off (the default). */
 int gsmpm_raster_set_forward_only(gsmpm_raster* r, int32_t on);
+/* Caller-owned workspace form of the forward (upstream's
+ * RasterizeGaussiansCUDA takes torch byte tensors for its geometry / binning /
+ * image buffers, rasterize_points.cu).  gsmpm_raster_workspace_size: the
+ * bytes a forward of P Gaussians into an H x W image needs when the frame
+ * bins at most `pairs` (Gaussian, tile) pairs (pairs = 0: the part that does
+ * not depend on the pair count).  gsmpm_raster_forward_ws: the forward with
+ * every buffer carved from `workspace` (device memory, 256-byte aligned,
+ * ws_bytes long, ZERO-FILLED ONCE when created: the hand-written depth order
+ * keeps its bucket state at the workspace's start and leaves it zero after
+ * every call); no allocation inside, forward-only (no backward state).
+ * The pair count is known only after the binning scan (upstream resizes its
+ * binning buffer at that point): when the frame needs more pairs than the
+ * workspace holds, the call returns GSMPM_ESPACE with *pairs_needed set and
+ * the outputs unwritten; the caller sizes a larger workspace for that many
+ * pairs and calls again. */
+int gsmpm_raster_workspace_size(int32_t P, int32_t H, int32_t W, int64_t pairs, uint64_t* bytes);
+int gsmpm_raster_forward_ws(const gsmpm_raster_args* a, float* out_color, int32_t* out_radii,
+                            int32_t* num_rendered, void* workspace, uint64_t ws_bytes, int64_t* pairs_needed,
+                            void* stream);
 /* Diagnostics of the context's last forward: *binned = the (Gaussian, tile)
  * pairs actually sorted and listed (each Gaussian binned into the tiles its
  * alpha >= 1/255 box reaches, a subset of the 3-sigma rect), *rendered = its

@@ -318,15 +318,97 @@ def test_tight_binning_pair_counts(dev, monkeypatch, P, W, H):
     counts = {}
     for mode in ("0", "1"):
         monkeypatch.setenv("GSMPM_RASTER_RENDER_MODE", mode)
+        ctx = raster.shared_context(dev.index or 0)
         K, _, _ = raster.forward(t(means), t(opa), t(view), t(full), t(campos), t(bgv), H, W, tx, ty,
-                                 sh_degree=3, shs=t(shs), cov3D_precomp=t(c6))
-        binned, rendered = raster.pair_counts(dev.index or 0)
+                                 sh_degree=3, shs=t(shs), cov3D_precomp=t(c6), context=ctx)
+        binned, rendered = raster.pair_counts(ctx)
         assert rendered == K
         counts[mode] = (binned, K)
     (b0, k0), (b1, k1) = counts["0"], counts["1"]
     assert k0 == k1 and b1 == k1, counts
     assert 0 < b0 < k0, counts
     print("binned / 3-sigma pairs", b0, k0, round(b0 / k0, 3))
+
+
+@pytest.mark.parametrize("case", ["spread", "wide", "layers", "flat", "many"])
+def test_depth_order_matches_library_sort(dev, monkeypatch, case):
+    """The hand-written depth order (csrc/dsort.h: bucketed on the depth bits,
+    each bucket ranked by (bits, index) in a wave or, above 256 entries, a
+    bitonic workgroup) against the library's stable radix sort + scan
+    (GSMPM_RASTER_DSORT=lib): num_rendered, radii and every pixel
+    bit-identical.  Cases: depths spread over a box ("spread"), a scene with a
+    far outlier stretching the bucket range ("wide"), depths on 3 exact values
+    (buckets of ~1,000: the workgroup sort, "layers"), all depths equal (one
+    bucket of 20,000 > 8,192: the overflow flag and the library fallback,
+    "flat"), and 300,000 Gaussians ("many")."""
+    import torch
+    from gsmpm import raster
+    P, W, H, yaw = {"spread": (3000, 256, 192, 0.3), "wide": (20000, 640, 480, 0.3), "layers": (3000, 256, 192, 0.0),
+                    "flat": (20000, 512, 512, 0.0), "many": (300000, 800, 800, 0.3)}[case]
+    means, c6, opa, shs = _scene(P, seed=P + 7)
+    if case == "wide":
+        means[0] = (0.0, 0.0, 60.0)  # far behind the scene
+    if case == "layers":
+        means[:, 2] = np.float32([-0.2, 0.1, 0.4])[np.arange(P) % 3]
+    if case == "flat":
+        means[:, 2] = np.float32(0.1)
+    view, full, campos, tx, ty = _camera(W, H, 0.9, yaw=yaw)
+    bgv = np.zeros(3, np.float32)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    args = (t(means), t(opa), t(view), t(full), t(campos), t(bgv), H, W, tx, ty)
+    kw = dict(sh_degree=3, shs=t(shs), cov3D_precomp=t(c6))
+    out = {}
+    for mode in ("own", "lib"):
+        if mode == "lib":
+            monkeypatch.setenv("GSMPM_RASTER_DSORT", "lib")
+        for ctx in (None, raster.RasterContext()):  # the workspace form and the context form
+            K, color, radii = raster.forward(*args, **kw, context=ctx)
+            torch.cuda.synchronize()
+            out[(mode, ctx is None)] = (K, color.cpu().numpy(), radii.cpu().numpy())
+    K0, c0, r0 = out[("lib", False)]
+    assert K0 > 0 and c0.max() > 0
+    for key, (K, c, r) in out.items():
+        assert K == K0, (key, K, K0)
+        assert np.array_equal(r, r0), key
+        assert np.array_equal(c, c0), (key, float(np.abs(c - c0).max()))
+
+
+@pytest.mark.parametrize("P,W,H", [(3000, 256, 192), (20000, 1100, 1000)])
+def test_workspace_forward_matches_context(dev, P, W, H):
+    """SURVEY 8(b) b2's caller-owned workspace: gsmpm_raster_forward_ws into a
+    torch byte tensor (gsmpm_raster_workspace_size) gives bit-identical pixels,
+    radii and num_rendered to the library-owned context form, at <= 4,096
+    tiles (chunked tile sort) and above (4,345 tiles: onesweep).  A workspace
+    sized for too few pairs reports GSMPM_ESPACE with the count it needs
+    (outputs unwritten), and one sized for that count then succeeds."""
+    import ctypes
+    import torch
+    from gsmpm import _lib, raster
+    means, c6, opa, shs = _scene(P, seed=P + 1)
+    view, full, campos, tx, ty = _camera(W, H, 0.9)
+    bgv = np.zeros(3, np.float32)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    args = (t(means), t(opa), t(view), t(full), t(campos), t(bgv), H, W, tx, ty)
+    kw = dict(sh_degree=3, shs=t(shs), cov3D_precomp=t(c6))
+    K0, c0, r0 = raster.forward(*args, **kw, context=raster.RasterContext())
+    ws = raster.Workspace(dev)
+    ws.ensure(P, H, W, 16)  # far too few pairs
+    a, keep = raster._args(*args, kw["sh_degree"], kw["shs"], None, None, None, kw["cov3D_precomp"], 1.0, False)
+    color = torch.full((3, H, W), -7.0, device=dev)
+    radii = torch.empty(P, dtype=torch.int32, device=dev)
+    nr, need = ctypes.c_int32(0), ctypes.c_int64(0)
+    rc = _lib.LIB.gsmpm_raster_forward_ws(ctypes.byref(a), _lib.ptr(color), _lib.ptr(radii), ctypes.byref(nr),
+                                         ws.ptr(), ws.nbytes(), ctypes.byref(need), _lib.stream_of(dev))
+    torch.cuda.synchronize()
+    assert rc == _lib.ESPACE and need.value > 16, (rc, need.value)
+    assert bool((color == -7.0).all())  # nothing rendered into the outputs
+    ws.ensure(P, H, W, int(need.value))
+    K1, c1, r1 = raster.forward(*args, **kw, ws=ws)
+    assert K1 == K0
+    assert torch.equal(r1, r0)
+    assert torch.equal(c1, c0)
+    K2, c2, _ = raster.forward(*args, **kw)  # the default: the device's cached workspace, grown on demand
+    assert K2 == K0 and torch.equal(c2, c0)
 
 
 @pytest.mark.parametrize("scene,onesweep", [("dense", "0"), ("sparse", "0"), ("sparse", "1")])

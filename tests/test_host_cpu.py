@@ -51,6 +51,29 @@ def test_library_loads_and_exports_every_declared_symbol():
     assert _lib.LIB.gsmpm_version() >= 1
 
 
+def test_raster_workspace_entry_points_validate_without_a_gpu():
+    """gsmpm_raster_workspace_size / gsmpm_raster_forward_ws (the caller-owned
+    workspace form): bad sizes and an unaligned workspace are
+    refused before any HIP call; sizing itself needs the device (rocPRIM's
+    temporary-size queries read its properties) and fails with the HIP error
+    here rather than crashing."""
+    import ctypes
+    from gsmpm import _lib
+    nb = ctypes.c_uint64(0)
+    assert _lib.LIB.gsmpm_raster_workspace_size(-1, 800, 800, 0, ctypes.byref(nb)) == _lib.GSMPM_EINVAL
+    assert "bad argument" in _lib.last_error()
+    assert _lib.LIB.gsmpm_raster_workspace_size(10, 0, 800, 0, ctypes.byref(nb)) == _lib.GSMPM_EINVAL
+    a = _lib.RasterArgs()
+    a.P, a.W, a.H = 10, 64, 64
+    need = ctypes.c_int64(0)
+    nr = ctypes.c_int32(0)
+    assert _lib.LIB.gsmpm_raster_forward_ws(ctypes.byref(a), None, None, ctypes.byref(nr), 0x1001, 1 << 20,
+                                            ctypes.byref(need), None) == _lib.GSMPM_EINVAL
+    assert "256-byte aligned" in _lib.last_error()
+    rc = _lib.LIB.gsmpm_raster_workspace_size(100_000, 800, 800, 500_000, ctypes.byref(nb))
+    assert rc == 0 or (rc == _lib.GSMPM_EHIP and _lib.last_error()), (rc, _lib.last_error())
+
+
 def test_null_arguments_fail_loudly_without_a_gpu():
     """Argument validation happens before any HIP call."""
     import ctypes

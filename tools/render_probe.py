@@ -49,5 +49,10 @@ t0 = time.perf_counter()
 for _ in range(reps):
     K = fwd()[0]
 torch.cuda.synchronize()
-binned, _ = raster.pair_counts(dev.index or 0)
-print(f"render {1e3 * (time.perf_counter() - t0) / reps:.4f} ms/frame, K {K}, binned {binned}")
+el = time.perf_counter() - t0
+ctx = raster.shared_context(dev.index or 0)
+raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg, cam.height, cam.width,
+               math.tan(cam.FovX * 0.5), math.tan(cam.FovY * 0.5), sh_degree=3, shs=feats, cov3D_precomp=covs_r,
+               context=ctx)
+binned, _ = raster.pair_counts(ctx)
+print(f"render {1e3 * el / reps:.4f} ms/frame, K {K}, binned {binned}")
