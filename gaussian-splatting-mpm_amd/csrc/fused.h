@@ -704,6 +704,7 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     const int q = threadIdx.x + (wt % kGridParts) * kGridT;
     const int l0 = q / (kFT1 * kFT2), l1 = (q / kFT2) % kFT1, l2 = q % kFT2;
     const int T = all ? wt / kGridParts : wt == (int)blockIdx.x ? T0 : ck.touched[wt / kGridParts];
+    if ((unsigned)T >= (unsigned)tl.ntiles) continue;  // workgroup-uniform; never taken (wt < parts x count)
     int ti, tj, tk;
     ftile_decode(tl, T, ti, tj, tk);
     if (sw.pass != 0 && slab_tile_in_window(sw, ti) != (sw.pass == 1)) continue;  // workgroup-uniform
@@ -713,7 +714,7 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     __syncthreads();
     if (wt == (int)blockIdx.x) stamp(3, 3);
     const int i = ti * kFT0 + l0, j = tj * kFT1 + l1, k = tk * kFT2 + l2;
-    if (i < ng && j < ng && k < ng) {
+    if ((unsigned)i < (unsigned)ng && (unsigned)j < (unsigned)ng && (unsigned)k < (unsigned)ng) {
       NodeReads r;
       node_reads(tl.max_chunks, s_c0, s_nc, s_bx, l0, l1, l2, r);
       float4 v[8];

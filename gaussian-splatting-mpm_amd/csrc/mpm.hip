@@ -2094,6 +2094,10 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
         return fail(e, "hipMalloc chunk");
       if ((e = hipMalloc(&h->ftouched[c], sizeof(int) * (size_t)h->ftl.ntiles)) != hipSuccess)
         return fail(e, "hipMalloc touched");
+      // entries past the live count are never used, but a read of one must see a valid tile (round 3's
+      // uncommitted three-tiles-per-workgroup k_grid_f read past the count: hipErrorIllegalAddress)
+      if ((e = hipMemset(h->ftouched[c], 0, sizeof(int) * (size_t)h->ftl.ntiles)) != hipSuccess)
+        return fail(e, "hipMemset touched");
       if ((e = hipMalloc(&h->ftflag[c], sizeof(int) * (size_t)h->ftl.ntiles)) != hipSuccess)
         return fail(e, "hipMalloc tflag");
       if ((e = hipMalloc(&h->fnchunk[c], sizeof(int) * 2)) != hipSuccess) return fail(e, "hipMalloc nchunk");
