@@ -54,6 +54,7 @@ enum : int {
   DS_PV = 20,      // visible Gaussians
   DS_LO = 21, DS_SHIFT = 22, DS_NB = 23,
   DS_TOT = 24,     // [2] u64 total of the tiles words (K | num_rendered << 32)
+  DS_MAXN = 26,    // the largest bucket (diagnostics)
   kDsWords = 32
 };
 
@@ -118,52 +119,66 @@ __global__ __launch_bounds__(256) void k_dsort_hist(int P, int nb, const float* 
   __hip_atomic_fetch_add(d.bsum + b, tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// one workgroup: exclusive scans of counts and sums over the nb buckets
+// one workgroup: exclusive scans of counts and sums over the nb buckets, in
+// coalesced passes of 1,024 buckets (a bucket per lane: wave scans, then the
+// 16 wave totals through LDS, a running carry across passes)
 __global__ __launch_bounds__(kDsScanT) void k_dsort_scan(int nb, DsortBufs d) {
-  __shared__ unsigned s_c[kDsScanT];
-  __shared__ unsigned long long s_s[kDsScanT];
-  __shared__ unsigned s_nl, s_nb, s_over;
-  const int t = threadIdx.x;
-  const int per = nb / kDsScanT;  // nb is a power of two >= 1024
-  const int b0 = t * per;
-  unsigned c = 0;
-  unsigned long long s = 0;
-  for (int k = 0; k < per; ++k) {
-    c += d.bcount[b0 + k];
-    s += d.bsum[b0 + k];
-  }
-  s_c[t] = c;
-  s_s[t] = s;
-  if (t == 0) s_nl = s_nb = s_over = 0;
-  __syncthreads();
-  for (int o = 1; o < kDsScanT; o <<= 1) {  // Hillis-Steele inclusive scan
-    const unsigned cc = t >= o ? s_c[t - o] : 0u;
-    const unsigned long long ss = t >= o ? s_s[t - o] : 0ull;
-    __syncthreads();
-    s_c[t] += cc;
-    s_s[t] += ss;
-    __syncthreads();
-  }
-  unsigned run = s_c[t] - c;
-  unsigned long long pre = s_s[t] - s;
-  for (int k = 0; k < per; ++k) {
-    const int b = b0 + k;
+  __shared__ unsigned s_wc[kDsScanT / 64];
+  __shared__ unsigned long long s_ws[kDsScanT / 64];
+  __shared__ unsigned s_nl, s_nb, s_over, s_maxn;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  if (t == 0) s_nl = s_nb = s_over = s_maxn = 0;
+  unsigned carry_c = 0;
+  unsigned long long carry_s = 0;
+  for (int b0 = 0; b0 < nb; b0 += kDsScanT) {  // workgroup-uniform
+    const int b = b0 + t;
     const unsigned n = d.bcount[b];
+    const unsigned long long sm = d.bsum[b];
+    unsigned ic = n;
+    unsigned long long is = sm;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned uc = (unsigned)__shfl_up((int)ic, o);
+      const unsigned long long us = __shfl_up(is, o);
+      if (lane >= o) {
+        ic += uc;
+        is += us;
+      }
+    }
+    if (lane == 63) {
+      s_wc[wv] = ic;
+      s_ws[wv] = is;
+    }
+    __syncthreads();
+    unsigned pc = carry_c, tc = 0;
+    unsigned long long ps = carry_s, ts = 0;
+#pragma unroll
+    for (int q = 0; q < kDsScanT / 64; ++q) {
+      const unsigned xc = s_wc[q];
+      const unsigned long long xs = s_ws[q];
+      if (q < wv) {
+        pc += xc;
+        ps += xs;
+      }
+      tc += xc;
+      ts += xs;
+    }
     if (n) {
-      d.bbase[b] = run;
-      d.bcur[b] = run;
-      d.bpre[b] = pre;
+      d.bbase[b] = pc + ic - n;
+      d.bcur[b] = pc + ic - n;
+      d.bpre[b] = ps + is - sm;
       if (n <= (unsigned)kDsSmall) {
         d.blist[atomicAdd(&s_nl, 1u)] = (unsigned)b;
       } else {
         d.bbig[atomicAdd(&s_nb, 1u)] = (unsigned)b;
         if (n > (unsigned)kDsBig) s_over = 1u;
       }
-      run += n;
-      pre += d.bsum[b];
+      atomicMax(&s_maxn, n);
     }
+    carry_c += tc;
+    carry_s += ts;
+    __syncthreads();  // s_wc / s_ws reused by the next pass
   }
-  __syncthreads();
   if (t == 0) {
     unsigned lo;
     int shift;
@@ -174,11 +189,11 @@ __global__ __launch_bounds__(kDsScanT) void k_dsort_scan(int nb, DsortBufs d) {
     d.st[DS_NLIST] = s_nl;
     d.st[DS_NBIG] = s_nb;
     d.st[DS_OVER] = s_over;
-    d.st[DS_PV] = s_c[kDsScanT - 1];
+    d.st[DS_MAXN] = s_maxn;
+    d.st[DS_PV] = carry_c;
     d.st[DS_CULL] = 0;
-    const unsigned long long tot = s_s[kDsScanT - 1];
-    d.st[DS_TOT] = (unsigned)tot;
-    d.st[DS_TOT + 1] = (unsigned)(tot >> 32);
+    d.st[DS_TOT] = (unsigned)carry_s;
+    d.st[DS_TOT + 1] = (unsigned)(carry_s >> 32);
   }
 }
 

@@ -228,6 +228,16 @@ __device__ __forceinline__ bool in_grid(const float (&x)[3], const GridDims& g) 
 #define GSMPM_ZERO_BOX 0
 #endif
 constexpr bool kZeroBox = GSMPM_ZERO_BOX != 0;
+// GSMPM_ATOMIC_GRID=1: the P2G half adds its window box into the dense
+// accumulator gacc with global float atomics (one lane per node channel)
+// instead of storing it to the chunk's slot, and k_grid_f reads one node of
+// gacc (and zeroes it) instead of summing <= 8 covering slots through the
+// 27-tile cover table.  The cross-chunk sum becomes order-dependent f32 (as
+// the reference's Taichi atomics are); within a chunk it stays exact (A/B)
+#ifndef GSMPM_ATOMIC_GRID
+#define GSMPM_ATOMIC_GRID 0
+#endif
+constexpr bool kAtomicGrid = GSMPM_ATOMIC_GRID != 0;
 template <int MAT, int MODE>
 __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTiles tl, ChunkIn ck, Touch tc, BinOutF bo,
                                                int bin, int use_box, const float4* __restrict__ gvel,
@@ -539,7 +549,24 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
       __syncthreads();
       if (w == (int)blockIdx.x) stamp(SK, 4);
       if (tc.perm && k < cnt) tc.perm[(size_t)w * 256 + balanced_lane(s_rcnt, cnt, res, rrank)] = (unsigned char)q;
-      {
+      if constexpr (kAtomicGrid) {  // the box into the dense accumulator, one lane per (node, channel)
+        int lo[3], hi[3];
+        box_unpack(box, lo, hi);
+        const int n1 = hi[1] - lo[1] + 1, n2 = hi[2] - lo[2] + 1, n12 = n1 * n2;
+        const int nvol = (hi[0] - lo[0] + 1) * n12;
+        const float r12 = 1.0f / (float)n12, r2 = 1.0f / (float)n2;
+        for (int e = k; e < 4 * nvol; e += 256) {
+          const int qn = e >> 2, ch = e & 3;
+          const int a = (int)(((float)qn + 0.5f) * r12), rem = qn - a * n12;
+          const int bq = (int)(((float)rem + 0.5f) * r2), c = rem - bq * n2;
+          const int wa = lo[0] + a, wb = lo[1] + bq, wc = lo[2] + c;
+          const int node = (wa * kFW1 + wb) * kFW2 + wc;
+          const int ix = o0 + wa, iy = o1 + wb, iz = o2 + wc;
+          const float val = from_fixed32(s_acc[ch * kFWin + node], S);
+          if (val != 0.f && (unsigned)ix < (unsigned)ng && (unsigned)iy < (unsigned)ng && (unsigned)iz < (unsigned)ng)
+            unsafeAtomicAdd(reinterpret_cast<float*>(gacc + (((size_t)ix * ng + iy) * ng + iz)) + ch, val);
+        }
+      } else {
         int lo[3], hi[3];
         box_unpack(box, lo, hi);
         const int n1 = hi[1] - lo[1] + 1, n2 = hi[2] - lo[2] + 1, n12 = n1 * n2;
@@ -708,26 +735,33 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     int ti, tj, tk;
     ftile_decode(tl, T, ti, tj, tk);
     if (sw.pass != 0 && slab_tile_in_window(sw, ti) != (sw.pass == 1)) continue;  // workgroup-uniform
-    __syncthreads();  // readers of the previous tile's ranges are done
-    if (wt == (int)blockIdx.x) stamp(3, 2);
-    load_cover27(ck, tbox, tl, ti, tj, tk, s_c0, s_nc, s_bx);
-    __syncthreads();
+    if constexpr (!kAtomicGrid) {
+      __syncthreads();  // readers of the previous tile's ranges are done
+      if (wt == (int)blockIdx.x) stamp(3, 2);
+      load_cover27(ck, tbox, tl, ti, tj, tk, s_c0, s_nc, s_bx);
+      __syncthreads();
+    }
     if (wt == (int)blockIdx.x) stamp(3, 3);
     const int i = ti * kFT0 + l0, j = tj * kFT1 + l1, k = tk * kFT2 + l2;
     if ((unsigned)i < (unsigned)ng && (unsigned)j < (unsigned)ng && (unsigned)k < (unsigned)ng) {
-      NodeReads r;
-      node_reads(tl.max_chunks, s_c0, s_nc, s_bx, l0, l1, l2, r);
-      float4 v[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = slots[r.off[e]];
-      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) add4(a, v[e]);
-      node_extra(slots, s_c0, s_nc, l0, l1, l2, r.extra, a);
       const size_t idx = ((size_t)i * ng + j) * ng + k;
-      if (all) {
-        add4(a, gacc[idx]);
-        gacc[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (kAtomicGrid) {  // the node's whole sum, added by the chunks' atomics
+        a = gacc[idx];
+        if (a.x != 0.f || a.y != 0.f || a.z != 0.f || a.w != 0.f) gacc[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        NodeReads r;
+        node_reads(tl.max_chunks, s_c0, s_nc, s_bx, l0, l1, l2, r);
+        float4 v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = slots[r.off[e]];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) add4(a, v[e]);
+        node_extra(slots, s_c0, s_nc, l0, l1, l2, r.extra, a);
+        if (all) {
+          add4(a, gacc[idx]);
+          gacc[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
       }
       const int sww = sw.W ? slab_window_of(sw, i) : -1;
       const bool inrect = sww >= 0 && (unsigned)(j - sw.y0[sww]) < (unsigned)sw.ny[sww] &&

@@ -2428,6 +2428,21 @@ int gsmpm_raster_set_forward_only(gsmpm_raster* r, int32_t on) {
   return GSMPM_OK;
 }
 
+int gsmpm_raster_dsort_stats(const gsmpm_raster* r, int64_t out8[8]) {
+  GSMPM_REQUIRE(r && out8, "gsmpm_raster_dsort_stats: null argument");
+  unsigned st[kDsWords] = {0};
+  if (r->ds_state) GSMPM_HIP(hipMemcpy(st, r->ds_state, sizeof(st), hipMemcpyDeviceToHost));
+  out8[0] = st[DS_NB];
+  out8[1] = st[DS_NLIST];
+  out8[2] = st[DS_NBIG];
+  out8[3] = st[DS_MAXN];
+  out8[4] = st[DS_OVER];
+  out8[5] = st[DS_PV];
+  out8[6] = r->dsort_fallbacks;
+  out8[7] = st[DS_SHIFT];
+  return GSMPM_OK;
+}
+
 int gsmpm_raster_workspace_size(int32_t P, int32_t H, int32_t W, int64_t pairs, uint64_t* bytes) {
   GSMPM_REQUIRE(bytes && P >= 0 && H > 0 && W > 0 && pairs >= 0, "gsmpm_raster_workspace_size: bad argument");
   const size_t ntiles = (size_t)div_up(W, kBX) * (size_t)div_up(H, kBY);

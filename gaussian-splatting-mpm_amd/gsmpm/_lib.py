@@ -141,6 +141,7 @@ _SIGS = {
     "gsmpm_raster_mark_visible": (ctypes.c_int, [c_void_p, ctypes.c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "gsmpm_raster_set_forward_only": (ctypes.c_int, [c_void_p, ctypes.c_int32]),
     "gsmpm_raster_pair_counts": (ctypes.c_int, [c_void_p, c_void_p, c_void_p]),
+    "gsmpm_raster_dsort_stats": (ctypes.c_int, [c_void_p, c_void_p]),
     "gsmpm_raster_workspace_size": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64,
                                                    ctypes.POINTER(ctypes.c_uint64)]),
     "gsmpm_raster_forward_ws": (ctypes.c_int, [ctypes.POINTER(RasterArgs), c_void_p, c_void_p,

@@ -38,6 +38,14 @@ def pair_counts(context) -> tuple:
     return int(b.value), int(n.value)
 
 
+def dsort_stats(context) -> dict:
+    """The hand-written depth order's diagnostics for `context`'s last forward (csrc/dsort.h)."""
+    o = (ctypes.c_int64 * 8)()
+    check(LIB.gsmpm_raster_dsort_stats(context.h, o), "gsmpm_raster_dsort_stats")
+    return dict(zip(("buckets", "wave_buckets", "wg_buckets", "max_bucket", "overflow", "visible", "fallbacks",
+                     "shift"), list(o)))
+
+
 class Workspace:
     """A caller-owned rasterizer workspace: one torch byte tensor
     (gsmpm_raster_workspace_size / gsmpm_raster_forward_ws), as upstream's

@@ -415,6 +415,10 @@ int gsmpm_raster_forward_ws(const gsmpm_raster_args* a, float* out_color, int32_
  * alpha >= 1/255 box reaches, a subset of the 3-sigma rect), *rendered = its
  * num_rendered (upstream's 3-sigma pair count).  Either pointer may be null. */
 int gsmpm_raster_pair_counts(const gsmpm_raster* r, uint32_t* binned, uint32_t* rendered);
+/* Diagnostics of the context's last hand-written depth order (csrc/dsort.h):
+ * out8 = {buckets, occupied buckets sorted by a wave, by a workgroup, largest
+ * bucket, overflow flag, visible Gaussians, library fallbacks so far, shift}. */
+int gsmpm_raster_dsort_stats(const gsmpm_raster* r, int64_t out8[8]);
 /* GaussianRasterizer.markVisible -> _C.mark_visible: visible[P] (u8) = view z > 0.2 */
 int gsmpm_raster_mark_visible(const float* means3D, int32_t P, const float* viewmatrix, const float* projmatrix,
                               uint8_t* visible, void* stream);
