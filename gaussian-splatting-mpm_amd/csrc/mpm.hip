@@ -1432,7 +1432,12 @@ struct gsmpm_mpm {
   int* mig_bcnt = nullptr;                   // [nblk][3] per-block destination counts
   int* mig_boff = nullptr;                   // [nblk][3] their exclusive scan
   int* mig_tot = nullptr;                    // [3] leavers to lower, stayers, leavers to upper
-  int* s_rec = nullptr;                      // [world][kRecInts] every rank's record (slab_records)
+  int* s_rec = nullptr;                      // [world][rec_ints_of(ng)] every rank's record (slab_records)
+  std::vector<int> s_bounds;                 // every rank's planes: [world + 1] (from the records)
+  bool s_rebal_on = true;                    // re-cut the slabs at call boundaries when unbalanced
+  float s_rebal_tol = 0.10f;                 // ... by more than this (max count / mean - 1)
+  bool s_rebal_pending = false;              // the next call starts with the migration to new bounds
+  long s_rebalances = 0;
   int* s_rec_host = nullptr;                 // pinned copy
   float* mig_send[2] = {nullptr, nullptr};   // fixed-size payloads: header + [NMIG][mig_cap]
   float* mig_recv[2] = {nullptr, nullptr};
@@ -1923,6 +1928,7 @@ static int graph_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc, 
     key.push_back(h->cold_alt && h->cold > h->cold_alt ? 1u : 0u);
     key.push_back(h->gid_alt && h->gid > h->gid_alt ? 1u : 0u);
     key.push_back((uint32_t)h->mig_cap);
+    key.push_back(h->s_rebal_pending ? 1u : 0u);  // the call opens with the re-cut's migration
   }
   for (int s = 0; s < nsub; ++s) key.push_back(bc ? bc[s] : 0xffffffffu);
   auto it = h->graphs.find(key);

@@ -1174,63 +1174,137 @@ __global__ __launch_bounds__(256) void k_tile_dsort_rank(const uint2* __restrict
   }
 }
 
-// Above kMaxTiles tiles: the same chunked counting sort, LSD over 8-bit
-// digits of the tile index (two passes up to 65,535 tiles, three above).  A
-// pass keeps 256 histogram entries per 2,048-pair chunk (the one-pass form's
-// entry per (tile, chunk) would be ~1e9 entries at the bicycle's 63,860 tiles
-// and 30M pairs), scans them digit-major, and scatters each chunk's stably
-// block-sorted pairs to their digit runs: no look-back chain.  Culled keys
-// (tile field all ones) carry digit 255 in every pass, so they sort after
-// every real tile (ntiles <= 256^passes - 1).
-__global__ __launch_bounds__(kSortT) void k_digit_hist(int K, int nch, int shift, const unsigned* __restrict__ keys,
-                                                       unsigned* __restrict__ H) {
+// Above kMaxTiles tiles: a stable LSD radix sort over 8-bit digits of the
+// tile index (two passes up to 65,535 tiles, three above), each pass
+// reduce-then-scan with no look-back chain and no library call:
+//   k_lsd_hist     per 4,096-pair chunk, its 256 digit counts (LDS atomics),
+//                  stored digit-major H[d][chunk]
+//   k_tile_rows    (256 rows) each digit's row prefix over the chunks + totals
+//   k_lsd_scatter  per chunk: every wave ranks its 1,024 pairs (16 slots of
+//                  64, in order) by digit with 8 ballots per slot and a
+//                  wave-private running count per digit -- no barrier between
+//                  slots; the four waves' counts then give each pair its
+//                  chunk-local sorted index; the chunk is staged sorted in LDS
+//                  and stored striped, so each digit run leaves as coalesced
+//                  stores at digit start + the run's row prefix.
+// Stable: a pair's rank follows (wave, slot, lane) = its chunk order.  Culled
+// keys (tile field all ones) carry digit 255 in every pass, so they sort after
+// every real tile (ntiles <= 256^passes - 1).  Round 3's form (2,048-pair
+// chunks, the library's block radix sort for the local ranks, the library's
+// device scan) ran 1.41 ms per bicycle render against 1.31 with the library's
+// onesweep.
+constexpr int kLsdT = 256, kLsdI = 16, kLsdChunk = kLsdT * kLsdI;
+__global__ __launch_bounds__(kLsdT) void k_lsd_hist(int K, int nch, int shift, const unsigned* __restrict__ keys,
+                                                    unsigned* __restrict__ H) {
   __shared__ unsigned s_h[256];
   s_h[threadIdx.x] = 0;
   __syncthreads();
   const int c = blockIdx.x;
+  unsigned k[kLsdI];
 #pragma unroll
-  for (int i = 0; i < kSortI; ++i) {
-    const int e = c * kChunk + i * kSortT + threadIdx.x;
-    if (e < K) atomicAdd(&s_h[(keys[e] >> shift) & 255u], 1u);
+  for (int i = 0; i < kLsdI; ++i) {
+    const int e = c * kLsdChunk + i * kLsdT + threadIdx.x;
+    k[i] = e < K ? keys[e] : 0u;
   }
+#pragma unroll
+  for (int i = 0; i < kLsdI; ++i)
+    if (c * kLsdChunk + i * kLsdT + (int)threadIdx.x < K) atomicAdd(&s_h[(k[i] >> shift) & 255u], 1u);
   __syncthreads();
   H[(size_t)threadIdx.x * nch + c] = s_h[threadIdx.x];
 }
-__global__ __launch_bounds__(kSortT) void k_digit_scatter(int K, int nch, int shift, const unsigned* __restrict__ keys,
-                                                          const unsigned* __restrict__ vals,
-                                                          const unsigned* __restrict__ Hs,
-                                                          unsigned* __restrict__ keys_out,
-                                                          unsigned* __restrict__ vals_out) {
-  using BRS = rocprim::block_radix_sort<unsigned, kSortT, kSortI, unsigned>;
-  __shared__ typename BRS::storage_type s_sort;
-  __shared__ unsigned s_k[kChunk], s_v[kChunk];
-  __shared__ int s_start[256];
-  const int c = blockIdx.x;
-  unsigned k[kSortI], v[kSortI];
+__global__ __launch_bounds__(kLsdT) void k_lsd_scatter(int K, int nch, int shift, const unsigned* __restrict__ keys,
+                                                       const unsigned* __restrict__ vals,
+                                                       const unsigned* __restrict__ Hs, const unsigned* __restrict__ tot,
+                                                       unsigned* __restrict__ keys_out,
+                                                       unsigned* __restrict__ vals_out) {
+  __shared__ unsigned s_k[kLsdChunk], s_v[kLsdChunk];
+  __shared__ unsigned s_wrun[4][256];  // per wave: running count of each digit, then its offset
+  __shared__ unsigned s_doff[256];     // chunk-local start of each digit's run
+  __shared__ unsigned s_gbase[256];    // global position of this chunk's run of each digit
+  __shared__ unsigned s_part[4][2];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, c = blockIdx.x;
 #pragma unroll
-  for (int i = 0; i < kSortI; ++i) {
-    const int e = c * kChunk + threadIdx.x * kSortI + i;  // blocked: the sort is stable in this order
-    k[i] = e < K ? keys[e] : 0xffffffffu;
-    v[i] = e < K ? vals[e] : kNoEntry;
+  for (int w = 0; w < 4; ++w) s_wrun[w][t] = 0;
+  // where each digit's run starts overall: exclusive scan of the 256 digit totals (thread t: digit t)
+  const unsigned dt = tot[t];
+  unsigned inc = dt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned u = (unsigned)__shfl_up((int)inc, o);
+    if (lane >= o) inc += u;
   }
-  BRS().sort(k, v, s_sort, shift, shift + 8);  // the chunk's tail (digit 255) sorts last
-  sorted_to_lds(k, v, s_k, s_v);
+  if (lane == 63) s_part[wv][0] = inc;
+  __syncthreads();
+  unsigned dstart = inc - dt;
+  for (int w = 0; w < wv; ++w) dstart += s_part[w][0];
+  s_gbase[t] = dstart + Hs[(size_t)t * nch + c];
+  // wave wv ranks pairs [c * 4096 + wv * 1024, +1024) in 16 slots of 64, in order
+  const int e0 = c * kLsdChunk + wv * (kLsdChunk / 4);
+  unsigned k[kLsdI], v[kLsdI], r[kLsdI];
 #pragma unroll
-  for (int i = 0; i < kSortI; ++i) {  // striped, as k_tile_scatter
-    const int sp = i * kSortT + threadIdx.x;
-    const unsigned d = (s_k[sp] >> shift) & 255u;
-    if (s_v[sp] != kNoEntry && (sp == 0 || ((s_k[sp - 1] >> shift) & 255u) != d)) s_start[d] = sp;
+  for (int j = 0; j < kLsdI; ++j) {
+    const int e = e0 + j * 64 + lane;
+    k[j] = e < K ? keys[e] : 0u;
+    v[j] = e < K ? vals[e] : 0u;
+  }
+  const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int j = 0; j < kLsdI; ++j) {
+    const bool ok = e0 + j * 64 + lane < K;
+    const unsigned d = ok ? (k[j] >> shift) & 255u : 256u;
+    unsigned long long peers = ~0ull;
+#pragma unroll
+    for (int b = 0; b < 9; ++b) {
+      const unsigned long long bal = __ballot((d >> b) & 1u);
+      peers &= ((d >> b) & 1u) ? bal : ~bal;
+    }
+    const unsigned rk = (unsigned)__popcll(peers & below);
+    const unsigned base = ok ? s_wrun[wv][d] : 0u;
+    r[j] = base + rk;
+    // the digit's lowest lane moves the count on; the wave's LDS operations
+    // execute in order, so the next slot's read sees it
+    if (ok && rk == 0) s_wrun[wv][d] = base + (unsigned)__popcll(peers);
+  }
+  __syncthreads();
+  {  // thread t = digit t: the four waves' counts -> the run start and each wave's offset in it
+    const unsigned c0 = s_wrun[0][t], c1 = s_wrun[1][t], c2 = s_wrun[2][t], c3 = s_wrun[3][t];
+    const unsigned n = c0 + c1 + c2 + c3;
+    unsigned inc2 = n;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned u = (unsigned)__shfl_up((int)inc2, o);
+      if (lane >= o) inc2 += u;
+    }
+    if (lane == 63) s_part[wv][1] = inc2;
+    __syncthreads();
+    unsigned off = inc2 - n;
+    for (int w = 0; w < wv; ++w) off += s_part[w][1];
+    s_doff[t] = off;
+    s_wrun[0][t] = off;
+    s_wrun[1][t] = off + c0;
+    s_wrun[2][t] = off + c0 + c1;
+    s_wrun[3][t] = off + c0 + c1 + c2;
   }
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < kSortI; ++i) {
-    const int sp = i * kSortT + threadIdx.x;
-    const unsigned vv = s_v[sp];
-    if (vv == kNoEntry) continue;
-    const unsigned kk = s_k[sp], d = (kk >> shift) & 255u;
-    const unsigned pos = Hs[(size_t)d * nch + c] + (unsigned)(sp - s_start[d]);
-    keys_out[pos] = kk;
-    vals_out[pos] = vv;
+  for (int j = 0; j < kLsdI; ++j) {
+    if (e0 + j * 64 + lane < K) {
+      const unsigned idx = s_wrun[wv][(k[j] >> shift) & 255u] + r[j];
+      s_k[idx] = k[j];
+      s_v[idx] = v[j];
+    }
+  }
+  __syncthreads();
+  const int nv = min(kLsdChunk, K - c * kLsdChunk);
+#pragma unroll
+  for (int i = 0; i < kLsdI; ++i) {  // striped: each digit run leaves as coalesced stores
+    const int sp = i * kLsdT + t;
+    if (sp < nv) {
+      const unsigned kk = s_k[sp], d = (kk >> shift) & 255u;
+      const unsigned pos = s_gbase[d] + (unsigned)sp - s_doff[d];
+      keys_out[pos] = kk;
+      vals_out[pos] = s_v[sp];
+    }
   }
 }
 
@@ -2190,23 +2264,21 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       unsigned* tile_keys = reinterpret_cast<unsigned*>(r->keys);
       unsigned* tile_sorted = reinterpret_cast<unsigned*>(r->keys_sorted);
       // the chunked counting sort needs the tile histogram in LDS; above kMaxTiles
-      // tiles rocPRIM onesweep (GSMPM_RASTER_ONESWEEP=1 forces it everywhere).
-      // GSMPM_RASTER_DIGIT_SORT=1: the LSD digit form of the chunked sort above
-      // kMaxTiles instead (bit-identical; bicycle render 2.09 against 1.30 ms)
-      const char* ds = std::getenv("GSMPM_RASTER_DIGIT_SORT");
-      const bool digits = !chunked && !force_onesweep && ds && ds[0] == '1';
+      // tiles the LSD digit sort (k_lsd_*).  GSMPM_RASTER_LSD=0: the library's
+      // onesweep above kMaxTiles instead; GSMPM_RASTER_ONESWEEP=1 forces it everywhere
+      const char* ls = std::getenv("GSMPM_RASTER_LSD");
+      const bool digits = !chunked && !force_onesweep && !(ls && ls[0] == '0');
       const int passes = (bits + 7) / 8;  // ntiles <= 256^passes - 1: the all-ones tile field stays the culled one
       const int nch = (int)div_up(K, kChunk);
+      const int nchl = (int)div_up(K, kLsdChunk);
       size_t need = 0;
       if (digits) {
-        const size_t nh = 256 * (size_t)nch;
+        const size_t nh = 256 * (size_t)nchl;
         if (nh > r->capH) {
           int rc;
           if ((rc = grow((void**)&r->hist, 2 * (nh + nh / 4 + 1024) * sizeof(unsigned)))) return rc;
           r->capH = nh + nh / 4 + 1024;
         }
-        GSMPM_HIP(rocprim::exclusive_scan(nullptr, need, r->hist, r->hist + r->capH, 0u, nh, rocprim::plus<unsigned>(),
-                                          st));
       } else if (chunked) {
         const size_t nh = (ntiles + 1) * (size_t)nch;
         if (nh > r->capH) {
@@ -2272,7 +2344,6 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
         ranges_written = true;
       } else {
         if (digits) {  // passes alternate between the final buffers and spare ones, ending in the final
-          const size_t nh = 256 * (size_t)nch;
           unsigned* Hs = r->hist + r->capH;
           unsigned* alt_k = tile_keys + r->capK;  // the upper half of the 8-byte key buffer
           unsigned* alt_v = r->vals_sorted;       // (the backward's slots; free in the forward)
@@ -2281,12 +2352,11 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
             const bool fin = (passes - 1 - p) % 2 == 0;
             unsigned* dk = fin ? tile_sorted : alt_k;
             unsigned* dv = fin ? r->ids_sorted : alt_v;
-            hipLaunchKernelGGL(k_digit_hist, dim3(nch), dim3(kSortT), 0, st, (int)K, nch, 8 * p, sk, r->hist);
-            GSMPM_LAUNCH_CHECK();
-            bytes = r->sort_tmp_bytes;
-            GSMPM_HIP(rocprim::exclusive_scan(r->sort_tmp, bytes, r->hist, Hs, 0u, nh, rocprim::plus<unsigned>(), st));
-            hipLaunchKernelGGL(k_digit_scatter, dim3(nch), dim3(kSortT), 0, st, (int)K, nch, 8 * p, sk, sv,
-                               (const unsigned*)Hs, dk, dv);
+            hipLaunchKernelGGL(k_lsd_hist, dim3(nchl), dim3(kLsdT), 0, st, (int)K, nchl, 8 * p, sk, r->hist);
+            hipLaunchKernelGGL(k_tile_rows, dim3(64), dim3(256), 0, st, 255, nchl, (const unsigned*)r->hist, Hs,
+                               r->ttot);
+            hipLaunchKernelGGL(k_lsd_scatter, dim3(nchl), dim3(kLsdT), 0, st, (int)K, nchl, 8 * p, sk, sv,
+                               (const unsigned*)Hs, (const unsigned*)r->ttot, dk, dv);
             GSMPM_LAUNCH_CHECK();
             sk = dk;
             sv = dv;

@@ -77,8 +77,12 @@ enum SlabRec : int {
   RF_DEFERRED = 13,                                 // leavers kept for a later migration (payload full)
   RF_CAP = 14,                                      // the slab's particle capacity
   RF_MMIN = 15,                                     // min particle mass (f32 bits; INT_MAX: no particle)
-  kRecInts = 16
+  RF_SLO = 16, RF_SHI = 17,                         // this rank's slab planes [lo, hi)
+  kRecHdr = 20                                      // then ng ints: the particles' base-plane histogram
 };
+// ints of one rank's record: the header and the base-plane histogram (the
+// load every rank needs to re-cut the slabs, slab_host.inc slab_rebalance)
+__host__ __device__ constexpr int rec_ints_of(int ng) { return kRecHdr + ng; }
 // Device flags of a slab (s_flags): sticky until the handle is reset.
 enum SlabFlag : int {
   SF_DRIFT = 0, SF_OOB = 1, SF_DEFERRED = 2, SF_NWANT_OVER = 3, SF_SENDMAX = 4, SF_MIGRATED = 5, kSlabFlags = 8
@@ -90,8 +94,9 @@ struct MigGeom {
   int has_lo, has_hi;
 };
 
-__global__ void k_rec_init(const int* __restrict__ flags, const int* __restrict__ nlive, int capacity,
-                           int* __restrict__ rec) {
+__global__ void k_rec_init(const int* __restrict__ flags, const int* __restrict__ nlive, int capacity, int lo, int hi,
+                           int nrec, int* __restrict__ rec) {
+  for (int i = kRecHdr + threadIdx.x; i < nrec; i += blockDim.x) rec[i] = 0;  // the histogram
   if (threadIdx.x != 0) return;
   rec[RF_FLAGS] = (flags[SF_DRIFT] ? 1 : 0) | (flags[SF_OOB] ? 2 : 0) | (flags[SF_NWANT_OVER] ? 8 : 0);
   rec[RF_N] = *nlive;
@@ -109,13 +114,20 @@ __global__ void k_rec_init(const int* __restrict__ flags, const int* __restrict_
   rec[RF_DEFERRED] = flags[SF_DEFERRED];
   rec[RF_CAP] = capacity;
   rec[RF_MMIN] = INT_MAX;
-  for (int i = RF_MMIN + 1; i < kRecInts; ++i) rec[i] = 0;
+  rec[RF_SLO] = lo;
+  rec[RF_SHI] = hi;
+  for (int i = RF_SHI + 1; i < kRecHdr; ++i) rec[i] = 0;
 }
 
 // yz box of the particles' base nodes (trunc(x * inv_dx - 0.5), utils.py:95),
 // max |v_y|, |v_z| and the particles within `margin` planes of each bound (the
 // most that can leave by the next migration) -> rec (after k_rec_init).
-__global__ __launch_bounds__(256) void k_slab_record(Particles ps, MigGeom mg, int margin, int* __restrict__ rec) {
+constexpr int kRecMaxNg = 4096;  // the LDS histogram of k_slab_record
+__global__ __launch_bounds__(256) void k_slab_record(Particles ps, MigGeom mg, int margin, int ng,
+                                                     int* __restrict__ rec) {
+  __shared__ int s_h[kRecMaxNg];
+  for (int i = threadIdx.x; i < ng; i += 256) s_h[i] = 0;
+  __syncthreads();
   int v[4] = {INT_MAX, INT_MIN, INT_MAX, INT_MIN};
   float vy = 0.f, vz = 0.f, mmin = __int_as_float(INT_MAX);  // INT_MAX bits: a NaN above every finite mass
   int blo = 0, bhi = 0;
@@ -132,7 +144,11 @@ __global__ __launch_bounds__(256) void k_slab_record(Particles ps, MigGeom mg, i
     mmin = __int_as_float(min(__float_as_int(mmin), __float_as_int(ps.ld(PMASS, p))));
     blo += (bx < mg.lo + margin) ? 1 : 0;
     bhi += (bx >= mg.hi - margin) ? 1 : 0;
+    atomicAdd(&s_h[min(max(bx, 0), ng - 1)], 1);
   }
+  __syncthreads();
+  for (int i = threadIdx.x; i < ng; i += 256)
+    if (s_h[i]) atomicAdd(rec + kRecHdr + i, s_h[i]);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     v[0] = min(v[0], __shfl_xor(v[0], o));

@@ -92,6 +92,9 @@ _SIGS = {
     "gsmpm_mpm_get_gid": (ctypes.c_int, [c_void_p, c_void_p, c_void_p]),
     "gsmpm_mpm_slab_stats": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int64)]),
     "gsmpm_mpm_slab_rects": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int32)]),
+    "gsmpm_mpm_slab_set_rebalance": (ctypes.c_int, [c_void_p, ctypes.c_int32, ctypes.c_float]),
+    "gsmpm_mpm_slab_bounds": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32,
+                                             ctypes.POINTER(ctypes.c_int64)]),
     "gsmpm_mpm_resort": (ctypes.c_int, [c_void_p, ctypes.c_int32, c_void_p]),
     "gsmpm_mpm_set_rebin_interval": (ctypes.c_int, [c_void_p, ctypes.c_int32]),
     "gsmpm_mpm_pipeline": (ctypes.c_int, [c_void_p]),

@@ -162,7 +162,8 @@ class SlabDomain:
 
     def __init__(self, x_grid, cov6, vol, *, rank: int, world: int, transport, n_grid: int, grid_extent: float = 2.0,
                  margin: int = 2, interval: int = 10, capacity: int | None = None, v=None, device=None,
-                 engine_factory=None, group=None, **sim_kwargs):
+                 engine_factory=None, group=None, rebalance: bool = True, rebalance_tol: float = 0.10,
+                 **sim_kwargs):
         from .sim import Simulator
         engine_factory = engine_factory or Simulator
         self.rank, self.world, self.transport = int(rank), int(world), transport
@@ -172,17 +173,33 @@ class SlabDomain:
         self.margin, self.interval = int(margin), int(interval)
         xh = (x_grid.detach().cpu().numpy() if torch.is_tensor(x_grid) else np.asarray(x_grid)).reshape(-1, 3)
         self.n_total = len(xh)
-        self.bounds = slab_bounds(xh, self.n_grid, self.grid_extent, self.world, margin)
-        owner = owner_of(xh, self.bounds, self.n_grid, self.grid_extent)
+        self._bounds0 = slab_bounds(xh, self.n_grid, self.grid_extent, self.world, margin)
+        owner = owner_of(xh, self._bounds0, self.n_grid, self.grid_extent)
         mine = torch.from_numpy(np.nonzero(owner == self.rank)[0]).to(self.device)
         cap = capacity or max(4096, 2 * (self.n_total // self.world) + 4096)
         self.engine = engine_factory(cap, n_grid=self.n_grid, grid_extent=self.grid_extent, device=self.device,
                                      **sim_kwargs)
-        self.engine.slab_init(self.rank, self.world, self.bounds[self.rank], self.bounds[self.rank + 1], margin,
+        self.engine.slab_init(self.rank, self.world, self._bounds0[self.rank], self._bounds0[self.rank + 1], margin,
                               interval)
+        if hasattr(self.engine, "slab_set_rebalance"):  # the library re-cuts by itself (slab_host.inc)
+            self.engine.slab_set_rebalance(rebalance, rebalance_tol)
         t = lambda a: (a if torch.is_tensor(a) else torch.from_numpy(np.ascontiguousarray(a))).to(self.device)
         sel = lambda a: None if a is None else t(a).reshape(self.n_total, -1)[mine]
         self.engine.slab_set_particles(sel(x_grid), sel(cov6), sel(vol), mine.to(torch.int32), v=sel(v))
+
+    @property
+    def bounds(self):
+        """Every slab's current planes [world + 1]: the init quantiles until the
+        library re-cuts them (every rank computes the same re-cut)."""
+        if hasattr(self.engine, "slab_bounds"):
+            b, _ = self.engine.slab_bounds(self.world)
+            if min(b) >= 0:
+                return b
+        return list(self._bounds0)
+
+    @property
+    def rebalances(self) -> int:
+        return self.engine.slab_bounds(self.world)[1] if hasattr(self.engine, "slab_bounds") else 0
 
     # configuration and stepping: the engine's, with the transport
     def add_fixed_cube(self, center, size):

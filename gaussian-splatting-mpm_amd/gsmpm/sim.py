@@ -150,6 +150,19 @@ class Simulator:
         check(LIB.gsmpm_mpm_slab_rects(self._h, b), "gsmpm_mpm_slab_rects")
         return [tuple(int(v) for v in b[4 * w:4 * w + 4]) for w in (0, 1)]
 
+    def slab_set_rebalance(self, on: bool = True, tolerance: float = 0.10):
+        """Re-cut the slabs at step-call boundaries when the most loaded one holds
+        more than (1 + tolerance) x the mean (gsmpm_mpm_slab_set_rebalance)."""
+        check(LIB.gsmpm_mpm_slab_set_rebalance(self._h, 1 if on else 0, ctypes.c_float(tolerance)),
+              "gsmpm_mpm_slab_set_rebalance")
+
+    def slab_bounds(self, world: int):
+        """(every slab's bounds [world + 1], re-cuts so far)."""
+        b = (ctypes.c_int32 * (world + 1))()
+        n = ctypes.c_int64(0)
+        check(LIB.gsmpm_mpm_slab_bounds(self._h, b, world + 1, ctypes.byref(n)), "gsmpm_mpm_slab_bounds")
+        return [int(v) for v in b], int(n.value)
+
     def profile(self, dt: float, masks):
         """Eager substeps with a hipEvent pair per kernel -> summed ms of
         (k_p2g, k_grid, k_g2p, binning); fused pipeline: (k_fused, k_grid_f, binning, 0)."""

@@ -167,6 +167,16 @@ int gsmpm_mpm_slab_stats(gsmpm_mpm* h, int64_t out12[12]);
  * upper one (ny = nz = 0: nothing to exchange; before the first slab_step, the
  * whole cross-section). */
 int gsmpm_mpm_slab_rects(gsmpm_mpm* h, int32_t out8[8]);
+/* Re-cutting the slabs ("rebalance per frame"; on by default,
+ * tolerance 0.10): at the end of a step call, when the most loaded slab holds
+ * more than (1 + tolerance) x the mean particle count, every rank moves the
+ * bounds to the count quantiles of all ranks' base-plane histograms (the same
+ * records on every rank: the same bounds), each bound staying inside its old
+ * neighbouring slabs; the next call opens with the migration to them. */
+int gsmpm_mpm_slab_set_rebalance(gsmpm_mpm* h, int32_t on, float tolerance);
+/* The current bounds of every slab, out[world + 1] (before the first step call
+ * only this rank's own two, the rest -1), and the re-cuts made so far. */
+int gsmpm_mpm_slab_bounds(gsmpm_mpm* h, int32_t* out, int32_t n, int64_t* rebalances);
 
 /* Re-sort particle storage into Morton order of the current cells now (only
  * summation order changes; rows stay in caller order).  interval >= 0 also sets

@@ -277,10 +277,11 @@ def test_num_rendered_and_radii_exact(dev, P, W, H, tiles):
 @pytest.mark.parametrize("P,W,H,tiles", [(6000, 272, 3856, 4097), (20000, 1600, 1200, 7500),
                                          (20000, 4200, 4200, 69169)])
 def test_digit_tile_sort_matches_onesweep(dev, monkeypatch, P, W, H, tiles):
-    """Above 4,096 tiles, the chunked LSD digit sort (GSMPM_RASTER_DIGIT_SORT=1:
-    two 8-bit passes; three above 65,535 tiles) against rocPRIM onesweep (the
-    default there): pixels, final T, last contributor and every gradient equal
-    bit for bit -- both are stable sorts of the same depth-ordered emission."""
+    """Above 4,096 tiles, the hand-written LSD digit sort (k_lsd_*, the default
+    there: two 8-bit passes, three above 65,535 tiles) against the library's
+    onesweep (GSMPM_RASTER_LSD=0): pixels, final T, last contributor and every
+    gradient equal bit for bit -- both are stable sorts of the same
+    depth-ordered emission."""
     import torch
     from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
     assert ((W + 15) // 16) * ((H + 15) // 16) == tiles
@@ -295,7 +296,7 @@ def test_digit_tile_sort_matches_onesweep(dev, monkeypatch, P, W, H, tiles):
                                        debug=False)
     out = {}
     for os_ in ("1", "0"):
-        monkeypatch.setenv("GSMPM_RASTER_DIGIT_SORT", "0" if os_ == "1" else "1")
+        monkeypatch.setenv("GSMPM_RASTER_LSD", "0" if os_ == "1" else "1")
         m3, o1, s1, cv = t(means, True), t(opa, True), t(shs, True), t(c6, True)
         img, radii = GaussianRasterizer(st)(means3D=m3, means2D=None, opacities=o1, shs=s1, cov3D_precomp=cv)
         (img * wgt).sum().backward()

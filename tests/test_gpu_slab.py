@@ -191,6 +191,97 @@ def test_gpu_slab_error_stops_every_rank(dev, tmp_path):
     assert int(migs) <= STEPS // 10, migs  # errors surface at the end of the step call, on every rank
 
 
+DRIFT_VX = 30.0  # grid units / s: ~19 planes over 200 substeps (0.096 a substep, < margin per interval)
+
+
+def _drift_scene():
+    x, v, cov, vol = scene()
+    v = v.copy()
+    v[:, 0] += np.float32(DRIFT_VX - 4.0)
+    return x, v, cov, vol
+
+
+def _rebalance_worker(rank, world, port, out, backend, rebalance):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if backend == "nccl-shared":
+        os.environ.update(shared_gpu_rccl_env(rank))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    if backend == "nccl-shared":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gsmpm.dist import SlabDomain, make_transport
+        x, v, cov, vol = _drift_scene()
+        xp = make_transport(rank, world, device=dev)
+        dom = SlabDomain(x, cov, vol, v=v, rank=rank, world=world, transport=xp, n_grid=NG, grid_extent=EXT,
+                         margin=2, interval=10, device=dev, jelly_fcr=True, rebalance=rebalance, **KW)
+        dom.add_plane_collider([0, 0, 0.4], [0, 0, 1])
+        b0 = list(dom.bounds)
+        imb = []
+        for _ in range(20):  # 20 calls of 10 substeps: a re-cut can follow every call
+            dom.step(DT, [1] * 10)
+            cnt = torch.tensor([dom.n], dtype=torch.int64, device=dev if backend != "gloo" else "cpu")
+            allc = [torch.zeros_like(cnt) for _ in range(world)]
+            dist.all_gather(allc, cnt)
+            c = [int(t.item()) for t in allc]
+            imb.append(max(c) / (sum(c) / world))
+        got = {k: dom.gather_field(k) for k in ("x", "v", "C", "F_trial")}
+        if rank == 0:
+            np.savez(os.path.join(out, "rebal.npz"), imb=np.array(imb), b0=np.array(b0), b1=np.array(dom.bounds),
+                     rebalances=dom.rebalances, **{k: g.cpu().numpy() for k, g in got.items()})
+        dom.engine.close()
+        xp.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("backend,world", [("gloo", 2), ("gloo", 3), ("nccl-shared", 2)])
+def test_gpu_slabs_rebalance_drifting_scene(dev, tmp_path, backend, world):
+    """SURVEY 8(e) "rebalance per frame": a scene drifting ~19 planes along
+    the cut axis -- more than half a slab -- over 200 substeps in 20 step
+    calls.  With re-cutting on (the default) the library moves the bounds to
+    the count quantiles of all ranks' base-plane histograms at call
+    boundaries (slab_host.inc slab_rebalance; the next call opens with the
+    migration to them): after every call the most loaded slab stays within
+    10 % of the mean (+ the ~1 plane one call drifts), and the state matches
+    the single-domain oracle.  The control without re-cutting ends far out
+    of balance."""
+    import oracle as O
+    mp.spawn(_rebalance_worker, args=(world, free_port(), str(tmp_path), backend, True), nprocs=world, join=True)
+    r = np.load(os.path.join(tmp_path, "rebal.npz"))
+    x, v, cov, vol = _drift_scene()
+    ref = O.OracleMPM(x, cov, vol, v=v, n_grid=NG, grid_extent=EXT, jelly_quirk=False, **KW)
+    ref.add_collider([0, 0, 0.4], [0, 0, 1])
+    for _ in range(200):
+        ref.substep(DT, op_active=[1])
+    moved = float((ref.x[:, 0] - x[:, 0]).mean() * NG / EXT)
+    half_slab = NG / world / 2
+    assert moved > half_slab, (moved, half_slab)  # the scene drifts more than half a slab
+    errs = {k: rel_err(r[k], getattr(ref, k)) for k in ("x", "v", "C", "F_trial")}
+    rec = {"backend": backend, "world": world, "rebalances": int(r["rebalances"]), "bounds_init": r["b0"].tolist(),
+           "bounds_end": r["b1"].tolist(), "imbalance_per_call": [round(float(v), 4) for v in r["imb"]],
+           "mean_drift_planes": moved, "errs": errs}
+    print("rebalance", rec)
+    from test_gpu_configs import _dump
+    _dump(f"slab_rebalance_{backend}_{world}", rec)
+    assert int(r["rebalances"]) >= 1 and r["b1"].tolist() != r["b0"].tolist(), rec
+    assert float(r["imb"][-5:].max()) <= 1.10 + 0.05, rec
+    for k, e in errs.items():
+        assert e < TOL.get(k, 1e-4), (k, e, errs)
+
+
+def test_gpu_slabs_no_rebalance_control(dev, tmp_path):
+    """The control of the test above: the same drifting scene with re-cutting
+    off ends out of balance (so the re-cut is what balances it)."""
+    world = 2
+    mp.spawn(_rebalance_worker, args=(world, free_port(), str(tmp_path), "gloo", False), nprocs=world, join=True)
+    r = np.load(os.path.join(tmp_path, "rebal.npz"))
+    assert int(r["rebalances"]) == 0 and r["b1"].tolist() == r["b0"].tolist()
+    assert float(r["imb"][-1]) > 1.3, r["imb"].tolist()
+
+
 IMPULSE = ([1.0, 1.0, 0.8], [0.4, 0.4, 0.4], [0.0, 300.0, 0.0])  # center, half-size, force (grid units)
 IMP_ON = range(10, 20)  # substeps of the one 100-substep call on which it fires
 
