@@ -16,8 +16,9 @@
 //   k_dsort_hist     bucket b = (bits - lo) >> shift (NB buckets spanning
 //                    [lo, hi]): count and tiles-word sum per bucket
 //                    (returnless global atomics)
-//   k_dsort_scan     one workgroup: exclusive scans of the bucket counts and
-//                    sums, the list of occupied buckets (small and big ones)
+//   k_dsort_scan1/2  exclusive scans of the bucket counts and sums (block
+//                    totals, then each block's scan), the lists of occupied
+//                    buckets (small and big ones)
 //   k_dsort_scatter  every visible Gaussian to its bucket's run (returning
 //                    atomic cursor: any order inside the run); culled ones to
 //                    the tail [Pv, P) (they carry no pair)
@@ -59,7 +60,8 @@ enum : int {
 };
 
 // bytes of the depth-order state (fixed layout at the start of a workspace)
-constexpr size_t kDsStateBytes = kDsWords * 4 + (size_t)kDsNBMax * (4 + 8);  // dstate, bcount, bsum
+constexpr size_t kDsStateBytes =  // dstate, bcount, bsum, then the block totals (scratch)
+    kDsWords * 4 + (size_t)kDsNBMax * (4 + 8) + (size_t)(kDsNBMax / 1024) * (4 + 8);
 
 struct DsortBufs {
   unsigned* st;                // dstate [kDsWords]
@@ -72,6 +74,8 @@ struct DsortBufs {
   unsigned* bbig;              // [kDsNBMax]  occupied buckets above
   unsigned* dkey;              // [P] depth bits by bucket run
   unsigned* dval;              // [P] Gaussian index by bucket run
+  unsigned* btc;               // [kDsNBMax / kDsBlk] block totals of the counts
+  unsigned long long* bts;     // [kDsNBMax / kDsBlk] ... of the tiles-word sums
 };
 
 __device__ __forceinline__ int ds_log2(int nb) { return 31 - __clz(nb); }
@@ -107,93 +111,185 @@ __device__ __forceinline__ void ds_minmax(unsigned* st, bool vis, unsigned bits)
 
 __global__ __launch_bounds__(256) void k_dsort_hist(int P, int nb, const float* __restrict__ depth,
                                                     const unsigned long long* __restrict__ tiles, DsortBufs d) {
+  __shared__ unsigned s_lo;
+  __shared__ int s_shift;
+  if (threadIdx.x == 0) {
+    unsigned lo;
+    int shift;
+    ds_range(d.st, nb, lo, shift);
+    s_lo = lo;
+    s_shift = shift;
+  }
+  __syncthreads();
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= P) return;
   const unsigned long long tw = tiles[i];
   if (tw == 0ull) return;  // culled (k_preprocess wrote no depth)
-  unsigned lo;
-  int shift;
-  ds_range(d.st, nb, lo, shift);
-  const unsigned b = (__float_as_uint(depth[i]) - lo) >> shift;
+  const unsigned b = (__float_as_uint(depth[i]) - s_lo) >> s_shift;
   __hip_atomic_fetch_add(d.bcount + b, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_fetch_add(d.bsum + b, tw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// one workgroup: exclusive scans of counts and sums over the nb buckets, in
-// coalesced passes of 1,024 buckets (a bucket per lane: wave scans, then the
-// 16 wave totals through LDS, a running carry across passes)
-__global__ __launch_bounds__(kDsScanT) void k_dsort_scan(int nb, DsortBufs d) {
-  __shared__ unsigned s_wc[kDsScanT / 64];
-  __shared__ unsigned long long s_ws[kDsScanT / 64];
-  __shared__ unsigned s_nl, s_nb, s_over, s_maxn;
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  if (t == 0) s_nl = s_nb = s_over = s_maxn = 0;
-  unsigned carry_c = 0;
-  unsigned long long carry_s = 0;
-  for (int b0 = 0; b0 < nb; b0 += kDsScanT) {  // workgroup-uniform
-    const int b = b0 + t;
-    const unsigned n = d.bcount[b];
-    const unsigned long long sm = d.bsum[b];
-    unsigned ic = n;
-    unsigned long long is = sm;
+// Exclusive scans of the bucket counts and tiles-word sums over the nb
+// buckets, in two launches of nb / 1,024 workgroups (a block of 1,024 buckets
+// each, 4 per lane, coalesced): k_dsort_scan1 writes every block's totals,
+// k_dsort_scan2 adds the totals of the blocks before its own (<= 64 values)
+// to its block's scan and lists the occupied buckets (one list reservation
+// per workgroup).  Round 4's first form scanned in one workgroup and cost
+// ~50 us on the lego frame (latency-bound passes over 16k buckets).
+constexpr int kDsBlk = 1024;
+__device__ __forceinline__ unsigned ds_block_sum_u32(unsigned v, unsigned* s_tmp) {
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const unsigned uc = (unsigned)__shfl_up((int)ic, o);
-      const unsigned long long us = __shfl_up(is, o);
-      if (lane >= o) {
-        ic += uc;
-        is += us;
-      }
-    }
-    if (lane == 63) {
-      s_wc[wv] = ic;
-      s_ws[wv] = is;
-    }
-    __syncthreads();
-    unsigned pc = carry_c, tc = 0;
-    unsigned long long ps = carry_s, ts = 0;
+  for (int o = 32; o > 0; o >>= 1) v += (unsigned)__shfl_xor((int)v, o);
+  if ((threadIdx.x & 63) == 0) s_tmp[threadIdx.x >> 6] = v;
+  __syncthreads();
+  v = s_tmp[0] + s_tmp[1] + s_tmp[2] + s_tmp[3];
+  __syncthreads();
+  return v;
+}
+__device__ __forceinline__ unsigned long long ds_block_sum_u64(unsigned long long v, unsigned long long* s_tmp) {
 #pragma unroll
-    for (int q = 0; q < kDsScanT / 64; ++q) {
-      const unsigned xc = s_wc[q];
-      const unsigned long long xs = s_ws[q];
-      if (q < wv) {
-        pc += xc;
-        ps += xs;
-      }
-      tc += xc;
-      ts += xs;
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) s_tmp[threadIdx.x >> 6] = v;
+  __syncthreads();
+  v = s_tmp[0] + s_tmp[1] + s_tmp[2] + s_tmp[3];
+  __syncthreads();
+  return v;
+}
+__global__ __launch_bounds__(256) void k_dsort_scan1(DsortBufs d, unsigned* __restrict__ btc,
+                                                     unsigned long long* __restrict__ bts) {
+  __shared__ unsigned s_c[4];
+  __shared__ unsigned long long s_s[4];
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the list counters k_dsort_scan2 reserves from
+    d.st[DS_NLIST] = 0;
+    d.st[DS_NBIG] = 0;
+    d.st[DS_OVER] = 0;
+    d.st[DS_MAXN] = 0;
+  }
+  const int b = blockIdx.x * kDsBlk + 4 * threadIdx.x;
+  const uint4 c4 = *reinterpret_cast<const uint4*>(d.bcount + b);
+  const ulonglong2 s01 = *reinterpret_cast<const ulonglong2*>(d.bsum + b);
+  const ulonglong2 s23 = *reinterpret_cast<const ulonglong2*>(d.bsum + b + 2);
+  const unsigned c = ds_block_sum_u32(c4.x + c4.y + c4.z + c4.w, s_c);
+  const unsigned long long sm = ds_block_sum_u64(s01.x + s01.y + s23.x + s23.y, s_s);
+  if (threadIdx.x == 0) {
+    btc[blockIdx.x] = c;
+    bts[blockIdx.x] = sm;
+  }
+}
+__global__ __launch_bounds__(256) void k_dsort_scan2(int nb, DsortBufs d, const unsigned* __restrict__ btc,
+                                                     const unsigned long long* __restrict__ bts) {
+  __shared__ unsigned s_c[4], s_f[4], s_wf[4], s_base[2];
+  __shared__ unsigned long long s_s[4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = blockIdx.x, ng = nb / kDsBlk;
+  // the totals of the blocks before this one (and of all, for the last block)
+  unsigned pc = 0, ac = 0;
+  unsigned long long ps = 0, as = 0;
+  for (int q = lane; q < ng; q += 64) {  // every wave alike: no LDS needed
+    const unsigned xc = btc[q];
+    const unsigned long long xs = bts[q];
+    if (q < g) {
+      pc += xc;
+      ps += xs;
     }
-    if (n) {
-      d.bbase[b] = pc + ic - n;
-      d.bcur[b] = pc + ic - n;
-      d.bpre[b] = ps + is - sm;
-      if (n <= (unsigned)kDsSmall) {
-        d.blist[atomicAdd(&s_nl, 1u)] = (unsigned)b;
-      } else {
-        d.bbig[atomicAdd(&s_nb, 1u)] = (unsigned)b;
-        if (n > (unsigned)kDsBig) s_over = 1u;
-      }
-      atomicMax(&s_maxn, n);
+    ac += xc;
+    as += xs;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    pc += (unsigned)__shfl_xor((int)pc, o);
+    ac += (unsigned)__shfl_xor((int)ac, o);
+    ps += __shfl_xor(ps, o);
+    as += __shfl_xor(as, o);
+  }
+  const int b = g * kDsBlk + 4 * t;
+  const uint4 c4 = *reinterpret_cast<const uint4*>(d.bcount + b);
+  const ulonglong2 s01 = *reinterpret_cast<const ulonglong2*>(d.bsum + b);
+  const ulonglong2 s23 = *reinterpret_cast<const ulonglong2*>(d.bsum + b + 2);
+  const unsigned n[4] = {c4.x, c4.y, c4.z, c4.w};
+  const unsigned long long sm[4] = {s01.x, s01.y, s23.x, s23.y};
+  unsigned lc = n[0] + n[1] + n[2] + n[3];
+  unsigned long long ls = sm[0] + sm[1] + sm[2] + sm[3];
+  unsigned fl = (n[0] != 0) + (n[1] != 0) + (n[2] != 0) + (n[3] != 0);  // occupied small
+  unsigned fb = 0, mx = max(max(n[0], n[1]), max(n[2], n[3]));
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    fl -= n[q] > (unsigned)kDsSmall ? 1u : 0u;
+    fb += n[q] > (unsigned)kDsSmall ? 1u : 0u;
+  }
+  // workgroup exclusive scans of (count, sum, small flags, big flags)
+  unsigned ic = lc, ifl = fl, ifb = fb;
+  unsigned long long is = ls;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned uc = (unsigned)__shfl_up((int)ic, o), uf = (unsigned)__shfl_up((int)ifl, o),
+                   ub = (unsigned)__shfl_up((int)ifb, o);
+    const unsigned long long us = __shfl_up(is, o);
+    if (lane >= o) {
+      ic += uc;
+      ifl += uf;
+      ifb += ub;
+      is += us;
     }
-    carry_c += tc;
-    carry_s += ts;
-    __syncthreads();  // s_wc / s_ws reused by the next pass
+  }
+  if (lane == 63) {
+    s_c[wv] = ic;
+    s_s[wv] = is;
+    s_f[wv] = ifl;
+    s_wf[wv] = ifb;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
+  __syncthreads();
+  unsigned wc = 0, wfl = 0, wfb = 0, tfl = 0, tfb = 0;
+  unsigned long long ws = 0;
+  for (int q = 0; q < 4; ++q) {
+    if (q < wv) {
+      wc += s_c[q];
+      ws += s_s[q];
+      wfl += s_f[q];
+      wfb += s_wf[q];
+    }
+    tfl += s_f[q];
+    tfb += s_wf[q];
   }
   if (t == 0) {
+    s_base[0] = tfl ? atomicAdd(d.st + DS_NLIST, tfl) : 0u;
+    s_base[1] = tfb ? atomicAdd(d.st + DS_NBIG, tfb) : 0u;
+  }
+  if (lane == 0 && mx) atomicMax(d.st + DS_MAXN, mx);
+  __syncthreads();
+  unsigned run = pc + wc + ic - lc;
+  unsigned long long pre = ps + ws + is - ls;
+  unsigned li = s_base[0] + wfl + ifl - fl, bi = s_base[1] + wfb + ifb - fb;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (n[q]) {
+      const int bb = b + q;
+      d.bbase[bb] = run;
+      d.bcur[bb] = run;
+      d.bpre[bb] = pre;
+      if (n[q] <= (unsigned)kDsSmall) {
+        d.blist[li++] = (unsigned)bb;
+      } else {
+        d.bbig[bi++] = (unsigned)bb;
+        if (n[q] > (unsigned)kDsBig) d.st[DS_OVER] = 1u;
+      }
+      run += n[q];
+      pre += sm[q];
+    }
+  }
+  if (g == ng - 1 && t == 0) {
     unsigned lo;
     int shift;
     ds_range(d.st, nb, lo, shift);
     d.st[DS_LO] = lo;
     d.st[DS_SHIFT] = (unsigned)shift;
     d.st[DS_NB] = (unsigned)nb;
-    d.st[DS_NLIST] = s_nl;
-    d.st[DS_NBIG] = s_nb;
-    d.st[DS_OVER] = s_over;
-    d.st[DS_MAXN] = s_maxn;
-    d.st[DS_PV] = carry_c;
+    d.st[DS_PV] = ac;
     d.st[DS_CULL] = 0;
-    d.st[DS_TOT] = (unsigned)carry_s;
-    d.st[DS_TOT + 1] = (unsigned)(carry_s >> 32);
+    d.st[DS_TOT] = (unsigned)as;
+    d.st[DS_TOT + 1] = (unsigned)(as >> 32);
   }
 }
 

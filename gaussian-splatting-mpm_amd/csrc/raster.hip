@@ -1865,6 +1865,8 @@ static DsortBufs dsort_bufs(gsmpm_raster* r) {
   d.bbig = r->ds_bbig;
   d.dkey = r->ds_key;
   d.dval = r->ds_val;
+  d.bts = d.st ? reinterpret_cast<unsigned long long*>(d.bsum + kDsNBMax) : nullptr;
+  d.btc = d.st ? reinterpret_cast<unsigned*>(d.bts + kDsNBMax / kDsBlk) : nullptr;
   return d;
 }
 // buckets of the depth order: a power of two, ~8 visible Gaussians a bucket, in [1024, kDsNBMax]
@@ -2187,10 +2189,14 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       const int nb = dsort_buckets(P);
       hipLaunchKernelGGL(k_dsort_hist, dim3(div_up(P, 256)), dim3(256), 0, st, P, nb, (const float*)r->depth,
                          (const unsigned long long*)r->tiles, db);
-      hipLaunchKernelGGL(k_dsort_scan, dim3(1), dim3(kDsScanT), 0, st, nb, db);
+      hipLaunchKernelGGL(k_dsort_scan1, dim3(nb / kDsBlk), dim3(256), 0, st, db, db.btc, db.bts);
+      hipLaunchKernelGGL(k_dsort_scan2, dim3(nb / kDsBlk), dim3(256), 0, st, nb, db, (const unsigned*)db.btc,
+                         (const unsigned long long*)db.bts);
       hipLaunchKernelGGL(k_dsort_scatter, dim3(div_up(P, 256)), dim3(256), 0, st, P, (const float*)r->depth,
                          (const unsigned long long*)r->tiles, db, r->dorder, r->offr);
-      hipLaunchKernelGGL(k_dsort_small, dim3((unsigned)std::max(1, std::min(4096, div_up(std::min(nb, P), 16)))),
+      // a wave per bucket, up to one bucket per wave at ~8 Gaussians a bucket (one pass: the loop's
+      // dependent loads -- list entry, bucket record, keys -- are the cost)
+      hipLaunchKernelGGL(k_dsort_small, dim3((unsigned)std::max(1, std::min(16384, div_up(std::min(nb, P), 4)))),
                          dim3(256), 0, st, (const unsigned long long*)r->tiles, db, r->dorder, r->offr);
       hipLaunchKernelGGL(k_dsort_big, dim3(256), dim3(1024), 0, st, (const unsigned long long*)r->tiles, db,
                          r->dorder, r->offr);

@@ -173,6 +173,15 @@ class SlabDomain:
         self.margin, self.interval = int(margin), int(interval)
         xh = (x_grid.detach().cpu().numpy() if torch.is_tensor(x_grid) else np.asarray(x_grid)).reshape(-1, 3)
         self.n_total = len(xh)
+        # SURVEY 8(e) cuts along the bbox's longest axis.  The library's slabs are
+        # planes of grid axis 0; every BASELINE scene has axis 0 among its longest
+        # (lego: x and y tie at 1.3; bicycle: a cube).  A scene whose axis 0 is
+        # clearly shorter is still correct, only less evenly cut: say so.
+        ext = (xh.max(0) - xh.min(0)) if len(xh) else np.zeros(3)
+        self.cut_axis_ratio = float(ext[0] / max(float(ext.max()), 1e-30)) if len(xh) else 1.0
+        if self.cut_axis_ratio < 0.9 and self.rank == 0:
+            import warnings
+            warnings.warn(f"slab cut along axis 0, which spans {self.cut_axis_ratio:.2f} of the bbox's longest axis")
         self._bounds0 = slab_bounds(xh, self.n_grid, self.grid_extent, self.world, margin)
         owner = owner_of(xh, self._bounds0, self.n_grid, self.grid_extent)
         mine = torch.from_numpy(np.nonzero(owner == self.rank)[0]).to(self.device)
