@@ -1006,6 +1006,11 @@ __global__ __launch_bounds__(256) void k_tile_rows(int ntiles, int nch, const un
   if (lane == 0) tot[t] = carry;
 }
 
+// GSMPM_TILE_BRS=1 (A/B build): the chunk's stable order from the library's
+// block radix sort instead of the wave-ballot ranks below
+#ifndef GSMPM_TILE_BRS
+#define GSMPM_TILE_BRS 0
+#endif
 __global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int nch, int bits,
                                                          const unsigned* __restrict__ keys,
                                                          const unsigned* __restrict__ vals,
@@ -1013,14 +1018,13 @@ __global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int 
                                                          const unsigned* __restrict__ tot,
                                                          unsigned* __restrict__ keys_out, unsigned* __restrict__ vals_out,
                                                          uint2* __restrict__ ranges, int* __restrict__ dsort_counts) {
-  using BRS = rocprim::block_radix_sort<unsigned, kSortT, kSortI, unsigned>;
   if (dsort_counts && blockIdx.x == 0 && threadIdx.x < 2) dsort_counts[threadIdx.x] = 0;  // k_tile_dsort's lists
-  __shared__ typename BRS::storage_type s_sort;
   __shared__ unsigned s_k[kChunk], s_v[kChunk];
-  __shared__ int s_start[kMaxTiles + 1];
+  __shared__ int s_start[kMaxTiles + 1];    // chunk-local start of each tile's run
   __shared__ unsigned s_ts[kMaxTiles + 2];  // exclusive scan of the tile totals: each tile's run start
   __shared__ unsigned s_part[kSortT];
   const int c = blockIdx.x;
+  const unsigned lowmask = (1u << bits) - 1u;  // >= ntiles
   {
     const int per = (ntiles + 1 + kSortT - 1) / kSortT, t0 = threadIdx.x * per;
     unsigned sum = 0;
@@ -1041,7 +1045,9 @@ __global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int 
       }
     if (threadIdx.x == kSortT - 1) s_ts[ntiles + 1] = run;
   }
-  const unsigned lowmask = (1u << bits) - 1u;  // >= ntiles
+#if GSMPM_TILE_BRS
+  using BRS = rocprim::block_radix_sort<unsigned, kSortT, kSortI, unsigned>;
+  __shared__ typename BRS::storage_type s_sort;
   unsigned k[kSortI], v[kSortI];
 #pragma unroll
   for (int i = 0; i < kSortI; ++i) {
@@ -1060,6 +1066,83 @@ __global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int 
     if (s_v[sp] != kNoEntry && (sp == 0 || sort_tile(s_k[sp - 1], lowmask, ntiles) != t)) s_start[t] = sp;
   }
   __syncthreads();
+#else
+  // The chunk's stable order by tile, without a block sort: wave w ranks its
+  // 512 pairs [w * 512, +512) of the chunk in 8 slots of 64, in order, by
+  // matching lanes of equal tile with 13 ballots and a wave-private running
+  // count per tile (LDS); the four waves' counts then give every tile's run
+  // start in the chunk and each wave's offset inside it.  The rank follows
+  // (wave, slot, lane) = the chunk's order: stable, as the block sort was.
+  __shared__ unsigned s_cnt[4][kMaxTiles + 1];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int e = threadIdx.x; e < 4 * (kMaxTiles + 1); e += kSortT) (&s_cnt[0][0])[e] = 0u;
+  __syncthreads();
+  constexpr int kW = kChunk / 4;  // pairs per wave
+  const int e0 = c * kChunk + wv * kW;
+  unsigned k[kSortI], v[kSortI], r[kSortI], tl[kSortI];
+#pragma unroll
+  for (int j = 0; j < kSortI; ++j) {
+    const int e = e0 + j * 64 + lane;
+    k[j] = e < K ? keys[e] : 0u;
+    v[j] = e < K ? vals[e] : 0u;
+    tl[j] = e < K ? sort_tile(k[j], lowmask, ntiles) : 8191u;  // 8191: no pair (13 bits, > any tile)
+  }
+  const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int j = 0; j < kSortI; ++j) {
+    const unsigned d = tl[j];
+    unsigned long long peers = ~0ull;
+#pragma unroll
+    for (int b = 0; b < 13; ++b) {
+      const unsigned long long bal = __ballot((d >> b) & 1u);
+      peers &= ((d >> b) & 1u) ? bal : ~bal;
+    }
+    const unsigned rk = (unsigned)__popcll(peers & below);
+    const bool ok = d != 8191u;
+    const unsigned base = ok ? s_cnt[wv][d] : 0u;
+    r[j] = base + rk;
+    // the tile's lowest lane moves the count on (the wave's LDS operations are in order)
+    if (ok && rk == 0) s_cnt[wv][d] = base + (unsigned)__popcll(peers);
+  }
+  __syncthreads();
+  {  // per tile: the run start in the chunk (scan of the four waves' counts) and each wave's offset
+    const int per = (ntiles + 1 + kSortT - 1) / kSortT, t0 = threadIdx.x * per;
+    unsigned sum = 0;
+    for (int q = 0; q < per; ++q)
+      if (t0 + q <= ntiles) sum += s_cnt[0][t0 + q] + s_cnt[1][t0 + q] + s_cnt[2][t0 + q] + s_cnt[3][t0 + q];
+    s_part[threadIdx.x] = sum;
+    __syncthreads();
+    for (int o = 1; o < kSortT; o <<= 1) {
+      const unsigned u = threadIdx.x >= (unsigned)o ? s_part[threadIdx.x - o] : 0u;
+      __syncthreads();
+      s_part[threadIdx.x] += u;
+      __syncthreads();
+    }
+    unsigned run = s_part[threadIdx.x] - sum;
+    for (int q = 0; q < per; ++q)
+      if (t0 + q <= ntiles) {
+        const int t = t0 + q;
+        const unsigned c0 = s_cnt[0][t], c1 = s_cnt[1][t], c2 = s_cnt[2][t], c3 = s_cnt[3][t];
+        s_start[t] = (int)run;
+        s_cnt[0][t] = run;
+        s_cnt[1][t] = run + c0;
+        s_cnt[2][t] = run + c0 + c1;
+        s_cnt[3][t] = run + c0 + c1 + c2;
+        run += c0 + c1 + c2 + c3;
+      }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kSortI; ++j)
+    if (tl[j] != 8191u) {
+      const unsigned idx = s_cnt[wv][tl[j]] + r[j];
+      s_k[idx] = k[j];
+      s_v[idx] = v[j];
+    }
+  const int nv = min(kChunk, K - c * kChunk);
+  for (int sp = nv + (int)threadIdx.x; sp < kChunk; sp += kSortT) s_v[sp] = kNoEntry;  // the tail: no pair
+  __syncthreads();
+#endif
 #pragma unroll
   for (int i = 0; i < kSortI; ++i) {
     const int sp = i * kSortT + threadIdx.x;
