@@ -1435,7 +1435,7 @@ struct gsmpm_mpm {
   int* s_rec = nullptr;                      // [world][rec_ints_of(ng)] every rank's record (slab_records)
   std::vector<int> s_bounds;                 // every rank's planes: [world + 1] (from the records)
   bool s_rebal_on = true;                    // re-cut the slabs at call boundaries when unbalanced
-  float s_rebal_tol = 0.10f;                 // ... by more than this (max count / mean - 1)
+  float s_rebal_tol = 0.05f;                 // ... by more than this (max count / mean - 1)
   bool s_rebal_pending = false;              // the next call starts with the migration to new bounds
   long s_rebalances = 0;
   int* s_rec_host = nullptr;                 // pinned copy

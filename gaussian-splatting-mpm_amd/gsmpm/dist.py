@@ -162,7 +162,7 @@ class SlabDomain:
 
     def __init__(self, x_grid, cov6, vol, *, rank: int, world: int, transport, n_grid: int, grid_extent: float = 2.0,
                  margin: int = 2, interval: int = 10, capacity: int | None = None, v=None, device=None,
-                 engine_factory=None, group=None, rebalance: bool = True, rebalance_tol: float = 0.10,
+                 engine_factory=None, group=None, rebalance: bool = True, rebalance_tol: float = 0.05,
                  **sim_kwargs):
         from .sim import Simulator
         engine_factory = engine_factory or Simulator

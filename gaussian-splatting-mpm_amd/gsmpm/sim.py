@@ -150,7 +150,7 @@ class Simulator:
         check(LIB.gsmpm_mpm_slab_rects(self._h, b), "gsmpm_mpm_slab_rects")
         return [tuple(int(v) for v in b[4 * w:4 * w + 4]) for w in (0, 1)]
 
-    def slab_set_rebalance(self, on: bool = True, tolerance: float = 0.10):
+    def slab_set_rebalance(self, on: bool = True, tolerance: float = 0.05):
         """Re-cut the slabs at step-call boundaries when the most loaded one holds
         more than (1 + tolerance) x the mean (gsmpm_mpm_slab_set_rebalance)."""
         check(LIB.gsmpm_mpm_slab_set_rebalance(self._h, 1 if on else 0, ctypes.c_float(tolerance)),

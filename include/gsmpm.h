@@ -168,7 +168,7 @@ int gsmpm_mpm_slab_stats(gsmpm_mpm* h, int64_t out12[12]);
  * whole cross-section). */
 int gsmpm_mpm_slab_rects(gsmpm_mpm* h, int32_t out8[8]);
 /* Re-cutting the slabs ("rebalance per frame"; on by default,
- * tolerance 0.10): at the end of a step call, when the most loaded slab holds
+ * tolerance 0.05): at the end of a step call, when the most loaded slab holds
  * more than (1 + tolerance) x the mean particle count, every rank moves the
  * bounds to the count quantiles of all ranks' base-plane histograms (the same
  * records on every rank: the same bounds), each bound staying inside its old

@@ -241,13 +241,15 @@ def _rebalance_worker(rank, world, port, out, backend, rebalance):
 def test_gpu_slabs_rebalance_drifting_scene(dev, tmp_path, backend, world):
     """SURVEY 8(e) "rebalance per frame": a scene drifting ~19 planes along
     the cut axis -- more than half a slab -- over 200 substeps in 20 step
-    calls.  With re-cutting on (the default) the library moves the bounds to
-    the count quantiles of all ranks' base-plane histograms at call
-    boundaries (slab_host.inc slab_rebalance; the next call opens with the
-    migration to them): after every call the most loaded slab stays within
-    10 % of the mean (+ the ~1 plane one call drifts), and the state matches
-    the single-domain oracle.  The control without re-cutting ends far out
-    of balance."""
+    calls.  With re-cutting on (the default, tolerance 5 %) the library
+    moves the bounds to the count quantiles of all ranks' base-plane
+    histograms at call boundaries (slab_host.inc slab_rebalance; the next
+    call opens with the migration to them): over the last 10 calls the most
+    loaded slab averages within 10 % of the mean and never exceeds it by 15 %
+    (the counts are read at call ends, after the ~1 plane each call drifts:
+    one plane holds 4-7 % of a slab of this 4,000-particle scene), and the
+    state matches the single-domain oracle.  The control without re-cutting
+    ends far out of balance (test_gpu_slabs_no_rebalance_control)."""
     import oracle as O
     mp.spawn(_rebalance_worker, args=(world, free_port(), str(tmp_path), backend, True), nprocs=world, join=True)
     r = np.load(os.path.join(tmp_path, "rebal.npz"))
@@ -267,7 +269,7 @@ def test_gpu_slabs_rebalance_drifting_scene(dev, tmp_path, backend, world):
     from test_gpu_configs import _dump
     _dump(f"slab_rebalance_{backend}_{world}", rec)
     assert int(r["rebalances"]) >= 1 and r["b1"].tolist() != r["b0"].tolist(), rec
-    assert float(r["imb"][-5:].max()) <= 1.10 + 0.05, rec
+    assert float(r["imb"][-10:].mean()) <= 1.10 and float(r["imb"][-10:].max()) <= 1.15, rec
     for k, e in errs.items():
         assert e < TOL.get(k, 1e-4), (k, e, errs)
 
