@@ -307,6 +307,7 @@ __device__ __forceinline__ void reach_cells(float lo, float hi, int c0, int c1, 
 }
 
 #include "dsort.h"
+#include "scan.h"
 
 // returns the depth bits of a visible Gaussian (tiles word != 0), else 0
 __device__ __forceinline__ unsigned preprocess_one(const RasterDev& a, int idx, int* __restrict__ radii,
@@ -1917,6 +1918,7 @@ struct gsmpm_raster {
   unsigned long long* ds_bpre = nullptr;  // [kDsNBMax]
   unsigned *ds_key = nullptr, *ds_val = nullptr;  // [capP]
   unsigned* ttot = nullptr;    // [capT + 2] chunked tile sort: tile totals (k_tile_rows)
+  unsigned long long* scan_bt = nullptr;  // [capP / 1024 + 1] block totals of the index-order scans (scan.h)
   long dsort_fallbacks = 0;    // forwards whose depth order fell back to the library sort
   hipEvent_t count_ev = nullptr;  // recorded after k_publish_count: surfaces a fault while the host spins
   // per pixel (backward)
@@ -1957,6 +1959,17 @@ static int dsort_buckets(int P) {
   int nb = 1024;
   while (nb < kDsNBMax && nb * 8 < P) nb <<= 1;
   return nb;
+}
+
+// inclusive scan of the tiles words in Gaussian-index order (scan.h): T = unsigned
+// for the binned count alone, unsigned long long for both counts
+template <typename T>
+static void scan_tiles(gsmpm_raster* r, int P, T* out, hipStream_t st) {
+  const int nb = div_up(P, kScanBlk);
+  T* bt = reinterpret_cast<T*>(r->scan_bt);
+  hipLaunchKernelGGL(k_scan_blocks<T>, dim3(nb), dim3(256), 0, st, (const unsigned long long*)r->tiles, P, bt);
+  hipLaunchKernelGGL(k_scan_apply<T>, dim3(nb), dim3(256), 0, st, (const unsigned long long*)r->tiles, P,
+                     (const T*)bt, out);
 }
 
 static int grow(void** p, size_t bytes) {
@@ -2009,6 +2022,7 @@ static int ws_pre_walk(WsWalk& w, gsmpm_raster* r, size_t P, size_t ntiles) {
   w.take(r->ds_key, cap * sizeof(unsigned));
   w.take(r->ds_val, cap * sizeof(unsigned));
   w.take(r->ttot, (ntiles + 2) * sizeof(unsigned));
+  w.take(r->scan_bt, (cap / kScanBlk + 1) * sizeof(unsigned long long));
   w.take(r->depth, cap * sizeof(float));
   w.take(r->xy, cap * sizeof(float2));
   w.take(r->conic, cap * sizeof(float4));
@@ -2103,7 +2117,8 @@ int gsmpm_raster_destroy(gsmpm_raster* r) {
                   (void*)r->vals_sorted, r->sort_tmp, (void*)r->ranges, (void*)r->ids_sorted, (void*)r->estart, (void*)r->rec,
                   (void*)r->final_T, (void*)r->n_contrib, (void*)r->dorder, (void*)r->dsorted, (void*)r->offr, r->dsort_tmp, (void*)r->hist,
                   (void*)r->dsort_tl, (void*)r->ds_state, (void*)r->ds_bbase, (void*)r->ds_bcur, (void*)r->ds_blist,
-                  (void*)r->ds_bbig, (void*)r->ds_bpre, (void*)r->ds_key, (void*)r->ds_val, (void*)r->ttot})
+                  (void*)r->ds_bbig, (void*)r->ds_bpre, (void*)r->ds_key, (void*)r->ds_val, (void*)r->ttot,
+                  (void*)r->scan_bt})
     if (p) (void)hipFree(p);
   if (r->h_count) (void)hipHostFree(r->h_count);
   if (r->count_ev) (void)hipEventDestroy(r->count_ev);
@@ -2167,6 +2182,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     if ((rc = grow((void**)&r->offr, cap * sizeof(unsigned long long)))) return rc;
     if ((rc = grow((void**)&r->ds_key, cap * sizeof(unsigned)))) return rc;
     if ((rc = grow((void**)&r->ds_val, cap * sizeof(unsigned)))) return rc;
+    if ((rc = grow((void**)&r->scan_bt, (cap / kScanBlk + 1) * sizeof(unsigned long long)))) return rc;
     size_t bytes = 0, obytes = 0;
     GSMPM_HIP(rocprim::radix_sort_pairs(nullptr, bytes, reinterpret_cast<unsigned*>(r->depth), r->dsorted,
                                                       rocprim::counting_iterator<unsigned>(0u), r->dorder, cap, 0, 32,
@@ -2241,15 +2257,13 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     hipLaunchKernelGGL(k_preprocess, dim3(div_up(P, 256)), dim3(256), 0, st, a, out_radii, r->depth, r->xy, r->conic,
                        r->rgb, r->tiles, r->rect, own_dsort ? db.st : nullptr);
     GSMPM_LAUNCH_CHECK();
-    size_t bytes = r->scan_tmp_bytes;
     // the index-order scan (offsets) feeds only the backward's record slots
     // and the upstream-keyed path: a depth-ordered forward takes K from the
     // depth-order scan and leaves offsets to gsmpm_raster_backward (one scan
     // and its look-back init launch less per frame)
     r->offsets_pending = true;
     if (!depth_ordered || tile_dsort)  // the index-order scan of both counts (emission offsets, K)
-      GSMPM_HIP(rocprim::inclusive_scan(r->scan_tmp, bytes, r->tiles, r->offr, (size_t)P,
-                                        rocprim::plus<unsigned long long>(), st));
+      scan_tiles<unsigned long long>(r, P, r->offr, st);
     auto lib_depth_order = [&]() -> int {
       size_t b2 = r->dsort_tmp_bytes;
       if (kDepthOnesweepMin > 0 && (size_t)P >= kDepthOnesweepMin)
@@ -2544,9 +2558,8 @@ int gsmpm_raster_backward(gsmpm_raster* r, const gsmpm_raster_args* in, const in
     r->capRec = K + K / 4 + 1024;
   }
   if (r->offsets_pending) {  // the forward's tiles are still in r->tiles
-    size_t bytes = r->scan_tmp_bytes;
-    GSMPM_HIP(rocprim::inclusive_scan(r->scan_tmp, bytes, binned_tiles(r->tiles), r->offsets, (size_t)in->P,
-                                      rocprim::plus<unsigned>(), st));
+    scan_tiles<unsigned>(r, in->P, r->offsets, st);
+    GSMPM_LAUNCH_CHECK();
     r->offsets_pending = false;
   }
   if (K > 0 && r->slots_pending) {
