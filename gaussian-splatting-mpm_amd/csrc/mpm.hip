@@ -26,7 +26,6 @@
 #include <hip/hip_runtime.h>
 #include <dlfcn.h>
 
-#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <climits>
@@ -1076,6 +1075,7 @@ __global__ __launch_bounds__(256) void k_scatter(int n, const int* __restrict__ 
 
 #include "fused.h"
 #include "slab.h"
+#include "lsd.h"
 
 // ------------------------------------------------------------ postprocess --
 // compute_cov_from_F (utils.py:401-433) + compute_R_from_F (utils.py:376-398)
@@ -1844,26 +1844,42 @@ static uint64_t morton3(uint32_t a, uint32_t b, uint32_t c) {
 // Re-establish Morton order of the particles' current cells so the transfer
 // kernels' per-workgroup windows stay compact.  Only the storage order (and so
 // the float-atomic summation order) changes; `orig` keeps rows in caller order.
+// The sort: 30-bit Morton keys with the particle index as value, stable LSD
+// by 8-bit digits (lsd.h, four passes between the two halves of sort_keys /
+// sort_idx: the result lands back in the first halves).
 static int resort(gsmpm_mpm* h, hipStream_t st) {
   const int n = h->n, np = h->np;
+  const int nch = std::max(1, div_up(np, kLsdChunk));
   if (!h->planes_tmp) {
     GSMPM_HIP(hipMalloc(&h->planes_tmp, sizeof(float) * (size_t)NPLANES * np));
     GSMPM_HIP(hipMalloc(&h->orig_tmp, sizeof(int) * (size_t)np));
     GSMPM_HIP(hipMalloc(&h->sort_keys, sizeof(uint32_t) * 2 * (size_t)np));
     GSMPM_HIP(hipMalloc(&h->sort_idx, sizeof(int) * 2 * (size_t)np));
-    size_t bytes = 0;
-    GSMPM_HIP(rocprim::radix_sort_pairs(nullptr, bytes, h->sort_keys, h->sort_keys + np, h->sort_idx,
-                                        h->sort_idx + np, (size_t)n, 0, 30, st));
-    GSMPM_HIP(hipMalloc(&h->sort_tmp, bytes ? bytes : 16));
-    h->sort_tmp_bytes = bytes;
+    // digit histograms and their row prefixes [2][256][nch], digit totals [256]
+    GSMPM_HIP(hipMalloc(&h->sort_tmp, sizeof(unsigned) * (2 * 256 * (size_t)nch + 256)));
+    h->sort_tmp_bytes = sizeof(unsigned) * (2 * 256 * (size_t)nch + 256);
   }
   const dim3 pb(div_up(n, 256));
   hipLaunchKernelGGL(k_morton, pb, dim3(256), 0, st, particles_of(h), h->g.inv_dx, h->sort_keys, h->sort_idx);
   GSMPM_LAUNCH_CHECK();
-  size_t bytes = h->sort_tmp_bytes;
-  GSMPM_HIP(rocprim::radix_sort_pairs(h->sort_tmp, bytes, h->sort_keys, h->sort_keys + np, h->sort_idx,
-                                      h->sort_idx + np, (size_t)n, 0, 30, st));
-  const int* perm = h->sort_idx + np;
+  if (n > 0) {
+    const int nc = div_up(n, kLsdChunk);
+    unsigned* H = reinterpret_cast<unsigned*>(h->sort_tmp);
+    unsigned* Hs = H + 256 * (size_t)nc;
+    unsigned* tot = H + 2 * 256 * (size_t)nch;
+    unsigned* kb[2] = {h->sort_keys, h->sort_keys + np};
+    unsigned* vb[2] = {reinterpret_cast<unsigned*>(h->sort_idx), reinterpret_cast<unsigned*>(h->sort_idx) + np};
+    for (int p = 0; p < 4; ++p) {
+      const unsigned* sk = kb[p & 1];
+      const unsigned* sv = vb[p & 1];
+      hipLaunchKernelGGL(k_lsd_hist, dim3(nc), dim3(kLsdT), 0, st, n, nc, 8 * p, sk, H);
+      hipLaunchKernelGGL(k_tile_rows, dim3(64), dim3(256), 0, st, 255, nc, (const unsigned*)H, Hs, tot);
+      hipLaunchKernelGGL(k_lsd_scatter, dim3(nc), dim3(kLsdT), 0, st, n, nc, 8 * p, sk, sv, (const unsigned*)Hs,
+                         (const unsigned*)tot, kb[(p + 1) & 1], vb[(p + 1) & 1]);
+    }
+    GSMPM_LAUNCH_CHECK();
+  }
+  const int* perm = h->sort_idx;
   hipLaunchKernelGGL(k_permute, dim3(div_up(n, 256), NPLANES + 1), dim3(256), 0, st, h->planes, h->planes_tmp, n,
                      (const int*)nullptr, np, perm, (const int*)h->orig, h->orig_tmp);
   GSMPM_LAUNCH_CHECK();

@@ -308,6 +308,7 @@ __device__ __forceinline__ void reach_cells(float lo, float hi, int c0, int c1, 
 
 #include "dsort.h"
 #include "scan.h"
+#include "lsd.h"
 
 // returns the depth bits of a visible Gaussian (tiles word != 0), else 0
 __device__ __forceinline__ unsigned preprocess_one(const RasterDev& a, int idx, int* __restrict__ radii,
@@ -980,33 +981,6 @@ __global__ __launch_bounds__(kSortT) void k_tile_hist(int K, int ntiles, int nch
   __syncthreads();
   for (int t = threadIdx.x; t <= ntiles; t += kSortT) H[(size_t)t * nch + c] = s_h[t];
 }
-// The chunk histograms' positions, without a device-wide scan: a wave per
-// tile row (H is tile-major, [tile][chunk]) writes the row's exclusive prefix
-// (the chunk's offset inside the tile's run) into Hs and the row total into
-// tot[tile]; k_tile_scatter's workgroups each scan the <= 4,097 totals in LDS
-// (redundantly: cheaper than one more launch and a look-back chain).
-__global__ __launch_bounds__(256) void k_tile_rows(int ntiles, int nch, const unsigned* __restrict__ H,
-                                                   unsigned* __restrict__ Hs, unsigned* __restrict__ tot) {
-  const int t = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
-  if (t > ntiles) return;  // wave-uniform
-  const unsigned* h = H + (size_t)t * nch;
-  unsigned* o = Hs + (size_t)t * nch;
-  unsigned carry = 0;
-  for (int c0 = 0; c0 < nch; c0 += 64) {
-    const int c = c0 + lane;
-    const unsigned v = c < nch ? h[c] : 0u;
-    unsigned inc = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const unsigned u = (unsigned)__shfl_up((int)inc, d);
-      if (lane >= d) inc += u;
-    }
-    if (c < nch) o[c] = carry + inc - v;
-    carry += (unsigned)__shfl((int)inc, 63);
-  }
-  if (lane == 0) tot[t] = carry;
-}
-
 // GSMPM_TILE_BRS=1 (A/B build): the chunk's stable order from the library's
 // block radix sort instead of the wave-ballot ranks below
 #ifndef GSMPM_TILE_BRS
@@ -1255,140 +1229,6 @@ __global__ __launch_bounds__(256) void k_tile_dsort_rank(const uint2* __restrict
       keys[rg.x + j] = scr_keys[rg.x + j];
     }
     __syncthreads();
-  }
-}
-
-// Above kMaxTiles tiles: a stable LSD radix sort over 8-bit digits of the
-// tile index (two passes up to 65,535 tiles, three above), each pass
-// reduce-then-scan with no look-back chain and no library call:
-//   k_lsd_hist     per 4,096-pair chunk, its 256 digit counts (LDS atomics),
-//                  stored digit-major H[d][chunk]
-//   k_tile_rows    (256 rows) each digit's row prefix over the chunks + totals
-//   k_lsd_scatter  per chunk: every wave ranks its 1,024 pairs (16 slots of
-//                  64, in order) by digit with 8 ballots per slot and a
-//                  wave-private running count per digit -- no barrier between
-//                  slots; the four waves' counts then give each pair its
-//                  chunk-local sorted index; the chunk is staged sorted in LDS
-//                  and stored striped, so each digit run leaves as coalesced
-//                  stores at digit start + the run's row prefix.
-// Stable: a pair's rank follows (wave, slot, lane) = its chunk order.  Culled
-// keys (tile field all ones) carry digit 255 in every pass, so they sort after
-// every real tile (ntiles <= 256^passes - 1).  Round 3's form (2,048-pair
-// chunks, the library's block radix sort for the local ranks, the library's
-// device scan) ran 1.41 ms per bicycle render against 1.31 with the library's
-// onesweep.
-constexpr int kLsdT = 256, kLsdI = 16, kLsdChunk = kLsdT * kLsdI;
-__global__ __launch_bounds__(kLsdT) void k_lsd_hist(int K, int nch, int shift, const unsigned* __restrict__ keys,
-                                                    unsigned* __restrict__ H) {
-  __shared__ unsigned s_h[256];
-  s_h[threadIdx.x] = 0;
-  __syncthreads();
-  const int c = blockIdx.x;
-  unsigned k[kLsdI];
-#pragma unroll
-  for (int i = 0; i < kLsdI; ++i) {
-    const int e = c * kLsdChunk + i * kLsdT + threadIdx.x;
-    k[i] = e < K ? keys[e] : 0u;
-  }
-#pragma unroll
-  for (int i = 0; i < kLsdI; ++i)
-    if (c * kLsdChunk + i * kLsdT + (int)threadIdx.x < K) atomicAdd(&s_h[(k[i] >> shift) & 255u], 1u);
-  __syncthreads();
-  H[(size_t)threadIdx.x * nch + c] = s_h[threadIdx.x];
-}
-__global__ __launch_bounds__(kLsdT) void k_lsd_scatter(int K, int nch, int shift, const unsigned* __restrict__ keys,
-                                                       const unsigned* __restrict__ vals,
-                                                       const unsigned* __restrict__ Hs, const unsigned* __restrict__ tot,
-                                                       unsigned* __restrict__ keys_out,
-                                                       unsigned* __restrict__ vals_out) {
-  __shared__ unsigned s_k[kLsdChunk], s_v[kLsdChunk];
-  __shared__ unsigned s_wrun[4][256];  // per wave: running count of each digit, then its offset
-  __shared__ unsigned s_doff[256];     // chunk-local start of each digit's run
-  __shared__ unsigned s_gbase[256];    // global position of this chunk's run of each digit
-  __shared__ unsigned s_part[4][2];
-  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, c = blockIdx.x;
-#pragma unroll
-  for (int w = 0; w < 4; ++w) s_wrun[w][t] = 0;
-  // where each digit's run starts overall: exclusive scan of the 256 digit totals (thread t: digit t)
-  const unsigned dt = tot[t];
-  unsigned inc = dt;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned u = (unsigned)__shfl_up((int)inc, o);
-    if (lane >= o) inc += u;
-  }
-  if (lane == 63) s_part[wv][0] = inc;
-  __syncthreads();
-  unsigned dstart = inc - dt;
-  for (int w = 0; w < wv; ++w) dstart += s_part[w][0];
-  s_gbase[t] = dstart + Hs[(size_t)t * nch + c];
-  // wave wv ranks pairs [c * 4096 + wv * 1024, +1024) in 16 slots of 64, in order
-  const int e0 = c * kLsdChunk + wv * (kLsdChunk / 4);
-  unsigned k[kLsdI], v[kLsdI], r[kLsdI];
-#pragma unroll
-  for (int j = 0; j < kLsdI; ++j) {
-    const int e = e0 + j * 64 + lane;
-    k[j] = e < K ? keys[e] : 0u;
-    v[j] = e < K ? vals[e] : 0u;
-  }
-  const unsigned long long below = (1ull << lane) - 1ull;
-#pragma unroll
-  for (int j = 0; j < kLsdI; ++j) {
-    const bool ok = e0 + j * 64 + lane < K;
-    const unsigned d = ok ? (k[j] >> shift) & 255u : 256u;
-    unsigned long long peers = ~0ull;
-#pragma unroll
-    for (int b = 0; b < 9; ++b) {
-      const unsigned long long bal = __ballot((d >> b) & 1u);
-      peers &= ((d >> b) & 1u) ? bal : ~bal;
-    }
-    const unsigned rk = (unsigned)__popcll(peers & below);
-    const unsigned base = ok ? s_wrun[wv][d] : 0u;
-    r[j] = base + rk;
-    // the digit's lowest lane moves the count on; the wave's LDS operations
-    // execute in order, so the next slot's read sees it
-    if (ok && rk == 0) s_wrun[wv][d] = base + (unsigned)__popcll(peers);
-  }
-  __syncthreads();
-  {  // thread t = digit t: the four waves' counts -> the run start and each wave's offset in it
-    const unsigned c0 = s_wrun[0][t], c1 = s_wrun[1][t], c2 = s_wrun[2][t], c3 = s_wrun[3][t];
-    const unsigned n = c0 + c1 + c2 + c3;
-    unsigned inc2 = n;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const unsigned u = (unsigned)__shfl_up((int)inc2, o);
-      if (lane >= o) inc2 += u;
-    }
-    if (lane == 63) s_part[wv][1] = inc2;
-    __syncthreads();
-    unsigned off = inc2 - n;
-    for (int w = 0; w < wv; ++w) off += s_part[w][1];
-    s_doff[t] = off;
-    s_wrun[0][t] = off;
-    s_wrun[1][t] = off + c0;
-    s_wrun[2][t] = off + c0 + c1;
-    s_wrun[3][t] = off + c0 + c1 + c2;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < kLsdI; ++j) {
-    if (e0 + j * 64 + lane < K) {
-      const unsigned idx = s_wrun[wv][(k[j] >> shift) & 255u] + r[j];
-      s_k[idx] = k[j];
-      s_v[idx] = v[j];
-    }
-  }
-  __syncthreads();
-  const int nv = min(kLsdChunk, K - c * kLsdChunk);
-#pragma unroll
-  for (int i = 0; i < kLsdI; ++i) {  // striped: each digit run leaves as coalesced stores
-    const int sp = i * kLsdT + t;
-    if (sp < nv) {
-      const unsigned kk = s_k[sp], d = (kk >> shift) & 255u;
-      const unsigned pos = s_gbase[d] + (unsigned)sp - s_doff[d];
-      keys_out[pos] = kk;
-      vals_out[pos] = s_v[sp];
-    }
   }
 }
 
