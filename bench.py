@@ -293,7 +293,8 @@ def cpu_baseline(scene, args, budget_s):
         if el > budget_s or n_done >= 2000:
             break
     sub_s = n_done / el
-    # the frame's render on the CPU restatement of the rasterizer (oracle/raster_oracle.c, serial), so the
+    # the frame's render on the CPU restatement of the rasterizer (oracle/raster_oracle.c, the same OpenMP
+    # -O3 -ffast-math build and threads as the simulation: tiles sorted and blended in parallel), so the
     # baseline times the same work as the GPU value: steps_per_frame substeps + one 800x800 SH3 render
     render_s = None
     if not args.no_render:
@@ -307,7 +308,7 @@ def cpu_baseline(scene, args, budget_s):
         O.raster_forward(means, opa, cam.view_mat.cpu().numpy(), cam.full_proj_mat.cpu().numpy(),
                          np.asarray(cam.cam_center.cpu().numpy(), np.float32), np.zeros(3, np.float32),
                          cam.width, cam.height, math.tan(cam.FovX * 0.5), math.tan(cam.FovY * 0.5), shs=shs,
-                         sh_degree=3, cov3D_precomp=covs)
+                         sh_degree=3, cov3D_precomp=covs, threaded="fast")
         render_s = time.perf_counter() - t0
     spf = sa.steps_per_frame
     frame_s = spf / sub_s + (render_s or 0.0)
@@ -317,7 +318,7 @@ def cpu_baseline(scene, args, budget_s):
                       f"-march=x86-64-v3, {el:.1f}s"
                       + ("" if render_s is None else
                          f"; plus one {cam.width}x{cam.height} SH3 render of the scene on oracle/raster_oracle.c "
-                         f"(serial, 1 thread), {render_s:.2f}s")
+                         f"(OpenMP, {threads} threads), {render_s:.2f}s")
                       + f"; value = particles x {spf} / (the frame's {spf} substeps at the measured rate + the "
                         "render): the same work per frame as the GPU value",
             "substeps_per_s": sub_s, "sim_only_particle_substeps_per_s": x.shape[0] * sub_s,
