@@ -746,6 +746,8 @@ def main():
         st = sim.stats()
         out["config"]["rank0_slab_planes"] = [st["lo"], st["hi"]]
         out["config"]["rank0_window_rects"] = sim.engine.slab_rects()
+        out["config"]["slab_bounds"] = sim.bounds  # after any re-cuts (gsmpm_mpm_slab_set_rebalance, on by default)
+        out["config"]["slab_recuts"] = sim.rebalances
     if rank == 0:
         print(json.dumps(out), flush=True)
     if slab:  # the simulator's captured graphs hold RCCL work: destroy them before the communicator
