@@ -341,7 +341,7 @@ def test_gpu_slabs_impulse_mid_call(dev, tmp_path):
     assert errs["x"] < 1e-4 and errs["F_trial"] < 1e-4 and errs["v"] < TOL["v"], errs
 
 
-def _bicycle_worker(rank, world, port, out, steps, calls):
+def _bicycle_worker(rank, world, port, out, steps, calls, fcr=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     os.environ.update(shared_gpu_rccl_env(rank))
     torch.cuda.set_device(0)
@@ -357,7 +357,7 @@ def _bicycle_worker(rank, world, port, out, steps, calls):
         dom = SlabDomain(prob["x"], prob["cov"], prob["vol"], v=v, rank=rank, world=world, transport=xp,
                          n_grid=256, grid_extent=cfg["grid_extent"], margin=2, interval=10, device=dev,
                          material=cfg["material"], E=cfg["E"], nu=cfg["nu"], density=cfg["density"],
-                         gravity=cfg["gravity"])
+                         gravity=cfg["gravity"], jelly_fcr=fcr)
         dom.add_plane_collider([0, 0, 0.4], [0, 0, 1])  # main.py:276 (bicycle.json has no BC list)
         per = steps // calls
         for _ in range(calls):
@@ -380,8 +380,8 @@ def _bicycle_worker(rank, world, port, out, steps, calls):
 BICYCLE_V0 = (2.0, 0.0, 0.0)  # +x drift (grid units / s) so particles cross the slab plane and migrate
 
 
-@pytest.mark.parametrize("world", [2, 8])
-def test_gpu_slabs_bicycle_rccl(dev, tmp_path, world):
+@pytest.mark.parametrize("world,fcr", [(2, False), (8, False), (8, True)])
+def test_gpu_slabs_bicycle_rccl(dev, tmp_path, world, fcr):
     """configs[3]'s workload through the slab path: bicycle.json, 1M Gaussians
     in [0.05, 0.95]^3, 256^3, `world` RCCL slab ranks sharing cuda:0 (8: the
     config's own "shard across 8 MI355X", here 8 processes on one device over
@@ -390,11 +390,14 @@ def test_gpu_slabs_bicycle_rccl(dev, tmp_path, world):
     plane), against the single-domain OpenMP oracle: x, F_trial, cov within
     1e-4.  Each step call is one captured graph with the counts kept on the
     device: the library syncs the host once per call (the record check), +1
-    on the first call, on every rank."""
+    on the first call, on every rank.  fcr=True: the stress-bearing jelly (the
+    fixed corotated stress the reference's F3 quirk disables), so the sharded
+    run carries real elastic forces across the slab windows, not only free
+    fall."""
     import oracle as O
     from scenarios import lego_problem
     steps, calls = 50, 5
-    mp.spawn(_bicycle_worker, args=(world, free_port(), str(tmp_path), steps, calls), nprocs=world, join=True)
+    mp.spawn(_bicycle_worker, args=(world, free_port(), str(tmp_path), steps, calls, fcr), nprocs=world, join=True)
     r = np.load(os.path.join(tmp_path, "bicycle.npz"))
     assert int(r["migrated"]) > 1000 * (world - 1), int(r["migrated"])
     assert int(r["calls"]) == world * calls
@@ -405,16 +408,18 @@ def test_gpu_slabs_bicycle_rccl(dev, tmp_path, world):
     v = np.tile(np.array(BICYCLE_V0, np.float32), (len(prob["x"]), 1))
     ref = O.OracleMPM(prob["x"], prob["cov"], prob["vol"], v=v, n_grid=256, grid_extent=cfg["grid_extent"],
                       material=cfg["material"], E=cfg["E"], nu=cfg["nu"], density=cfg["density"],
-                      gravity=cfg["gravity"], threaded=True)
+                      gravity=cfg["gravity"], threaded=True, jelly_quirk=not fcr)
     ref.add_collider([0.0, 0.0, 0.4], [0.0, 0.0, 1.0], 0.0)
     for _ in range(steps):
         ref.substep(cfg["substep_dt"], [], [1])
     ref.postprocess()
     errs = {"x": rel_err(r["x"], ref.x), "F_trial": rel_err(r["F_trial"], ref.F_trial), "cov": rel_err(r["cov"], ref.cov)}
-    rec = {"world": world, "errs": errs, "migrated": int(r["migrated"]), "bounds": r["bounds"].tolist(),
+    rec = {"world": world, "fcr": fcr,
+           "F_trial_max_dev_from_I": float(np.abs(ref.F_trial - np.eye(3, dtype=np.float32).reshape(1, 9)).max()),
+           "errs": errs, "migrated": int(r["migrated"]), "bounds": r["bounds"].tolist(),
            "host_syncs": int(r["host_syncs"]), "calls": int(r["calls"])}
     print(f"bicycle slab{world}", rec)
     from test_gpu_configs import _dump
-    _dump(f"D_bicycle_slab{world}_rccl", rec)
+    _dump(f"D_bicycle_slab{world}_rccl" + ("_fcr" if fcr else ""), rec)
     for k, e in errs.items():
         assert e < 1e-4, (k, e, errs)
