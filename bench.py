@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--dp", action="store_true",
                     help="N > 1: independent scenes per rank (no exchange) instead of the default slab sharding")
     ap.add_argument("--rebin", type=int, default=0, help="fused pipeline: substeps between re-binnings (0: library default)")
+    ap.add_argument("--render-overlap", type=int, default=int(os.environ.get("GSMPM_BENCH_RENDER_OVERLAP", "1")),
+                    help="1: frame f-1 renders on a second stream while frame f simulates; 0: each frame renders "
+                         "right after its simulation on the simulator's stream (main.py's order)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch check only: start the ranks, form the process group, print the JSON line's "
                          "rank bookkeeping (n_gpus, parallelism) with value null; no GPU work")
@@ -579,12 +582,20 @@ def main():
                 means_r, covs_r = sim.gather_world(w_scale, w_center, render_space=True)
             else:
                 means_r, covs_r = sim.world_outputs(w_scale, w_center, render_space=True)
-            ev = torch.cuda.Event()
-            ev.record()
-            t.append(time.perf_counter())
-            flush()  # the previous frame renders while this one simulates
-            pending.append((means_r, covs_r, ev))
-            t.append(time.perf_counter())
+            if not args.render_overlap and means_r is not None:  # main.py's order, one stream
+                t.append(time.perf_counter())
+                K, _, _ = raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg,
+                                         cam.height, cam.width, tanx, tany, sh_degree=3, shs=feats,
+                                         cov3D_precomp=covs_r)
+                state["K"] = K
+                t.append(time.perf_counter())
+            else:
+                ev = torch.cuda.Event()
+                ev.record()
+                t.append(time.perf_counter())
+                flush()  # the previous frame renders while this one simulates
+                pending.append((means_r, covs_r, ev))
+                t.append(time.perf_counter())
         if host_t is not None:
             host_t.append([1e6 * (b - a) for a, b in zip(t, t[1:])])
 
@@ -689,7 +700,7 @@ def main():
         "config": {"workload": f"{args.config} frame: {spf} substeps + postprocess + render "
                                f"{cam.width}x{cam.height} SH3", "particles_per_gpu": n_local,
                    "particles_total": n_total, "n_grid": sa.n_grid, "material": sa.material,
-                   "substep_dt": dt,
+                   "substep_dt": dt, "render_overlap": bool(args.render_overlap),
                    "parallelism": (f"slab{world}" if slab else f"dp{world} independent scenes") if world > 1
                    else "single"},
         "substeps_per_s": spf * args.steps / elapsed,
