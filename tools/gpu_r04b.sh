@@ -21,10 +21,3 @@ for i in 1 2; do for ov in 1 0; do
   GSMPM_BENCH_RENDER_OVERLAP=$ov timeout -k 10 120 python3 bench.py --no-cpu-baseline --no-extra-configs --steps 20 --warmup 3 > $O/ov_${ov}_$i.json 2> $O/ov_${ov}_$i.err || exit 1
   python3 -c "import json; d=json.load(open('$O/ov_${ov}_$i.json')); print('render_overlap=$ov', round(d['value']/1e9,4), 'ms/frame', round(d['ms_per_step'],4), 'sim', round(d['sim_ms_per_frame'],4), 'render', d['render_ms_per_frame'], d['render_host_ms_per_frame'])"
 done; done | tee $O/ab_overlap.txt
-REPS=2 bash tools/ab_libs.sh base zbox svdnr > $O/ab_lego.txt 2>&1 || exit 1
-cat $O/ab_lego.txt
-BENCH_ARGS="--config lego-fracture.json --material metal" REPS=2 bash tools/ab_libs.sh base svdnr > $O/ab_metal.txt 2>&1 || exit 1
-cat $O/ab_metal.txt
-GSMPM_LIB=$PWD/gaussian-splatting-mpm_amd/libgsmpm_svdnr.so GSMPM_PARITY_OUT=$O/parity_svdnr timeout -k 10 500 python -u -m pytest tests/test_gpu_parity_long.py -x -q -k "metal or sand" --timeout 400 --timeout-method thread -s > $O/svdnr_parity.log 2>&1
-echo "svdnr parity rc $?"
-grep -E "passed|failed|substep|Error" $O/svdnr_parity.log | tail -20
