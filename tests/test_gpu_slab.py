@@ -38,7 +38,7 @@ def shared_gpu_rccl_env(rank):
     return {"NCCL_HOSTID": f"gsmpm-slab-rank{rank}", "NCCL_SOCKET_IFNAME": "lo", "NCCL_IB_DISABLE": "1"}
 
 
-def _gpu_worker(rank, world, port, out, backend, steps, full_top=False, env=None):
+def _gpu_worker(rank, world, port, out, backend, steps, full_top=False, env=None, rebalance=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     os.environ.update(env or {})
     if backend == "nccl-shared":
@@ -59,7 +59,8 @@ def _gpu_worker(rank, world, port, out, backend, steps, full_top=False, env=None
         xp = make_transport(rank, world, device=dev)
         cap = top_rank_start_count(x, world) if full_top and rank == world - 1 else None
         dom = SlabDomain(x, cov, vol, v=v, rank=rank, world=world, transport=xp, n_grid=NG, grid_extent=EXT,
-                         margin=2, interval=10, capacity=cap, device=dev, jelly_fcr=True, **KW)
+                         margin=2, interval=10, capacity=cap, device=dev, jelly_fcr=True, rebalance=rebalance,
+                         **KW)
         dom.add_fixed_cube(*FIXED)
         dom.add_plane_collider([0, 0, 0.4], [0, 0, 1])
         if full_top:  # every rank must raise, at the same migration, with the same message
@@ -97,9 +98,9 @@ def _gpu_worker(rank, world, port, out, backend, steps, full_top=False, env=None
         dist.destroy_process_group()
 
 
-def _run(world, tmp_path, backend="gloo", steps=STEPS, env=None):
-    mp.spawn(_gpu_worker, args=(world, free_port(), str(tmp_path), backend, steps, False, env), nprocs=world,
-             join=True)
+def _run(world, tmp_path, backend="gloo", steps=STEPS, env=None, rebalance=True):
+    mp.spawn(_gpu_worker, args=(world, free_port(), str(tmp_path), backend, steps, False, env, rebalance),
+             nprocs=world, join=True)
     return np.load(os.path.join(tmp_path, "res.npz"))
 
 
@@ -146,8 +147,10 @@ def test_gpu_slabs_deferred_migration(dev, tmp_path, backend):
     """Migration payloads of 2 particles in the first step call
     (GSMPM_SLAB_MIG_CAP; the library grows them after): most leavers cannot
     be sent at their first migration and stay with their old slab for a later
-    one -- ownership must not change the physics."""
-    r = _run(3, tmp_path, backend=backend, env={"GSMPM_SLAB_MIG_CAP": "2"})
+    one -- ownership must not change the physics.  Re-cutting is off here:
+    the first call's re-cut would size the payloads for the particles it
+    moves (>= 256) before any deferral could happen."""
+    r = _run(3, tmp_path, backend=backend, env={"GSMPM_SLAB_MIG_CAP": "2"}, rebalance=False)
     assert int(r["migrated"]) > 50 and int(r["deferred"]) > 0, (int(r["migrated"]), int(r["deferred"]))
     errs = _check(r)
     print("deferred", backend, errs, "migrated", int(r["migrated"]))
@@ -182,7 +185,7 @@ def test_gpu_slab_error_stops_every_rank(dev, tmp_path):
     it, and all 4 ranks raise the same error after the same migration count
     (gsmpm_mpm_slab_step exchanges every rank's migration record)."""
     world = 4
-    mp.spawn(_gpu_worker, args=(world, free_port(), str(tmp_path), "gloo", STEPS, True, None), nprocs=world,
+    mp.spawn(_gpu_worker, args=(world, free_port(), str(tmp_path), "gloo", STEPS, True, None, False), nprocs=world,
              join=True)
     errs = read_errors(tmp_path, world)
     assert len(set(errs)) == 1, errs
