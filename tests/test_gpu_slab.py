@@ -355,11 +355,11 @@ def _bicycle_worker(rank, world, port, out, steps, calls, fcr=False):
         from scenarios import lego_problem
         prob = lego_problem(1_000_000, 256, config="bicycle.json")
         cfg = prob["cfg"]
-        v = np.tile(np.array(BICYCLE_V0, np.float32), (len(prob["x"]), 1))
+        v, E = _bicycle_start(prob, fcr)
         xp = make_transport(rank, world, device=dev)
         dom = SlabDomain(prob["x"], prob["cov"], prob["vol"], v=v, rank=rank, world=world, transport=xp,
                          n_grid=256, grid_extent=cfg["grid_extent"], margin=2, interval=10, device=dev,
-                         material=cfg["material"], E=cfg["E"], nu=cfg["nu"], density=cfg["density"],
+                         material=cfg["material"], E=E, nu=cfg["nu"], density=cfg["density"],
                          gravity=cfg["gravity"], jelly_fcr=fcr)
         dom.add_plane_collider([0, 0, 0.4], [0, 0, 1])  # main.py:276 (bicycle.json has no BC list)
         per = steps // calls
@@ -383,6 +383,24 @@ def _bicycle_worker(rank, world, port, out, steps, calls, fcr=False):
 BICYCLE_V0 = (2.0, 0.0, 0.0)  # +x drift (grid units / s) so particles cross the slab plane and migrate
 
 
+def _bicycle_start(prob, fcr):
+    """Initial velocities and Young's modulus of the bicycle slab runs.
+    Stress-free jelly: the uniform +x drift.  fcr: the drift plus a converging
+    flow in x and y (-5 / s about the scene's centre), which strains the jelly
+    (|F - I| ~ 0.08 and stress-driven |dv| ~ 0.37 after 50 substeps, oracle),
+    with E scaled by (50 / 256)^2 so that the explicit step keeps the CFL
+    number the config has at its own n_grid 50: bicycle.json's E = 2e5 at
+    256^3 and dt 1e-4 is unstable (the oracle itself reaches NaN within 20
+    substeps)."""
+    x, cfg = prob["x"], prob["cfg"]
+    v = np.tile(np.array(BICYCLE_V0, np.float32), (len(x), 1))
+    if not fcr:
+        return v, cfg["E"]
+    v[:, 0] -= 5.0 * (x[:, 0] - 1.0)
+    v[:, 1] -= 5.0 * (x[:, 1] - 1.0)
+    return v, cfg["E"] * (50.0 / 256.0) ** 2
+
+
 @pytest.mark.parametrize("world,fcr", [(2, False), (8, False), (8, True)])
 def test_gpu_slabs_bicycle_rccl(dev, tmp_path, world, fcr):
     """configs[3]'s workload through the slab path: bicycle.json, 1M Gaussians
@@ -394,9 +412,9 @@ def test_gpu_slabs_bicycle_rccl(dev, tmp_path, world, fcr):
     1e-4.  Each step call is one captured graph with the counts kept on the
     device: the library syncs the host once per call (the record check), +1
     on the first call, on every rank.  fcr=True: the stress-bearing jelly (the
-    fixed corotated stress the reference's F3 quirk disables), so the sharded
-    run carries real elastic forces across the slab windows, not only free
-    fall."""
+    fixed corotated stress the reference's F3 quirk disables) under a
+    converging flow (_bicycle_start), so the sharded run carries real elastic
+    forces across the slab windows, not only free fall."""
     import oracle as O
     from scenarios import lego_problem
     steps, calls = 50, 5
@@ -408,16 +426,17 @@ def test_gpu_slabs_bicycle_rccl(dev, tmp_path, world, fcr):
     assert len(r["bounds"]) == world + 1
     prob = lego_problem(1_000_000, 256, config="bicycle.json")
     cfg = prob["cfg"]
-    v = np.tile(np.array(BICYCLE_V0, np.float32), (len(prob["x"]), 1))
+    v, E = _bicycle_start(prob, fcr)
     ref = O.OracleMPM(prob["x"], prob["cov"], prob["vol"], v=v, n_grid=256, grid_extent=cfg["grid_extent"],
-                      material=cfg["material"], E=cfg["E"], nu=cfg["nu"], density=cfg["density"],
+                      material=cfg["material"], E=E, nu=cfg["nu"], density=cfg["density"],
                       gravity=cfg["gravity"], threaded=True, jelly_quirk=not fcr)
     ref.add_collider([0.0, 0.0, 0.4], [0.0, 0.0, 1.0], 0.0)
     for _ in range(steps):
         ref.substep(cfg["substep_dt"], [], [1])
     ref.postprocess()
     errs = {"x": rel_err(r["x"], ref.x), "F_trial": rel_err(r["F_trial"], ref.F_trial), "cov": rel_err(r["cov"], ref.cov)}
-    rec = {"world": world, "fcr": fcr,
+    rec = {"world": world, "fcr": fcr, "E": E,
+           "max_dv_from_start": float(np.abs(ref.v - v).max()),
            "F_trial_max_dev_from_I": float(np.abs(ref.F_trial - np.eye(3, dtype=np.float32).reshape(1, 9)).max()),
            "errs": errs, "migrated": int(r["migrated"]), "bounds": r["bounds"].tolist(),
            "host_syncs": int(r["host_syncs"]), "calls": int(r["calls"])}
