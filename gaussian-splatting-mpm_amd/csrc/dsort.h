@@ -11,8 +11,8 @@
 //
 // Instead of a device-wide radix sort, the visible Gaussians are bucketed on
 // their depth bits and each bucket is sorted where it lies:
-//   k_preprocess     also reduces the visible depth bits' min and max into 8
-//                    shards each (one atomic per wave)
+//   k_preprocess     also reduces the visible depth bits' min and max into 64
+//                    shards (one atomic pair per workgroup)
 //   k_dsort_hist     bucket b = (bits - lo) >> shift (NB buckets spanning
 //                    [lo, hi]): count and tiles-word sum per bucket
 //                    (returnless global atomics)
@@ -46,8 +46,6 @@ constexpr int kDsBig = 8192;      // entries a workgroup sorts
 constexpr int kDsScanT = 1024;
 // dstate words
 enum : int {
-  DS_MIN = 0,      // [8] shards: max of ~bits (zero = identity)
-  DS_MAX = 8,      // [8] shards: max of bits
   DS_CULL = 16,    // culled cursor
   DS_NLIST = 17,   // occupied buckets of <= kDsSmall
   DS_NBIG = 18,    // occupied buckets above
@@ -59,9 +57,17 @@ enum : int {
   kDsWords = 32
 };
 
+// The visible depth bits' min / max: 64 shards, one 256-byte line each (word 0:
+// max of ~bits, zero = identity; word 1: max of bits).  Round 4's first form
+// had 8 shards in one line and an atomic pair per wave: 2,000 device-scope
+// atomics on each word of one line (bicycle, 1M Gaussians) took k_preprocess
+// from 65 to 373 us.  Device-scope atomics resolve past the XCDs' L2s, and
+// those on one address are serialized there.
+constexpr int kDsShards = 64, kDsShardWords = 64;
 // bytes of the depth-order state (fixed layout at the start of a workspace)
-constexpr size_t kDsStateBytes =  // dstate, bcount, bsum, then the block totals (scratch)
-    kDsWords * 4 + (size_t)kDsNBMax * (4 + 8) + (size_t)(kDsNBMax / 1024) * (4 + 8);
+constexpr size_t kDsShardOff =  // dstate, bcount, bsum, the block totals (scratch), then the shards
+    ((kDsWords * 4 + (size_t)kDsNBMax * (4 + 8) + (size_t)(kDsNBMax / 1024) * (4 + 8)) + 255) / 256 * 256;
+constexpr size_t kDsStateBytes = kDsShardOff + (size_t)kDsShards * kDsShardWords * 4;
 
 struct DsortBufs {
   unsigned* st;                // dstate [kDsWords]
@@ -76,17 +82,21 @@ struct DsortBufs {
   unsigned* dval;              // [P] Gaussian index by bucket run
   unsigned* btc;               // [kDsNBMax / kDsBlk] block totals of the counts
   unsigned long long* bts;     // [kDsNBMax / kDsBlk] ... of the tiles-word sums
+  unsigned* shard;             // [kDsShards][kDsShardWords] min / max shards (zero when idle)
 };
 
 __device__ __forceinline__ int ds_log2(int nb) { return 31 - __clz(nb); }
 
-// the bucket map: lo and shift from the shards
-__device__ __forceinline__ void ds_range(const unsigned* st, int nb, unsigned& lo, int& shift) {
-  unsigned nlo = 0, hi = 0;
+// the bucket map: lo and shift from the shards, by one whole wave (lane l
+// reads shard l; every lane gets the result)
+__device__ __forceinline__ void ds_range_wave(const unsigned* shard, int nb, unsigned& lo, int& shift) {
+  const int lane = threadIdx.x & 63;
+  unsigned nlo = __hip_atomic_load(shard + lane * kDsShardWords, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned hi = __hip_atomic_load(shard + lane * kDsShardWords + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    nlo = max(nlo, __hip_atomic_load(st + DS_MIN + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    hi = max(hi, __hip_atomic_load(st + DS_MAX + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  for (int o = 32; o > 0; o >>= 1) {
+    nlo = max(nlo, (unsigned)__shfl_xor((int)nlo, o));
+    hi = max(hi, (unsigned)__shfl_xor((int)hi, o));
   }
   lo = ~nlo;
   const unsigned span = hi >= lo ? hi - lo : 0u;
@@ -94,18 +104,33 @@ __device__ __forceinline__ void ds_range(const unsigned* st, int nb, unsigned& l
   shift = max(0, nbits - ds_log2(nb));
 }
 
-// k_preprocess's contribution: min / max of the visible depth bits, per wave
-__device__ __forceinline__ void ds_minmax(unsigned* st, bool vis, unsigned bits) {
+// k_preprocess's contribution: min / max of the visible depth bits, reduced
+// over the workgroup (shuffles, then LDS), one atomic pair per workgroup into
+// shard blockIdx mod 64.  Every thread of the workgroup calls it.
+__device__ __forceinline__ void ds_minmax(unsigned* shard, bool vis, unsigned bits) {
+  __shared__ unsigned s_mm[2][8];
   unsigned nlo = vis ? ~bits : 0u, hi = vis ? bits : 0u;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     nlo = max(nlo, (unsigned)__shfl_xor((int)nlo, o));
     hi = max(hi, (unsigned)__shfl_xor((int)hi, o));
   }
-  if ((threadIdx.x & 63) == 0 && hi != 0u) {
-    const int sh = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & 7;
-    __hip_atomic_fetch_max(st + DS_MIN + sh, nlo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_max(st + DS_MAX + sh, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int nw = (int)(blockDim.x >> 6), wv = (int)(threadIdx.x >> 6);
+  if ((threadIdx.x & 63) == 0) {
+    s_mm[0][wv] = nlo;
+    s_mm[1][wv] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < nw; ++w) {
+      nlo = max(nlo, s_mm[0][w]);
+      hi = max(hi, s_mm[1][w]);
+    }
+    if (hi != 0u) {
+      unsigned* sh = shard + (blockIdx.x & (kDsShards - 1)) * kDsShardWords;
+      __hip_atomic_fetch_max(sh, nlo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_max(sh + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -113,12 +138,14 @@ __global__ __launch_bounds__(256) void k_dsort_hist(int P, int nb, const float* 
                                                     const unsigned long long* __restrict__ tiles, DsortBufs d) {
   __shared__ unsigned s_lo;
   __shared__ int s_shift;
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {
     unsigned lo;
     int shift;
-    ds_range(d.st, nb, lo, shift);
-    s_lo = lo;
-    s_shift = shift;
+    ds_range_wave(d.shard, nb, lo, shift);
+    if (threadIdx.x == 0) {
+      s_lo = lo;
+      s_shift = shift;
+    }
   }
   __syncthreads();
   const int i = blockIdx.x * 256 + threadIdx.x;
@@ -279,17 +306,19 @@ __global__ __launch_bounds__(256) void k_dsort_scan2(int nb, DsortBufs d, const 
       pre += sm[q];
     }
   }
-  if (g == ng - 1 && t == 0) {
+  if (g == ng - 1 && wv == 0) {
     unsigned lo;
     int shift;
-    ds_range(d.st, nb, lo, shift);
-    d.st[DS_LO] = lo;
-    d.st[DS_SHIFT] = (unsigned)shift;
-    d.st[DS_NB] = (unsigned)nb;
-    d.st[DS_PV] = ac;
-    d.st[DS_CULL] = 0;
-    d.st[DS_TOT] = (unsigned)as;
-    d.st[DS_TOT + 1] = (unsigned)(as >> 32);
+    ds_range_wave(d.shard, nb, lo, shift);
+    if (lane == 0) {
+      d.st[DS_LO] = lo;
+      d.st[DS_SHIFT] = (unsigned)shift;
+      d.st[DS_NB] = (unsigned)nb;
+      d.st[DS_PV] = ac;
+      d.st[DS_CULL] = 0;
+      d.st[DS_TOT] = (unsigned)as;
+      d.st[DS_TOT + 1] = (unsigned)(as >> 32);
+    }
   }
 }
 
@@ -297,7 +326,8 @@ __global__ __launch_bounds__(256) void k_dsort_scatter(int P, const float* __res
                                                        const unsigned long long* __restrict__ tiles, DsortBufs d,
                                                        unsigned* __restrict__ order,
                                                        unsigned long long* __restrict__ offr) {
-  if (blockIdx.x == 0 && threadIdx.x < 16) d.st[DS_MIN + threadIdx.x] = 0u;  // the shards: read for the last time by k_dsort_scan
+  if (blockIdx.x == 0 && threadIdx.x < 2 * kDsShards)  // the shards: read for the last time by k_dsort_scan2
+    d.shard[(threadIdx.x >> 1) * kDsShardWords + (threadIdx.x & 1)] = 0u;
   const int i = blockIdx.x * 256 + threadIdx.x;
   const unsigned lo = d.st[DS_LO], shift = d.st[DS_SHIFT], pv = d.st[DS_PV];
   const bool in = i < P;

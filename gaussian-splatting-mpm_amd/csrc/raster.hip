@@ -1792,6 +1792,7 @@ static DsortBufs dsort_bufs(gsmpm_raster* r) {
   d.dval = r->ds_val;
   d.bts = d.st ? reinterpret_cast<unsigned long long*>(d.bsum + kDsNBMax) : nullptr;
   d.btc = d.st ? reinterpret_cast<unsigned*>(d.bts + kDsNBMax / kDsBlk) : nullptr;
+  d.shard = d.st ? reinterpret_cast<unsigned*>(r->ds_state + kDsShardOff) : nullptr;
   return d;
 }
 // buckets of the depth order: a power of two, ~8 visible Gaussians a bucket, in [1024, kDsNBMax]
@@ -2095,7 +2096,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     const bool own_dsort = depth_ordered && !tile_dsort && !lib_dsort;
     const DsortBufs db = dsort_bufs(r);
     hipLaunchKernelGGL(k_preprocess, dim3(div_up(P, 256)), dim3(256), 0, st, a, out_radii, r->depth, r->xy, r->conic,
-                       r->rgb, r->tiles, r->rect, own_dsort ? db.st : nullptr);
+                       r->rgb, r->tiles, r->rect, own_dsort ? db.shard : nullptr);
     GSMPM_LAUNCH_CHECK();
     // the index-order scan (offsets) feeds only the backward's record slots
     // and the upstream-keyed path: a depth-ordered forward takes K from the
