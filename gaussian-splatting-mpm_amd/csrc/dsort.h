@@ -473,3 +473,297 @@ __global__ __launch_bounds__(1024) void k_dsort_big(const unsigned long long* __
     __syncthreads();
   }
 }
+
+// ---------------------------------------------------------------------------
+// The LSD form of the depth order (the default above kDlMin Gaussians; the
+// bucket form's histogram and scatter take a device-scope atomic per
+// Gaussian, which resolves past the XCDs' L2s: 87 + 71 us for bicycle's 1M).
+//
+// Keys: key = bits - lo for a visible Gaussian (lo: the smallest visible
+// depth bits, from the shards), all ones for a culled one.  A stable LSD sort
+// over 8-bit digits from index order gives exactly the (bits, index) order,
+// culled ones last.  Only R = ceil(nb1 / 8) passes can move anything, nb1 the
+// bit length of (span + 1): every visible key is then below 2^(8R) - 1, the
+// low 8R bits of a culled key, so after R passes the order is final and the
+// remaining passes are identities.  The host launches all 4 passes (it does
+// not know the span); a pass at or beyond R returns at once, and the final
+// scan reads the buffer the last real pass wrote.  Each pass is
+// reduce-then-scan without look-back or atomics on global memory:
+//   k_dl_hist     per 2,048-key chunk its 256 digit counts (LDS), digit-major
+//   k_dl_rows     a wave per digit: the chunk prefix of that digit + its total
+//   k_dl_scatter  per chunk: wave-ballot digit ranks (in order: stable), the
+//                 chunk staged sorted in LDS, striped coalesced stores
+// Pass 0 reads the depth bits and tiles words itself (no key-building pass).
+// Then k_dl_scan_blocks / k_dl_scan_apply: the inclusive scan of the tiles
+// words in that order (gathered through it), writing the order and offr.
+constexpr int kDlI = 8, kDlChunk = 256 * kDlI, kDlPasses = 4;
+constexpr int kDlMin = 262144;  // below: the bucket form
+enum : int { DS_DL_LO = 27, DS_DL_NB1 = 28 };
+
+struct DlBufs {
+  unsigned* st;
+  unsigned* shard;
+  unsigned *k0, *v0, *k1, *v1;  // pass p writes (k, v)[p & 1]
+  unsigned *H, *Hs, *tot;       // [256][nch] digit-major counts, their row prefixes, [256] digit totals
+};
+
+// lo and nb1 from the shards, by one whole wave
+__device__ __forceinline__ void dl_span_wave(const unsigned* shard, unsigned& lo, int& nb1) {
+  const int lane = threadIdx.x & 63;
+  unsigned nlo = __hip_atomic_load(shard + lane * kDsShardWords, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned hi = __hip_atomic_load(shard + lane * kDsShardWords + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    nlo = max(nlo, (unsigned)__shfl_xor((int)nlo, o));
+    hi = max(hi, (unsigned)__shfl_xor((int)hi, o));
+  }
+  lo = ~nlo;
+  const unsigned span = hi >= lo ? hi - lo : 0u;  // < 0x7F800000: span + 1 does not wrap
+  nb1 = 32 - __clz(span + 1u);
+}
+__device__ __forceinline__ bool dl_trivial(const unsigned* st, int pass) {
+  return pass > 0 && (unsigned)(8 * pass) >= st[DS_DL_NB1];
+}
+__device__ __forceinline__ unsigned dl_key0(const float* depth, const unsigned long long* tiles, int e,
+                                            unsigned lo) {
+  return tiles[e] ? __float_as_uint(depth[e]) - lo : 0xFFFFFFFFu;  // culled: no depth was written
+}
+
+template <bool FIRST>
+__global__ __launch_bounds__(256) void k_dl_hist(int P, int nch, int pass, const float* __restrict__ depth,
+                                                 const unsigned long long* __restrict__ tiles, DlBufs b) {
+  __shared__ unsigned s_h[256];
+  __shared__ unsigned s_lo;
+  __shared__ int s_skip;
+  const int t = threadIdx.x, c = blockIdx.x;
+  s_h[t] = 0;
+  if (FIRST) {
+    if (t < 64) {
+      unsigned lo;
+      int nb1;
+      dl_span_wave(b.shard, lo, nb1);
+      if (t == 0) s_lo = lo;
+    }
+  } else {
+    if (t == 0) s_skip = dl_trivial(b.st, pass) ? 1 : 0;
+    if (pass == 1 && c == 0 && t < 2 * kDsShards)  // idle state: pass 0 read the shards for the last time
+      b.shard[(t >> 1) * kDsShardWords + (t & 1)] = 0u;
+  }
+  __syncthreads();
+  if (!FIRST && s_skip) return;  // workgroup-uniform
+  const unsigned* keys = (pass & 1) ? b.k0 : b.k1;
+  const int sh = 8 * pass;
+#pragma unroll
+  for (int i = 0; i < kDlI; ++i) {
+    const int e = c * kDlChunk + i * 256 + t;
+    if (e < P) {
+      const unsigned k = FIRST ? dl_key0(depth, tiles, e, s_lo) : keys[e];
+      atomicAdd(&s_h[(k >> sh) & 255u], 1u);
+    }
+  }
+  __syncthreads();
+  b.H[(size_t)t * nch + c] = s_h[t];
+}
+
+// 64 workgroups of 4 waves: wave d = digit d's row
+__global__ __launch_bounds__(256) void k_dl_rows(int nch, int pass, DlBufs b) {
+  if (dl_trivial(b.st, pass)) return;
+  const int d = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const unsigned* h = b.H + (size_t)d * nch;
+  unsigned* o = b.Hs + (size_t)d * nch;
+  unsigned carry = 0;
+  for (int c0 = 0; c0 < nch; c0 += 64) {
+    const int c = c0 + lane;
+    const unsigned v = c < nch ? h[c] : 0u;
+    unsigned inc = v;
+#pragma unroll
+    for (int s = 1; s < 64; s <<= 1) {
+      const unsigned u = (unsigned)__shfl_up((int)inc, s);
+      if (lane >= s) inc += u;
+    }
+    if (c < nch) o[c] = carry + inc - v;
+    carry += (unsigned)__shfl((int)inc, 63);
+  }
+  if (lane == 0) b.tot[d] = carry;
+}
+
+template <bool FIRST>
+__global__ __launch_bounds__(256) void k_dl_scatter(int P, int nch, int pass, const float* __restrict__ depth,
+                                                    const unsigned long long* __restrict__ tiles, DlBufs b) {
+  __shared__ unsigned s_k[kDlChunk], s_v[kDlChunk];
+  __shared__ unsigned s_wrun[4][256];  // per wave: running count of each digit, then its offset
+  __shared__ unsigned s_doff[256];     // chunk-local start of each digit's run
+  __shared__ unsigned s_gbase[256];    // global position of this chunk's run of each digit
+  __shared__ unsigned s_part[4][2];
+  __shared__ unsigned s_lo;
+  __shared__ int s_skip;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6, c = blockIdx.x;
+  if (FIRST) {
+    if (t < 64) {
+      unsigned lo;
+      int nb1;
+      dl_span_wave(b.shard, lo, nb1);
+      if (t == 0) {
+        s_lo = lo;
+        if (c == 0) {
+          b.st[DS_DL_LO] = lo;
+          b.st[DS_DL_NB1] = (unsigned)nb1;
+        }
+      }
+    }
+  } else if (t == 0) {
+    s_skip = dl_trivial(b.st, pass) ? 1 : 0;
+  }
+#pragma unroll
+  for (int w = 0; w < 4; ++w) s_wrun[w][t] = 0;
+  __syncthreads();
+  if (!FIRST && s_skip) return;  // workgroup-uniform
+  const unsigned* keys = (pass & 1) ? b.k0 : b.k1;
+  const unsigned* vals = (pass & 1) ? b.v0 : b.v1;
+  unsigned* keys_out = (pass & 1) ? b.k1 : b.k0;
+  unsigned* vals_out = (pass & 1) ? b.v1 : b.v0;
+  const int sh = 8 * pass;
+  // where each digit's run starts overall: exclusive scan of the 256 digit totals (thread t: digit t)
+  const unsigned dt = b.tot[t];
+  unsigned inc = dt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned u = (unsigned)__shfl_up((int)inc, o);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) s_part[wv][0] = inc;
+  __syncthreads();
+  unsigned dstart = inc - dt;
+  for (int w = 0; w < wv; ++w) dstart += s_part[w][0];
+  s_gbase[t] = dstart + b.Hs[(size_t)t * nch + c];
+  // wave wv ranks keys [c * 2048 + wv * 512, +512) in 8 slots of 64, in order
+  const int e0 = c * kDlChunk + wv * (kDlChunk / 4);
+  unsigned k[kDlI], v[kDlI], r[kDlI];
+#pragma unroll
+  for (int j = 0; j < kDlI; ++j) {
+    const int e = e0 + j * 64 + lane;
+    if (FIRST) {
+      k[j] = e < P ? dl_key0(depth, tiles, e, s_lo) : 0u;
+      v[j] = (unsigned)e;
+    } else {
+      k[j] = e < P ? keys[e] : 0u;
+      v[j] = e < P ? vals[e] : 0u;
+    }
+  }
+  const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int j = 0; j < kDlI; ++j) {
+    const bool ok = e0 + j * 64 + lane < P;
+    const unsigned d = ok ? (k[j] >> sh) & 255u : 256u;
+    unsigned long long peers = ~0ull;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) {
+      const unsigned long long bal = __ballot((d >> q) & 1u);
+      peers &= ((d >> q) & 1u) ? bal : ~bal;
+    }
+    const unsigned rk = (unsigned)__popcll(peers & below);
+    const unsigned base = ok ? s_wrun[wv][d & 255u] : 0u;
+    r[j] = base + rk;
+    // the digit's lowest lane moves the count on; the wave's LDS operations
+    // execute in order, so the next slot's read sees it
+    if (ok && rk == 0) s_wrun[wv][d] = base + (unsigned)__popcll(peers);
+  }
+  __syncthreads();
+  {  // thread t = digit t: the four waves' counts -> the run start and each wave's offset in it
+    const unsigned c0 = s_wrun[0][t], c1 = s_wrun[1][t], c2 = s_wrun[2][t], c3 = s_wrun[3][t];
+    const unsigned n = c0 + c1 + c2 + c3;
+    unsigned inc2 = n;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned u = (unsigned)__shfl_up((int)inc2, o);
+      if (lane >= o) inc2 += u;
+    }
+    if (lane == 63) s_part[wv][1] = inc2;
+    __syncthreads();
+    unsigned off = inc2 - n;
+    for (int w = 0; w < wv; ++w) off += s_part[w][1];
+    s_doff[t] = off;
+    s_wrun[0][t] = off;
+    s_wrun[1][t] = off + c0;
+    s_wrun[2][t] = off + c0 + c1;
+    s_wrun[3][t] = off + c0 + c1 + c2;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kDlI; ++j) {
+    if (e0 + j * 64 + lane < P) {
+      const unsigned idx = s_wrun[wv][(k[j] >> sh) & 255u] + r[j];
+      s_k[idx] = k[j];
+      s_v[idx] = v[j];
+    }
+  }
+  __syncthreads();
+  const int nv = min(kDlChunk, P - c * kDlChunk);
+#pragma unroll
+  for (int i = 0; i < kDlI; ++i) {  // striped: each digit run leaves as coalesced stores
+    const int sp = i * 256 + t;
+    if (sp < nv) {
+      const unsigned kk = s_k[sp], d = (kk >> sh) & 255u;
+      const unsigned pos = s_gbase[d] + (unsigned)sp - s_doff[d];
+      keys_out[pos] = kk;
+      vals_out[pos] = s_v[sp];
+    }
+  }
+}
+
+// the order the last real pass wrote
+__device__ __forceinline__ const unsigned* dl_final(const DlBufs& b) {
+  const int R = ((int)b.st[DS_DL_NB1] + 7) >> 3;
+  return (R & 1) ? b.v0 : b.v1;
+}
+// the inclusive scan of the tiles words in that order (scan.h's two launches, gathered)
+__global__ __launch_bounds__(256) void k_dl_scan_blocks(int P, const unsigned long long* __restrict__ tiles, DlBufs b,
+                                                        unsigned long long* __restrict__ btot) {
+  __shared__ unsigned long long s_w[4];
+  const unsigned* ord = dl_final(b);
+  const int i0 = blockIdx.x * kScanBlk + 4 * threadIdx.x;
+  unsigned long long v = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (i0 + q < P) v += tiles[ord[i0 + q]];
+  v = scan_block_sum(v, s_w);
+  if (threadIdx.x == 0) btot[blockIdx.x] = v;
+}
+__global__ __launch_bounds__(256) void k_dl_scan_apply(int P, const unsigned long long* __restrict__ tiles, DlBufs b,
+                                                       const unsigned long long* __restrict__ btot,
+                                                       unsigned* __restrict__ order,
+                                                       unsigned long long* __restrict__ offr) {
+  __shared__ unsigned long long s_w[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = blockIdx.x;
+  const unsigned* ord = dl_final(b);
+  unsigned long long pb = 0;
+  for (int q = threadIdx.x; q < g; q += 256) pb += btot[q];
+  pb = scan_block_sum(pb, s_w);
+  const int i0 = g * kScanBlk + 4 * threadIdx.x;
+  unsigned o[4];
+  unsigned long long e[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    o[q] = i0 + q < P ? ord[i0 + q] : 0u;
+    e[q] = i0 + q < P ? tiles[o[q]] : 0ull;
+  }
+  const unsigned long long lt = e[0] + e[1] + e[2] + e[3];
+  unsigned long long inc = lt;
+#pragma unroll
+  for (int s = 1; s < 64; s <<= 1) {
+    const unsigned long long u = __shfl_up(inc, s);
+    if (lane >= s) inc += u;
+  }
+  if (lane == 63) s_w[wv] = inc;
+  __syncthreads();
+  unsigned long long run = pb + inc - lt;
+  for (int w = 0; w < wv; ++w) run += s_w[w];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    run += e[q];
+    if (i0 + q < P) {
+      order[i0 + q] = o[q];
+      offr[i0 + q] = run;
+    }
+  }
+}

@@ -306,8 +306,8 @@ __device__ __forceinline__ void reach_cells(float lo, float hi, int c0, int c1, 
   last = a - 1;
 }
 
-#include "dsort.h"
 #include "scan.h"
+#include "dsort.h"
 #include "lsd.h"
 
 // returns the depth bits of a visible Gaussian (tiles word != 0), else 0
@@ -1759,6 +1759,7 @@ struct gsmpm_raster {
   unsigned *ds_key = nullptr, *ds_val = nullptr;  // [capP]
   unsigned* ttot = nullptr;    // [capT + 2] chunked tile sort: tile totals (k_tile_rows)
   unsigned long long* scan_bt = nullptr;  // [capP / 1024 + 1] block totals of the index-order scans (scan.h)
+  unsigned* dl_h = nullptr;    // [2 * 256 * (capP / kDlChunk + 1) + 256] the LSD depth order's counts, prefixes, totals
   long dsort_fallbacks = 0;    // forwards whose depth order fell back to the library sort
   hipEvent_t count_ev = nullptr;  // recorded after k_publish_count: surfaces a fault while the host spins
   // per pixel (backward)
@@ -1794,6 +1795,21 @@ static DsortBufs dsort_bufs(gsmpm_raster* r) {
   d.btc = d.st ? reinterpret_cast<unsigned*>(d.bts + kDsNBMax / kDsBlk) : nullptr;
   d.shard = d.st ? reinterpret_cast<unsigned*>(r->ds_state + kDsShardOff) : nullptr;
   return d;
+}
+static size_t dl_h_words(size_t cap) { return 2 * 256 * (cap / kDlChunk + 1) + 256; }
+static DlBufs dl_bufs(gsmpm_raster* r, int P) {
+  const size_t nch = (size_t)div_up(P, kDlChunk);
+  DlBufs b;
+  b.st = reinterpret_cast<unsigned*>(r->ds_state);
+  b.shard = reinterpret_cast<unsigned*>(r->ds_state + kDsShardOff);
+  b.k0 = r->ds_key;
+  b.v0 = r->ds_val;
+  b.k1 = r->dsorted;
+  b.v1 = r->dorder;  // free until the final scan writes the order (in place when it is the last pass's)
+  b.H = r->dl_h;
+  b.Hs = r->dl_h + 256 * nch;
+  b.tot = r->dl_h + 2 * 256 * nch;
+  return b;
 }
 // buckets of the depth order: a power of two, ~8 visible Gaussians a bucket, in [1024, kDsNBMax]
 static int dsort_buckets(int P) {
@@ -1864,6 +1880,7 @@ static int ws_pre_walk(WsWalk& w, gsmpm_raster* r, size_t P, size_t ntiles) {
   w.take(r->ds_val, cap * sizeof(unsigned));
   w.take(r->ttot, (ntiles + 2) * sizeof(unsigned));
   w.take(r->scan_bt, (cap / kScanBlk + 1) * sizeof(unsigned long long));
+  w.take(r->dl_h, dl_h_words(cap) * sizeof(unsigned));
   w.take(r->depth, cap * sizeof(float));
   w.take(r->xy, cap * sizeof(float2));
   w.take(r->conic, cap * sizeof(float4));
@@ -1959,7 +1976,7 @@ int gsmpm_raster_destroy(gsmpm_raster* r) {
                   (void*)r->final_T, (void*)r->n_contrib, (void*)r->dorder, (void*)r->dsorted, (void*)r->offr, r->dsort_tmp, (void*)r->hist,
                   (void*)r->dsort_tl, (void*)r->ds_state, (void*)r->ds_bbase, (void*)r->ds_bcur, (void*)r->ds_blist,
                   (void*)r->ds_bbig, (void*)r->ds_bpre, (void*)r->ds_key, (void*)r->ds_val, (void*)r->ttot,
-                  (void*)r->scan_bt})
+                  (void*)r->scan_bt, (void*)r->dl_h})
     if (p) (void)hipFree(p);
   if (r->h_count) (void)hipHostFree(r->h_count);
   if (r->count_ev) (void)hipEventDestroy(r->count_ev);
@@ -2024,6 +2041,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     if ((rc = grow((void**)&r->ds_key, cap * sizeof(unsigned)))) return rc;
     if ((rc = grow((void**)&r->ds_val, cap * sizeof(unsigned)))) return rc;
     if ((rc = grow((void**)&r->scan_bt, (cap / kScanBlk + 1) * sizeof(unsigned long long)))) return rc;
+    if ((rc = grow((void**)&r->dl_h, dl_h_words(cap) * sizeof(unsigned)))) return rc;
     size_t bytes = 0, obytes = 0;
     GSMPM_HIP(rocprim::radix_sort_pairs(nullptr, bytes, reinterpret_cast<unsigned*>(r->depth), r->dsorted,
                                                       rocprim::counting_iterator<unsigned>(0u), r->dorder, cap, 0, 32,
@@ -2091,9 +2109,14 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
   if (P > 0) {
     // GSMPM_RASTER_DSORT=lib: the library's radix sort + scan for the depth order (A/B; also the
     // fallback when a depth bucket overflows, dsort.h)
+    // GSMPM_RASTER_DSORT=bucket / lsd force a form of the hand-written one
+    // (default: the LSD form from kDlMin Gaussians, the bucket form below)
     const char* dl = std::getenv("GSMPM_RASTER_DSORT");
-    const bool lib_dsort = dl && dl[0] == 'l';
+    const bool lib_dsort = dl && std::strcmp(dl, "lib") == 0;
     const bool own_dsort = depth_ordered && !tile_dsort && !lib_dsort;
+    const bool lsd_dsort = own_dsort && (dl && std::strcmp(dl, "lsd") == 0 ? true
+                                         : dl && std::strcmp(dl, "bucket") == 0 ? false
+                                                                                : P >= kDlMin);
     const DsortBufs db = dsort_bufs(r);
     hipLaunchKernelGGL(k_preprocess, dim3(div_up(P, 256)), dim3(256), 0, st, a, out_radii, r->depth, r->xy, r->conic,
                        r->rgb, r->tiles, r->rect, own_dsort ? db.shard : nullptr);
@@ -2123,7 +2146,28 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     };
     // the depth order depends on P only: it runs before the count read-back,
     // queued behind whatever the stream is still doing
-    if (own_dsort) {
+    if (lsd_dsort) {
+      const DlBufs b = dl_bufs(r, P);
+      const int nch = div_up(P, kDlChunk);
+      const float* dp = r->depth;
+      const unsigned long long* tw = r->tiles;
+      for (int pass = 0; pass < kDlPasses; ++pass) {
+        if (pass == 0) {
+          hipLaunchKernelGGL(k_dl_hist<true>, dim3(nch), dim3(256), 0, st, P, nch, pass, dp, tw, b);
+          hipLaunchKernelGGL(k_dl_rows, dim3(64), dim3(256), 0, st, nch, pass, b);
+          hipLaunchKernelGGL(k_dl_scatter<true>, dim3(nch), dim3(256), 0, st, P, nch, pass, dp, tw, b);
+        } else {
+          hipLaunchKernelGGL(k_dl_hist<false>, dim3(nch), dim3(256), 0, st, P, nch, pass, dp, tw, b);
+          hipLaunchKernelGGL(k_dl_rows, dim3(64), dim3(256), 0, st, nch, pass, b);
+          hipLaunchKernelGGL(k_dl_scatter<false>, dim3(nch), dim3(256), 0, st, P, nch, pass, dp, tw, b);
+        }
+      }
+      const int nsb = div_up(P, kScanBlk);
+      hipLaunchKernelGGL(k_dl_scan_blocks, dim3(nsb), dim3(256), 0, st, P, tw, b, r->scan_bt);
+      hipLaunchKernelGGL(k_dl_scan_apply, dim3(nsb), dim3(256), 0, st, P, tw, b,
+                         (const unsigned long long*)r->scan_bt, r->dorder, r->offr);
+      GSMPM_LAUNCH_CHECK();
+    } else if (own_dsort) {
       const int nb = dsort_buckets(P);
       hipLaunchKernelGGL(k_dsort_hist, dim3(div_up(P, 256)), dim3(256), 0, st, P, nb, (const float*)r->depth,
                          (const unsigned long long*)r->tiles, db);
@@ -2172,9 +2216,9 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       }
       return GSMPM_OK;
     };
-    int rc = publish(own_dsort ? db.st + DS_OVER : nullptr);
+    int rc = publish(own_dsort && !lsd_dsort ? db.st + DS_OVER : nullptr);
     if (rc) return rc;
-    if (own_dsort && hc[2]) {  // a depth bucket above kDsBig entries: the library sort instead (dsort.h)
+    if (own_dsort && !lsd_dsort && hc[2]) {  // a depth bucket above kDsBig entries: the library sort instead (dsort.h)
       r->dsort_fallbacks += 1;
       if ((rc = lib_depth_order()) || (rc = publish(nullptr))) return rc;
     }

@@ -331,21 +331,25 @@ def test_tight_binning_pair_counts(dev, monkeypatch, P, W, H):
     print("binned / 3-sigma pairs", b0, k0, round(b0 / k0, 3))
 
 
-@pytest.mark.parametrize("case", ["spread", "wide", "layers", "flat", "many"])
+@pytest.mark.parametrize("case", ["spread", "wide", "layers", "flat", "culled", "many"])
 def test_depth_order_matches_library_sort(dev, monkeypatch, case):
-    """The hand-written depth order (csrc/dsort.h: bucketed on the depth bits,
+    """Both forms of the hand-written depth order (csrc/dsort.h) against the
+    library's stable radix sort + scan (GSMPM_RASTER_DSORT=lib): num_rendered,
+    radii and every pixel bit-identical.  "bucket": bucketed on the depth bits,
     each bucket ranked by (bits, index) in a wave or, above 256 entries, a
-    bitonic workgroup) against the library's stable radix sort + scan
-    (GSMPM_RASTER_DSORT=lib): num_rendered, radii and every pixel
-    bit-identical.  Cases: depths spread over a box ("spread"), a scene with a
-    far outlier stretching the bucket range ("wide"), depths on 3 exact values
-    (buckets of ~1,000: the workgroup sort, "layers"), all depths equal (one
-    bucket of 20,000 > 8,192: the overflow flag and the library fallback,
-    "flat"), and 300,000 Gaussians ("many")."""
+    bitonic workgroup; "lsd": 8-bit LSD passes over (bits - lo), the passes
+    beyond the span's bit length skipped on the device.  Cases: depths spread
+    over a box ("spread"), a far outlier stretching the range ("wide": all four
+    LSD passes), depths on 3 exact values (buckets of ~1,000: the workgroup
+    sort, "layers"), all depths equal (one bucket of 20,000 > 8,192: the
+    overflow flag and the library fallback; one LSD pass, "flat"), a third of
+    the Gaussians behind the camera (culled: the tail of the order, "culled"),
+    and 300,000 Gaussians ("many")."""
     import torch
     from gsmpm import raster
     P, W, H, yaw = {"spread": (3000, 256, 192, 0.3), "wide": (20000, 640, 480, 0.3), "layers": (3000, 256, 192, 0.0),
-                    "flat": (20000, 512, 512, 0.0), "many": (300000, 800, 800, 0.3)}[case]
+                    "flat": (20000, 512, 512, 0.0), "culled": (20000, 640, 480, 0.3),
+                    "many": (300000, 800, 800, 0.3)}[case]
     means, c6, opa, shs = _scene(P, seed=P + 7)
     if case == "wide":
         means[0] = (0.0, 0.0, 60.0)  # far behind the scene
@@ -353,21 +357,24 @@ def test_depth_order_matches_library_sort(dev, monkeypatch, case):
         means[:, 2] = np.float32([-0.2, 0.1, 0.4])[np.arange(P) % 3]
     if case == "flat":
         means[:, 2] = np.float32(0.1)
+    if case == "culled":
+        means[::3, 2] = np.float32(-4.0)  # view depth < 0.2: culled
     view, full, campos, tx, ty = _camera(W, H, 0.9, yaw=yaw)
     bgv = np.zeros(3, np.float32)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     args = (t(means), t(opa), t(view), t(full), t(campos), t(bgv), H, W, tx, ty)
     kw = dict(sh_degree=3, shs=t(shs), cov3D_precomp=t(c6))
     out = {}
-    for mode in ("own", "lib"):
-        if mode == "lib":
-            monkeypatch.setenv("GSMPM_RASTER_DSORT", "lib")
+    for mode in ("bucket", "lsd", "lib"):
+        monkeypatch.setenv("GSMPM_RASTER_DSORT", mode)
         for ctx in (None, raster.RasterContext()):  # the workspace form and the context form
             K, color, radii = raster.forward(*args, **kw, context=ctx)
             torch.cuda.synchronize()
             out[(mode, ctx is None)] = (K, color.cpu().numpy(), radii.cpu().numpy())
     K0, c0, r0 = out[("lib", False)]
     assert K0 > 0 and c0.max() > 0
+    if case == "culled":
+        assert (r0 == 0).sum() >= P // 3, int((r0 == 0).sum())
     for key, (K, c, r) in out.items():
         assert K == K0, (key, K, K0)
         assert np.array_equal(r, r0), key
