@@ -16,7 +16,7 @@ cp $(find $O/prof_render -name 'run_kernel_stats.csv' | head -n 1) $O/render_ker
 CONFIG=bicycle.json N=1000000 NG=256 REPS=10 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_render_D -o run -- python3 tools/render_probe.py > $O/prof_render_D.log 2>&1 || exit 1
 cp $(find $O/prof_render_D -name 'run_kernel_stats.csv' | head -n 1) $O/render_kernel_stats_bicycle.csv && rm -rf $O/prof_render_D
 timeout -k 10 120 python3 tools/dsort_stats.py > $O/dsort_stats.txt 2>&1; cat $O/dsort_stats.txt
-bash tools/ab_env_render.sh GSMPM_RASTER_DSORT own lib $O/ab_dsort > $O/ab_dsort.txt 2>&1; cat $O/ab_dsort.txt
+bash tools/ab_env_render.sh GSMPM_RASTER_DSORT "own lib" $O/ab_dsort > $O/ab_dsort.txt 2>&1; cat $O/ab_dsort.txt
 for i in 1 2; do for ov in 1 0; do
   GSMPM_BENCH_RENDER_OVERLAP=$ov timeout -k 10 120 python3 bench.py --no-cpu-baseline --no-extra-configs --steps 20 --warmup 3 > $O/ov_${ov}_$i.json 2> $O/ov_${ov}_$i.err || exit 1
   python3 -c "import json; d=json.load(open('$O/ov_${ov}_$i.json')); print('render_overlap=$ov', round(d['value']/1e9,4), 'ms/frame', round(d['ms_per_step'],4), 'sim', round(d['sim_ms_per_frame'],4), 'render', d['render_ms_per_frame'], d['render_host_ms_per_frame'])"

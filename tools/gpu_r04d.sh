@@ -9,7 +9,7 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_raster.py -m gpu -x -v --ti
 rc=$?
 tail -3 $O/tests.log
 [ $rc -eq 0 ] || { grep -E "Error|error|assert|FAILED" $O/tests.log | head -30; exit $rc; }
-bash tools/ab_env_render.sh GSMPM_RASTER_DSORT own lib $O/ab_dsort > $O/ab_dsort.txt 2>&1; cat $O/ab_dsort.txt
+bash tools/ab_env_render.sh GSMPM_RASTER_DSORT "own lib" $O/ab_dsort > $O/ab_dsort.txt 2>&1; cat $O/ab_dsort.txt
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 CONFIG=bicycle.json N=1000000 NG=256 REPS=10 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_render_D -o run -- python3 tools/render_probe.py > $O/prof_render_D.log 2>&1 || exit 1
 cp $(find $O/prof_render_D -name 'run_kernel_stats.csv' | head -n 1) $O/render_kernel_stats_bicycle.csv && rm -rf $O/prof_render_D
