@@ -33,6 +33,55 @@ static __global__ __launch_bounds__(256) void k_tile_rows(int ntiles, int nch, c
   if (lane == 0) tot[t] = carry;
 }
 
+// The same row prefixes for long rows (many chunks): a workgroup per row.
+// The row is read into LDS with coalesced loads, each thread scans a
+// contiguous segment of it, the 256 segment sums are scanned across the
+// workgroup, and the prefixes leave with coalesced stores.  k_tile_rows' wave
+// walks a row of 7,275 chunks (bicycle's 29.8M pairs) in 114 dependent steps:
+// 63.5 us per digit pass.  skip (optional): the row pass is a no-op when
+// *skip <= skip_at (the LSD depth order's passes past the span, dsort.h).
+constexpr int kRowsWideMin = 512, kRowsWideMax = 16384;  // chunks (dynamic LDS: 4 B each)
+static __global__ __launch_bounds__(256) void k_rows_wide(int nch, const unsigned* __restrict__ H,
+                                                   unsigned* __restrict__ Hs, unsigned* __restrict__ tot,
+                                                   const unsigned* __restrict__ skip, unsigned skip_at) {
+  extern __shared__ unsigned s_row[];
+  __shared__ unsigned s_w[4];
+  if (skip && *skip <= skip_at) return;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const unsigned* h = H + (size_t)blockIdx.x * nch;
+  unsigned* o = Hs + (size_t)blockIdx.x * nch;
+  for (int c = t; c < nch; c += 1024) {
+    unsigned v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = c + 256 * q < nch ? h[c + 256 * q] : 0u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (c + 256 * q < nch) s_row[c + 256 * q] = v[q];
+  }
+  __syncthreads();
+  const int S = (nch + 255) / 256, c0 = min(nch, t * S), c1 = min(nch, c0 + S);
+  unsigned sum = 0;
+  for (int c = c0; c < c1; ++c) sum += s_row[c];
+  unsigned inc = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const unsigned u = (unsigned)__shfl_up((int)inc, d);
+    if (lane >= d) inc += u;
+  }
+  if (lane == 63) s_w[wv] = inc;
+  __syncthreads();
+  unsigned run = inc - sum;
+  for (int w = 0; w < wv; ++w) run += s_w[w];
+  for (int c = c0; c < c1; ++c) {
+    const unsigned v = s_row[c];
+    s_row[c] = run;
+    run += v;
+  }
+  __syncthreads();
+  for (int c = t; c < nch; c += 256) o[c] = s_row[c];
+  if (t == 0) tot[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+}
+
 // Above kMaxTiles tiles: a stable LSD radix sort over 8-bit digits of the
 // tile index (two passes up to 65,535 tiles, three above), each pass
 // reduce-then-scan with no look-back chain and no library call:

@@ -2151,14 +2151,22 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       const int nch = div_up(P, kDlChunk);
       const float* dp = r->depth;
       const unsigned long long* tw = r->tiles;
+      // digit rows of >= 128 chunks (>= 262,144 Gaussians): a workgroup per row
+      auto rows = [&](int pass) {
+        if (nch >= 128 && nch <= kRowsWideMax)
+          hipLaunchKernelGGL(k_rows_wide, dim3(256), dim3(256), nch * sizeof(unsigned), st, nch, (const unsigned*)b.H,
+                             b.Hs, b.tot, pass ? (const unsigned*)(b.st + DS_DL_NB1) : nullptr, 8u * pass);
+        else
+          hipLaunchKernelGGL(k_dl_rows, dim3(64), dim3(256), 0, st, nch, pass, b);
+      };
       for (int pass = 0; pass < kDlPasses; ++pass) {
         if (pass == 0) {
           hipLaunchKernelGGL(k_dl_hist<true>, dim3(nch), dim3(256), 0, st, P, nch, pass, dp, tw, b);
-          hipLaunchKernelGGL(k_dl_rows, dim3(64), dim3(256), 0, st, nch, pass, b);
+          rows(pass);
           hipLaunchKernelGGL(k_dl_scatter<true>, dim3(nch), dim3(256), 0, st, P, nch, pass, dp, tw, b);
         } else {
           hipLaunchKernelGGL(k_dl_hist<false>, dim3(nch), dim3(256), 0, st, P, nch, pass, dp, tw, b);
-          hipLaunchKernelGGL(k_dl_rows, dim3(64), dim3(256), 0, st, nch, pass, b);
+          rows(pass);
           hipLaunchKernelGGL(k_dl_scatter<false>, dim3(nch), dim3(256), 0, st, P, nch, pass, dp, tw, b);
         }
       }
@@ -2259,6 +2267,9 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       const int passes = (bits + 7) / 8;  // ntiles <= 256^passes - 1: the all-ones tile field stays the culled one
       const int nch = (int)div_up(K, kChunk);
       const int nchl = (int)div_up(K, kLsdChunk);
+      // digit rows of at least this many chunks: a workgroup per row (k_rows_wide); tests lower it
+      const char* rw = std::getenv("GSMPM_RASTER_ROWS_WIDE_MIN");
+      const int rows_wide_min = rw ? std::atoi(rw) : kRowsWideMin;
       size_t need = 0;
       if (digits) {
         const size_t nh = 256 * (size_t)nchl;
@@ -2341,8 +2352,12 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
             unsigned* dk = fin ? tile_sorted : alt_k;
             unsigned* dv = fin ? r->ids_sorted : alt_v;
             hipLaunchKernelGGL(k_lsd_hist, dim3(nchl), dim3(kLsdT), 0, st, (int)K, nchl, 8 * p, sk, r->hist);
-            hipLaunchKernelGGL(k_tile_rows, dim3(64), dim3(256), 0, st, 255, nchl, (const unsigned*)r->hist, Hs,
-                               r->ttot);
+            if (nchl >= rows_wide_min && nchl <= kRowsWideMax)
+              hipLaunchKernelGGL(k_rows_wide, dim3(256), dim3(256), nchl * sizeof(unsigned), st, nchl,
+                                 (const unsigned*)r->hist, Hs, r->ttot, (const unsigned*)nullptr, 0u);
+            else
+              hipLaunchKernelGGL(k_tile_rows, dim3(64), dim3(256), 0, st, 255, nchl, (const unsigned*)r->hist, Hs,
+                                 r->ttot);
             hipLaunchKernelGGL(k_lsd_scatter, dim3(nchl), dim3(kLsdT), 0, st, (int)K, nchl, 8 * p, sk, sv,
                                (const unsigned*)Hs, (const unsigned*)r->ttot, dk, dv);
             GSMPM_LAUNCH_CHECK();

@@ -295,15 +295,19 @@ def test_digit_tile_sort_matches_onesweep(dev, monkeypatch, P, W, H, tiles):
                                        projmatrix=t(full), sh_degree=3, campos=t(campos), prefiltered=False,
                                        debug=False)
     out = {}
-    for os_ in ("1", "0"):
-        monkeypatch.setenv("GSMPM_RASTER_LSD", "0" if os_ == "1" else "1")
+    # "wide": the digit rows' prefixes by a workgroup per row (k_rows_wide), as bicycle-sized frames take them
+    for form, lsd, wide in (("onesweep", "0", None), ("lsd", "1", None), ("wide", "1", "1")):
+        monkeypatch.setenv("GSMPM_RASTER_LSD", lsd)
+        if wide:
+            monkeypatch.setenv("GSMPM_RASTER_ROWS_WIDE_MIN", wide)
         m3, o1, s1, cv = t(means, True), t(opa, True), t(shs, True), t(c6, True)
         img, radii = GaussianRasterizer(st)(means3D=m3, means2D=None, opacities=o1, shs=s1, cov3D_precomp=cv)
         (img * wgt).sum().backward()
-        out[os_] = [x.detach().cpu().numpy() for x in (img, radii, m3.grad, o1.grad, s1.grad, cv.grad)]
-    assert (out["0"][1] > 0).sum() > P // 4
-    for a, b in zip(out["0"], out["1"]):
-        assert np.array_equal(a, b)
+        out[form] = [x.detach().cpu().numpy() for x in (img, radii, m3.grad, o1.grad, s1.grad, cv.grad)]
+    assert (out["lsd"][1] > 0).sum() > P // 4
+    for form in ("lsd", "wide"):
+        for a, b in zip(out[form], out["onesweep"]):
+            assert np.array_equal(a, b), form
 
 
 @pytest.mark.parametrize("P,W,H", [(20000, 1024, 1024), (6000, 272, 3856)])
