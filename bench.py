@@ -640,7 +640,7 @@ def main():
     barrier()
     sim_ms = e0.elapsed_time(e1)
     state["t"] = t_after
-    render_ms = render_host_ms = None
+    render_ms = render_host_ms = render_cold_ms = None
     if not args.no_render and rank == 0 and world == 1:
         # on the stream the timed frames rendered on, after one warm-up render
         # there; device time between hipEvents recorded on that stream around 5
@@ -648,6 +648,14 @@ def main():
         # it the host wall time of the same 5 calls
         means_r, covs_r = sim.world_outputs(w_scale, w_center, render_space=True)
         torch.cuda.synchronize()
+        # round 3's form beside it: one render on the current (default) stream,
+        # no warm-up there, host wall time (that breakdown read 0.685 ms on the
+        # driver's box against 0.263 in the builder's runs)
+        c0 = time.perf_counter()
+        raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg, cam.height, cam.width,
+                       tanx, tany, sh_degree=3, shs=feats, cov3D_precomp=covs_r)
+        torch.cuda.synchronize()
+        render_cold_ms = (time.perf_counter() - c0) * 1e3
         with torch.cuda.stream(render_stream):
             raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg, cam.height, cam.width,
                            tanx, tany, sh_degree=3, shs=feats, cov3D_precomp=covs_r)
@@ -709,6 +717,7 @@ def main():
         "sim_substeps_per_s": spf / (sim_ms / 1e3),
         "render_ms_per_frame": render_ms,
         "render_host_ms_per_frame": render_host_ms,
+        "render_default_stream_first_ms": render_cold_ms,
         "num_rendered": state["K"],
     }
     if kern is not None:
