@@ -223,7 +223,10 @@ __device__ __forceinline__ bool in_grid(const float (&x)[3], const GridDims& g) 
 // GSMPM_ZERO_BOX=1: the P2G half zeroes only its chunk's store box of the LDS
 // window (the nodes its stencils reach: ~57 % of the 1,584 on the lego
 // frame), once the box is known, with one more workgroup barrier, instead
-// of the whole window before it (A/B)
+// of the whole window before it.  Measured and rejected (round 4, 2 A/B
+// rounds on the lego bench, profiles/r04/ab_libs_r04e.txt): sim 3.120 / 3.129
+// against 3.115 / 3.100 ms/frame, k_fused 17.0 against 16.9 us -- the zeroing
+// is hidden under the particle loads it overlaps; the barrier is not
 #ifndef GSMPM_ZERO_BOX
 #define GSMPM_ZERO_BOX 0
 #endif

@@ -18,32 +18,39 @@ namespace gsmpm {
 
 // FAST: reciprocal square roots and square roots by the hardware
 // instructions (v_rsq_f32 / v_sqrt_f32, ~1 ulp) instead of the correctly
-// rounded sequences (27 / 18 VALU each, 25 per SVD).  Off by default (round
-// 3): at the BASELINE sizes the ~1 ulp per SVD put the plastic materials ~10x
+// rounded sequences (27 / 18 VALU each, 25 per SVD).  The bare instructions
+// are not used (round 3): at the BASELINE sizes the ~1 ulp per SVD put the plastic materials ~10x
 // further from the oracle than the oracle is from itself under a reordered
 // P2G sum (metal, 100k / 128^3, substep 100: F_trial 1.2e-4 with it, 1.7e-5
 // without, reorder spread 1.5e-5; sand v 2.3e-3 vs 4.3e-4 vs 4.4e-4;
 // tests/test_gpu_parity_long.py), for 2.3 us of k_fused<metal>.  Where a
 // result depends on the SVD basis itself (foam's element-wise U * diag * V^T,
 // SURVEY F13) the correctly rounded form is used regardless.
-// GSMPM_SVD_FAST=1 at build time: the hardware instructions (A/B).
-// GSMPM_SVD_FAST=2: the hardware rsqrt refined by one Newton-Raphson step
-// (y (3 - x y^2) / 2, ~0.5 ulp) and sqrt as x * rsqrt plus one Heron
-// correction: 6 / 8 VALU instead of 27 / 18, not bit-identical to the oracle's
-// 1 / sqrtf (A/B against the long-horizon spread).
+// GSMPM_SVD_FAST (build time) selects the FAST form:
+//   2 (default, round 4): the hardware rsqrt refined by one Newton-Raphson
+//     step (y (3 - x y^2) / 2, ~0.5 ulp) and sqrt as x * rsqrt plus one Heron
+//     correction: 6 / 8 VALU instead of 27 / 18.  Not bit-identical to the
+//     oracle's 1 / sqrtf, but metal and sand stay inside the long-horizon
+//     spread; metal k_fused 25.7 -> 24.3 us, sim 3.86 -> 3.71 ms/frame
+//     (tools/ab_libs.sh, profiles/r04/).
+//   1: the bare hardware instructions (A/B; ~10x outside the spread, above).
+//   0: the correctly rounded sequences (round 3's default; A/B).
 #ifndef GSMPM_SVD_FAST
-#define GSMPM_SVD_FAST 0
+#define GSMPM_SVD_FAST 2
 #endif
 __device__ __forceinline__ float svd_rsqrt_nr(float x) {
   const float y0 = __builtin_amdgcn_rsqf(x);
   const float y = y0 * fmaf(-0.5f * x, y0 * y0, 1.5f);
-  return x > 0.0f ? y : y0;  // 0 -> inf as 1 / sqrtf(0) (the Newton step would give NaN)
+  // the step only for normal finite x: 0 -> inf as 1 / sqrtf(0), inf -> 0, where
+  // x y0^2 is NaN (foam's degenerate F reached them: R came out NaN); subnormal
+  // x -> the hardware result unrefined
+  return x >= 1.17549435e-38f && x <= 3.40282347e38f ? y : y0;
 }
 __device__ __forceinline__ float svd_sqrt_nr(float x) {
   const float y = svd_rsqrt_nr(x);
   const float s = x * y;
   const float r = fmaf(0.5f * y, fmaf(-s, s, x), s);
-  return x > 0.0f ? r : sqrtf(x);  // 0 -> 0, negative -> NaN
+  return x >= 1.17549435e-38f && x <= 3.40282347e38f ? r : sqrtf(x);  // 0, subnormal, inf, negative: sqrtf
 }
 template <bool FAST>
 __device__ __forceinline__ float svd_rsqrt(float x) {

@@ -1,0 +1,59 @@
+"""Overlap of the slab window exchange with the interior grid pass, from one
+rank's rocprofv3 kernel trace (tools/gpu_r04f.sh runs a 2-rank RCCL slab bench,
+every rank under its own rocprofv3 --kernel-trace).
+
+Per substep a slab rank launches k_fused, k_grid_f over the window tiles
+(pass 1), then -- inside the captured graph, on a forked branch -- k_grid_f
+over the interior tiles (pass 2) while the RCCL group (ncclDevKernel_*)
+swaps the window partials, then k_win_update.  This reads the trace's
+begin/end stamps and reports how much of each exchange kernel's interval the
+interior pass covers.
+
+    python3 tools/overlap_trace.py path/to/run_kernel_trace.csv
+"""
+import csv
+import sys
+
+
+def main(path):
+    rows = list(csv.DictReader(open(path)))
+    ks = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows))
+    grid = [(a, b) for a, b, n in ks if "k_grid_f" in n]
+    nccl = [(a, b) for a, b, n in ks if "nccl" in n.lower()]
+    fused = [a for a, b, n in ks if "k_fused" in n]
+    # the interior pass: the second k_grid_f after each k_fused
+    interior = []
+    fi = 0
+    seen = 0
+    for a, b in grid:
+        while fi < len(fused) and fused[fi] < a:
+            fi += 1
+            seen = 0
+        seen += 1
+        if seen == 2:
+            interior.append((a, b))
+    tot = cov = 0
+    concurrent = 0
+    for a, b in nccl:
+        tot += b - a
+        o = 0
+        for c, d in interior:
+            if d <= a:
+                continue
+            if c >= b:
+                break
+            o += min(b, d) - max(a, c)
+        cov += o
+        concurrent += 1 if o > 0 else 0
+    print(f"kernels {len(ks)}, k_grid_f {len(grid)} (interior {len(interior)}), exchange kernels {len(nccl)}")
+    if nccl:
+        print(f"exchange kernels overlapping an interior pass: {concurrent} of {len(nccl)}; "
+              f"exchange time {tot / 1e3:.1f} us, of it under an interior pass {cov / 1e3:.1f} us "
+              f"({100.0 * cov / max(tot, 1):.1f} %)")
+    if interior:
+        it = sum(b - a for a, b in interior)
+        print(f"interior pass time {it / 1e3:.1f} us total, {it / len(interior) / 1e3:.2f} us each")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
