@@ -38,6 +38,32 @@ constexpr int kFW0 = kFT0 + 4, kFW1 = kFT1 + 4, kFW2 = kFT2 + 4;  // window node
 constexpr int kFWin = kFW0 * kFW1 * kFW2;                      // 1584
 constexpr int kFTN = kFT0 * kFT1 * kFT2;                       // owned nodes per tile (448)
 
+// Where window node (w0, w1, w2) lives in its chunk's slot.  Default: window
+// order ([kFW0][kFW1][kFW2]).  GSMPM_OWNER_SLOTS=1 (A/B): grouped by the tile
+// that owns the node -- per axis the window's coords split into sections
+// w = 0 (the lower neighbour's last plane), 1..T (the tile's own), T+1..T+3
+// (the upper neighbour's first three), and the 27 section boxes are stored
+// one after another, each in its owner tile's node order.  A grid-update wave
+// (64 consecutive owned nodes of one tile) then reads the own tile's box and
+// the lower-x neighbour's as one contiguous 1 KB run instead of 9 runs of 7
+// nodes 11 apart.
+#ifndef GSMPM_OWNER_SLOTS
+#define GSMPM_OWNER_SLOTS 0
+#endif
+constexpr bool kOwnerSlots = GSMPM_OWNER_SLOTS != 0;
+__device__ __forceinline__ int slot_sec_pre(int w, int T) { return w == 0 ? 0 : (w <= T ? 1 : T + 1); }
+__device__ __forceinline__ int slot_sec_n(int w, int T) { return w == 0 ? 1 : (w <= T ? T : 3); }
+__device__ __forceinline__ int slot_loc(int w0, int w1, int w2) {
+  if constexpr (!kOwnerSlots) {
+    return (w0 * kFW1 + w1) * kFW2 + w2;
+  } else {
+    const int p0 = slot_sec_pre(w0, kFT0), n0 = slot_sec_n(w0, kFT0);
+    const int p1 = slot_sec_pre(w1, kFT1), n1 = slot_sec_n(w1, kFT1);
+    const int p2 = slot_sec_pre(w2, kFT2), n2 = slot_sec_n(w2, kFT2);
+    return p0 * (kFW1 * kFW2) + n0 * (p1 * kFW2 + n1 * p2) + ((w0 - p0) * n1 + (w1 - p1)) * n2 + (w2 - p2);
+  }
+}
+
 // ---- multi-GPU slab hooks (slab.h has the exchange and migration kernels) ----
 struct SlabWin {
   int W;            // window planes (0: not a slab)
@@ -580,6 +606,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
           const int a = (int)(((float)qn + 0.5f) * r12), rem = qn - a * n12;
           const int bq = (int)(((float)rem + 0.5f) * r2), c = rem - bq * n2;
           const int node = ((lo[0] + a) * kFW1 + lo[1] + bq) * kFW2 + lo[2] + c;
+          const int sl = kOwnerSlots ? slot_loc(lo[0] + a, lo[1] + bq, lo[2] + c) : node;
           float4 r;
           r.x = from_fixed32(s_acc[0 * kFWin + node], S);
           r.y = from_fixed32(s_acc[1 * kFWin + node], S);
@@ -588,7 +615,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
           // write-through: a slot is read by other XCDs' grid updates, and a dirty
           // line left in this XCD's L2 would be written back by the end-of-kernel
           // release (k_fused 21.9 -> 18.2 us on the lego frame)
-          wt_store4(dst + node, r);
+          wt_store4(dst + sl, r);
         }
       }
       __syncthreads();  // LDS reuse by the next chunk
@@ -634,7 +661,7 @@ __device__ __forceinline__ void node_cover(int l0, int l1, int l2, int e, int& c
   const int sec2 = l2 < 3 ? -1 : (l2 == kFT2 - 1 ? 1 : 0);
   const int a = (e >> 2) ? sec0 : 0, b = ((e >> 1) & 1) ? sec1 : 0, c = (e & 1) ? sec2 : 0;
   ci = (a + 1) * 9 + (b + 1) * 3 + (c + 1);
-  loc = ((l0 - a * kFT0 + 1) * kFW1 + (l1 - b * kFT1 + 1)) * kFW2 + (l2 - c * kFT2 + 1);
+  loc = slot_loc(l0 - a * kFT0 + 1, l1 - b * kFT1 + 1, l2 - c * kFT2 + 1);
 }
 __device__ __forceinline__ void node_reads(int max_chunks, const int* s_c0, const int* s_nc, const int* s_bx, int l0,
                                            int l1, int l2, NodeReads& r) {
@@ -652,7 +679,7 @@ __device__ __forceinline__ void node_reads(int max_chunks, const int* s_c0, cons
     const int w0 = l0 - a * kFT0 + 1, w1 = l1 - b * kFT1 + 1, w2 = l2 - c * kFT2 + 1;
     on = on && nc > 0 && w0 >= (bx & 15) && w1 >= ((bx >> 4) & 15) && w2 >= ((bx >> 8) & 15) &&
          w0 <= ((bx >> 12) & 15) && w1 <= ((bx >> 16) & 15) && w2 <= ((bx >> 20) & 15);
-    const int loc = (w0 * kFW1 + w1) * kFW2 + w2;
+    const int loc = slot_loc(w0, w1, w2);
     r.off[e] = on ? s_c0[ci] * kFWin + loc : max_chunks * kFWin;
     r.extra |= (on && nc > 1) ? (1 << e) : 0;
   }
