@@ -39,18 +39,25 @@ namespace gsmpm {
 #define GSMPM_SVD_FAST 2
 #endif
 __device__ __forceinline__ float svd_rsqrt_nr(float x) {
-  const float y0 = __builtin_amdgcn_rsqf(x);
-  const float y = y0 * fmaf(-0.5f * x, y0 * y0, 1.5f);
-  // the step only for normal finite x: 0 -> inf as 1 / sqrtf(0), inf -> 0, where
-  // x y0^2 is NaN (foam's degenerate F reached them: R came out NaN); subnormal
-  // x -> the hardware result unrefined
-  return x >= 1.17549435e-38f && x <= 3.40282347e38f ? y : y0;
+  // normal finite x only; anything else (0, subnormal, inf, NaN, negative)
+  // takes the correctly rounded form on a branch the wave skips when no lane
+  // needs it.  v_rsq_f32 flushes a subnormal input (rsq -> inf where
+  // 1 / sqrtf gives ~1e20), and at 0 / inf the step's x y0^2 is NaN: foam's
+  // degenerate F reached both in the Jacobi sweeps (its R came out NaN)
+  if (x >= 1.17549435e-38f && x <= 3.40282347e38f) {
+    const float y0 = __builtin_amdgcn_rsqf(x);
+    return y0 * fmaf(-0.5f * x, y0 * y0, 1.5f);
+  }
+  return 1.0f / sqrtf(x);
 }
 __device__ __forceinline__ float svd_sqrt_nr(float x) {
-  const float y = svd_rsqrt_nr(x);
-  const float s = x * y;
-  const float r = fmaf(0.5f * y, fmaf(-s, s, x), s);
-  return x >= 1.17549435e-38f && x <= 3.40282347e38f ? r : sqrtf(x);  // 0, subnormal, inf, negative: sqrtf
+  if (x >= 1.17549435e-38f && x <= 3.40282347e38f) {
+    const float y0 = __builtin_amdgcn_rsqf(x);
+    const float y = y0 * fmaf(-0.5f * x, y0 * y0, 1.5f);
+    const float s = x * y;
+    return fmaf(0.5f * y, fmaf(-s, s, x), s);
+  }
+  return sqrtf(x);  // 0, subnormal, inf, negative
 }
 template <bool FAST>
 __device__ __forceinline__ float svd_rsqrt(float x) {
