@@ -33,29 +33,35 @@ def test_device_svd_matches_oracle(dev):
             assert np.abs(np.abs(U[i]) - np.abs(u)).max() < 1e-3
 
 
-@pytest.mark.parametrize("scale", [0.0, 1e-21, 1e-19, 1e18, 1e19, 3e19])
+@pytest.mark.parametrize("scale", [0.0, 1e-21, 1e-19, 1e-6, 1e6, 1e18, 1e19, 3e19])
 def test_device_svd_degenerate_scales(dev, scale):
     """The fast SVD (GSMPM_SVD_FAST=2: refined hardware rsqrt) on matrices
     whose Jacobi sums reach 0, subnormals and infinity: finite wherever the
-    correctly rounded oracle is, and the same singular values there.  Foam's
-    degenerate F reached these in round 4 (its R came out NaN) before the
-    refined form fell back to 1 / sqrtf off the normal range."""
+    correctly rounded oracle is, and a valid factorisation wherever the
+    oracle's is (the f32 algorithm itself stops reconstructing A once A^T A
+    under- or overflows: the oracle's error is O(1) at 1e-19 and 1e18).
+    Foam's degenerate F reached these in round 4 (its R came out NaN) before
+    the refined form fell back to 1 / sqrtf off the normal range."""
     rng = np.random.default_rng(int(scale > 1) + 7)
     A = rng.standard_normal((512, 3, 3)).astype(np.float32)
     A[:128, :, 2] = 0.0  # rank 2
     A[128:256, :, 1:] = 0.0  # rank 1
     A = (A * np.float32(scale)).astype(np.float32)
     U, S, V = _device_svd(A, dev)
+    rec_err = lambda u, sv, v, a: np.abs(u.astype(np.float64) @ np.diag(sv) @ v.T.astype(np.float64) - a).max() / \
+        max(np.abs(a).max(), 1e-38)
+    checked = 0
     for i in range(len(A)):
         with np.errstate(all="ignore"):
             u, sv, v = O.svd3(A[i])
-        for name, g, o in (("U", U[i], u), ("S", S[i], sv), ("V", V[i], v)):
-            assert np.isfinite(g).all() or not np.isfinite(o).all(), (scale, i, name, g, o)
-        if np.isfinite(sv).all() and np.isfinite(S[i]).all() and scale > 0:
-            # a valid factorisation (the Jacobi sums are subnormal at 1e-21 / 1e-19: a few digits)
-            tol = 1e-3 if scale >= 1 else 5e-2
-            rec = U[i].astype(np.float64) @ np.diag(S[i]) @ V[i].T.astype(np.float64)
-            assert np.abs(rec - A[i]).max() <= tol * np.abs(A[i]).max(), (scale, i)
+            ok = all(np.isfinite(x).all() for x in (u, sv, v))
+            for name, g, o in (("U", U[i], u), ("S", S[i], sv), ("V", V[i], v)):
+                assert np.isfinite(g).all() or not np.isfinite(o).all(), (scale, i, name, g, o)
+            if ok and scale > 0 and rec_err(u, sv, v, A[i]) < 1e-3:
+                assert rec_err(U[i], S[i], V[i], A[i]) < 2e-3, (scale, i)
+                checked += 1
+    if scale in (1e-6, 1e6):
+        assert checked == len(A)
 
 
 def _oracle_stress(material, quirk, F, mu, lam, yld, dt):
