@@ -163,7 +163,7 @@ class SlabDomain:
     def __init__(self, x_grid, cov6, vol, *, rank: int, world: int, transport, n_grid: int, grid_extent: float = 2.0,
                  margin: int = 2, interval: int = 10, capacity: int | None = None, v=None, device=None,
                  engine_factory=None, group=None, rebalance: bool = True, rebalance_tol: float = 0.05,
-                 **sim_kwargs):
+                 cut_axis="longest", **sim_kwargs):
         from .sim import Simulator
         engine_factory = engine_factory or Simulator
         self.rank, self.world, self.transport = int(rank), int(world), transport
@@ -174,14 +174,28 @@ class SlabDomain:
         xh = (x_grid.detach().cpu().numpy() if torch.is_tensor(x_grid) else np.asarray(x_grid)).reshape(-1, 3)
         self.n_total = len(xh)
         # SURVEY 8(e) cuts along the bbox's longest axis.  The library's slabs are
-        # planes of grid axis 0; every BASELINE scene has axis 0 among its longest
-        # (lego: x and y tie at 1.3; bicycle: a cube).  A scene whose axis 0 is
-        # clearly shorter is still correct, only less evenly cut: say so.
+        # planes of its grid axis 0, so the domain runs the engine in a frame whose
+        # axis 0 is the cut axis: coordinates, velocities, matrices, covariances,
+        # gravity and every BC are permuted on the way in and back on the way out
+        # (the grid is cubic and the update is axis-symmetric, so this is the same
+        # computation up to f32 operand order).  A tie keeps axis 0 (lego: x and y
+        # at 1.3; bicycle: a cube), where nothing is permuted.
         ext = (xh.max(0) - xh.min(0)) if len(xh) else np.zeros(3)
-        self.cut_axis_ratio = float(ext[0] / max(float(ext.max()), 1e-30)) if len(xh) else 1.0
-        if self.cut_axis_ratio < 0.9 and self.rank == 0:
-            import warnings
-            warnings.warn(f"slab cut along axis 0, which spans {self.cut_axis_ratio:.2f} of the bbox's longest axis")
+        a = int(np.argmax(ext)) if cut_axis == "longest" else int(cut_axis)
+        if not 0 <= a < 3:
+            raise ValueError(f"cut_axis must be 'longest' or 0, 1, 2 (got {cut_axis!r})")
+        self.cut_axis = a
+        self.cut_axis_ratio = float(ext[a] / max(float(ext.max()), 1e-30)) if len(xh) else 1.0
+        self._perm = [a] + [i for i in range(3) if i != a]  # engine axis i = scene axis _perm[i]
+        self._inv = [self._perm.index(i) for i in range(3)]  # scene axis i = engine axis _inv[i]
+        self._permuted = a != 0
+        if self._permuted:
+            xh = xh[:, self._perm]
+            x_grid = self._vec_in(x_grid)
+            cov6 = self._cov_in(cov6)
+            v = None if v is None else self._vec_in(v)
+            if "gravity" in sim_kwargs:
+                sim_kwargs["gravity"] = self._p3(sim_kwargs["gravity"])
         self._bounds0 = slab_bounds(xh, self.n_grid, self.grid_extent, self.world, margin)
         owner = owner_of(xh, self._bounds0, self.n_grid, self.grid_extent)
         mine = torch.from_numpy(np.nonzero(owner == self.rank)[0]).to(self.device)
@@ -195,6 +209,49 @@ class SlabDomain:
         t = lambda a: (a if torch.is_tensor(a) else torch.from_numpy(np.ascontiguousarray(a))).to(self.device)
         sel = lambda a: None if a is None else t(a).reshape(self.n_total, -1)[mine]
         self.engine.slab_set_particles(sel(x_grid), sel(cov6), sel(vol), mine.to(torch.int32), v=sel(v))
+
+    # ---- the cut-axis frame (engine axis 0 = the cut axis) ----
+    _UP = ((0, 0), (0, 1), (0, 2), (1, 1), (1, 2), (2, 2))  # upper-6 layout [xx, xy, xz, yy, yz, zz]
+
+    def _p3(self, a):
+        return [float(a[i]) for i in self._perm]
+
+    @staticmethod
+    def _take(t, idx):
+        if torch.is_tensor(t):
+            return t[..., torch.as_tensor(idx, device=t.device)]
+        return np.asarray(t)[..., list(idx)]
+
+    def _vec_in(self, t):
+        return self._take(self._rows(t, 3), self._perm)
+
+    def _vec_out(self, t):
+        return self._take(t, self._inv)
+
+    def _mat_idx(self, p):
+        return [3 * p[i] + p[j] for i in range(3) for j in range(3)]
+
+    def _cov_idx(self, p):
+        up = self._UP
+        return [up.index(tuple(sorted((p[i], p[j])))) for i, j in up]
+
+    def _cov_in(self, t):
+        return self._take(self._rows(t, 6), self._cov_idx(self._perm))
+
+    def _rows(self, t, w):
+        return t.reshape(-1, w) if torch.is_tensor(t) else np.asarray(t).reshape(-1, w)
+
+    def _out(self, name, t):
+        """An engine field in the scene's axes."""
+        if not self._permuted:
+            return t
+        if name in ("x", "v"):
+            return self._vec_out(t)
+        if name in ("C", "F_trial", "R"):
+            return self._take(t, self._mat_idx(self._inv))
+        if name in ("cov", "init_cov"):
+            return self._take(t, self._cov_idx(self._inv))
+        return t
 
     @property
     def bounds(self):
@@ -211,13 +268,20 @@ class SlabDomain:
         return self.engine.slab_bounds(self.world)[1] if hasattr(self.engine, "slab_bounds") else 0
 
     # configuration and stepping: the engine's, with the transport
+    # (BC geometry in the scene's axes, permuted into the engine's)
     def add_fixed_cube(self, center, size):
+        if self._permuted:
+            center, size = self._p3(center), self._p3(size)
         return self.engine.add_fixed_cube(center, size)
 
     def add_impulse(self, center, size, force, substep_dt):
+        if self._permuted:
+            center, size, force = self._p3(center), self._p3(size), self._p3(force)
         return self.engine.add_impulse(center, size, force, substep_dt)
 
     def add_plane_collider(self, point, normal, friction=0.0):
+        if self._permuted:
+            point, normal = self._p3(point), self._p3(normal)
         return self.engine.add_plane_collider(point, normal, friction)
 
     def step(self, dt: float, masks):
@@ -274,11 +338,17 @@ class SlabDomain:
         return out
 
     def gather_field(self, name: str, dst: int = 0):
-        return self.gather(self.engine.get(name), dst)
+        out = self.gather(self.engine.get(name), dst)
+        return None if out is None else self._out(name, out)
 
     def gather_world(self, scale, center, render_space: bool, dst: int = 0):
         """Fused grid2world (+ render shift) of every particle, on rank `dst`:
         (means [N, 3], cov6 [N, 6]) in global order."""
+        if self._permuted:
+            center = self._p3(center)
         m, c = self.engine.world_outputs(scale, center, render_space)
         full = self.gather(torch.cat([m, c], 1), dst)
-        return (None, None) if full is None else (full[:, :3].contiguous(), full[:, 3:].contiguous())
+        if full is None:
+            return None, None
+        m, c = full[:, :3], full[:, 3:]
+        return self._out("x", m).contiguous(), self._out("cov", c).contiguous()

@@ -159,3 +159,57 @@ def test_slab_error_stops_every_rank(tmp_path):
     since, msg = errs[0].split("|", 1)
     assert f"rank {world - 1}:" in msg and "capacity" in msg, msg
     assert int(since) % 10 == 0 and int(since) < STEPS, since
+
+
+AX = [2, 1, 0]  # the test scene with x and z swapped: its longest axis (1.4) is z
+
+
+def _axis_scene():
+    x, v, cov, vol = scene()
+    up = ((0, 0), (0, 1), (0, 2), (1, 1), (1, 2), (2, 2))
+    cidx = [up.index(tuple(sorted((AX[i], AX[j])))) for i, j in up]
+    return (np.ascontiguousarray(x[:, AX]), np.ascontiguousarray(v[:, AX]), np.ascontiguousarray(cov[:, cidx]),
+            vol)
+
+
+def _axis_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gsmpm.dist import CallbackTransport, SlabDomain
+        from slab_oracle import OracleSlabEngine
+        x, v, cov, vol = _axis_scene()
+        xp = CallbackTransport(rank, world)
+        dom = SlabDomain(x, cov, vol, v=v, rank=rank, world=world, transport=xp, n_grid=NG, grid_extent=EXT,
+                         margin=2, interval=10, device="cpu", engine_factory=OracleSlabEngine, jelly_quirk=False,
+                         **KW)
+        dom.add_fixed_cube(*FIXED)
+        dom.add_plane_collider([0, 0, 0.4], [0, 0, 1])
+        dom.step(DT, [0b11] * STEPS)
+        got = {k: dom.gather_field(k) for k in ("x", "v", "C", "F_trial")}
+        mig = torch.tensor([dom.engine.migrated], dtype=torch.int64)
+        dist.all_reduce(mig)
+        if rank == 0:
+            np.savez(os.path.join(out, "res.npz"), axis=dom.cut_axis, migrated=int(mig.item()),
+                     **{k: g.numpy() for k, g in got.items()})
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_slab_cut_along_longest_axis(tmp_path, world):
+    """slabs cut along the particle bbox's longest axis.  The test
+    scene with x and z swapped is longest along z, with gravity and the drift
+    along it: SlabDomain runs the engine in a frame whose axis 0 is z (x, v,
+    cov, gravity, the fixed cube and the collider permuted in, every field
+    permuted back) and the gathered state equals the single-domain oracle run
+    in the scene's own axes."""
+    x, v, cov, vol = _axis_scene()
+    mp.spawn(_axis_worker, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
+    r = np.load(os.path.join(tmp_path, "res.npz"))
+    assert int(r["axis"]) == 2
+    assert int(r["migrated"]) > 50
+    ref = reference(x, v, cov, vol)
+    errs = {k: rel_err(r[k], getattr(ref, k)) for k in TOL}
+    for k, e in errs.items():
+        assert e < TOL[k], (world, k, e, errs)

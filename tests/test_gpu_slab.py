@@ -22,8 +22,8 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from conftest import rel_err
-from test_dist_slab import (DT, EXT, FIXED, KW, NG, STEPS, TOL, free_port, read_errors, reference, scene,
-                            top_rank_start_count)
+from test_dist_slab import (DT, EXT, FIXED, KW, NG, STEPS, TOL, _axis_scene, free_port, read_errors, reference,
+                            scene, top_rank_start_count)
 
 pytestmark = pytest.mark.gpu
 
@@ -445,3 +445,57 @@ def test_gpu_slabs_bicycle_rccl(dev, tmp_path, world, fcr):
     _dump(f"D_bicycle_slab{world}_rccl" + ("_fcr" if fcr else ""), rec)
     for k, e in errs.items():
         assert e < 1e-4, (k, e, errs)
+
+
+def _gpu_axis_worker(rank, world, port, out, backend):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if backend == "nccl-shared":
+        os.environ.update(shared_gpu_rccl_env(rank))
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    if backend == "nccl-shared":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gsmpm.dist import SlabDomain, make_transport
+        x, v, cov, vol = _axis_scene()
+        xp = make_transport(rank, world, device=dev)
+        dom = SlabDomain(x, cov, vol, v=v, rank=rank, world=world, transport=xp, n_grid=NG, grid_extent=EXT,
+                         margin=2, interval=10, device=dev, jelly_fcr=True, **KW)
+        dom.add_fixed_cube(*FIXED)
+        dom.add_plane_collider([0, 0, 0.4], [0, 0, 1])
+        for s in range(0, STEPS, 50):
+            dom.step(DT, [0b11] * 50)
+        got = {k: dom.gather_field(k) for k in ("x", "v", "C", "F_trial")}
+        dom.postprocess()
+        got["cov"] = dom.gather_field("cov")
+        mig = torch.tensor([dom.stats()["migrated"]], dtype=torch.int64, device=dev if backend != "gloo" else "cpu")
+        dist.all_reduce(mig)
+        if rank == 0:
+            np.savez(os.path.join(out, "res.npz"), axis=dom.cut_axis, migrated=int(mig[0].item()),
+                     **{k: g.cpu().numpy() for k, g in got.items()})
+        dom.engine.close()
+        xp.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("backend", ["gloo", "nccl-shared"])
+def test_gpu_slabs_cut_along_longest_axis(dev, tmp_path, backend):
+    """SURVEY 8(e)'s cut along the bbox's longest axis on the library
+    (tests/test_dist_slab.py::test_slab_cut_along_longest_axis on the CPU): the
+    x<->z-swapped scene, longest along z with gravity and drift along it, cut
+    into 2 slabs of z; x, v, C, F_trial and cov (postprocess) against the
+    single-domain oracle in the scene's own axes."""
+    x, v, cov, vol = _axis_scene()
+    mp.spawn(_gpu_axis_worker, args=(2, free_port(), str(tmp_path), backend), nprocs=2, join=True)
+    r = np.load(os.path.join(tmp_path, "res.npz"))
+    assert int(r["axis"]) == 2 and int(r["migrated"]) > 50
+    ref = reference(x, v, cov, vol)
+    errs = {k: rel_err(r[k], getattr(ref, k)) for k in TOL}
+    ref.postprocess()
+    errs["cov"] = rel_err(r["cov"], ref.cov)
+    for k, e in errs.items():
+        assert e < TOL.get(k, 1e-4), (k, e, errs)
+    print("longest-axis cut", backend, errs)
