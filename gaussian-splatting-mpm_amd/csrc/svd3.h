@@ -38,26 +38,29 @@ namespace gsmpm {
 #ifndef GSMPM_SVD_FAST
 #define GSMPM_SVD_FAST 2
 #endif
+// The refined forms run for x in [2^-100, 2^100], where y0^2 and x y0^2 stay
+// normal; anything else (0, subnormal, huge, inf, NaN, negative) takes the
+// correctly rounded form on a branch the wave skips when no lane needs it:
+// v_rsq_f32 flushes a subnormal input (rsq -> inf where 1 / sqrtf gives
+// ~1e20), at 0 / inf the step's x y0^2 is NaN, and near FLT_MAX y0^2 is
+// subnormal.  Foam's degenerate F reaches these in the Jacobi sweeps (its R
+// came out NaN with the unguarded step).
+constexpr float kNrLo = 7.88860905e-31f, kNrHi = 1.26765060e30f;  // 2^-100, 2^100
 __device__ __forceinline__ float svd_rsqrt_nr(float x) {
-  // normal finite x only; anything else (0, subnormal, inf, NaN, negative)
-  // takes the correctly rounded form on a branch the wave skips when no lane
-  // needs it.  v_rsq_f32 flushes a subnormal input (rsq -> inf where
-  // 1 / sqrtf gives ~1e20), and at 0 / inf the step's x y0^2 is NaN: foam's
-  // degenerate F reached both in the Jacobi sweeps (its R came out NaN)
-  if (x >= 1.17549435e-38f && x <= 3.40282347e38f) {
+  if (x >= kNrLo && x <= kNrHi) {
     const float y0 = __builtin_amdgcn_rsqf(x);
     return y0 * fmaf(-0.5f * x, y0 * y0, 1.5f);
   }
   return 1.0f / sqrtf(x);
 }
 __device__ __forceinline__ float svd_sqrt_nr(float x) {
-  if (x >= 1.17549435e-38f && x <= 3.40282347e38f) {
+  if (x >= kNrLo && x <= kNrHi) {
     const float y0 = __builtin_amdgcn_rsqf(x);
     const float y = y0 * fmaf(-0.5f * x, y0 * y0, 1.5f);
     const float s = x * y;
     return fmaf(0.5f * y, fmaf(-s, s, x), s);
   }
-  return sqrtf(x);  // 0, subnormal, inf, negative
+  return sqrtf(x);
 }
 template <bool FAST>
 __device__ __forceinline__ float svd_rsqrt(float x) {

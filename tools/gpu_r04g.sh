@@ -7,6 +7,10 @@
 set -o pipefail
 O=gpurun_out/r04g
 mkdir -p $O
+for L in libgsmpm.so libgsmpm_svdexact.so; do
+  GSMPM_LIB=$PWD/gaussian-splatting-mpm_amd/$L timeout -k 10 120 python -u -m pytest tests/test_gpu_constitutive.py -q -k degenerate --timeout 100 --timeout-method thread > $O/svd_degenerate_$L.log 2>&1
+  echo "$L degenerate-scale SVD rc $?"; grep -E "passed|failed|^E .*Assertion" $O/svd_degenerate_$L.log | head -4
+done
 GSMPM_PARITY_OUT=$O/parity timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread --durations=15 > $O/tests.log 2>&1
 rc=$?
 tail -22 $O/tests.log
