@@ -1102,7 +1102,10 @@ __global__ __launch_bounds__(256) void k_postprocess(Particles ps, const int* __
   ps.stc(PCOV + 4, o, Cv[1][2]);
   ps.stc(PCOV + 5, o, Cv[2][2]);
   float U[3][3], V[3][3], s[3];
-  svd3(F, U, s, V);
+  // R is an output, once per frame: the correctly rounded SVD (the substep's
+  // refined rsqrt differs from 1 / sqrtf by < 1 ulp, which a degenerate F --
+  // foam's -- can turn into a different rotation)
+  svd3<false>(F, U, s, V);
   if (det3(U) < 0.f) {
     U[0][2] = -U[0][2];
     U[1][2] = -U[1][2];
