@@ -178,10 +178,16 @@ class SlabDomain:
         # axis 0 is the cut axis: coordinates, velocities, matrices, covariances,
         # gravity and every BC are permuted on the way in and back on the way out
         # (the grid is cubic and the update is axis-symmetric, so this is the same
-        # computation up to f32 operand order).  A tie keeps axis 0 (lego: x and y
-        # at 1.3; bicycle: a cube), where nothing is permuted.
+        # computation up to f32 operand order).  Axis 0 is kept unless another is
+        # more than 1 / 0.9 times longer (lego: x and y tie at 1.3; bicycle: a
+        # cube, whose sampled extents differ in the 5th digit), where nothing is
+        # permuted.
         ext = (xh.max(0) - xh.min(0)) if len(xh) else np.zeros(3)
-        a = int(np.argmax(ext)) if cut_axis == "longest" else int(cut_axis)
+        if cut_axis == "longest":
+            a = int(np.argmax(ext))
+            a = 0 if ext[0] >= 0.9 * ext[a] else a
+        else:
+            a = int(cut_axis)
         if not 0 <= a < 3:
             raise ValueError(f"cut_axis must be 'longest' or 0, 1, 2 (got {cut_axis!r})")
         self.cut_axis = a
