@@ -52,7 +52,31 @@ def main(path):
               f"({100.0 * cov / max(tot, 1):.1f} %)")
     if interior:
         it = sum(b - a for a, b in interior)
-        print(f"interior pass time {it / 1e3:.1f} us total, {it / len(interior) / 1e3:.2f} us each")
+        under = 0
+        for c, d in interior:
+            for a, b in nccl:
+                if b <= c:
+                    continue
+                if a >= d:
+                    break
+                under += min(b, d) - max(a, c)
+        print(f"interior pass time {it / 1e3:.1f} us total, {it / len(interior) / 1e3:.2f} us each; "
+              f"under an exchange kernel {under / 1e3:.1f} us ({100.0 * under / max(it, 1):.1f} %)")
+    # the window pass (first k_grid_f after each k_fused) to the next exchange kernel's start
+    gaps = []
+    fi = seen = 0
+    for a, b in grid:
+        while fi < len(fused) and fused[fi] < a:
+            fi += 1
+            seen = 0
+        seen += 1
+        if seen == 1:
+            nxt = next((x for x, _ in nccl if x >= a), None)
+            if nxt is not None and nxt - b < 5e5:
+                gaps.append(nxt - b)
+    if gaps:
+        gaps.sort()
+        print(f"window pass end -> exchange kernel start: median {gaps[len(gaps) // 2] / 1e3:.2f} us over {len(gaps)}")
 
 
 if __name__ == "__main__":
