@@ -186,7 +186,7 @@ def algorithmic_bytes_live(n, live_nodes, material):
 
 # translation units whose kernels are not the simulator's (the rasterizer, the
 # differentiable MPM): their edits do not change k_fused / k_grid_f
-NON_SIM_SOURCES = ("raster.hip", "fit.hip", "dsort.h", "scan.h")  # rasterizer / fit translation units only
+NON_SIM_SOURCES = ("raster.hip", "fit.hip", "dsort.h", "scan.h", "lsd.h")  # rasterizer / fit units, the one-time sorts
 
 
 def source_sha():

@@ -101,31 +101,39 @@ static __global__ __launch_bounds__(256) void k_rows_wide(int nch, const unsigne
 // chunks, the library's block radix sort for the local ranks, the library's
 // device scan) ran 1.41 ms per bicycle render against 1.31 with the library's
 // onesweep.
+// I: keys per thread (chunk = 256 I); 16 by default.  The rasterizer's tile
+// sort can take 32 (GSMPM_RASTER_LSD_I=32, A/B): 8,192-pair chunks, digit runs
+// of 32 pairs on average instead of 16 (128-byte store runs), half the chunk
+// histograms, 2 workgroups per CU (68 KB of LDS).
 constexpr int kLsdT = 256, kLsdI = 16, kLsdChunk = kLsdT * kLsdI;
+template <int I = kLsdI>
 static __global__ __launch_bounds__(kLsdT) void k_lsd_hist(int K, int nch, int shift, const unsigned* __restrict__ keys,
                                                     unsigned* __restrict__ H) {
+  constexpr int kChunkI = kLsdT * I;
   __shared__ unsigned s_h[256];
   s_h[threadIdx.x] = 0;
   __syncthreads();
   const int c = blockIdx.x;
-  unsigned k[kLsdI];
+  unsigned k[I];
 #pragma unroll
-  for (int i = 0; i < kLsdI; ++i) {
-    const int e = c * kLsdChunk + i * kLsdT + threadIdx.x;
+  for (int i = 0; i < I; ++i) {
+    const int e = c * kChunkI + i * kLsdT + threadIdx.x;
     k[i] = e < K ? keys[e] : 0u;
   }
 #pragma unroll
-  for (int i = 0; i < kLsdI; ++i)
-    if (c * kLsdChunk + i * kLsdT + (int)threadIdx.x < K) atomicAdd(&s_h[(k[i] >> shift) & 255u], 1u);
+  for (int i = 0; i < I; ++i)
+    if (c * kChunkI + i * kLsdT + (int)threadIdx.x < K) atomicAdd(&s_h[(k[i] >> shift) & 255u], 1u);
   __syncthreads();
   H[(size_t)threadIdx.x * nch + c] = s_h[threadIdx.x];
 }
+template <int I = kLsdI>
 static __global__ __launch_bounds__(kLsdT) void k_lsd_scatter(int K, int nch, int shift, const unsigned* __restrict__ keys,
                                                        const unsigned* __restrict__ vals,
                                                        const unsigned* __restrict__ Hs, const unsigned* __restrict__ tot,
                                                        unsigned* __restrict__ keys_out,
                                                        unsigned* __restrict__ vals_out) {
-  __shared__ unsigned s_k[kLsdChunk], s_v[kLsdChunk];
+  constexpr int kChunkI = kLsdT * I;
+  __shared__ unsigned s_k[kChunkI], s_v[kChunkI];
   __shared__ unsigned s_wrun[4][256];  // per wave: running count of each digit, then its offset
   __shared__ unsigned s_doff[256];     // chunk-local start of each digit's run
   __shared__ unsigned s_gbase[256];    // global position of this chunk's run of each digit
@@ -146,18 +154,18 @@ static __global__ __launch_bounds__(kLsdT) void k_lsd_scatter(int K, int nch, in
   unsigned dstart = inc - dt;
   for (int w = 0; w < wv; ++w) dstart += s_part[w][0];
   s_gbase[t] = dstart + Hs[(size_t)t * nch + c];
-  // wave wv ranks pairs [c * 4096 + wv * 1024, +1024) in 16 slots of 64, in order
-  const int e0 = c * kLsdChunk + wv * (kLsdChunk / 4);
-  unsigned k[kLsdI], v[kLsdI], r[kLsdI];
+  // wave wv ranks pairs [c * 256 I + wv * 64 I, + 64 I) in I slots of 64, in order
+  const int e0 = c * kChunkI + wv * (kChunkI / 4);
+  unsigned k[I], v[I], r[I];
 #pragma unroll
-  for (int j = 0; j < kLsdI; ++j) {
+  for (int j = 0; j < I; ++j) {
     const int e = e0 + j * 64 + lane;
     k[j] = e < K ? keys[e] : 0u;
     v[j] = e < K ? vals[e] : 0u;
   }
   const unsigned long long below = (1ull << lane) - 1ull;
 #pragma unroll
-  for (int j = 0; j < kLsdI; ++j) {
+  for (int j = 0; j < I; ++j) {
     const bool ok = e0 + j * 64 + lane < K;
     const unsigned d = ok ? (k[j] >> shift) & 255u : 256u;
     unsigned long long peers = ~0ull;
@@ -195,7 +203,7 @@ static __global__ __launch_bounds__(kLsdT) void k_lsd_scatter(int K, int nch, in
   }
   __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kLsdI; ++j) {
+  for (int j = 0; j < I; ++j) {
     if (e0 + j * 64 + lane < K) {
       const unsigned idx = s_wrun[wv][(k[j] >> shift) & 255u] + r[j];
       s_k[idx] = k[j];
@@ -203,9 +211,9 @@ static __global__ __launch_bounds__(kLsdT) void k_lsd_scatter(int K, int nch, in
     }
   }
   __syncthreads();
-  const int nv = min(kLsdChunk, K - c * kLsdChunk);
+  const int nv = min(kChunkI, K - c * kChunkI);
 #pragma unroll
-  for (int i = 0; i < kLsdI; ++i) {  // striped: each digit run leaves as coalesced stores
+  for (int i = 0; i < I; ++i) {  // striped: each digit run leaves as coalesced stores
     const int sp = i * kLsdT + t;
     if (sp < nv) {
       const unsigned kk = s_k[sp], d = (kk >> shift) & 255u;

@@ -2266,7 +2266,10 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       const bool digits = !chunked && !force_onesweep && !(ls && ls[0] == '0');
       const int passes = (bits + 7) / 8;  // ntiles <= 256^passes - 1: the all-ones tile field stays the culled one
       const int nch = (int)div_up(K, kChunk);
-      const int nchl = (int)div_up(K, kLsdChunk);
+      // GSMPM_RASTER_LSD_I=32: 8,192-pair chunks for the digit sort (A/B; lsd.h)
+      const char* li = std::getenv("GSMPM_RASTER_LSD_I");
+      const bool lsd32 = li && std::atoi(li) == 32;
+      const int nchl = (int)div_up(K, lsd32 ? 32 * kLsdT : kLsdChunk);
       // digit rows of at least this many chunks: a workgroup per row (k_rows_wide); tests lower it
       const char* rw = std::getenv("GSMPM_RASTER_ROWS_WIDE_MIN");
       const int rows_wide_min = rw ? std::atoi(rw) : kRowsWideMin;
@@ -2351,15 +2354,22 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
             const bool fin = (passes - 1 - p) % 2 == 0;
             unsigned* dk = fin ? tile_sorted : alt_k;
             unsigned* dv = fin ? r->ids_sorted : alt_v;
-            hipLaunchKernelGGL(k_lsd_hist, dim3(nchl), dim3(kLsdT), 0, st, (int)K, nchl, 8 * p, sk, r->hist);
+            if (lsd32)
+              hipLaunchKernelGGL(k_lsd_hist<32>, dim3(nchl), dim3(kLsdT), 0, st, (int)K, nchl, 8 * p, sk, r->hist);
+            else
+              hipLaunchKernelGGL(k_lsd_hist<kLsdI>, dim3(nchl), dim3(kLsdT), 0, st, (int)K, nchl, 8 * p, sk, r->hist);
             if (nchl >= rows_wide_min && nchl <= kRowsWideMax)
               hipLaunchKernelGGL(k_rows_wide, dim3(256), dim3(256), nchl * sizeof(unsigned), st, nchl,
                                  (const unsigned*)r->hist, Hs, r->ttot, (const unsigned*)nullptr, 0u);
             else
               hipLaunchKernelGGL(k_tile_rows, dim3(64), dim3(256), 0, st, 255, nchl, (const unsigned*)r->hist, Hs,
                                  r->ttot);
-            hipLaunchKernelGGL(k_lsd_scatter, dim3(nchl), dim3(kLsdT), 0, st, (int)K, nchl, 8 * p, sk, sv,
-                               (const unsigned*)Hs, (const unsigned*)r->ttot, dk, dv);
+            if (lsd32)
+              hipLaunchKernelGGL(k_lsd_scatter<32>, dim3(nchl), dim3(kLsdT), 0, st, (int)K, nchl, 8 * p, sk, sv,
+                                 (const unsigned*)Hs, (const unsigned*)r->ttot, dk, dv);
+            else
+              hipLaunchKernelGGL(k_lsd_scatter<kLsdI>, dim3(nchl), dim3(kLsdT), 0, st, (int)K, nchl, 8 * p, sk, sv,
+                                 (const unsigned*)Hs, (const unsigned*)r->ttot, dk, dv);
             GSMPM_LAUNCH_CHECK();
             sk = dk;
             sv = dv;

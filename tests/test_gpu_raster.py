@@ -296,16 +296,20 @@ def test_digit_tile_sort_matches_onesweep(dev, monkeypatch, P, W, H, tiles):
                                        debug=False)
     out = {}
     # "wide": the digit rows' prefixes by a workgroup per row (k_rows_wide), as bicycle-sized frames take them
-    for form, lsd, wide in (("onesweep", "0", None), ("lsd", "1", None), ("wide", "1", "1")):
+    # "lsd32": 8,192-pair chunks (GSMPM_RASTER_LSD_I=32)
+    for form, lsd, wide, li in (("onesweep", "0", None, None), ("lsd", "1", None, None), ("wide", "1", "1", None),
+                                ("lsd32", "1", "1", "32")):
         monkeypatch.setenv("GSMPM_RASTER_LSD", lsd)
         if wide:
             monkeypatch.setenv("GSMPM_RASTER_ROWS_WIDE_MIN", wide)
+        if li:
+            monkeypatch.setenv("GSMPM_RASTER_LSD_I", li)
         m3, o1, s1, cv = t(means, True), t(opa, True), t(shs, True), t(c6, True)
         img, radii = GaussianRasterizer(st)(means3D=m3, means2D=None, opacities=o1, shs=s1, cov3D_precomp=cv)
         (img * wgt).sum().backward()
         out[form] = [x.detach().cpu().numpy() for x in (img, radii, m3.grad, o1.grad, s1.grad, cv.grad)]
     assert (out["lsd"][1] > 0).sum() > P // 4
-    for form in ("lsd", "wide"):
+    for form in ("lsd", "wide", "lsd32"):
         for a, b in zip(out[form], out["onesweep"]):
             assert np.array_equal(a, b), form
 
