@@ -101,10 +101,11 @@ static __global__ __launch_bounds__(256) void k_rows_wide(int nch, const unsigne
 // chunks, the library's block radix sort for the local ranks, the library's
 // device scan) ran 1.41 ms per bicycle render against 1.31 with the library's
 // onesweep.
-// I: keys per thread (chunk = 256 I); 16 by default.  The rasterizer's tile
-// sort can take 32 (GSMPM_RASTER_LSD_I=32, A/B): 8,192-pair chunks, digit runs
-// of 32 pairs on average instead of 16 (128-byte store runs), half the chunk
-// histograms, 2 workgroups per CU (68 KB of LDS).
+// I: keys per thread (chunk = 256 I); 16 by default (the simulator's
+// re-sort).  The rasterizer's tile sort takes 32: 8,192-pair chunks, digit
+// runs of 32 pairs on average instead of 16 (128-byte store runs), half the
+// chunk histograms, 2 workgroups per CU (68 KB of LDS); GSMPM_RASTER_LSD_I=16
+// restores 16 there (A/B).
 constexpr int kLsdT = 256, kLsdI = 16, kLsdChunk = kLsdT * kLsdI;
 template <int I = kLsdI>
 static __global__ __launch_bounds__(kLsdT) void k_lsd_hist(int K, int nch, int shift, const unsigned* __restrict__ keys,

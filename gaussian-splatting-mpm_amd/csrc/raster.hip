@@ -2266,9 +2266,11 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       const bool digits = !chunked && !force_onesweep && !(ls && ls[0] == '0');
       const int passes = (bits + 7) / 8;  // ntiles <= 256^passes - 1: the all-ones tile field stays the culled one
       const int nch = (int)div_up(K, kChunk);
-      // GSMPM_RASTER_LSD_I=32: 8,192-pair chunks for the digit sort (A/B; lsd.h)
+      // 8,192-pair chunks for the digit sort (lsd.h): bicycle render 1.078-1.080 against
+      // 1.082-1.088 ms with 4,096 (3 rounds, profiles/r04/render/ab_lsd_chunk_r04i.txt);
+      // GSMPM_RASTER_LSD_I=16 restores 4,096 (A/B)
       const char* li = std::getenv("GSMPM_RASTER_LSD_I");
-      const bool lsd32 = li && std::atoi(li) == 32;
+      const bool lsd32 = !(li && std::atoi(li) == 16);
       const int nchl = (int)div_up(K, lsd32 ? 32 * kLsdT : kLsdChunk);
       // digit rows of at least this many chunks: a workgroup per row (k_rows_wide); tests lower it
       const char* rw = std::getenv("GSMPM_RASTER_ROWS_WIDE_MIN");

@@ -296,9 +296,9 @@ def test_digit_tile_sort_matches_onesweep(dev, monkeypatch, P, W, H, tiles):
                                        debug=False)
     out = {}
     # "wide": the digit rows' prefixes by a workgroup per row (k_rows_wide), as bicycle-sized frames take them
-    # "lsd32": 8,192-pair chunks (GSMPM_RASTER_LSD_I=32)
+    # "lsd16": 4,096-pair chunks (GSMPM_RASTER_LSD_I=16; the default takes 8,192)
     for form, lsd, wide, li in (("onesweep", "0", None, None), ("lsd", "1", None, None), ("wide", "1", "1", None),
-                                ("lsd32", "1", "1", "32")):
+                                ("lsd16", "1", "1", "16")):
         monkeypatch.setenv("GSMPM_RASTER_LSD", lsd)
         if wide:
             monkeypatch.setenv("GSMPM_RASTER_ROWS_WIDE_MIN", wide)
@@ -309,7 +309,7 @@ def test_digit_tile_sort_matches_onesweep(dev, monkeypatch, P, W, H, tiles):
         (img * wgt).sum().backward()
         out[form] = [x.detach().cpu().numpy() for x in (img, radii, m3.grad, o1.grad, s1.grad, cv.grad)]
     assert (out["lsd"][1] > 0).sum() > P // 4
-    for form in ("lsd", "wide", "lsd32"):
+    for form in ("lsd", "wide", "lsd16"):
         for a, b in zip(out[form], out["onesweep"]):
             assert np.array_equal(a, b), form
 
