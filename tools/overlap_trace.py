@@ -77,6 +77,27 @@ def main(path):
     if gaps:
         gaps.sort()
         print(f"window pass end -> exchange kernel start: median {gaps[len(gaps) // 2] / 1e3:.2f} us over {len(gaps)}")
+    # off the critical path: interior-pass time inside [its window pass's end, the next exchange kernel's end]
+    # (the exchange -- RCCL's launch and its kernel -- follows the window pass; k_win_update waits for both)
+    hid = tot_i = 0
+    wins = []
+    fi = seen = 0
+    for a, b in grid:
+        while fi < len(fused) and fused[fi] < a:
+            fi += 1
+            seen = 0
+        seen += 1
+        if seen == 1:
+            wins.append(b)
+    for c, d in interior:
+        w_end = max((x for x in wins if x <= c), default=None)
+        x_end = next((e for x, e in nccl if x >= (w_end if w_end is not None else c)), None)
+        tot_i += d - c
+        if w_end is not None and x_end is not None:
+            hid += max(0, min(d, x_end) - max(c, w_end))
+    if tot_i:
+        print(f"interior pass time between its window pass's end and the exchange kernel's end: "
+              f"{100.0 * hid / tot_i:.1f} % (off the critical path)")
 
 
 if __name__ == "__main__":
