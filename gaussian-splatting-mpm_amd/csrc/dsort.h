@@ -49,11 +49,12 @@ enum : int {
   DS_CULL = 16,    // culled cursor
   DS_NLIST = 17,   // occupied buckets of <= kDsSmall
   DS_NBIG = 18,    // occupied buckets above
-  DS_OVER = 19,    // a bucket above kDsBig (host fallback)
+  DS_OVER = 19,    // a bucket above kDsBig (host fallback): set by k_dsort_scan1, reset by k_dsort_scatter
   DS_PV = 20,      // visible Gaussians
   DS_LO = 21, DS_SHIFT = 22, DS_NB = 23,
   DS_TOT = 24,     // [2] u64 total of the tiles words (K | num_rendered << 32)
   DS_MAXN = 26,    // the largest bucket (diagnostics)
+  DS_OVERD = 29,   // the overflow flag the last bucket-form forward published (diagnostics)
   kDsWords = 32
 };
 
@@ -86,6 +87,18 @@ struct DsortBufs {
 };
 
 __device__ __forceinline__ int ds_log2(int nb) { return 31 - __clz(nb); }
+
+// The pair counts to the host (pinned, coherent; the host spins on pub[0]):
+// pub[2] = the overflow flag, pub[1] = num_rendered, then pub[0] = K.  The
+// depth order publishes them itself as soon as they are known -- the bucket
+// form from k_dsort_scan2 (the total of the tiles words), before its scatter
+// and in-bucket sorts run, the LSD form from the last element of its scan --
+// so the host queues the post-count launches while the order is finished.
+__device__ __forceinline__ void ds_publish(unsigned* pub, unsigned long long v, unsigned over) {
+  __hip_atomic_store(pub + 2, over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(pub + 1, (unsigned)(v >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(pub, (unsigned)v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // the bucket map: lo and shift from the shards, by one whole wave (lane l
 // reads shard l; every lane gets the result)
@@ -190,11 +203,12 @@ __global__ __launch_bounds__(256) void k_dsort_scan1(DsortBufs d, unsigned* __re
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // the list counters k_dsort_scan2 reserves from
     d.st[DS_NLIST] = 0;
     d.st[DS_NBIG] = 0;
-    d.st[DS_OVER] = 0;
     d.st[DS_MAXN] = 0;
   }
   const int b = blockIdx.x * kDsBlk + 4 * threadIdx.x;
   const uint4 c4 = *reinterpret_cast<const uint4*>(d.bcount + b);
+  // a bucket above kDsBig: the flag k_dsort_scan2 publishes (zero here: k_dsort_scatter resets it)
+  if (max(max(c4.x, c4.y), max(c4.z, c4.w)) > (unsigned)kDsBig) d.st[DS_OVER] = 1u;
   const ulonglong2 s01 = *reinterpret_cast<const ulonglong2*>(d.bsum + b);
   const ulonglong2 s23 = *reinterpret_cast<const ulonglong2*>(d.bsum + b + 2);
   const unsigned c = ds_block_sum_u32(c4.x + c4.y + c4.z + c4.w, s_c);
@@ -205,7 +219,8 @@ __global__ __launch_bounds__(256) void k_dsort_scan1(DsortBufs d, unsigned* __re
   }
 }
 __global__ __launch_bounds__(256) void k_dsort_scan2(int nb, DsortBufs d, const unsigned* __restrict__ btc,
-                                                     const unsigned long long* __restrict__ bts) {
+                                                     const unsigned long long* __restrict__ bts,
+                                                     unsigned* __restrict__ pub) {
   __shared__ unsigned s_c[4], s_f[4], s_wf[4], s_base[2];
   __shared__ unsigned long long s_s[4];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6, g = blockIdx.x, ng = nb / kDsBlk;
@@ -300,7 +315,6 @@ __global__ __launch_bounds__(256) void k_dsort_scan2(int nb, DsortBufs d, const 
         d.blist[li++] = (unsigned)bb;
       } else {
         d.bbig[bi++] = (unsigned)bb;
-        if (n[q] > (unsigned)kDsBig) d.st[DS_OVER] = 1u;
       }
       run += n[q];
       pre += sm[q];
@@ -318,6 +332,9 @@ __global__ __launch_bounds__(256) void k_dsort_scan2(int nb, DsortBufs d, const 
       d.st[DS_CULL] = 0;
       d.st[DS_TOT] = (unsigned)as;
       d.st[DS_TOT + 1] = (unsigned)(as >> 32);
+      const unsigned over = d.st[DS_OVER];
+      d.st[DS_OVERD] = over;
+      if (pub) ds_publish(pub, as, over);  // K and num_rendered are the total of the tiles words
     }
   }
 }
@@ -328,6 +345,7 @@ __global__ __launch_bounds__(256) void k_dsort_scatter(int P, const float* __res
                                                        unsigned long long* __restrict__ offr) {
   if (blockIdx.x == 0 && threadIdx.x < 2 * kDsShards)  // the shards: read for the last time by k_dsort_scan2
     d.shard[(threadIdx.x >> 1) * kDsShardWords + (threadIdx.x & 1)] = 0u;
+  if (blockIdx.x == 0 && threadIdx.x == 0) d.st[DS_OVER] = 0u;  // published by k_dsort_scan2
   const int i = blockIdx.x * 256 + threadIdx.x;
   const unsigned lo = d.st[DS_LO], shift = d.st[DS_SHIFT], pv = d.st[DS_PV];
   const bool in = i < P;
@@ -732,7 +750,8 @@ __global__ __launch_bounds__(256) void k_dl_scan_blocks(int P, const unsigned lo
 __global__ __launch_bounds__(256) void k_dl_scan_apply(int P, const unsigned long long* __restrict__ tiles, DlBufs b,
                                                        const unsigned long long* __restrict__ btot,
                                                        unsigned* __restrict__ order,
-                                                       unsigned long long* __restrict__ offr) {
+                                                       unsigned long long* __restrict__ offr,
+                                                       unsigned* __restrict__ pub) {
   __shared__ unsigned long long s_w[4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = blockIdx.x;
   const unsigned* ord = dl_final(b);
@@ -764,6 +783,7 @@ __global__ __launch_bounds__(256) void k_dl_scan_apply(int P, const unsigned lon
     if (i0 + q < P) {
       order[i0 + q] = o[q];
       offr[i0 + q] = run;
+      if (pub && i0 + q == P - 1) ds_publish(pub, run, 0u);  // the total: K, num_rendered
     }
   }
 }

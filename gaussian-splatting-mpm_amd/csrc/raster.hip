@@ -1761,7 +1761,7 @@ struct gsmpm_raster {
   unsigned long long* scan_bt = nullptr;  // [capP / 1024 + 1] block totals of the index-order scans (scan.h)
   unsigned* dl_h = nullptr;    // [2 * 256 * (capP / kDlChunk + 1) + 256] the LSD depth order's counts, prefixes, totals
   long dsort_fallbacks = 0;    // forwards whose depth order fell back to the library sort
-  hipEvent_t count_ev = nullptr;  // recorded after k_publish_count: surfaces a fault while the host spins
+  hipEvent_t count_ev = nullptr;  // recorded after the publishing kernels: surfaces a fault while the host spins
   // per pixel (backward)
   size_t capPix = 0;
   float* final_T = nullptr;
@@ -2144,8 +2144,51 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
                                         rocprim::plus<unsigned long long>(), st));
       return GSMPM_OK;
     };
+    // K straight into pinned, coherent host memory by the depth order's own
+    // last kernels (dsort.h ds_publish; the library path: a one-lane kernel),
+    // and a spin on it: no copy-engine packet and no sleeping stream sync
+    // between the scan and the post-count launches.  Every 256 polls the event
+    // recorded behind the publishing kernels is queried, so a device fault
+    // surfaces at once instead of after a timeout; a completed event with no
+    // count is an error.  The count needs the host, so a capturing stream is
+    // refused.
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    GSMPM_HIP(hipStreamIsCapturing(st, &cap));
+    GSMPM_REQUIRE(cap == hipStreamCaptureStatusNone,
+                  "gsmpm_raster_forward: the pair count is read on the host; the stream must not be capturing");
+    volatile unsigned* hc = r->h_count;
+    auto arm = [&]() {
+      hc[0] = kNoCount;
+      hc[1] = kNoCount;
+      hc[2] = 0;
+    };
+    auto wait_count = [&]() -> int {
+      GSMPM_HIP(hipEventRecord(r->count_ev, st));
+      for (unsigned polls = 1; *hc == kNoCount; ++polls) {
+        if ((polls & 255) == 0) {
+          const hipError_t q = hipEventQuery(r->count_ev);
+          if (q == hipSuccess) break;  // everything up to the publish finished: K is visible below
+          if (q != hipErrorNotReady) GSMPM_HIP(q);
+        }
+        __builtin_ia32_pause();
+      }
+      return GSMPM_OK;
+    };
+    auto publish = [&](const unsigned* over) -> int {  // a one-lane kernel behind everything so far
+      arm();
+      hipLaunchKernelGGL(k_publish_count, dim3(1), dim3(1), 0, st, (const unsigned long long*)(r->offr + (P - 1)),
+                         over, r->h_count);
+      GSMPM_LAUNCH_CHECK();
+      return wait_count();
+    };
+    // GSMPM_RASTER_EARLY_COUNT=0: the hand-written depth order leaves the publish to the one-lane
+    // kernel after its last launch, as rounds 1-3 did (A/B)
+    const char* ec = std::getenv("GSMPM_RASTER_EARLY_COUNT");
+    const bool early = own_dsort && !(ec && ec[0] == '0');
+    unsigned* pub = early ? r->h_count : nullptr;
     // the depth order depends on P only: it runs before the count read-back,
     // queued behind whatever the stream is still doing
+    if (early) arm();  // before the kernels that publish
     if (lsd_dsort) {
       const DlBufs b = dl_bufs(r, P);
       const int nch = div_up(P, kDlChunk);
@@ -2173,7 +2216,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       const int nsb = div_up(P, kScanBlk);
       hipLaunchKernelGGL(k_dl_scan_blocks, dim3(nsb), dim3(256), 0, st, P, tw, b, r->scan_bt);
       hipLaunchKernelGGL(k_dl_scan_apply, dim3(nsb), dim3(256), 0, st, P, tw, b,
-                         (const unsigned long long*)r->scan_bt, r->dorder, r->offr);
+                         (const unsigned long long*)r->scan_bt, r->dorder, r->offr, pub);
       GSMPM_LAUNCH_CHECK();
     } else if (own_dsort) {
       const int nb = dsort_buckets(P);
@@ -2181,7 +2224,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
                          (const unsigned long long*)r->tiles, db);
       hipLaunchKernelGGL(k_dsort_scan1, dim3(nb / kDsBlk), dim3(256), 0, st, db, db.btc, db.bts);
       hipLaunchKernelGGL(k_dsort_scan2, dim3(nb / kDsBlk), dim3(256), 0, st, nb, db, (const unsigned*)db.btc,
-                         (const unsigned long long*)db.bts);
+                         (const unsigned long long*)db.bts, pub);
       hipLaunchKernelGGL(k_dsort_scatter, dim3(div_up(P, 256)), dim3(256), 0, st, P, (const float*)r->depth,
                          (const unsigned long long*)r->tiles, db, r->dorder, r->offr);
       // a wave per bucket, up to one bucket per wave at ~8 Gaussians a bucket (one pass: the loop's
@@ -2195,36 +2238,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       const int rc = lib_depth_order();
       if (rc) return rc;
     }
-    // K straight into pinned, coherent host memory by a one-lane kernel, and a
-    // spin on it: no copy-engine packet and no sleeping stream sync between
-    // the scan and the post-count launches.  Every 256 polls the event
-    // recorded behind the publish is queried, so a device fault surfaces at
-    // once instead of after a timeout; a completed event with no count is an
-    // error.  The count needs the host, so a capturing stream is refused.
-    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    GSMPM_HIP(hipStreamIsCapturing(st, &cap));
-    GSMPM_REQUIRE(cap == hipStreamCaptureStatusNone,
-                  "gsmpm_raster_forward: the pair count is read on the host; the stream must not be capturing");
-    volatile unsigned* hc = r->h_count;
-    auto publish = [&](const unsigned* over) -> int {
-      *hc = kNoCount;
-      hc[1] = kNoCount;
-      hc[2] = 0;
-      hipLaunchKernelGGL(k_publish_count, dim3(1), dim3(1), 0, st, (const unsigned long long*)(r->offr + (P - 1)),
-                         over, r->h_count);
-      GSMPM_LAUNCH_CHECK();
-      GSMPM_HIP(hipEventRecord(r->count_ev, st));
-      for (unsigned polls = 1; *hc == kNoCount; ++polls) {
-        if ((polls & 255) == 0) {
-          const hipError_t q = hipEventQuery(r->count_ev);
-          if (q == hipSuccess) break;  // everything up to the publish finished: K is visible below
-          if (q != hipErrorNotReady) GSMPM_HIP(q);
-        }
-        __builtin_ia32_pause();
-      }
-      return GSMPM_OK;
-    };
-    int rc = publish(own_dsort && !lsd_dsort ? db.st + DS_OVER : nullptr);
+    int rc = early ? wait_count() : publish(own_dsort && !lsd_dsort ? db.st + DS_OVERD : nullptr);
     if (rc) return rc;
     if (own_dsort && !lsd_dsort && hc[2]) {  // a depth bucket above kDsBig entries: the library sort instead (dsort.h)
       r->dsort_fallbacks += 1;
@@ -2520,7 +2534,7 @@ int gsmpm_raster_dsort_stats(const gsmpm_raster* r, int64_t out8[8]) {
   out8[1] = st[DS_NLIST];
   out8[2] = st[DS_NBIG];
   out8[3] = st[DS_MAXN];
-  out8[4] = st[DS_OVER];
+  out8[4] = st[DS_OVERD];
   out8[5] = st[DS_PV];
   out8[6] = r->dsort_fallbacks;
   out8[7] = st[DS_SHIFT];

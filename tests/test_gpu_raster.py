@@ -373,13 +373,16 @@ def test_depth_order_matches_library_sort(dev, monkeypatch, case):
     args = (t(means), t(opa), t(view), t(full), t(campos), t(bgv), H, W, tx, ty)
     kw = dict(sh_degree=3, shs=t(shs), cov3D_precomp=t(c6))
     out = {}
-    for mode in ("bucket", "lsd", "lib"):
+    # early: the hand-written forms publish the pair count from their own kernels (dsort.h ds_publish);
+    # "0": from the one-lane kernel after the order, as the library path does
+    for mode, early in (("bucket", "1"), ("lsd", "1"), ("bucket", "0"), ("lsd", "0"), ("lib", "1")):
         monkeypatch.setenv("GSMPM_RASTER_DSORT", mode)
+        monkeypatch.setenv("GSMPM_RASTER_EARLY_COUNT", early)
         for ctx in (None, raster.RasterContext()):  # the workspace form and the context form
             K, color, radii = raster.forward(*args, **kw, context=ctx)
             torch.cuda.synchronize()
-            out[(mode, ctx is None)] = (K, color.cpu().numpy(), radii.cpu().numpy())
-    K0, c0, r0 = out[("lib", False)]
+            out[(mode, early, ctx is None)] = (K, color.cpu().numpy(), radii.cpu().numpy())
+    K0, c0, r0 = out[("lib", "1", False)]
     assert K0 > 0 and c0.max() > 0
     if case == "culled":
         assert (r0 == 0).sum() >= P // 3, int((r0 == 0).sum())
