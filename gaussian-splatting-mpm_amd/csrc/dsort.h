@@ -55,6 +55,7 @@ enum : int {
   DS_TOT = 24,     // [2] u64 total of the tiles words (K | num_rendered << 32)
   DS_MAXN = 26,    // the largest bucket (diagnostics)
   DS_OVERD = 29,   // the overflow flag the last bucket-form forward published (diagnostics)
+  DS_BIGANY = 30,  // a bucket above kDsSmall (k_dsort_big has work): set by k_dsort_scan1, reset by k_dsort_scatter
   kDsWords = 32
 };
 
@@ -89,12 +90,14 @@ struct DsortBufs {
 __device__ __forceinline__ int ds_log2(int nb) { return 31 - __clz(nb); }
 
 // The pair counts to the host (pinned, coherent; the host spins on pub[0]):
-// pub[2] = the overflow flag, pub[1] = num_rendered, then pub[0] = K.  The
+// pub[3] = a bucket above kDsSmall exists, pub[2] = the overflow flag, pub[1]
+// = num_rendered, then pub[0] = K.  The
 // depth order publishes them itself as soon as they are known -- the bucket
 // form from k_dsort_scan2 (the total of the tiles words), before its scatter
 // and in-bucket sorts run, the LSD form from the last element of its scan --
 // so the host queues the post-count launches while the order is finished.
-__device__ __forceinline__ void ds_publish(unsigned* pub, unsigned long long v, unsigned over) {
+__device__ __forceinline__ void ds_publish(unsigned* pub, unsigned long long v, unsigned over, unsigned big = 1u) {
+  __hip_atomic_store(pub + 3, big, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(pub + 2, over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(pub + 1, (unsigned)(v >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(pub, (unsigned)v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -208,7 +211,9 @@ __global__ __launch_bounds__(256) void k_dsort_scan1(DsortBufs d, unsigned* __re
   const int b = blockIdx.x * kDsBlk + 4 * threadIdx.x;
   const uint4 c4 = *reinterpret_cast<const uint4*>(d.bcount + b);
   // a bucket above kDsBig: the flag k_dsort_scan2 publishes (zero here: k_dsort_scatter resets it)
-  if (max(max(c4.x, c4.y), max(c4.z, c4.w)) > (unsigned)kDsBig) d.st[DS_OVER] = 1u;
+  const unsigned cmax = max(max(c4.x, c4.y), max(c4.z, c4.w));
+  if (cmax > (unsigned)kDsBig) d.st[DS_OVER] = 1u;
+  if (cmax > (unsigned)kDsSmall) d.st[DS_BIGANY] = 1u;  // the host skips k_dsort_big without it
   const ulonglong2 s01 = *reinterpret_cast<const ulonglong2*>(d.bsum + b);
   const ulonglong2 s23 = *reinterpret_cast<const ulonglong2*>(d.bsum + b + 2);
   const unsigned c = ds_block_sum_u32(c4.x + c4.y + c4.z + c4.w, s_c);
@@ -334,7 +339,7 @@ __global__ __launch_bounds__(256) void k_dsort_scan2(int nb, DsortBufs d, const 
       d.st[DS_TOT + 1] = (unsigned)(as >> 32);
       const unsigned over = d.st[DS_OVER];
       d.st[DS_OVERD] = over;
-      if (pub) ds_publish(pub, as, over);  // K and num_rendered are the total of the tiles words
+      if (pub) ds_publish(pub, as, over, d.st[DS_BIGANY]);  // K and num_rendered: the total of the tiles words
     }
   }
 }
@@ -345,7 +350,10 @@ __global__ __launch_bounds__(256) void k_dsort_scatter(int P, const float* __res
                                                        unsigned long long* __restrict__ offr) {
   if (blockIdx.x == 0 && threadIdx.x < 2 * kDsShards)  // the shards: read for the last time by k_dsort_scan2
     d.shard[(threadIdx.x >> 1) * kDsShardWords + (threadIdx.x & 1)] = 0u;
-  if (blockIdx.x == 0 && threadIdx.x == 0) d.st[DS_OVER] = 0u;  // published by k_dsort_scan2
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // published by k_dsort_scan2
+    d.st[DS_OVER] = 0u;
+    d.st[DS_BIGANY] = 0u;
+  }
   const int i = blockIdx.x * 256 + threadIdx.x;
   const unsigned lo = d.st[DS_LO], shift = d.st[DS_SHIFT], pv = d.st[DS_PV];
   const bool in = i < P;

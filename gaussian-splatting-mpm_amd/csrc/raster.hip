@@ -1751,7 +1751,7 @@ struct gsmpm_raster {
   size_t capT = 0;
   uint2* ranges = nullptr;
   int* dsort_tl = nullptr;  // [2 + 2 * capT] k_tile_dsort's size-class lists
-  unsigned* h_count = nullptr;  // [4] pinned, mapped + coherent (the device writes K, num_rendered, overflow into it)
+  unsigned* h_count = nullptr;  // [4] pinned, mapped + coherent (the device writes K, num_rendered, overflow, big-bucket flag)
   // the hand-written depth order (dsort.h): state + bucket arrays (fixed size), per-Gaussian runs
   char* ds_state = nullptr;    // kDsStateBytes, zero when idle
   unsigned *ds_bbase = nullptr, *ds_bcur = nullptr, *ds_blist = nullptr, *ds_bbig = nullptr;  // [kDsNBMax]
@@ -2161,6 +2161,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       hc[0] = kNoCount;
       hc[1] = kNoCount;
       hc[2] = 0;
+      hc[3] = 1;
     };
     auto wait_count = [&]() -> int {
       GSMPM_HIP(hipEventRecord(r->count_ev, st));
@@ -2231,8 +2232,11 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       // dependent loads -- list entry, bucket record, keys -- are the cost)
       hipLaunchKernelGGL(k_dsort_small, dim3((unsigned)std::max(1, std::min(16384, div_up(std::min(nb, P), 4)))),
                          dim3(256), 0, st, (const unsigned long long*)r->tiles, db, r->dorder, r->offr);
-      hipLaunchKernelGGL(k_dsort_big, dim3(256), dim3(1024), 0, st, (const unsigned long long*)r->tiles, db,
-                         r->dorder, r->offr);
+      // the buckets above kDsSmall: launched after the count when it says there are any (early
+      // publish), else here, before the one-lane publish reads the last element
+      if (!early)
+        hipLaunchKernelGGL(k_dsort_big, dim3(256), dim3(1024), 0, st, (const unsigned long long*)r->tiles, db,
+                           r->dorder, r->offr);
       GSMPM_LAUNCH_CHECK();
     } else if (depth_ordered && !tile_dsort) {
       const int rc = lib_depth_order();
@@ -2240,6 +2244,11 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     }
     int rc = early ? wait_count() : publish(own_dsort && !lsd_dsort ? db.st + DS_OVERD : nullptr);
     if (rc) return rc;
+    if (early && !lsd_dsort && hc[3]) {
+      hipLaunchKernelGGL(k_dsort_big, dim3(256), dim3(1024), 0, st, (const unsigned long long*)r->tiles, db,
+                         r->dorder, r->offr);
+      GSMPM_LAUNCH_CHECK();
+    }
     if (own_dsort && !lsd_dsort && hc[2]) {  // a depth bucket above kDsBig entries: the library sort instead (dsort.h)
       r->dsort_fallbacks += 1;
       if ((rc = lib_depth_order()) || (rc = publish(nullptr))) return rc;
