@@ -101,7 +101,8 @@ class RasterContext:
         check(LIB.gsmpm_raster_create(ctypes.byref(self.h)), "gsmpm_raster_create")
 
     def __del__(self):
-        if getattr(self, "h", None) is not None and self.h.value:
+        # LIB is None when the interpreter tears the module down before this object
+        if getattr(self, "h", None) is not None and self.h.value and LIB is not None:
             LIB.gsmpm_raster_destroy(self.h)
             self.h = None
 

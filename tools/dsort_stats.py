@@ -8,6 +8,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), '..'))
 import torch  # noqa: E402
 
+os.environ.setdefault("GSMPM_RASTER_DSORT", "bucket")  # the bucket form's statistics at both sizes
+
 import bench  # noqa: E402
 from gsmpm import raster  # noqa: E402
 
