@@ -40,7 +40,7 @@ static __global__ __launch_bounds__(256) void k_tile_rows(int ntiles, int nch, c
 // walks a row of 7,275 chunks (bicycle's 29.8M pairs) in 114 dependent steps:
 // 63.5 us per digit pass.  skip (optional): the row pass is a no-op when
 // *skip <= skip_at (the LSD depth order's passes past the span, dsort.h).
-constexpr int kRowsWideMin = 512, kRowsWideMax = 16384;  // chunks (dynamic LDS: 4 B each)
+constexpr int kRowsWideMin = 512, kRowsWideMax = 16000;  // chunks (dynamic LDS: 4 B each, under 64 KB with s_w)
 static __global__ __launch_bounds__(256) void k_rows_wide(int nch, const unsigned* __restrict__ H,
                                                    unsigned* __restrict__ Hs, unsigned* __restrict__ tot,
                                                    const unsigned* __restrict__ skip, unsigned skip_at) {
