@@ -267,6 +267,17 @@ constexpr bool kZeroBox = GSMPM_ZERO_BOX != 0;
 #define GSMPM_ATOMIC_GRID 0
 #endif
 constexpr bool kAtomicGrid = GSMPM_ATOMIC_GRID != 0;
+// GSMPM_SIM_PRIO=n (A/B): the simulator's waves raise their issue priority
+// (s_setprio n, 0..3) so that a SIMD's arbiter serves them before the waves of
+// the render of the previous frame, which runs on a second stream beside them
+// (the frame costs sim + ~0.25 ms of that render's interference, §6)
+#ifndef GSMPM_SIM_PRIO
+#define GSMPM_SIM_PRIO 0
+#endif
+constexpr int kSimPrio = GSMPM_SIM_PRIO;
+__device__ __forceinline__ void sim_prio() {
+  if constexpr (kSimPrio > 0) __builtin_amdgcn_s_setprio(kSimPrio);
+}
 template <int MAT, int MODE>
 __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTiles tl, ChunkIn ck, Touch tc, BinOutF bo,
                                                int bin, int use_box, const float4* __restrict__ gvel,
@@ -284,6 +295,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
   float4* s_win = reinterpret_cast<float4*>(s_acc);
   const int ng = g.ng;
   constexpr int SK = MODE == 3 ? 0 : 1;  // diagnostics slot (k_p2g's / k_g2p's in the per-phase pipeline)
+  sim_prio();
   stamp(SK, 0);
   const int nch = ck.nchunk[0];
   // the first chunk's record, box and lane order are requested with the chunk
@@ -740,6 +752,7 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
                                                     GridStep gs, const int* __restrict__ esc_in,
                                                     int* __restrict__ esc_clear, int* __restrict__ zc,
                                                     int* __restrict__ zf, SlabWin sw) {
+  sim_prio();
   stamp(3, 0);
   // a slab's grid update runs as two passes (window tiles first, so their
   // partials can travel while the rest updates): the flag and the zeroing go

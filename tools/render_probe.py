@@ -41,15 +41,23 @@ def fwd():
                           cov3D_precomp=covs_r)
 
 
-for _ in range(3):
-    fwd()
-torch.cuda.synchronize()
-reps = int(os.environ.get('REPS', 20))
-t0 = time.perf_counter()
-for _ in range(reps):
-    K = fwd()[0]
-torch.cuda.synchronize()
-el = time.perf_counter() - t0
+# RSTREAM=1: render on a second stream, as bench.py's frame loop does (EVENTS=1: hipEvents on it, 5 renders)
+rstream = torch.cuda.Stream() if os.environ.get('RSTREAM') == '1' else torch.cuda.current_stream()
+with torch.cuda.stream(rstream):
+    for _ in range(3):
+        fwd()
+    torch.cuda.synchronize()
+    reps = int(os.environ.get('REPS', 20))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(rstream)
+    for _ in range(reps):
+        K = fwd()[0]
+    e1.record(rstream)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if os.environ.get('EVENTS') == '1':
+        el = e0.elapsed_time(e1) / 1e3
 ctx = raster.shared_context(dev.index or 0)
 raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg, cam.height, cam.width,
                math.tan(cam.FovX * 0.5), math.tan(cam.FovY * 0.5), sh_degree=3, shs=feats, cov3D_precomp=covs_r,
