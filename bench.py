@@ -63,6 +63,11 @@ def parse():
     ap.add_argument("--render-overlap", type=int, default=int(os.environ.get("GSMPM_BENCH_RENDER_OVERLAP", "1")),
                     help="1: frame f-1 renders on a second stream while frame f simulates; 0: each frame renders "
                          "right after its simulation on the simulator's stream (main.py's order)")
+    ap.add_argument("--render-cus", type=int, default=int(os.environ.get("GSMPM_BENCH_RENDER_CUS", "0")),
+                    help="N > 0: the overlapped render gets N of the device's CUs (every (CUs / N)-th CU-mask bit) "
+                         "and the simulator the rest, on CU-masked streams (hipExtStreamCreateWithCUMask), so the "
+                         "render never takes the CU slots of the simulator's one-round launches; 0: both streams "
+                         "on every CU")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch check only: start the ranks, form the process group, print the JSON line's "
                          "rank bookkeeping (n_gpus, parallelism) with value null; no GPU work")
@@ -87,6 +92,34 @@ def launch_ranks(n):
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     return subprocess.call(cmd, env=env)
+
+
+def cu_split_streams(dev, n_render):
+    """Two streams on disjoint CU masks (hipExtStreamCreateWithCUMask through the
+    HIP runtime torch already loaded): the simulator's (every CU but the
+    render's) and the render's (every (CUs / n_render)-th mask bit)."""
+    import ctypes
+    import torch
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    n_render = max(1, min(int(n_render), ncu - 1))
+    step = max(1, ncu // n_render)
+    rbits = {i for i in range(ncu) if i % step == step - 1}
+    words = (ncu + 31) // 32
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipExtStreamCreateWithCUMask.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
+                                                 ctypes.POINTER(ctypes.c_uint32)]
+
+    def make(bits):
+        arr = (ctypes.c_uint32 * words)()
+        for i in bits:
+            arr[i // 32] |= 1 << (i % 32)
+        h = ctypes.c_void_p()
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), words, arr)
+        if rc != 0:
+            raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
+        return torch.cuda.ExternalStream(h.value, device=dev)
+
+    return make(set(range(ncu)) - rbits), make(rbits)
 
 
 def resolve_world(args):
@@ -511,6 +544,12 @@ def main():
         else:
             dist.init_process_group(backend)
     red_dev = dev if backend == "nccl" else torch.device("cpu")
+    # --render-cus: the simulator's stream (made current: everything below runs on it) and the
+    # render's stream on disjoint CU masks
+    masked_render_stream = None
+    if args.render_cus > 0 and args.render_overlap and not args.no_render:
+        sim_stream, masked_render_stream = cu_split_streams(dev, args.render_cus)
+        torch.cuda.set_stream(sim_stream)
 
     from gsmpm import raster
     from gsmpm.bc import substep_masks
@@ -548,7 +587,7 @@ def main():
     # (the rasterizer's pair-count read-back waits on the host for frame f - 1
     # only).  Every timed step still simulates AND renders one frame: the
     # timed region ends with the last frame's render.
-    render_stream = torch.cuda.Stream(dev)
+    render_stream = masked_render_stream if masked_render_stream is not None else torch.cuda.Stream(dev)
     pending = []
 
     def render(item):
@@ -709,6 +748,7 @@ def main():
                                f"{cam.width}x{cam.height} SH3", "particles_per_gpu": n_local,
                    "particles_total": n_total, "n_grid": sa.n_grid, "material": sa.material,
                    "substep_dt": dt, "render_overlap": bool(args.render_overlap),
+                   "render_cus": args.render_cus if masked_render_stream is not None else None,
                    "parallelism": (f"slab{world}" if slab else f"dp{world} independent scenes") if world > 1
                    else "single"},
         "substeps_per_s": spf * args.steps / elapsed,
