@@ -83,6 +83,52 @@ def trial(sim_on_default, work, reps=3):
     return out
 
 
+def trial_bench(timing, reps=3):
+    """bench.py's pattern: B waits on an event recorded behind the previous
+    frame's world_outputs, i.e. one that completes as this frame's graph starts."""
+    sim, specs = bench.make_sim(scene, dev)
+    bstream = torch.cuda.Stream()
+    t = 0.0
+    for _ in range(2):
+        masks, t = substep_masks(specs, t, sa.substep_dt, sa.steps_per_frame)
+        sim.step(sa.substep_dt, masks)
+    torch.cuda.synchronize()
+    out = []
+    for _ in range(reps + 1):
+        masks, t = substep_masks(specs, t, sa.substep_dt, sa.steps_per_frame)
+        t0 = time.perf_counter()
+        sim.step(sa.substep_dt, masks)  # frame f - 1
+        sim.postprocess()
+        means_r, covs_r = sim.world_outputs(float(scene['s']), [float(v) for v in scene['c'].reshape(-1).tolist()],
+                                            render_space=True)
+        ev = torch.cuda.Event(enable_timing=timing)
+        ev.record()
+        masks, t = substep_masks(specs, t, sa.substep_dt, sa.steps_per_frame)
+        sim.step(sa.substep_dt, masks)  # frame f
+        ea = torch.cuda.Event()
+        ea.record()
+        with torch.cuda.stream(bstream):
+            bstream.wait_event(ev)
+            raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg, cam.height,
+                           cam.width, math.tan(cam.FovX * 0.5), math.tan(cam.FovY * 0.5), sh_degree=3,
+                           shs=feats, cov3D_precomp=covs_r)
+            eb = torch.cuda.Event()
+            eb.record(bstream)
+        eb.synchronize()
+        t_b = time.perf_counter()
+        ea.synchronize()
+        t_a = time.perf_counter()
+        out.append((1e3 * (t_b - t0), 1e3 * (t_a - t0)))
+    torch.cuda.synchronize()
+    del sim
+    return out[1:]
+
+
+for timing in (False, True):
+    for b_done, a_done in trial_bench(timing):
+        print(f"bench pattern, event timing={timing}: render done at {b_done:6.3f} ms, the two frames done at "
+              f"{a_done:6.3f} ms", flush=True)
+
 for sim_on_default in (True, False):
     for work in ('elementwise', 'render'):
         r = trial(sim_on_default, work)
