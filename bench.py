@@ -63,6 +63,10 @@ def parse():
     ap.add_argument("--render-overlap", type=int, default=int(os.environ.get("GSMPM_BENCH_RENDER_OVERLAP", "1")),
                     help="1: frame f-1 renders on a second stream while frame f simulates; 0: each frame renders "
                          "right after its simulation on the simulator's stream (main.py's order)")
+    ap.add_argument("--render-delay-us", type=float, default=float(os.environ.get("GSMPM_BENCH_RENDER_DELAY_US", "0")),
+                    help="overlapped render: the render stream idles this long (a one-wave spin kernel) after the "
+                         "previous frame's snapshot before rendering it, so the render meets the next frame's "
+                         "substeps instead of its first launches")
     ap.add_argument("--render-cus", type=int, default=int(os.environ.get("GSMPM_BENCH_RENDER_CUS", "0")),
                     help="N > 0: the overlapped render gets N of the device's CUs (every (CUs / N)-th CU-mask bit) "
                          "and the simulator the rest, on CU-masked streams (hipExtStreamCreateWithCUMask), so the "
@@ -590,12 +594,25 @@ def main():
     render_stream = masked_render_stream if masked_render_stream is not None else torch.cuda.Stream(dev)
     pending = []
 
+    delay_cycles = 0
+    if args.render_delay_us > 0 and args.render_overlap and not args.no_render:
+        # torch.cuda._sleep spins a one-wave kernel for N clock cycles: calibrate cycles per us
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda._sleep(1000)
+        e0.record()
+        torch.cuda._sleep(4_000_000)
+        e1.record()
+        e1.synchronize()
+        delay_cycles = int(args.render_delay_us * 4_000_000 / (e0.elapsed_time(e1) * 1e3))
+
     def render(item):
         means_r, covs_r, ev = item
         if means_r is None or args.no_render:
             return
         with torch.cuda.stream(render_stream):
             render_stream.wait_event(ev)
+            if delay_cycles:
+                torch.cuda._sleep(delay_cycles)
             K, _, _ = raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg,
                                      cam.height, cam.width, tanx, tany, sh_degree=3, shs=feats, cov3D_precomp=covs_r)
         means_r.record_stream(render_stream)  # allocated on the simulator's stream
@@ -749,6 +766,7 @@ def main():
                    "particles_total": n_total, "n_grid": sa.n_grid, "material": sa.material,
                    "substep_dt": dt, "render_overlap": bool(args.render_overlap),
                    "render_cus": args.render_cus if masked_render_stream is not None else None,
+                   "render_delay_us": args.render_delay_us if args.render_overlap else None,
                    "parallelism": (f"slab{world}" if slab else f"dp{world} independent scenes") if world > 1
                    else "single"},
         "substeps_per_s": spf * args.steps / elapsed,
