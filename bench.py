@@ -67,6 +67,10 @@ def parse():
                     help="overlapped render: the render stream idles this long (a one-wave spin kernel) after the "
                          "previous frame's snapshot before rendering it, so the render meets the next frame's "
                          "substeps instead of its first launches")
+    ap.add_argument("--render-first", type=int, default=int(os.environ.get("GSMPM_BENCH_RENDER_FIRST", "0")),
+                    help="overlapped render: 1 = frame f - 1 is rendered (its launches submitted) BEFORE frame f's "
+                         "graph is launched, so the render's work is already queued when the graph starts; 0 = "
+                         "after frame f's graph, postprocess and snapshot")
     ap.add_argument("--render-cus", type=int, default=int(os.environ.get("GSMPM_BENCH_RENDER_CUS", "0")),
                     help="N > 0: the overlapped render gets N of the device's CUs (every (CUs / N)-th CU-mask bit) "
                          "and the simulator the rest, on CU-masked streams (hipExtStreamCreateWithCUMask), so the "
@@ -626,6 +630,8 @@ def main():
     def frame(render_frame=True):
         t = [time.perf_counter()]
         masks, state["t"] = substep_masks(specs, state["t"], dt, spf)
+        if args.render_first and args.render_overlap:
+            flush()  # frame f - 1 renders while this one simulates, its launches queued first
         sim.step(dt, masks)
         t.append(time.perf_counter())
         sim.postprocess()
@@ -649,7 +655,8 @@ def main():
                 ev = torch.cuda.Event()
                 ev.record()
                 t.append(time.perf_counter())
-                flush()  # the previous frame renders while this one simulates
+                if not args.render_first:
+                    flush()  # the previous frame renders while this one simulates
                 pending.append((means_r, covs_r, ev))
                 t.append(time.perf_counter())
         if host_t is not None:
@@ -767,6 +774,7 @@ def main():
                    "substep_dt": dt, "render_overlap": bool(args.render_overlap),
                    "render_cus": args.render_cus if masked_render_stream is not None else None,
                    "render_delay_us": args.render_delay_us if args.render_overlap else None,
+                   "render_first": bool(args.render_first) if args.render_overlap else None,
                    "parallelism": (f"slab{world}" if slab else f"dp{world} independent scenes") if world > 1
                    else "single"},
         "substeps_per_s": spf * args.steps / elapsed,
