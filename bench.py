@@ -71,6 +71,9 @@ def parse():
                     help="overlapped render: 1 = frame f - 1 is rendered (its launches submitted) BEFORE frame f's "
                          "graph is launched, so the render's work is already queued when the graph starts; 0 = "
                          "after frame f's graph, postprocess and snapshot")
+    ap.add_argument("--render-thread", type=int, default=int(os.environ.get("GSMPM_BENCH_RENDER_THREAD", "0")),
+                    help="overlapped render: 1 = a host thread of its own issues the renders (its pair-count wait "
+                         "no longer holds back the launch of the next frame's graph); 0 = the frame loop's thread")
     ap.add_argument("--render-cus", type=int, default=int(os.environ.get("GSMPM_BENCH_RENDER_CUS", "0")),
                     help="N > 0: the overlapped render gets N of the device's CUs (every (CUs / N)-th CU-mask bit) "
                          "and the simulator the rest, on CU-masked streams (hipExtStreamCreateWithCUMask), so the "
@@ -623,7 +626,40 @@ def main():
         covs_r.record_stream(render_stream)
         state["K"] = K
 
+    # --render-thread: renders issued by a worker thread (ctypes drops the GIL in
+    # the library's pair-count wait), fed up to two frames ahead
+    rq = worker = None
+    if args.render_thread and args.render_overlap and not args.no_render:
+        import queue
+        import threading
+        rq = queue.Queue(maxsize=2)
+        werr = []
+
+        def render_worker():
+            torch.cuda.set_device(dev)
+            while True:
+                item = rq.get()
+                try:
+                    if item is None:
+                        return
+                    if not werr:
+                        render(item)
+                except Exception as e:  # surfaced by flush()
+                    werr.append(e)
+                finally:
+                    rq.task_done()
+
+        worker = threading.Thread(target=render_worker, daemon=True)
+        worker.start()
+
     def flush():
+        if rq is not None:
+            while pending:
+                rq.put(pending.pop(0))
+            rq.join()
+            if werr:
+                raise werr[0]
+            return
         while pending:
             render(pending.pop(0))
 
@@ -655,9 +691,12 @@ def main():
                 ev = torch.cuda.Event()
                 ev.record()
                 t.append(time.perf_counter())
-                if not args.render_first:
-                    flush()  # the previous frame renders while this one simulates
-                pending.append((means_r, covs_r, ev))
+                if rq is not None:
+                    rq.put((means_r, covs_r, ev))  # the worker renders it while the next frames simulate
+                else:
+                    if not args.render_first:
+                        flush()  # the previous frame renders while this one simulates
+                    pending.append((means_r, covs_r, ev))
                 t.append(time.perf_counter())
         if host_t is not None:
             host_t.append([1e6 * (b - a) for a, b in zip(t, t[1:])])
@@ -677,6 +716,9 @@ def main():
     flush()
     barrier()
     elapsed = time.perf_counter() - t0
+    if rq is not None:  # the render worker's last frame is done (flush): stop it
+        rq.put(None)
+        worker.join()
     if host_t:
         print("host us per call (step, postprocess, world_outputs, render of the previous frame):",
               [round(sum(c) / len(host_t[-args.steps:]), 1) for c in zip(*host_t[-args.steps:])], file=sys.stderr)
@@ -775,6 +817,7 @@ def main():
                    "render_cus": args.render_cus if masked_render_stream is not None else None,
                    "render_delay_us": args.render_delay_us if args.render_overlap else None,
                    "render_first": bool(args.render_first) if args.render_overlap else None,
+                   "render_thread": bool(rq is not None),
                    "parallelism": (f"slab{world}" if slab else f"dp{world} independent scenes") if world > 1
                    else "single"},
         "substeps_per_s": spf * args.steps / elapsed,
