@@ -71,7 +71,7 @@ def parse():
                     help="overlapped render: 1 = frame f - 1 is rendered (its launches submitted) BEFORE frame f's "
                          "graph is launched, so the render's work is already queued when the graph starts; 0 = "
                          "after frame f's graph, postprocess and snapshot")
-    ap.add_argument("--render-thread", type=int, default=int(os.environ.get("GSMPM_BENCH_RENDER_THREAD", "0")),
+    ap.add_argument("--render-thread", type=int, default=int(os.environ.get("GSMPM_BENCH_RENDER_THREAD", "1")),
                     help="overlapped render: 1 = a host thread of its own issues the renders (its pair-count wait "
                          "no longer holds back the launch of the next frame's graph); 0 = the frame loop's thread")
     ap.add_argument("--render-cus", type=int, default=int(os.environ.get("GSMPM_BENCH_RENDER_CUS", "0")),
