@@ -2094,7 +2094,9 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
   // the chunked tile sort (<= kMaxTiles tiles; GSMPM_RASTER_ONESWEEP=1 forces rocPRIM onesweep everywhere)
   const char* os = std::getenv("GSMPM_RASTER_ONESWEEP");
   const bool force_onesweep = os && os[0] == '1';
-  const bool chunked = ntiles <= (size_t)kMaxTiles && !force_onesweep;
+  // GSMPM_RASTER_CHUNKED=0: the LSD digit sort below kMaxTiles tiles too (A/B)
+  const char* ck = std::getenv("GSMPM_RASTER_CHUNKED");
+  const bool chunked = ntiles <= (size_t)kMaxTiles && !force_onesweep && !(ck && ck[0] == '0');
   // GSMPM_RASTER_TILE_DSORT=1 (chunked path): depth order per tile after the tile sort (k_tile_dsort)
   // instead of the global depth sort before the emission.  Bit-identical (the raster, golden, e2e and
   // config tests pass with it) but slower: lego render alone 0.311 vs 0.194 ms (3 rounds), so off

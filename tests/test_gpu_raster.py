@@ -314,6 +314,34 @@ def test_digit_tile_sort_matches_onesweep(dev, monkeypatch, P, W, H, tiles):
             assert np.array_equal(a, b), form
 
 
+@pytest.mark.parametrize("P,W,H", [(20000, 800, 800), (20000, 1024, 1024)])
+def test_digit_sort_below_4096_tiles_matches_chunked(dev, monkeypatch, P, W, H):
+    """GSMPM_RASTER_CHUNKED=0 takes the LSD digit sort (k_lsd_*, k_ranges32) at
+    tile counts where the chunked counting sort is the default (2,500 and
+    4,096 tiles): pixels, radii and every gradient equal bit for bit."""
+    import torch
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    means, c6, opa, shs = _scene(P, seed=P + W + 1)
+    view, full, campos, tx, ty = _camera(W, H, 0.9)
+    rng = np.random.default_rng(5)
+    wgt = torch.from_numpy(rng.normal(0, 1, (3, H, W)).astype(np.float32)).to(dev)
+    t = lambda a, g=False: torch.from_numpy(np.ascontiguousarray(a)).to(dev).requires_grad_(g)
+    st = GaussianRasterizationSettings(image_height=H, image_width=W, tanfovx=tx, tanfovy=ty,
+                                       bg=t(np.full(3, 0.1, np.float32)), scale_modifier=1.0, viewmatrix=t(view),
+                                       projmatrix=t(full), sh_degree=3, campos=t(campos), prefiltered=False,
+                                       debug=False)
+    out = {}
+    for form in ("1", "0"):
+        monkeypatch.setenv("GSMPM_RASTER_CHUNKED", form)
+        m3, o1, s1, cv = t(means, True), t(opa, True), t(shs, True), t(c6, True)
+        img, radii = GaussianRasterizer(st)(means3D=m3, means2D=None, opacities=o1, shs=s1, cov3D_precomp=cv)
+        (img * wgt).sum().backward()
+        out[form] = [x.detach().cpu().numpy() for x in (img, radii, m3.grad, o1.grad, s1.grad, cv.grad)]
+    assert (out["1"][1] > 0).sum() > P // 4
+    for a, b in zip(out["0"], out["1"]):
+        assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("P,W,H", [(20000, 1024, 1024), (6000, 272, 3856)])
 def test_tight_binning_pair_counts(dev, monkeypatch, P, W, H):
     """The tight binning sorts fewer pairs than upstream's 3-sigma count (which
