@@ -666,7 +666,7 @@ def main():
     def frame(render_frame=True):
         t = [time.perf_counter()]
         masks, state["t"] = substep_masks(specs, state["t"], dt, spf)
-        if args.render_first and args.render_overlap:
+        if args.render_first and args.render_overlap and rq is None:
             flush()  # frame f - 1 renders while this one simulates, its launches queued first
         sim.step(dt, masks)
         t.append(time.perf_counter())
