@@ -367,7 +367,7 @@ def test_tight_binning_pair_counts(dev, monkeypatch, P, W, H):
     print("binned / 3-sigma pairs", b0, k0, round(b0 / k0, 3))
 
 
-@pytest.mark.parametrize("case", ["spread", "wide", "layers", "flat", "culled", "many"])
+@pytest.mark.parametrize("case", ["spread", "wide", "layers", "flat", "culled", "none", "many"])
 def test_depth_order_matches_library_sort(dev, monkeypatch, case):
     """Both forms of the hand-written depth order (csrc/dsort.h) against the
     library's stable radix sort + scan (GSMPM_RASTER_DSORT=lib): num_rendered,
@@ -380,11 +380,12 @@ def test_depth_order_matches_library_sort(dev, monkeypatch, case):
     sort, "layers"), all depths equal (one bucket of 20,000 > 8,192: the
     overflow flag and the library fallback; one LSD pass, "flat"), a third of
     the Gaussians behind the camera (culled: the tail of the order, "culled"),
-    and 300,000 Gaussians ("many")."""
+    all of them behind it (no pair: K = 0, "none"), and 300,000 Gaussians
+    ("many")."""
     import torch
     from gsmpm import raster
     P, W, H, yaw = {"spread": (3000, 256, 192, 0.3), "wide": (20000, 640, 480, 0.3), "layers": (3000, 256, 192, 0.0),
-                    "flat": (20000, 512, 512, 0.0), "culled": (20000, 640, 480, 0.3),
+                    "flat": (20000, 512, 512, 0.0), "culled": (20000, 640, 480, 0.3), "none": (5000, 256, 192, 0.3),
                     "many": (300000, 800, 800, 0.3)}[case]
     means, c6, opa, shs = _scene(P, seed=P + 7)
     if case == "wide":
@@ -395,6 +396,8 @@ def test_depth_order_matches_library_sort(dev, monkeypatch, case):
         means[:, 2] = np.float32(0.1)
     if case == "culled":
         means[::3, 2] = np.float32(-4.0)  # view depth < 0.2: culled
+    if case == "none":
+        means[:, 2] = np.float32(-4.0)  # every Gaussian culled: no pair, the image is the background
     view, full, campos, tx, ty = _camera(W, H, 0.9, yaw=yaw)
     bgv = np.zeros(3, np.float32)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
@@ -411,7 +414,10 @@ def test_depth_order_matches_library_sort(dev, monkeypatch, case):
             torch.cuda.synchronize()
             out[(mode, early, ctx is None)] = (K, color.cpu().numpy(), radii.cpu().numpy())
     K0, c0, r0 = out[("lib", "1", False)]
-    assert K0 > 0 and c0.max() > 0
+    if case == "none":
+        assert K0 == 0 and (r0 == 0).all() and c0.max() == 0.0  # bgv is black
+    else:
+        assert K0 > 0 and c0.max() > 0
     if case == "culled":
         assert (r0 == 0).sum() >= P // 3, int((r0 == 0).sum())
     for key, (K, c, r) in out.items():
