@@ -108,13 +108,15 @@ def launch_ranks(n):
 def cu_split_streams(dev, n_render):
     """Two streams on disjoint CU masks (hipExtStreamCreateWithCUMask through the
     HIP runtime torch already loaded): the simulator's (every CU but the
-    render's) and the render's (every (CUs / n_render)-th mask bit)."""
+    render's) and the render's: exactly n_render evenly spaced CUs.  Returns
+    (sim stream, render stream, render CU count)."""
     import ctypes
     import torch
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     n_render = max(1, min(int(n_render), ncu - 1))
-    step = max(1, ncu // n_render)
-    rbits = {i for i in range(ncu) if i % step == step - 1}
+    rbits = {min(ncu - 1, round((i + 0.5) * ncu / n_render)) for i in range(n_render)}
+    sbits = set(range(ncu)) - rbits
+    assert len(rbits) == n_render and sbits, (ncu, n_render)
     words = (ncu + 31) // 32
     hip = ctypes.CDLL("libamdhip64.so")
     hip.hipExtStreamCreateWithCUMask.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32,
@@ -130,7 +132,7 @@ def cu_split_streams(dev, n_render):
             raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
         return torch.cuda.ExternalStream(h.value, device=dev)
 
-    return make(set(range(ncu)) - rbits), make(rbits)
+    return make(sbits), make(rbits), len(rbits)
 
 
 def resolve_world(args):
@@ -559,7 +561,7 @@ def main():
     # render's stream on disjoint CU masks
     masked_render_stream = None
     if args.render_cus > 0 and args.render_overlap and not args.no_render:
-        sim_stream, masked_render_stream = cu_split_streams(dev, args.render_cus)
+        sim_stream, masked_render_stream, render_cus_actual = cu_split_streams(dev, args.render_cus)
         torch.cuda.set_stream(sim_stream)
 
     from gsmpm import raster
@@ -814,7 +816,7 @@ def main():
                                f"{cam.width}x{cam.height} SH3", "particles_per_gpu": n_local,
                    "particles_total": n_total, "n_grid": sa.n_grid, "material": sa.material,
                    "substep_dt": dt, "render_overlap": bool(args.render_overlap),
-                   "render_cus": args.render_cus if masked_render_stream is not None else None,
+                   "render_cus": render_cus_actual if masked_render_stream is not None else None,
                    "render_delay_us": args.render_delay_us if args.render_overlap else None,
                    "render_first": bool(args.render_first) if args.render_overlap else None,
                    "render_thread": bool(rq is not None),

@@ -555,9 +555,22 @@ __device__ __forceinline__ unsigned dl_key0(const float* depth, const unsigned l
   return tiles[e] ? __float_as_uint(depth[e]) - lo : 0xFFFFFFFFu;  // culled: no depth was written
 }
 
+// lo and nb1 of pass 0.  from_state: the overflow fallback of the bucket form
+// (raster.hip), which has already read (and zeroed) the shards: lo from the
+// state it left (DS_LO) and all four passes (nb1 = 32: any span fits)
+__device__ __forceinline__ void dl_span0(const DlBufs& b, int from_state, unsigned& lo, int& nb1) {
+  if (from_state) {
+    lo = b.st[DS_LO];
+    nb1 = 32;
+  } else {
+    dl_span_wave(b.shard, lo, nb1);
+  }
+}
+
 template <bool FIRST>
 __global__ __launch_bounds__(256) void k_dl_hist(int P, int nch, int pass, const float* __restrict__ depth,
-                                                 const unsigned long long* __restrict__ tiles, DlBufs b) {
+                                                 const unsigned long long* __restrict__ tiles, DlBufs b,
+                                                 int from_state) {
   __shared__ unsigned s_h[256];
   __shared__ unsigned s_lo;
   __shared__ int s_skip;
@@ -567,7 +580,7 @@ __global__ __launch_bounds__(256) void k_dl_hist(int P, int nch, int pass, const
     if (t < 64) {
       unsigned lo;
       int nb1;
-      dl_span_wave(b.shard, lo, nb1);
+      dl_span0(b, from_state, lo, nb1);
       if (t == 0) s_lo = lo;
     }
   } else {
@@ -615,7 +628,8 @@ __global__ __launch_bounds__(256) void k_dl_rows(int nch, int pass, DlBufs b) {
 
 template <bool FIRST>
 __global__ __launch_bounds__(256) void k_dl_scatter(int P, int nch, int pass, const float* __restrict__ depth,
-                                                    const unsigned long long* __restrict__ tiles, DlBufs b) {
+                                                    const unsigned long long* __restrict__ tiles, DlBufs b,
+                                                    int from_state) {
   __shared__ unsigned s_k[kDlChunk], s_v[kDlChunk];
   __shared__ unsigned s_wrun[4][256];  // per wave: running count of each digit, then its offset
   __shared__ unsigned s_doff[256];     // chunk-local start of each digit's run
@@ -628,7 +642,7 @@ __global__ __launch_bounds__(256) void k_dl_scatter(int P, int nch, int pass, co
     if (t < 64) {
       unsigned lo;
       int nb1;
-      dl_span_wave(b.shard, lo, nb1);
+      dl_span0(b, from_state, lo, nb1);
       if (t == 0) {
         s_lo = lo;
         if (c == 0) {

@@ -91,11 +91,18 @@ __device__ __forceinline__ bool slab_tile_in_window(const SlabWin& sw, int ti) {
   return r;
 }
 
-// drift check of the P2G half of k_fused: base plane allowed in [xlo, xhi)
+// per-particle checks of k_fused: the slab drift check (base plane allowed in
+// [xlo, xhi)) and the non-finite check (a NaN / Inf position sets
+// *nonfin, which the step call reports as GSMPM_ESTATE; without it a
+// non-finite particle is silently binned "outside" and scatters nowhere)
 struct SlabK {
   int xlo, xhi;
   int* drift;
+  int* nonfin;
 };
+__device__ __forceinline__ bool finite3(const float (&x)[3]) {
+  return __builtin_isfinite(x[0]) && __builtin_isfinite(x[1]) && __builtin_isfinite(x[2]);
+}
 
 struct FTiles {
   int td0, td1, td2;  // tiles per axis
@@ -412,6 +419,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
           x[d] = x[d] + dt * v[d];
           ps.st(PX + d, p, x[d]);
         }
+        if (!finite3(x)) *sk.nonfin = 1;
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
           if (!P2G || GSMPM_STORE_VC) ps.st(PC + i, p, C[i / 3][i % 3]);
@@ -493,6 +501,23 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
           for (int i = 0; i < 3; ++i)
 #pragma unroll
             for (int j = 0; j < 3; ++j) nvt[i][j] = nvol * tau[i][j];
+        }
+        // non-finite inputs of the scatter (a NaN / Inf would turn into finite
+        // garbage through the fixed-point conversion, not propagate as the
+        // reference's float atomics do): mass, velocity (impulse), stress, and
+        // in a P2G-only launch the x and C it starts from
+        {
+          float chk = m + v[0] + v[1] + v[2];
+          if constexpr (MAT != 0) {
+#pragma unroll
+            for (int i = 0; i < 9; ++i) chk += nvt[i / 3][i % 3];
+          }
+          if constexpr (!G2P) {
+            chk += x[0] + x[1] + x[2];
+#pragma unroll
+            for (int i = 0; i < 9; ++i) chk += C[i / 3][i % 3];
+          }
+          if (!__builtin_isfinite(chk)) *sk.nonfin = 1;
         }
         float vm = 0.f, cm = 0.f, sm = 0.f;
 #pragma unroll
@@ -665,6 +690,7 @@ __device__ __forceinline__ void load_cover27(const ChunkIn& ck, const int* __res
 struct NodeReads {
   int off[8];  // slot offsets (float4 units) of the first chunk of each covering tile
   int extra;   // bit e: covering tile e has further chunks
+  int live;    // bit e: the node lies inside covering tile e's stencil box (some stencil may reach it)
 };
 // covering tile e of node (l0, l1, l2): its index in the 27-neighbourhood and the node's window offset there
 __device__ __forceinline__ void node_cover(int l0, int l1, int l2, int e, int& ci, int& loc) {
@@ -681,6 +707,7 @@ __device__ __forceinline__ void node_reads(int max_chunks, const int* s_c0, cons
   const int sec1 = l1 < 3 ? -1 : (l1 == kFT1 - 1 ? 1 : 0);
   const int sec2 = l2 < 3 ? -1 : (l2 == kFT2 - 1 ? 1 : 0);
   r.extra = 0;
+  r.live = 0;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int ax = e >> 2, ay = (e >> 1) & 1, az = e & 1;
@@ -694,6 +721,7 @@ __device__ __forceinline__ void node_reads(int max_chunks, const int* s_c0, cons
     const int loc = slot_loc(w0, w1, w2);
     r.off[e] = on ? s_c0[ci] * kFWin + loc : max_chunks * kFWin;
     r.extra |= (on && nc > 1) ? (1 << e) : 0;
+    r.live |= on ? (1 << e) : 0;
   }
 }
 __device__ __forceinline__ void add4(float4& a, const float4& b) {
@@ -729,19 +757,17 @@ __device__ __forceinline__ void node_extra(const float4* __restrict__ slots, con
 #endif
 constexpr int kGridParts = GSMPM_GRID_PARTS;  // workgroups per touched tile
 constexpr int kGridT = kFTN / kGridParts;     // lanes per grid workgroup
-// Nodes that received no mass at all keep whatever v_out they held: the next
-// G2P gathers only the stencils of particles whose P2G built this grid, and a
-// stencil node of such a particle has mass -- except in one case: the
-// fixed-point sums are exact, so a node's mass rounds to zero only when every
-// contribution to it is below 2^-51 of its chunk's largest, i.e. a particle
-// lighter than 2^-51 of the heaviest in its chunk.  That particle's G2P weight
-// at the node is still O(0.1-0.75), so its gathered velocity picks up the
-// node's stale v_out (any finite O(1) value) where the reference's reset grid
-// gives 0 (utils.py:177-183).  The scenes here have particle masses within a
-// few orders of magnitude of each other; GSMPM_GRID_SKIP0=0 restores the
-// store of every node.  A node of mass in (0, 1e-15] still stores 0.
-// About half the touched tiles' nodes are massless on the lego frame; A/B
-// (tools/ab_skip0.sh, 3 interleaved pairs): sim 3.136 -> 3.116 ms/frame.
+// Nodes that no particle stencil can reach keep whatever v_out they held: a
+// node outside every covering chunk's stencil box (the union of its
+// particles' stencils at this P2G, which the next G2P gathers from unmoved)
+// is read by no G2P before the next grid update rewrites it.  Every node
+// inside a box is stored, massless or not, so a stencil node of a particle
+// too light to register in the fixed-point sums (below 2^-51 of its chunk's
+// heaviest: its mass rounds to zero) reads 0 as from the reference's reset
+// grid (utils.py:177-183), not a stale value (round 4 skipped every massless
+// node; test_gpu_mpm.py::test_heterogeneous_masses).  GSMPM_GRID_SKIP0=0
+// stores every node of the touched tiles, =2 only nodes with mass (round 4's
+// form, A/B).
 #ifndef GSMPM_GRID_SKIP0
 #define GSMPM_GRID_SKIP0 1
 #endif
@@ -789,12 +815,14 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     if ((unsigned)i < (unsigned)ng && (unsigned)j < (unsigned)ng && (unsigned)k < (unsigned)ng) {
       const size_t idx = ((size_t)i * ng + j) * ng + k;
       float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      bool reach = true;  // some stencil box covers the node (the atomic A/B form: mass only)
       if constexpr (kAtomicGrid) {  // the node's whole sum, added by the chunks' atomics
         a = gacc[idx];
         if (a.x != 0.f || a.y != 0.f || a.z != 0.f || a.w != 0.f) gacc[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
       } else {
         NodeReads r;
         node_reads(tl.max_chunks, s_c0, s_nc, s_bx, l0, l1, l2, r);
+        reach = r.live != 0;
         float4 v[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = slots[r.off[e]];
@@ -812,7 +840,7 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
       if (sww >= 0 && !inrect && a.w != 0.f) *sw.oob = 1;
       if (inrect)  // a window node: this rank's partial, totalled after the exchange (k_win_update)
         sw.part[sww][((size_t)(i - sw.a[sww]) * sw.ny[sww] + (j - sw.y0[sww])) * sw.nz[sww] + (k - sw.z0[sww])] = a;
-      else if (!kGridSkip0 || a.w != 0.f)
+      else if (!kGridSkip0 || a.w != 0.f || (reach && !kAtomicGrid && GSMPM_GRID_SKIP0 == 1))
         gvel[idx] = node_update(a, i, j, k, g, gs, bct);
     }
     if (wt == (int)blockIdx.x) stamp(3, 4);

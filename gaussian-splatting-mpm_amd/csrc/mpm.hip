@@ -344,7 +344,8 @@ __device__ __forceinline__ void p2g_scatter(unsigned long long* cell0, const flo
 template <int MAT>
 __global__ __launch_bounds__(256) void k_p2g(Particles ps, GridDims g, Tiles tl, ChunkIn ck,
                                              const BcTable* __restrict__ bct, uint32_t mask, float dt, MatConsts mc,
-                                             float4* __restrict__ slots, float4* __restrict__ gacc) {
+                                             float4* __restrict__ slots, float4* __restrict__ gacc,
+                                             int* __restrict__ nonfin) {
   // channel-planar window: a wave's 8-byte atomics to random nodes of one
   // channel spread over all 64 banks (the node-interleaved float4 layout put
   // every channel on 16 of them: 75 % of LDS cycles were bank conflicts)
@@ -376,6 +377,12 @@ __global__ __launch_bounds__(256) void k_p2g(Particles ps, GridDims g, Tiles tl,
       const int p = ck.list[first + k];
       particle_front<MAT>(ps, p, bct, mask, dt, mc, x, v, C, m, nvt);
       bspline(x, g.inv_dx, base, fx, ww, dw);
+      {  // non-finite scatter inputs (the fixed-point conversion would hide them; fused.h)
+        float chk = m + v[0] + v[1] + v[2];
+#pragma unroll
+        for (int i = 0; i < 9; ++i) chk += nvt[i / 3][i % 3] + C[i / 3][i % 3];
+        if (!__builtin_isfinite(chk)) *nonfin = 1;
+      }
       float vm = 0.f, cm = 0.f, sm = 0.f;
 #pragma unroll
       for (int r = 0; r < 3; ++r) {
@@ -690,6 +697,15 @@ __device__ __forceinline__ void g2p_particle(const Particles& ps, int p, const f
   f_trial(nF, F, dt, Fn);
 #pragma unroll
   for (int i = 0; i < 9; ++i) ps.st(PF + i, p, Fn[i / 3][i % 3]);
+}
+
+// SURVEY 5's per-frame NaN / Inf check of x for the per-phase pipeline
+__global__ __launch_bounds__(256) void k_check_finite(Particles ps, int* __restrict__ flag) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < ps.count()) {
+    const float a = ps.ld(PX, p), b = ps.ld(PX + 1, p), c = ps.ld(PX + 2, p);
+    if (!(__builtin_isfinite(a) && __builtin_isfinite(b) && __builtin_isfinite(c))) *flag = 1;
+  }
 }
 
 // One workgroup per chunk: stage the tile's 10^3 window of v_out in LDS,
@@ -1442,6 +1458,8 @@ struct gsmpm_mpm {
   bool s_rebal_pending = false;              // the next call starts with the migration to new bounds
   long s_rebalances = 0;
   int* s_rec_host = nullptr;                 // pinned copy
+  int* nonfin_host = nullptr;                // non-finite particle position seen (pinned, device-mapped; sticky)
+  int* nonfin_dev = nullptr;                 // its device address
   float* mig_send[2] = {nullptr, nullptr};   // fixed-size payloads: header + [NMIG][mig_cap]
   float* mig_recv[2] = {nullptr, nullptr};
   int mig_cap = 0;                           // leavers one migration may send one way (all ranks agree)
@@ -1514,7 +1532,7 @@ static void launch(const hipEvent_t* ev, F kernel, dim3 grid, dim3 block, hipStr
 template <int MAT>
 static void launch_p2g(gsmpm_mpm* h, int c, uint32_t mask, float dt, hipStream_t st, const hipEvent_t* ev) {
   launch(ev, k_p2g<MAT>, dim3(p2g_grid(h)), dim3(kChunk), st, particles_of(h), h->g, h->tl, chunk_in(h, c),
-         (const BcTable*)h->dev_bc, mask, dt, h->mc, h->slots, h->gacc);
+         (const BcTable*)h->dev_bc, mask, dt, h->mc, h->slots, h->gacc, h->nonfin_dev);
 }
 
 // counts -> list offsets + chunk list, then the per-tile lists
@@ -1655,6 +1673,10 @@ static int launch_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc,
     if (rc) return rc;
     parity ^= 1;
   }
+  // the per-phase pipeline's non-finite check: one pass over x per call (the
+  // fused pipeline checks inside k_fused)
+  hipLaunchKernelGGL(k_check_finite, dim3(div_up(h->n, 256)), dim3(256), 0, st, particles_of(h), h->nonfin_dev);
+  GSMPM_LAUNCH_CHECK();
   if (ev) {
     GSMPM_HIP(hipStreamSynchronize(st));
     for (int s = 0; s < nsub; ++s)
@@ -1678,8 +1700,8 @@ static int fused_grid(gsmpm_mpm* h) { return std::min(h->ftl.max_chunks, h->fuse
 template <int MAT, int MODE>
 static void launch_fused_t(gsmpm_mpm* h, int c, const BinOutF& bo, int bin, int use_box, uint32_t mask, float dt,
                            int* esc, hipStream_t st, const hipEvent_t* ev) {
-  const SlabK sk = h->slab ? SlabK{h->s_lo - h->s_margin, h->s_hi + h->s_margin, h->s_drift}
-                          : SlabK{INT_MIN, INT_MAX, nullptr};
+  const SlabK sk = h->slab ? SlabK{h->s_lo - h->s_margin, h->s_hi + h->s_margin, h->s_drift, h->s_drift + SF_NONFIN}
+                          : SlabK{INT_MIN, INT_MAX, nullptr, h->nonfin_dev};
   launch(ev, k_fused<MAT, MODE>, dim3(fused_grid(h)), dim3(256), st, particles_of(h), h->g, h->ftl, chunk_in_f(h, c),
          touch_f(h, c), bo, bin, use_box, (const float4*)h->gvel, (const BcTable*)h->dev_bc, mask, dt, h->mc, h->fslots, h->gacc,
          esc, sk);
@@ -2155,6 +2177,13 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
   if ((e = hipMemset(h->gvel, 0, sizeof(float4) * nn)) != hipSuccess) return fail(e, "hipMemset");
   if ((e = hipMemset(h->planes, 0, sizeof(float) * (size_t)NPLANES * h->np)) != hipSuccess) return fail(e, "hipMemset");
   if ((e = hipStreamCreateWithFlags(&h->cap, hipStreamNonBlocking)) != hipSuccess) return fail(e, "hipStreamCreate");
+  // the non-finite word: written by the kernels only when a position is NaN / Inf,
+  // read by the host without a sync (step reports it at its next call)
+  if ((e = hipHostMalloc((void**)&h->nonfin_host, 64, hipHostMallocMapped)) != hipSuccess)
+    return fail(e, "hipHostMalloc");
+  *(volatile int*)h->nonfin_host = 0;
+  if ((e = hipHostGetDevicePointer((void**)&h->nonfin_dev, h->nonfin_host, 0)) != hipSuccess)
+    return fail(e, "hipHostGetDevicePointer");
   h->host_bc = BcTable{};
   if ((e = hipMemcpy(h->dev_bc, &h->host_bc, sizeof(BcTable), hipMemcpyHostToDevice)) != hipSuccess)
     return fail(e, "hipMemcpy bc");
@@ -2225,6 +2254,7 @@ int gsmpm_mpm_destroy(gsmpm_mpm* h) {
   (void)hipFree(h->mig_tot);
   (void)hipFree(h->s_rec);
   if (h->s_rec_host) (void)hipHostFree(h->s_rec_host);
+  if (h->nonfin_host) (void)hipHostFree(h->nonfin_host);
   if (h->x_host) (void)hipHostFree(h->x_host);
   if (h->s_ev_pack) (void)hipEventDestroy(h->s_ev_pack);
   if (h->s_ev_x) (void)hipEventDestroy(h->s_ev_x);
@@ -2276,6 +2306,7 @@ int gsmpm_mpm_set_particles(gsmpm_mpm* h, const float* x, const float* cov6, con
   int rc = rebin(h, st);
   if (rc) return rc;
   GSMPM_HIP(hipStreamSynchronize(st));
+  *(volatile int*)h->nonfin_host = 0;  // a new state
   h->has_particles = true;
   return GSMPM_OK;
 }
@@ -2350,6 +2381,11 @@ int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t nsub, const uint32_t* bc, voi
     set_error("gsmpm_mpm_step: this simulator is one slab of a multi-GPU domain; step it with gsmpm_mpm_slab_step");
     return GSMPM_ESTATE;
   }
+  if (*(volatile int*)h->nonfin_host) {
+    set_error("gsmpm_mpm_step: a particle position became non-finite (NaN / Inf) in an earlier step; the state is "
+              "invalid");
+    return GSMPM_ESTATE;
+  }
   if (nsub == 0) return GSMPM_OK;
   hipStream_t st = (hipStream_t)stream;
   // the fused pipeline keeps storage in bin order; the per-phase one re-sorts
@@ -2368,6 +2404,26 @@ int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t nsub, const uint32_t* bc, voi
     return rc;
   }
   return graph_substeps(h, dt, nsub, bc, st, nullptr);
+}
+
+int gsmpm_mpm_check_finite(gsmpm_mpm* h, int32_t clear, void* stream) {
+  GSMPM_REQUIRE(h, "gsmpm_mpm_check_finite: null handle");
+  GSMPM_HIP(hipStreamSynchronize((hipStream_t)stream));
+  if (h->slab && h->s_drift) {  // a slab's word is one of its device flags
+    int f = 0;
+    GSMPM_HIP(hipMemcpy(&f, h->s_drift + SF_NONFIN, sizeof(int), hipMemcpyDeviceToHost));
+    if (f) *(volatile int*)h->nonfin_host = 1;
+  }
+  const int f = *(volatile int*)h->nonfin_host;
+  if (clear) {
+    *(volatile int*)h->nonfin_host = 0;
+    if (h->slab && h->s_drift) GSMPM_HIP(hipMemset(h->s_drift + SF_NONFIN, 0, sizeof(int)));
+  }
+  if (f) {
+    set_error("non-finite (NaN / Inf) particle position");
+    return GSMPM_ESTATE;
+  }
+  return GSMPM_OK;
 }
 
 int gsmpm_mpm_set_rebin_interval(gsmpm_mpm* h, int32_t substeps) {

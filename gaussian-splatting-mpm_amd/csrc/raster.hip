@@ -2192,7 +2192,8 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     // the depth order depends on P only: it runs before the count read-back,
     // queued behind whatever the stream is still doing
     if (early) arm();  // before the kernels that publish
-    if (lsd_dsort) {
+    // the LSD form; from_state = 1: the bucket form's overflow fallback (lo from its state, all 4 passes)
+    auto lsd_depth_order = [&](int from_state, unsigned* pubp) {
       const DlBufs b = dl_bufs(r, P);
       const int nch = div_up(P, kDlChunk);
       const float* dp = r->depth;
@@ -2207,19 +2208,22 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       };
       for (int pass = 0; pass < kDlPasses; ++pass) {
         if (pass == 0) {
-          hipLaunchKernelGGL(k_dl_hist<true>, dim3(nch), dim3(256), 0, st, P, nch, pass, dp, tw, b);
+          hipLaunchKernelGGL(k_dl_hist<true>, dim3(nch), dim3(256), 0, st, P, nch, pass, dp, tw, b, from_state);
           rows(pass);
-          hipLaunchKernelGGL(k_dl_scatter<true>, dim3(nch), dim3(256), 0, st, P, nch, pass, dp, tw, b);
+          hipLaunchKernelGGL(k_dl_scatter<true>, dim3(nch), dim3(256), 0, st, P, nch, pass, dp, tw, b, from_state);
         } else {
-          hipLaunchKernelGGL(k_dl_hist<false>, dim3(nch), dim3(256), 0, st, P, nch, pass, dp, tw, b);
+          hipLaunchKernelGGL(k_dl_hist<false>, dim3(nch), dim3(256), 0, st, P, nch, pass, dp, tw, b, from_state);
           rows(pass);
-          hipLaunchKernelGGL(k_dl_scatter<false>, dim3(nch), dim3(256), 0, st, P, nch, pass, dp, tw, b);
+          hipLaunchKernelGGL(k_dl_scatter<false>, dim3(nch), dim3(256), 0, st, P, nch, pass, dp, tw, b, from_state);
         }
       }
       const int nsb = div_up(P, kScanBlk);
       hipLaunchKernelGGL(k_dl_scan_blocks, dim3(nsb), dim3(256), 0, st, P, tw, b, r->scan_bt);
       hipLaunchKernelGGL(k_dl_scan_apply, dim3(nsb), dim3(256), 0, st, P, tw, b,
-                         (const unsigned long long*)r->scan_bt, r->dorder, r->offr, pub);
+                         (const unsigned long long*)r->scan_bt, r->dorder, r->offr, pubp);
+    };
+    if (lsd_dsort) {
+      lsd_depth_order(0, pub);
       GSMPM_LAUNCH_CHECK();
     } else if (own_dsort) {
       const int nb = dsort_buckets(P);
@@ -2251,9 +2255,14 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
                          r->dorder, r->offr);
       GSMPM_LAUNCH_CHECK();
     }
-    if (own_dsort && !lsd_dsort && hc[2]) {  // a depth bucket above kDsBig entries: the library sort instead (dsort.h)
+    if (own_dsort && !lsd_dsort && hc[2]) {
+      // a depth bucket above kDsBig entries (a degenerate depth distribution): the
+      // hand-written LSD form from the bucket form's state instead (dsort.h)
       r->dsort_fallbacks += 1;
-      if ((rc = lib_depth_order()) || (rc = publish(nullptr))) return rc;
+      arm();
+      lsd_depth_order(1, r->h_count);
+      GSMPM_LAUNCH_CHECK();
+      if ((rc = wait_count())) return rc;
     }
     K = hc[0];
     K_full = hc[1];

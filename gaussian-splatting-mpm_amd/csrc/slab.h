@@ -66,7 +66,8 @@ __global__ __launch_bounds__(256) void k_win_update(GridDims g, SlabWin sw, cons
 // Every slab's state after a step call, exchanged with every rank (one round,
 // 64 bytes a peer) so all ranks see the same errors, counts and boxes.
 enum SlabRec : int {
-  RF_FLAGS = 0,   // bit 0 drift past the margin, 1 window mass outside the rect, 3 over capacity
+  RF_FLAGS = 0,   // bit 0 drift past the margin, 1 window mass outside the rect, 3 over capacity,
+                  // 4 a non-finite particle position
   RF_N = 1,       // live particles
   RF_NWANT = 2,   // the most particles a migration tried to hold (capacity overflow)
   RF_SENDMAX = 3, // the most leavers one migration sent one way (send capacity)
@@ -85,7 +86,8 @@ enum SlabRec : int {
 __host__ __device__ constexpr int rec_ints_of(int ng) { return kRecHdr + ng; }
 // Device flags of a slab (s_flags): sticky until the handle is reset.
 enum SlabFlag : int {
-  SF_DRIFT = 0, SF_OOB = 1, SF_DEFERRED = 2, SF_NWANT_OVER = 3, SF_SENDMAX = 4, SF_MIGRATED = 5, kSlabFlags = 8
+  SF_DRIFT = 0, SF_OOB = 1, SF_DEFERRED = 2, SF_NWANT_OVER = 3, SF_SENDMAX = 4, SF_MIGRATED = 5, SF_NONFIN = 6,
+  kSlabFlags = 8
 };
 
 struct MigGeom {
@@ -98,7 +100,8 @@ __global__ void k_rec_init(const int* __restrict__ flags, const int* __restrict_
                            int nrec, int* __restrict__ rec) {
   for (int i = kRecHdr + threadIdx.x; i < nrec; i += blockDim.x) rec[i] = 0;  // the histogram
   if (threadIdx.x != 0) return;
-  rec[RF_FLAGS] = (flags[SF_DRIFT] ? 1 : 0) | (flags[SF_OOB] ? 2 : 0) | (flags[SF_NWANT_OVER] ? 8 : 0);
+  rec[RF_FLAGS] = (flags[SF_DRIFT] ? 1 : 0) | (flags[SF_OOB] ? 2 : 0) | (flags[SF_NWANT_OVER] ? 8 : 0) |
+                  (flags[SF_NONFIN] ? 16 : 0);
   rec[RF_N] = *nlive;
   rec[RF_NWANT] = flags[SF_NWANT_OVER];
   rec[RF_SENDMAX] = flags[SF_SENDMAX];

@@ -150,6 +150,20 @@ def make_transport(rank: int, world: int, group=None, device=None):
 
 
 # ------------------------------------------------------------------ domain --
+def _default_gravity(engine_factory):
+    """The gravity an engine uses when none is passed: the ``gravity`` default
+    of its constructor (Simulator: (0, -9.81, 0), utils/solver defaults), else
+    that same vector."""
+    import inspect
+    try:
+        p = inspect.signature(engine_factory).parameters.get("gravity")
+    except (TypeError, ValueError):
+        p = None
+    if p is not None and p.default is not inspect.Parameter.empty:
+        return tuple(float(g) for g in p.default)
+    return (0.0, -9.81, 0.0)
+
+
 class SlabDomain:
     """Rank `rank`'s slab of one MPM scene.
 
@@ -200,8 +214,9 @@ class SlabDomain:
             x_grid = self._vec_in(x_grid)
             cov6 = self._cov_in(cov6)
             v = None if v is None else self._vec_in(v)
-            if "gravity" in sim_kwargs:
-                sim_kwargs["gravity"] = self._p3(sim_kwargs["gravity"])
+            # gravity is a scene vector too: the engine's default is read in the
+            # engine's (permuted) axes, so it is filled in before the swap
+            sim_kwargs["gravity"] = self._p3(sim_kwargs.get("gravity", _default_gravity(engine_factory)))
         self._bounds0 = slab_bounds(xh, self.n_grid, self.grid_extent, self.world, margin)
         owner = owner_of(xh, self._bounds0, self.n_grid, self.grid_extent)
         mine = torch.from_numpy(np.nonzero(owner == self.rank)[0]).to(self.device)

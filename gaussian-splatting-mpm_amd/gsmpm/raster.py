@@ -68,6 +68,11 @@ class Workspace:
         nb = ctypes.c_uint64()
         check(LIB.gsmpm_raster_workspace_size(int(P), int(H), int(W), int(pairs), ctypes.byref(nb)),
               "gsmpm_raster_workspace_size")
+        if self.buf is not None:
+            # the old buffer may still be in use by kernels queued on this stream
+            # (GSMPM_ESPACE returns with the depth-order kernels queued): the
+            # caching allocator must not hand it out before they finish
+            self.buf.record_stream(torch.cuda.current_stream(self.device))
         self.buf = None  # release before allocating the larger one
         # zero-filled once: the library keeps its depth-order state zero between forwards (csrc/dsort.h)
         self.buf = torch.zeros(int(nb.value) + 256, dtype=torch.uint8, device=self.device)
@@ -82,12 +87,22 @@ class Workspace:
 
 
 _WS = {}
+_WS_LOCK = __import__("threading").Lock()
 
 
-def workspace(device_index: int = 0) -> Workspace:
-    w = _WS.get(device_index)
-    if w is None:
-        w = _WS[device_index] = Workspace(torch.device("cuda", device_index))
+def workspace(device_index: int = 0, stream=None) -> Workspace:
+    """The default workspace of (device, stream).  One per stream: the library
+    keeps the workspace's depth-order state zero between forwards
+    (csrc/dsort.h), which holds only while its forwards are ordered, so two
+    streams (e.g. bench's render worker and the default stream) never share
+    one."""
+    if stream is None:
+        stream = torch.cuda.current_stream(torch.device("cuda", device_index))
+    key = (device_index, int(stream.cuda_stream))
+    with _WS_LOCK:
+        w = _WS.get(key)
+        if w is None:
+            w = _WS[key] = Workspace(torch.device("cuda", device_index))
     return w
 
 
@@ -216,7 +231,7 @@ def forward(means3D, opacities, viewmatrix, projmatrix, campos, bg, image_height
             check(LIB.gsmpm_raster_forward(context.h, ctypes.byref(a), ptr(color), ptr(radii), ctypes.byref(nr),
                                            stream_of(dev)), "rasterize_gaussians")
     else:
-        w = ws if ws is not None else workspace(dev.index or 0)
+        w = ws if ws is not None else workspace(dev.index or 0, torch.cuda.current_stream(dev))
         H, W = int(image_height), int(image_width)
         w.ensure(P, H, W, w.key[3] if w.key else 8 * P + 4096)
         need = ctypes.c_int64(0)

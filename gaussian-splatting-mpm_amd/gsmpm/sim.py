@@ -94,6 +94,12 @@ class Simulator:
         arr = (ctypes.c_uint32 * n)(*[int(m) & 0xFFFFFFFF for m in masks])
         check(LIB.gsmpm_mpm_step(self._h, ctypes.c_float(dt), n, arr, stream_of(self.device)), "gsmpm_mpm_step")
 
+    def check_finite(self, clear: bool = False):
+        """SURVEY 5's per-frame NaN / Inf check on x: waits for the stream and
+        raises RuntimeError if any substep so far produced a non-finite
+        particle position (``step`` also raises, at the call after)."""
+        check(LIB.gsmpm_mpm_check_finite(self._h, int(bool(clear)), stream_of(self.device)), "check_finite")
+
     # ---------------------------------------------------------- slab mode --
     def slab_init(self, rank: int, world: int, lo: int, hi: int, margin: int = 2, interval: int = 10):
         """Make this simulator (created with n_particles = capacity) rank `rank`

@@ -89,8 +89,16 @@ int gsmpm_mpm_add_plane_collider(gsmpm_mpm* h, const double point[3], const doub
 /* MPM_Simulator.p2g2p (solver.py:27-52) x n_substeps.  bc_active[s] holds
  * the activity bits of substep s, decided by the caller from the f64 host
  * clock exactly as BasicBC.isActive (boundary_conditions.py:30-31); NULL =
- * all active.  Asynchronous on `stream`. */
+ * all active.  Asynchronous on `stream`.  Returns GSMPM_ESTATE (and launches
+ * nothing) once an earlier call's substeps produced a non-finite (NaN / Inf)
+ * particle position (SURVEY 5's per-frame check on x; the kernels set a
+ * sticky host-mapped word, read here without a sync: the error surfaces at
+ * the call after the frame that produced it, or at gsmpm_mpm_check_finite). */
 int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t n_substeps, const uint32_t* bc_active, void* stream);
+/* Synchronizes `stream`, then GSMPM_ESTATE if any substep so far produced a
+ * non-finite particle position (clear != 0 resets the word; set_particles
+ * does too), else GSMPM_OK.  No reference counterpart. */
+int gsmpm_mpm_check_finite(gsmpm_mpm* h, int32_t clear, void* stream);
 
 /* ------------------------------------------------- multi-GPU slabs ---
  * SURVEY 8(e); no reference counterpart (the reference is one device,
@@ -413,9 +421,13 @@ int gsmpm_raster_set_forward_only(gsmpm_raster* r, int32_t on);
  * every call); no allocation inside, forward-only (no backward state).
  * The pair count is known only after the binning scan (upstream resizes its
  * binning buffer at that point): when the frame needs more pairs than the
- * workspace holds, the call returns GSMPM_ESPACE with *pairs_needed set and
- * the outputs unwritten; the caller sizes a larger workspace for that many
- * pairs and calls again. */
+ * workspace holds, the call returns GSMPM_ESPACE with *pairs_needed set,
+ * out_color and num_rendered unwritten, and out_radii possibly overwritten
+ * (k_preprocess runs before the count is known); the depth-order kernels may
+ * still be queued on `stream` at return (they leave the workspace's state
+ * zero), so the old workspace must not be freed for reuse by another stream
+ * before `stream` reaches that point.  The caller sizes a larger workspace
+ * for that many pairs and calls again. */
 int gsmpm_raster_workspace_size(int32_t P, int32_t H, int32_t W, int64_t pairs, uint64_t* bytes);
 int gsmpm_raster_forward_ws(const gsmpm_raster_args* a, float* out_color, int32_t* out_radii,
                             int32_t* num_rendered, void* workspace, uint64_t ws_bytes, int64_t* pairs_needed,
@@ -427,7 +439,8 @@ int gsmpm_raster_forward_ws(const gsmpm_raster_args* a, float* out_color, int32_
 int gsmpm_raster_pair_counts(const gsmpm_raster* r, uint32_t* binned, uint32_t* rendered);
 /* Diagnostics of the context's last hand-written depth order (csrc/dsort.h):
  * out8 = {buckets, occupied buckets sorted by a wave, by a workgroup, largest
- * bucket, overflow flag, visible Gaussians, library fallbacks so far, shift}. */
+ * bucket, overflow flag, visible Gaussians, fallbacks so far (a bucket above
+ * 8,192 entries: the LSD form instead), shift}. */
 int gsmpm_raster_dsort_stats(const gsmpm_raster* r, int64_t out8[8]);
 /* GaussianRasterizer.markVisible -> _C.mark_visible: visible[P] (u8) = view z > 0.2 */
 int gsmpm_raster_mark_visible(const float* means3D, int32_t P, const float* viewmatrix, const float* projmatrix,

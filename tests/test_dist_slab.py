@@ -164,25 +164,25 @@ def test_slab_error_stops_every_rank(tmp_path):
 AX = [2, 1, 0]  # the test scene with x and z swapped: its longest axis (1.4) is z
 
 
-def _axis_scene():
+def _axis_scene(ax=AX):
     x, v, cov, vol = scene()
     up = ((0, 0), (0, 1), (0, 2), (1, 1), (1, 2), (2, 2))
-    cidx = [up.index(tuple(sorted((AX[i], AX[j])))) for i, j in up]
-    return (np.ascontiguousarray(x[:, AX]), np.ascontiguousarray(v[:, AX]), np.ascontiguousarray(cov[:, cidx]),
+    cidx = [up.index(tuple(sorted((ax[i], ax[j])))) for i, j in up]
+    return (np.ascontiguousarray(x[:, ax]), np.ascontiguousarray(v[:, ax]), np.ascontiguousarray(cov[:, cidx]),
             vol)
 
 
-def _axis_worker(rank, world, port, out):
+def _axis_worker(rank, world, port, out, ax=AX, kw=KW):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from gsmpm.dist import CallbackTransport, SlabDomain
         from slab_oracle import OracleSlabEngine
-        x, v, cov, vol = _axis_scene()
+        x, v, cov, vol = _axis_scene(ax)
         xp = CallbackTransport(rank, world)
         dom = SlabDomain(x, cov, vol, v=v, rank=rank, world=world, transport=xp, n_grid=NG, grid_extent=EXT,
                          margin=2, interval=10, device="cpu", engine_factory=OracleSlabEngine, jelly_quirk=False,
-                         **KW)
+                         **kw)
         dom.add_fixed_cube(*FIXED)
         dom.add_plane_collider([0, 0, 0.4], [0, 0, 1])
         dom.step(DT, [0b11] * STEPS)
@@ -213,3 +213,27 @@ def test_slab_cut_along_longest_axis(tmp_path, world):
     errs = {k: rel_err(r[k], getattr(ref, k)) for k in TOL}
     for k, e in errs.items():
         assert e < TOL[k], (world, k, e, errs)
+
+
+def test_slab_cut_axis_default_gravity(tmp_path):
+    """The advisor's round-4 finding: a scene longest along y (x and y
+    swapped), built WITHOUT a gravity argument.  The engine's default gravity
+    (0, -9.81, 0) is a scene vector, so SlabDomain must permute it into the
+    engine's frame like an explicit one (the engine would otherwise pull along
+    scene x).  Over 200 substeps the wrong axis moves v by ~0.2 of ~4: the v
+    bound (2e-3) catches it."""
+    ax = [1, 0, 2]
+    kw = {k: val for k, val in KW.items() if k != "gravity"}
+    x, v, cov, vol = _axis_scene(ax)
+    mp.spawn(_axis_worker, args=(2, free_port(), str(tmp_path), ax, kw), nprocs=2, join=True)
+    r = np.load(os.path.join(tmp_path, "res.npz"))
+    assert int(r["axis"]) == 1
+    import oracle as O
+    ref = O.OracleMPM(x, cov, vol, v=v, n_grid=NG, grid_extent=EXT, jelly_quirk=False, **kw)
+    ref.add_fixed_box(*FIXED)
+    ref.add_collider([0, 0, 0.4], [0, 0, 1])
+    for _ in range(STEPS):
+        ref.substep(DT, op_active=[1, 1])
+    errs = {k: rel_err(r[k], getattr(ref, k)) for k in TOL}
+    for k, e in errs.items():
+        assert e < TOL[k], (k, e, errs)

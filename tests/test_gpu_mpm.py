@@ -218,3 +218,92 @@ def test_fused_margin_escapes(dev, material):
     for k in got:
         e = rel_err(got[k].cpu().numpy().reshape(exp[k].shape), exp[k])
         assert e < TOL_DERIVED.get(k, TOL), (k, e)
+
+
+@pytest.mark.parametrize("pipe", PIPES)
+def test_heterogeneous_masses(dev, pipe):
+    """The round-4 verdict's reference-semantics gap: one chunk whose masses
+    span more than 2^52.  A particle 1e-17 as heavy as the 200 others of its
+    tile (one chunk) has a contribution below the chunk's fixed-point
+    resolution, so the nodes only its stencil reaches sum to mass 0 -- where
+    the reference's grid_m (2e-21) is <= 1e-15 and v_out stays at the reset
+    value 0 (utils.py:177-183).  The heavy blob moves away (+x, 3 m/s) from
+    the light particle, whose stencil shares nodes with the blob's trailing
+    edge at first: those nodes had v_out ~ 3 while the blob covered them.  A
+    grid update that skipped every massless node left that stale 3 for the
+    light particle to keep gathering (it would follow the blob); one that
+    stores every node inside a stencil box gives it the reference's 0."""
+    import torch
+    import oracle as O
+    from gsmpm.sim import Simulator
+    rng = np.random.default_rng(7)
+    ng, ext, dt, steps = 32, 2.0, 1e-3, 60
+    nb = 200
+    blob = np.stack([rng.uniform(0.80, 0.95, nb), rng.uniform(0.85, 1.0, nb), rng.uniform(0.60, 0.75, nb)], 1)
+    light = np.array([[0.66, 0.92, 0.67]])
+    x = np.concatenate([blob, light]).astype(np.float32)
+    v = np.zeros_like(x)
+    v[:nb, 0] = 3.0
+    cov = np.tile(np.array([1e-4, 0, 0, 1e-4, 0, 1e-4], np.float32), (len(x), 1))
+    vol = O.particle_volume(x, ng, ext).astype(np.float32)
+    vol[nb] = vol[:nb].mean() * 1e-17
+    kw = dict(n_grid=ng, grid_extent=ext, material="jelly", E=2e4, nu=0.3, density=200.0, gravity=(0.0, 0.0, 0.0))
+    ref = O.OracleMPM(x, cov, vol, v=v, jelly_quirk=False, **kw)
+    sim = Simulator(len(x), phased=pipe == "phased", **kw)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    sim.set_particles(t(x), t(cov), t(vol), t(v))
+    for _ in range(steps):
+        ref.substep(dt, [], [])
+    sim.step(dt, [0] * steps)
+    gx = sim.get("x").cpu().numpy().reshape(-1, 3)
+    gv = sim.get("v").cpu().numpy().reshape(-1, 3)
+    # the blob really left the light particle's stencil, so some of its nodes
+    # went from heavy to (reference) massless during the run
+    assert ref.x[:nb, 0].min() - ref.x[nb, 0] > 3 * ext / ng
+    vmax = np.abs(ref.v).max()
+    assert np.abs(gv[nb] - ref.v[nb]).max() < 1e-4 * vmax, (gv[nb], ref.v[nb])
+    assert np.abs(gx[nb] - ref.x[nb]).max() < 1e-4 * np.abs(ref.x).max(), (gx[nb], ref.x[nb])
+    assert rel_err(gx, ref.x) < TOL and rel_err(gv, ref.v) < TOL
+
+
+@pytest.mark.parametrize("pipe", PIPES)
+def test_nonfinite_position_reported(dev, pipe):
+    """SURVEY 5's per-frame NaN / Inf check on x: a non-finite particle
+    position -- given at set_particles, or produced during a step -- is
+    reported by check_finite() and by the next step() call (GSMPM_ESTATE, a
+    RuntimeError), and a fresh state clears it."""
+    import torch
+    import oracle as O
+    from gsmpm.sim import Simulator
+    rng = np.random.default_rng(0)
+    n, ng, dt = 2000, 32, 1e-4
+    x = rng.uniform(0.7, 1.3, size=(n, 3)).astype(np.float32)
+    cov = np.tile(np.array([1e-4, 0, 0, 1e-4, 0, 1e-4], np.float32), (n, 1))
+    vol = O.particle_volume(x, ng, 2.0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    sim = Simulator(n, n_grid=ng, grid_extent=2.0, material="metal", E=2e5, nu=0.3, density=200.0,
+                    phased=pipe == "phased")
+    sim.set_particles(t(x), t(cov), t(vol))
+    sim.step(dt, [0] * 10)
+    sim.check_finite()  # a finite state raises nothing
+    # NaN given at set_particles
+    xb = x.copy()
+    xb[17, 1] = np.nan
+    sim.set_particles(t(xb), t(cov), t(vol))
+    sim.step(dt, [0] * 10)
+    with pytest.raises(RuntimeError, match="non-finite"):
+        sim.check_finite()
+    with pytest.raises(RuntimeError, match="non-finite"):
+        sim.step(dt, [0] * 10)
+    # a fresh finite state clears it
+    sim.set_particles(t(x), t(cov), t(vol))
+    sim.step(dt, [0] * 10)
+    sim.check_finite()
+    # Inf produced during a step: one particle's velocity is infinite
+    vb = sim.get("v").clone()
+    vb.view(-1, 3)[5, 0] = float("inf")
+    sim.set("v", vb)
+    sim.step(dt, [0] * 10)
+    with pytest.raises(RuntimeError, match="non-finite"):
+        sim.check_finite(clear=True)
+    sim.check_finite()  # cleared
