@@ -535,6 +535,10 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
         // chunk of particles binned outside the grid: bounds-checked global path
         if (k < cnt) p2g_global<MAT>(x, v, C, m, nvt, g, dt, gacc);
         if (k == 0 && cnt > 0) *esc = 1;
+        // the next launch on these bins reads this chunk's lane order too: the
+        // identity (round 4 left it unwritten, so a lane of the next G2P took a
+        // stale row -- another chunk's particle, or one past the live rows)
+        if (tc.perm && k < cnt) tc.perm[(size_t)w * 256 + k] = (unsigned char)q;
         __syncthreads();
         continue;  // workgroup-uniform
       }

@@ -2155,6 +2155,7 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
         return fail(e, "hipMalloc boxes");
       if ((e = hipMalloc(&h->fperm[c], (size_t)h->ftl.max_chunks * 256)) != hipSuccess)
         return fail(e, "hipMalloc lane balance");
+      if ((e = hipMemset(h->fperm[c], 0, (size_t)h->ftl.max_chunks * 256)) != hipSuccess) return fail(e, "hipMemset");
       if ((e = hipMemset(h->fcount[c], 0, sizeof(int) * E)) != hipSuccess) return fail(e, "hipMemset");
       if ((e = hipMemset(h->ftflag[c], 0, sizeof(int) * (size_t)h->ftl.ntiles)) != hipSuccess) return fail(e, "hipMemset");
       if ((e = hipMemset(h->fnchunk[c], 0, sizeof(int) * 2)) != hipSuccess) return fail(e, "hipMemset");
