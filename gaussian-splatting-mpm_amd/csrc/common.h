@@ -42,5 +42,10 @@ __device__ __forceinline__ void wt_store4(float4* p, const float4& v) {
   nt_f4 t = {v.x, v.y, v.z, v.w};
   asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(t) : "memory");
 }
+// streaming (non-temporal) vector store (nt): A/B form of the grid update's v_out store
+__device__ __forceinline__ void nt_store4(float4* p, const float4& v) {
+  nt_f4 t = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(p), "v"(t) : "memory");
+}
 
 }  // namespace gsmpm

@@ -776,6 +776,13 @@ constexpr int kGridT = kFTN / kGridParts;     // lanes per grid workgroup
 #define GSMPM_GRID_SKIP0 1
 #endif
 constexpr bool kGridSkip0 = GSMPM_GRID_SKIP0 != 0;
+// GSMPM_GVEL_STORE (A/B): the v_out store of k_grid_f plain (0), streaming nt
+// (1) or write-through sc1 (2; round 2: the gap after k_grid_f 2.6 -> 1.5 us,
+// k_grid_f +0.8 us)
+#ifndef GSMPM_GVEL_STORE
+#define GSMPM_GVEL_STORE 0
+#endif
+constexpr int kGvelStore = GSMPM_GVEL_STORE;
 __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_grid_f(GridDims g, FTiles tl, ChunkIn ck, const int* __restrict__ tbox,
                                                     const float4* __restrict__ slots, float4* __restrict__ gacc,
                                                     float4* __restrict__ gvel, const BcTable* __restrict__ bct,
@@ -844,8 +851,14 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
       if (sww >= 0 && !inrect && a.w != 0.f) *sw.oob = 1;
       if (inrect)  // a window node: this rank's partial, totalled after the exchange (k_win_update)
         sw.part[sww][((size_t)(i - sw.a[sww]) * sw.ny[sww] + (j - sw.y0[sww])) * sw.nz[sww] + (k - sw.z0[sww])] = a;
-      else if (!kGridSkip0 || a.w != 0.f || (reach && !kAtomicGrid && GSMPM_GRID_SKIP0 == 1))
-        gvel[idx] = node_update(a, i, j, k, g, gs, bct);
+      else if (!kGridSkip0 || a.w != 0.f || (reach && !kAtomicGrid && GSMPM_GRID_SKIP0 == 1)) {
+        if constexpr (kGvelStore == 1)
+          nt_store4(gvel + idx, node_update(a, i, j, k, g, gs, bct));
+        else if constexpr (kGvelStore == 2)
+          wt_store4(gvel + idx, node_update(a, i, j, k, g, gs, bct));
+        else
+          gvel[idx] = node_update(a, i, j, k, g, gs, bct);
+      }
     }
     if (wt == (int)blockIdx.x) stamp(3, 4);
   }
