@@ -5,7 +5,8 @@ numpy, independent of gaussian_splatting/scene.
 
 The PLY is read as data (header + little-endian f32 records); no reference
 code runs.  Run in the build container only; outputs are committed:
-  udon64.ply, udon64_expected.npz
+  udon64.ply, udon64_expected.npz, and the whole file as udon_point_cloud4.ply
+  (round 5: the GPU path's one real 3DGS scene, tests/test_gpu_udon.py)
 """
 import os
 
@@ -19,6 +20,8 @@ N = 64
 def main():
     with open(SRC, "rb") as f:
         raw = f.read()
+    with open(os.path.join(HERE, "udon_point_cloud4.ply"), "wb") as f:  # the whole scene, byte for byte
+        f.write(raw)
     end = raw.index(b"end_header\n") + len(b"end_header\n")
     lines = raw[:end].decode("ascii").splitlines()
     props = [l.split()[2] for l in lines if l.startswith("property")]
@@ -47,7 +50,7 @@ def main():
     feats = np.concatenate([dc, rest], 1)
     np.savez(os.path.join(HERE, "udon64_expected.npz"), xyz=xyz, opacity=opacity, cov6=cov6, features=feats,
              scaling=s, rotation=q)
-    print("wrote udon64.ply, udon64_expected.npz")
+    print("wrote udon64.ply, udon64_expected.npz, udon_point_cloud4.ply")
 
 
 if __name__ == "__main__":

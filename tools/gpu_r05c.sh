@@ -7,7 +7,7 @@ mkdir -p $O
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread \
   "tests/test_gpu_mpm.py::test_particles_binned_outside_the_grid" \
   "tests/test_gpu_mpm.py::test_nonfinite_position_reported" "tests/test_gpu_mpm.py::test_heterogeneous_masses" \
-  "tests/test_gpu_mpm.py::test_fused_margin_escapes" > $O/new.log 2>&1
+  "tests/test_gpu_mpm.py::test_fused_margin_escapes" tests/test_gpu_udon.py > $O/new.log 2>&1
 rc=$?
 tail -12 $O/new.log
 [ $rc -eq 0 ] || exit $rc
