@@ -12,17 +12,28 @@ n_grid 128 (--n_grid override), jelly as written.
 
     python bench.py [--gpus N --steps K --warmup W]
 
-Multi-GPU (torch.distributed.run, one rank per GPU), two modes:
-* default -- strong scaling of ONE lego scene sharded by spatial slab
+Multi-GPU (torch.distributed.run, one rank per GPU), two modes for the
+headline line:
+* default (--multi dp) -- every rank simulates and renders its own lego scene
+  (synthetic seed = rank): independent objects, no collective in the data
+  path; value = all ranks' particle-substeps / the slowest rank's time
+  ("scaling": "weak").  One lego scene is latency-bound on one GPU (SURVEY
+  8(e): "report honestly"): sharding it cannot beat one GPU per substep, so
+  the job's throughput at N GPUs is N scenes.
+* --multi slab -- strong scaling of ONE lego scene sharded by spatial slab
   (gsmpm.dist.SlabDomain, csrc/slab.h): every substep each pair of
   neighbouring ranks swaps the partial sums of the grid planes around their
   shared bound over RCCL (the pairwise all-reduce of boundary grid nodes),
   particles migrate between slabs every 10 substeps; the frame's means/covs
   are gathered to rank 0, which renders it.  value = scene particles x
   substeps / time.
-* --dp -- every rank simulates and renders its own lego scene (synthetic seed
-  = rank): independent objects, no collective in the data path.
-Timing is barrier + max over ranks.
+Either way an N > 1 line also carries `multi_gpu`: north_star's slab
+sharding measured on lego and on config D (bicycle 1M, 256^3) with the
+render-aware re-cut (rank 0 renders the gathered frame and takes the
+particle share sim / (sim + render)), per-rank sim ms, rank-0 render and
+gather ms, and lego's sim / render split (rank 1 simulates, rank 0 renders
+frame f - 1 from a snapshot sent over RCCL).  Timing is barrier + max over
+ranks.
 
 Prints ONE JSON line (rank 0).  value = particle-substeps/s over all ranks.
 """
@@ -57,8 +68,16 @@ def parse():
     ap.add_argument("--no-extra-configs", action="store_true",
                     help="skip the driver-timed config C (metal) / D (bicycle 1M, 256^3) side runs")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--dp", action="store_true",
-                    help="N > 1: independent scenes per rank (no exchange) instead of the default slab sharding")
+    ap.add_argument("--multi", choices=("dp", "slab"), default="dp",
+                    help="N > 1 headline: dp = independent lego scenes per rank (default, weak scaling); slab = one "
+                         "lego scene sharded by spatial slab over RCCL (strong scaling)")
+    ap.add_argument("--dp", action="store_const", const="dp", dest="multi", help="= --multi dp")
+    ap.add_argument("--slab", action="store_const", const="slab", dest="multi", help="= --multi slab")
+    ap.add_argument("--no-multi-configs", action="store_true",
+                    help="N > 1: skip the slab / sim-render-split side measurements (multi_gpu)")
+    ap.add_argument("--multi-configs", default="lego,bicycle,split",
+                    help="N > 1: which side measurements multi_gpu holds (lego slab, bicycle slab, lego sim/render "
+                         "split)")
     ap.add_argument("--rebin", type=int, default=0, help="fused pipeline: substeps between re-binnings (0: library default)")
     ap.add_argument("--render-overlap", type=int, default=int(os.environ.get("GSMPM_BENCH_RENDER_OVERLAP", "1")),
                     help="1: frame f-1 renders on a second stream while frame f simulates; 0: each frame renders "
@@ -74,6 +93,10 @@ def parse():
     ap.add_argument("--render-thread", type=int, default=int(os.environ.get("GSMPM_BENCH_RENDER_THREAD", "1")),
                     help="overlapped render: 1 = a host thread of its own issues the renders (its pair-count wait "
                          "no longer holds back the launch of the next frame's graph); 0 = the frame loop's thread")
+    ap.add_argument("--render-async", type=int, default=int(os.environ.get("GSMPM_BENCH_RENDER_ASYNC", "1")),
+                    help="1: frames render through gsmpm_raster_forward_async (the pair count stays on the device: "
+                         "no host wait, no render thread; a frame whose counts flag an overflow is rendered again "
+                         "by the synchronous form inside the timed region); 0: the synchronous form")
     ap.add_argument("--render-cus", type=int, default=int(os.environ.get("GSMPM_BENCH_RENDER_CUS", "0")),
                     help="N > 0: the overlapped render gets N of the device's CUs (every (CUs / N)-th CU-mask bit) "
                          "and the simulator the rest, on CU-masked streams (hipExtStreamCreateWithCUMask), so the "
@@ -461,6 +484,194 @@ def other_configs(args, dev, frames=3, rank=0, world=1, xp=None, sync=None):
     return res
 
 
+def slab_frames(args, dev, rank, world, xp, barrier, red_dev, cfg, n, ng, frames=3, settle=4, weighted=True):
+    """One scene sharded by slab over the N ranks, frame by frame as main.py
+    runs it (step, postprocess, gather to rank 0, rank 0 renders), with the
+    render-aware re-cut: rank 0 measures its simulation and render times and
+    takes the particle share sim / (sim + render) (SlabDomain.set_render_share,
+    gsmpm_mpm_slab_set_weight), `settle` frames let the library's re-cut move
+    the bounds, then `frames` frames are timed barrier to barrier (max over
+    ranks).  Per-rank fields: each rank's simulation device time per frame
+    (hipEvents around its step call), its particle count, and rank 0's render
+    and gather host times (the gather includes the wait for the slowest
+    rank's simulation)."""
+    import copy
+    import torch
+    import torch.distributed as dist
+    from gsmpm import raster
+    from gsmpm.bc import substep_masks
+    a = copy.copy(args)
+    a.config, a.material, a.particles, a.n_grid = cfg, None, n, ng
+    sc = build_scene(a, dev)
+    sim, specs = make_sim(sc, dev, slab=(rank, world, xp))
+    sa = sc["sargs"]
+    dt, spf = sa.substep_dt, sa.steps_per_frame
+    st = {"t": 0.0}
+    cam, g, mask = sc["cam"], sc["g"], sc["mask"]
+    w_args = (float(sc["s"]), [float(v) for v in sc["c"].reshape(-1).tolist()])
+    feats = g.get_features[mask].contiguous() if rank == 0 else None
+    opac = g.get_opacity[mask].reshape(-1).contiguous() if rank == 0 else None
+    tx, ty = math.tan(cam.FovX * 0.5), math.tan(cam.FovY * 0.5)
+    bg = torch.zeros(3, device=dev)
+    ev = lambda: torch.cuda.Event(enable_timing=True)
+    acc = {"sim": 0.0, "render": 0.0, "gather": 0.0, "K": 0}
+
+    def frame(timed):
+        masks, st["t"] = substep_masks(specs, st["t"], dt, spf)
+        e0, e1 = ev(), ev()
+        e0.record()
+        sim.step(dt, masks)
+        e1.record()
+        sim.postprocess()
+        g0 = time.perf_counter()
+        m, c = sim.gather_world(*w_args, render_space=True)
+        g1 = time.perf_counter()
+        if rank == 0:
+            acc["K"], _, _ = raster.forward(m, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg, cam.height,
+                                            cam.width, tx, ty, sh_degree=3, shs=feats, cov3D_precomp=c)
+            torch.cuda.current_stream().synchronize()
+        g2 = time.perf_counter()
+        e1.synchronize()
+        if timed:
+            acc["sim"] += e0.elapsed_time(e1)
+            acc["gather"] += (g1 - g0) * 1e3
+            acc["render"] += (g2 - g1) * 1e3
+
+    frame(False)  # graph capture
+    barrier()
+    frame(True)  # this rank's sim and rank 0's render, for the share
+    sim_ms, render_ms = acc["sim"], acc["render"]
+    weight = 1.0
+    if weighted and rank == 0:
+        weight = sim.set_render_share(sim_ms, render_ms)
+    for _ in range(settle):
+        frame(False)
+    barrier()
+    acc.update(sim=0.0, render=0.0, gather=0.0)
+    t0 = time.perf_counter()
+    for _ in range(frames):
+        frame(True)
+    barrier()
+    el = time.perf_counter() - t0
+    tt = torch.tensor([el], dtype=torch.float64, device=red_dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    el = float(tt.item())
+    mine = torch.tensor([acc["sim"] / frames, float(sim.n)], dtype=torch.float64, device=red_dev)
+    allr = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    nsim = sc["xg"].shape[0]
+    r = {"config": cfg, "particles": nsim, "n_grid": sa.n_grid, "parallelism": f"slab{world}", "scaling": "strong",
+         "frame_ms": round(el / frames * 1e3, 4), "particle_substeps_per_s": nsim * spf * frames / el,
+         "per_rank_sim_ms": [round(float(x[0]), 4) for x in allr],
+         "per_rank_particles": [int(x[1]) for x in allr],
+         "rank0_render_ms": round(acc["render"] / frames, 4), "rank0_gather_ms": round(acc["gather"] / frames, 4),
+         "rank0_weight": round(weight, 4), "rank0_first_frame": {"sim_ms": round(sim_ms, 4),
+                                                                 "render_ms": round(render_ms, 4)},
+         "render": f"{cam.width}x{cam.height} SH3", "num_rendered": acc["K"] if rank == 0 else None,
+         "slab_bounds": sim.bounds, "slab_recuts": sim.rebalances}
+    sim.engine.close()
+    barrier()
+    del sim, sc
+    torch.cuda.empty_cache()
+    return r
+
+
+def sim_render_split(args, dev, rank, world, barrier, red_dev, frames=5):
+    """Lego with the simulation and the render on different GPUs (the round-4
+    verdict's item 2, N >= 2): rank 1 simulates the whole scene on one GPU
+    (no slab exchange), sends each frame's render-space snapshot (means,
+    cov6: 36 B a particle) to rank 0 over RCCL, and goes on with the next
+    frame; rank 0 renders frame f while rank 1 simulates frame f + 1.  Ranks
+    >= 2 idle.  frame_ms against the one-GPU line's ms_per_step is the gain of
+    taking the render off the simulating GPU."""
+    import torch
+    import torch.distributed as dist
+    from gsmpm import raster
+    from gsmpm.bc import substep_masks
+    sc = build_scene(args, dev)
+    n = sc["xg"].shape[0]
+    sa = sc["sargs"]
+    dt, spf = sa.substep_dt, sa.steps_per_frame
+    bm = torch.empty((n, 3), dtype=torch.float32, device=dev)  # the snapshot: render-space means, cov6
+    bc = torch.empty((n, 6), dtype=torch.float32, device=dev)
+    acc = {"render": 0.0, "sim": 0.0, "K": 0}
+    if rank == 1:
+        sim, specs = make_sim(sc, dev)
+        w_args = (float(sc["s"]), [float(v) for v in sc["c"].reshape(-1).tolist()])
+        st = {"t": 0.0}
+        ev = lambda: torch.cuda.Event(enable_timing=True)
+
+        def frame(timed):
+            masks, st["t"] = substep_masks(specs, st["t"], dt, spf)
+            e0, e1 = ev(), ev()
+            e0.record()
+            sim.step(dt, masks)
+            e1.record()
+            sim.postprocess()
+            sim.world_outputs(*w_args, render_space=True, means_out=bm, cov_out=bc)
+            dist.send(bm, dst=0)
+            dist.send(bc, dst=0)
+            if timed:
+                e1.synchronize()
+                acc["sim"] += e0.elapsed_time(e1)
+    elif rank == 0:
+        cam, g, mask = sc["cam"], sc["g"], sc["mask"]
+        feats, opac = g.get_features[mask].contiguous(), g.get_opacity[mask].reshape(-1).contiguous()
+        tx, ty = math.tan(cam.FovX * 0.5), math.tan(cam.FovY * 0.5)
+        bg = torch.zeros(3, device=dev)
+
+        def frame(timed):
+            dist.recv(bm, src=1)
+            dist.recv(bc, src=1)
+            r0 = time.perf_counter()
+            acc["K"], _, _ = raster.forward(bm, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg,
+                                            cam.height, cam.width, tx, ty, sh_degree=3, shs=feats, cov3D_precomp=bc)
+            torch.cuda.current_stream().synchronize()
+            if timed:
+                acc["render"] += (time.perf_counter() - r0) * 1e3
+    else:
+        frame = None
+    for _ in range(2):  # capture + warm-up
+        if frame:
+            frame(False)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(frames):
+        if frame:
+            frame(True)
+    barrier()
+    el = time.perf_counter() - t0
+    tt = torch.tensor([el], dtype=torch.float64, device=red_dev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    el = float(tt.item())
+    mine = torch.tensor([acc["sim"] / frames, acc["render"] / frames], dtype=torch.float64, device=red_dev)
+    allr = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    return {"config": args.config, "particles": n, "parallelism": "sim on rank 1, render on rank 0",
+            "frame_ms": round(el / frames * 1e3, 4), "particle_substeps_per_s": n * spf * frames / el,
+            "rank1_sim_ms": round(float(allr[1][0]), 4), "rank0_render_ms": round(float(allr[0][1]), 4),
+            "snapshot_bytes": int((bm.numel() + bc.numel()) * 4), "num_rendered": acc["K"] if rank == 0 else None}
+
+
+def multi_gpu_configs(args, dev, rank, world, xp, barrier, red_dev):
+    """N > 1 side measurements (north_star's slab sharding; the round-4
+    verdict's items 2 and 3): lego and config D through the slab path with the
+    render-aware re-cut, and lego's sim / render split."""
+    import torch
+    res = {}
+    which = set(args.multi_configs.split(","))
+    torch.cuda.empty_cache()
+    if "lego" in which:
+        res["B_lego_slab"] = slab_frames(args, dev, rank, world, xp, barrier, red_dev, args.config, args.particles,
+                                         args.n_grid)
+    if "bicycle" in which:
+        res["D_bicycle_slab"] = slab_frames(args, dev, rank, world, xp, barrier, red_dev, "bicycle.json", 1_000_000,
+                                            256, frames=2, settle=3)
+    if "split" in which:
+        res["B_lego_sim_render_split"] = sim_render_split(args, dev, rank, world, barrier, red_dev)
+    return res
+
+
 def config_e(dev, iters=5):
     """BASELINE configs[4] (extra.py system identification): extra.py training
     iterations of the differentiable MPM (30 forward substeps + postprocess,
@@ -520,7 +731,7 @@ def dry_run(args, rank, world):
         ranks = int(t.item())
     else:
         ranks = 1
-    slab = world > 1 and not args.dp
+    slab = world > 1 and args.multi == "slab"
     out = {"metric": METRIC, "value": None, "unit": "particle-substeps/s", "n_gpus": ranks, "dry_run": True,
            "scaling": "strong" if slab else "weak",
            "config": {"parallelism": (f"slab{world}" if slab else f"dp{world} independent scenes") if world > 1
@@ -567,11 +778,12 @@ def main():
     from gsmpm import raster
     from gsmpm.bc import substep_masks
 
-    # N > 1: one scene sharded by spatial slab over RCCL (default), or --dp:
-    # independent scenes, one per rank
-    slab = world > 1 and not args.dp
+    # N > 1: independent scenes, one per rank (default), or --multi slab: one
+    # scene sharded by spatial slab over RCCL; the RCCL transport serves the
+    # slab side measurements (multi_gpu) in either mode
+    slab = world > 1 and args.multi == "slab"
     xp = None
-    if slab:
+    if slab or (world > 1 and not args.no_multi_configs and not args.no_extra_configs):
         from gsmpm.dist import make_transport
         xp = make_transport(rank, world, device=dev)
     scene = build_scene(args, dev, rank=0 if slab else rank)
@@ -628,10 +840,18 @@ def main():
         covs_r.record_stream(render_stream)
         state["K"] = K
 
-    # --render-thread: renders issued by a worker thread (ctypes drops the GIL in
-    # the library's pair-count wait), fed up to two frames ahead
+    # --render-async: the forward with the pair count left on the device
+    # (gsmpm_raster_forward_async), enqueued right behind the frame's
+    # snapshot -- on the render stream (overlap) or the simulator's -- with no
+    # host wait; pairs_cap from one synchronous render of the first snapshot.
+    # Every frame keeps its snapshot until flush() has read its counts: a
+    # flagged frame (more pairs than the capacity, or a depth bucket overflow)
+    # is rendered again by the synchronous form before the timed region ends.
+    ren_async = bool(args.render_async) and not slab and not args.no_render
+    aq = []  # (AsyncRender, means, covs) of frames not yet checked
+    acap = {"cap": 0, "reissued": 0}
     rq = worker = None
-    if args.render_thread and args.render_overlap and not args.no_render:
+    if args.render_thread and args.render_overlap and not args.no_render and not ren_async:
         import queue
         import threading
         rq = queue.Queue(maxsize=2)
@@ -655,6 +875,19 @@ def main():
         worker.start()
 
     def flush():
+        if ren_async:
+            for ar, m, c in aq:
+                nr, flags = ar.result()
+                if flags:  # the synchronous form renders it (counted in the frame's time)
+                    state["K"], _, _ = raster.forward(m, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg,
+                                                      cam.height, cam.width, tanx, tany, sh_degree=3, shs=feats,
+                                                      cov3D_precomp=c)
+                    acap["reissued"] += 1
+                    acap["cap"] = max(acap["cap"], int(ar.counts[0]) + int(ar.counts[0]) // 4 + 4096)
+                else:
+                    state["K"] = nr
+            aq.clear()
+            return
         if rq is not None:
             while pending:
                 rq.put(pending.pop(0))
@@ -682,7 +915,33 @@ def main():
                 means_r, covs_r = sim.gather_world(w_scale, w_center, render_space=True)
             else:
                 means_r, covs_r = sim.world_outputs(w_scale, w_center, render_space=True)
-            if not args.render_overlap and means_r is not None:  # main.py's order, one stream
+            if ren_async:
+                if not acap["cap"]:  # the capacity: one synchronous render of the first snapshot
+                    nr, _, _ = raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg,
+                                              cam.height, cam.width, tanx, tany, sh_degree=3, shs=feats,
+                                              cov3D_precomp=covs_r)
+                    acap["cap"] = nr + nr // 2 + 4096  # num_rendered (3 sigma) >= the binned pairs
+                t.append(time.perf_counter())
+                rs = render_stream if args.render_overlap else torch.cuda.current_stream()
+                ev = torch.cuda.Event()
+                ev.record()
+                with torch.cuda.stream(rs):
+                    rs.wait_event(ev)
+                    ar = raster.forward_async(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg,
+                                              cam.height, cam.width, tanx, tany, sh_degree=3, shs=feats,
+                                              cov3D_precomp=covs_r, pairs_cap=acap["cap"])
+                means_r.record_stream(rs)
+                covs_r.record_stream(rs)
+                aq.append((ar, means_r, covs_r))
+                if len(aq) > 8:  # bounded: check the oldest (long done) frames
+                    done = aq[:4]
+                    del aq[:4]
+                    keep = list(aq)
+                    aq[:] = done
+                    flush()
+                    aq[:] = keep
+                t.append(time.perf_counter())
+            elif not args.render_overlap and means_r is not None:  # main.py's order, one stream
                 t.append(time.perf_counter())
                 K, _, _ = raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg,
                                          cam.height, cam.width, tanx, tany, sh_degree=3, shs=feats,
@@ -820,6 +1079,9 @@ def main():
                    "render_delay_us": args.render_delay_us if args.render_overlap else None,
                    "render_first": bool(args.render_first) if args.render_overlap else None,
                    "render_thread": bool(rq is not None),
+                   "render_async": ren_async,
+                   "render_async_pairs_cap": acap["cap"] if ren_async else None,
+                   "render_async_reissued": acap["reissued"] if ren_async else None,
                    "parallelism": (f"slab{world}" if slab else f"dp{world} independent scenes") if world > 1
                    else "single"},
         "substeps_per_s": spf * args.steps / elapsed,
@@ -866,11 +1128,11 @@ def main():
             n_local, sa.n_grid, sa.material, live,
             {k: frame_prof[k] / nl[k] * 1e3 for k in ("k_fused", "k_grid_f") if k in frame_prof},
             {"config": args.config, "particles": args.particles, "n_grid": sa.n_grid, "material": sa.material})
-    if not args.no_extra_configs:
-        oc = other_configs(args, dev, rank=rank, world=world, xp=xp, sync=barrier) if slab else \
-            (other_configs(args, dev) if world == 1 else None)
-        if oc is not None:
-            out["other_configs"] = oc
+    if not args.no_extra_configs and world == 1:
+        out["other_configs"] = other_configs(args, dev)
+    if world > 1 and xp is not None and not args.no_multi_configs and not args.no_extra_configs:
+        # the headline's scene and graphs are done with: free them first
+        out["multi_gpu"] = multi_gpu_configs(args, dev, rank, world, xp, barrier, red_dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(scene, args, args.cpu_seconds)
     if slab:
@@ -883,6 +1145,7 @@ def main():
         print(json.dumps(out), flush=True)
     if slab:  # the simulator's captured graphs hold RCCL work: destroy them before the communicator
         sim.engine.close()
+    if xp is not None:
         barrier()
         xp.close()
     if world > 1:

@@ -170,6 +170,9 @@ struct Touch {
   int* cbox;    // [max_chunks] stencil box of the chunk's last P2G (packed, window coordinates)
   int* tbox;    // [ntiles] the same per tile (the full window when the tile has several chunks)
   unsigned char* perm;  // [max_chunks][256] lane -> particle of the chunk (lane balance, below); null: off
+  int2* rcov;           // cover records per touched position (ChunkIn): an appended tile's gets the "none" flag
+  const int* tpos;      // [ntiles] touched position of each tile (-1: none); null: no box publishing
+  int* rbox;            // [ntiles][kRecStride] the neighbours' stencil boxes of this substep, per touched position
 };
 
 // Lane balance.  A wave's LDS accesses to the chunk window (G2P's ds_read_b128
@@ -220,7 +223,12 @@ __device__ __forceinline__ void add_lower_tiles(const Touch& tc, const FTiles& t
     const int x = tx + a, y = ty + b, z = tz + c;
     if (need && (unsigned)x < (unsigned)tl.td0 && (unsigned)y < (unsigned)tl.td1 && (unsigned)z < (unsigned)tl.td2) {
       const int t = (x * tl.td1 + y) * tl.td2 + z;
-      if (atomicCAS(&tc.tflag[t], 0, 1) == 0) tc.touched[atomicAdd(&tc.nchunk[1], 1)] = t;
+      if (atomicCAS(&tc.tflag[t], 0, 1) == 0) {
+        const int pos = atomicAdd(&tc.nchunk[1], 1);
+        tc.touched[pos] = t;
+        // no cover record (its neighbours publish no boxes for it): k_grid_f reads the tile tables
+        if (tc.rcov) tc.rcov[(size_t)pos * kRecStride + 27] = make_int2(1, 0);
+      }
     }
   }
 }
@@ -285,6 +293,11 @@ constexpr int kSimPrio = GSMPM_SIM_PRIO;
 __device__ __forceinline__ void sim_prio() {
   if constexpr (kSimPrio > 0) __builtin_amdgcn_s_setprio(kSimPrio);
 }
+// GSMPM_G2P_B128 (A/B, default 1): G2P's 27 LDS gathers as ds_read_b128
+#ifndef GSMPM_G2P_B128
+#define GSMPM_G2P_B128 1
+#endif
+constexpr bool kG2pB128 = GSMPM_G2P_B128 != 0;
 template <int MAT, int MODE>
 __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTiles tl, ChunkIn ck, Touch tc, BinOutF bo,
                                                int bin, int use_box, const float4* __restrict__ gvel,
@@ -329,6 +342,15 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
     int tx = 0, ty = 0, tz = 0;
     if (!outside) ftile_decode(tl, t, tx, ty, tz);
     const int o0 = tx * kFT0 - 1, o1 = ty * kFT1 - 1, o2 = tz * kFT2 - 1;  // first window node
+    // lane e < 27: the touched position of tile T = t - (a, b, c), whose cover
+    // record takes this chunk's stencil box as its neighbour e (published after
+    // the P2G below); requested now, used at the end
+    int tpos_e = -1;
+    if (tc.tpos && !outside && k < 27) {
+      const int x0 = tx - (k / 9 - 1), y0 = ty - ((k / 3) % 3 - 1), z0 = tz - (k % 3 - 1);
+      if ((unsigned)x0 < (unsigned)tl.td0 && (unsigned)y0 < (unsigned)tl.td1 && (unsigned)z0 < (unsigned)tl.td2)
+        tpos_e = tc.tpos[(x0 * tl.td1 + y0) * tl.td2 + z0];
+    }
     int p = -1;
     float x[3] = {0.f, 0.f, 0.f}, v[3] = {0.f, 0.f, 0.f}, C[3][3], F[3][3], m = 0.f;
     // this lane's particle: the lane balance of the last P2G on these bins (use_box), else in order
@@ -391,10 +413,10 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
         base_of(x, g.inv_dx, b);
         float gvd[3][3];
         if (!outside && in_grid(x, g) && in_window(b, o0, o1, o2)) {
-          g2p_gather(x, g,
+          g2p_gather<kG2pB128>(x, g,
                      [&](const int (&base)[3], int i, int j, int kk) {
-                       const float4* wb = s_win + ((base[0] - o0) * kFW1 + (base[1] - o1)) * kFW2 + (base[2] - o2);
-                       return wb[(i * kFW1 + j) * kFW2 + kk];
+                       const int q = ((base[0] - o0 + i) * kFW1 + (base[1] - o1 + j)) * kFW2 + (base[2] - o2 + kk);
+                       return s_win[q];
                      },
                      v, C, gvd);
         } else {
@@ -550,12 +572,11 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
       // window coordinates covered by this particle's stencil, as per-axis bit masks
       int mxy = win ? (7 << (b[0] - o0)) | (7 << (16 + b[1] - o1)) : 0;
       int mz = win ? 7 << (b[2] - o2) : 0;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        bound = fmaxf(bound, __shfl_xor(bound, o));
-        mxy |= __shfl_xor(mxy, o);
-        mz |= __shfl_xor(mz, o);
-      }
+      // wave reductions by DPP (the bound is >= 0; a NaN bound -- non-finite
+      // inputs, flagged above -- orders above every finite one as integer bits)
+      bound = wave_max_nonneg_dpp(bound);
+      mxy = wave_or_dpp(mxy);
+      mz = wave_or_dpp(mz);
       if ((k & 63) == 0) {
         s_max[k >> 6] = bound;
         s_mxy[k >> 6] = mxy;
@@ -585,6 +606,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
         tc.cbox[w] = box;
         tc.tbox[t] = (cr.w & 8) ? kFullBox : box;  // tiles with several chunks: whole windows
       }
+      if (tpos_e >= 0) tc.rbox[(size_t)tpos_e * kRecStride + k] = (cr.w & 8) ? kFullBox : box;
       if (cr.w & 8) box = kFullBox;
       if constexpr (kZeroBox) {  // only the nodes the scatter can reach and the store reads
         int lo[3], hi[3];
@@ -804,9 +826,22 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
   const int ng = g.ng;
   const bool all = *esc_in != 0;
   const int ntouch = kGridParts * (all ? tl.ntiles : ck.nchunk[1]);
-  // the first touched tile requested with the count (clamped), one round trip less
-  const int T0 = ck.touched[min((int)blockIdx.x / kGridParts, tl.ntiles - 1)];
+  // the first touched tile requested with the count (clamped), one round trip
+  // less; and with it the tile's cover record -- its 27 neighbours' chunk
+  // ranges (from the binning) and stencil boxes (published by this substep's
+  // k_fused) -- so the slot addresses need no hop through the tile tables
+  const int i0 = min((int)blockIdx.x / kGridParts, tl.ntiles - 1);
+  const int T0 = ck.touched[i0];
+  const bool recs = ck.rcov != nullptr && !kAtomicGrid;
+  const int le = threadIdx.x;  // lane: record entry
+  int2 cov0 = make_int2(1, 0);
+  int bx0 = 0;
+  if (recs && le < 28) {
+    cov0 = ck.rcov[(size_t)i0 * kRecStride + le];
+    bx0 = ck.rbox[(size_t)i0 * kRecStride + le];
+  }
   __shared__ int s_c0[27], s_nc[27], s_bx[27];
+  __shared__ int s_none;
   for (int wt = blockIdx.x; wt < ntouch; wt += gridDim.x) {
     const int q = threadIdx.x + (wt % kGridParts) * kGridT;
     const int l0 = q / (kFT1 * kFT2), l1 = (q / kFT2) % kFT1, l2 = q % kFT2;
@@ -818,8 +853,28 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     if constexpr (!kAtomicGrid) {
       __syncthreads();  // readers of the previous tile's ranges are done
       if (wt == (int)blockIdx.x) stamp(3, 2);
-      load_cover27(ck, tbox, tl, ti, tj, tk, s_c0, s_nc, s_bx);
-      __syncthreads();
+      bool tables = all || !recs;  // workgroup-uniform
+      if (!tables) {
+        int2 cv = cov0;
+        int bx = bx0;
+        if (wt != (int)blockIdx.x && le < 28) {
+          const size_t r = (size_t)(wt / kGridParts) * kRecStride + le;
+          cv = ck.rcov[r];
+          bx = ck.rbox[r];
+        }
+        if (le < 27) {
+          s_c0[le] = cv.x;
+          s_nc[le] = cv.y;
+          s_bx[le] = bx;
+        }
+        if (le == 27) s_none = cv.x;
+        __syncthreads();
+        tables = s_none != 0;  // a tile k_fused appended (add_lower_tiles): no record
+      }
+      if (tables) {
+        load_cover27(ck, tbox, tl, ti, tj, tk, s_c0, s_nc, s_bx);
+        __syncthreads();
+      }
     }
     if (wt == (int)blockIdx.x) stamp(3, 3);
     const int i = ti * kFT0 + l0, j = tj * kFT1 + l1, k = tk * kFT2 + l2;

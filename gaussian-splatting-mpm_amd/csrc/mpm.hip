@@ -89,6 +89,11 @@ struct ChunkIn {
   const int* nchunk;   // [2] {chunks, touched tiles}
   const int* list;     // [n] particle (storage) indices grouped by tile
   const int* touched;  // [ntiles] tiles whose nodes the next grid update owns
+  // fused pipeline (fused.h k_grid_f): per touched position, the 27 neighbour
+  // tiles' {first chunk, chunks} ([27].x = 1: no record, use the tile tables)
+  // and their stencil boxes of this substep; null: the tile tables only
+  const int2* rcov = nullptr;
+  const int* rbox = nullptr;
 };
 struct BinOut {
   int* count;    // [ntiles + 1], zeroed before G2P
@@ -592,7 +597,11 @@ __device__ __forceinline__ void load_x(const Particles& ps, int p, float (&x)[3]
   for (int d = 0; d < 3; ++d) x[d] = ps.ld(PX + d, p);
 }
 
-template <typename Fetch>
+// KEEPW: every fetched node's .w is kept live (an empty asm reads the nine of a
+// slab once they are all fetched), so an LDS gather stays one ds_read_b128 a
+// node -- 4 LDS cycles a wave -- instead of the ds_read_b96 of .xyz the
+// compiler would pick (8 cycles a wave, CDNA4 LDS table)
+template <bool KEEPW = false, typename Fetch>
 __device__ __forceinline__ void g2p_gather(const float (&x)[3], const GridDims& g, Fetch fetch, float (&nv)[3],
                                            float (&nC)[3][3], float (&nF)[3][3]) {
   int base[3];
@@ -626,12 +635,20 @@ __device__ __forceinline__ void g2p_gather(const float (&x)[3], const GridDims& 
     const float a = i == 0 ? w[0][0] : (i == 1 ? w[0][1] : w[0][2]);
     const float da = i == 0 ? dw[0][0] : (i == 1 ? dw[0][1] : dw[0][2]);
     const float di = ((float)i - fx[0]) * a;
+    float4 gs[3][3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) gs[j][k] = fetch(base, i, j, k);
+    if constexpr (KEEPW)
+      asm volatile("" ::"v"(gs[0][0].w), "v"(gs[0][1].w), "v"(gs[0][2].w), "v"(gs[1][0].w), "v"(gs[1][1].w),
+                   "v"(gs[1][2].w), "v"(gs[2][0].w), "v"(gs[2][1].w), "v"(gs[2][2].w));
 #pragma unroll
     for (int j = 0; j < 3; ++j) {
       float P[3] = {0.f, 0.f, 0.f}, K[3] = {0.f, 0.f, 0.f}, R[3] = {0.f, 0.f, 0.f};
 #pragma unroll
       for (int k = 0; k < 3; ++k) {
-        const float4 gv = fetch(base, i, j, k);
+        const float4 gv = gs[j][k];
         const float gg[3] = {gv.x, gv.y, gv.z};
 #pragma unroll
         for (int r = 0; r < 3; ++r) {
@@ -845,7 +862,30 @@ struct ChunkOut {
   int* nchunk;         // [2] {chunks, touched tiles}
   const int* tflag;    // [ntiles] touched flags from the binning
   int* touched;        // [ntiles] compacted touched tiles
+  int2* rcov = nullptr;  // fused pipeline: [ntiles][32] cover records per touched position (ChunkIn)
+  int* tpos = nullptr;   // [ntiles] touched position of each tile, -1: none
+  int td1 = 0, td2 = 0;  // tile grid (fused tiles: td0 = ntiles / (td1 td2))
 };
+
+constexpr int kRecStride = 32;  // cover-record entries per touched position (27 neighbours + the flag)
+// the cover record of touched tile t (position rk) from the binning's per-tile
+// first chunks / offsets in LDS (k_finish_bins)
+__device__ __forceinline__ void write_cover_record(const ChunkOut& co, int ntiles, int E, int t, int rk,
+                                                   const int* s_off, const int* s_aux, int total) {
+  const int td12 = co.td1 * co.td2, td0 = ntiles / td12;
+  const int tz = t % co.td2, ty = (t / co.td2) % co.td1, tx = t / td12;
+  for (int e = 0; e < 27; ++e) {
+    const int x = tx + e / 9 - 1, y = ty + (e / 3) % 3 - 1, z = tz + e % 3 - 1;
+    int2 r = make_int2(0, 0);
+    if ((unsigned)x < (unsigned)td0 && (unsigned)y < (unsigned)co.td1 && (unsigned)z < (unsigned)co.td2) {
+      const int u = (x * co.td1 + y) * co.td2 + z;
+      const int cnt = (u + 1 < E ? s_off[u + 1] : total) - s_off[u];
+      r = make_int2(s_aux[u] & 0xffff, (cnt + kChunk - 1) / kChunk);
+    }
+    co.rcov[(size_t)rk * kRecStride + e] = r;
+  }
+  co.rcov[(size_t)rk * kRecStride + 27] = make_int2(0, 0);
+}
 
 __device__ __forceinline__ int wave_incl_scan(int v) {
   const int lane = threadIdx.x & 63;
@@ -969,6 +1009,10 @@ __global__ __launch_bounds__(256) void k_finish_bins(Tiles tl, const int* __rest
     for (int k = 0; k * kChunk < c; ++k)
       co.chunk[cb + k] = make_int4(t, off + k * kChunk, min(kChunk, c - k * kChunk), c > kChunk ? 8 : 0);
     if (touched) co.touched[rk] = t;
+    if (co.tpos && t < tl.ntiles) {
+      co.tpos[t] = touched ? rk : -1;
+      if (touched) write_cover_record(co, tl.ntiles, E, t, rk, s_off, s_aux, tot[0]);
+    }
   }
   if (p < n) {
     const int d = s_off[pt] + psl;
@@ -1073,6 +1117,9 @@ __global__ __launch_bounds__(1024) void k_scan_tiles(Tiles tl, const int* __rest
     for (int k = 0; k < v[1]; ++k)
       co.chunk[o[1] + k] = make_int4(t, o[0] + k * kChunk, min(kChunk, v[0] - k * kChunk), v[0] > kChunk ? 8 : 0);
     if (v[2]) co.touched[o[2]] = t;
+    // no cover records on this path (k_grid_f reads the tile tables)
+    if (co.tpos && t < tl.ntiles) co.tpos[t] = -1;
+    if (v[2] && co.rcov) co.rcov[(size_t)o[2] * kRecStride + 27] = make_int2(1, 0);
   }
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 1023) {
     co.nchunk[0] = o[1] + v[1];
@@ -1404,9 +1451,13 @@ struct gsmpm_mpm {
   int* fesc = nullptr;                    // [2] escape flags (alternating per grid update)
   int* fcbox[2] = {nullptr, nullptr};     // [max_chunks] per-chunk stencil boxes (fused.h)
   int* ftbox[2] = {nullptr, nullptr};     // [ntiles] per-tile stencil boxes
+  int2* frcov[2] = {nullptr, nullptr};    // [ntiles][kRecStride] cover records per touched position (k_grid_f)
+  int* frbox[2] = {nullptr, nullptr};     // [ntiles][kRecStride] their neighbours' stencil boxes (k_fused writes)
+  int* ftpos[2] = {nullptr, nullptr};     // [ntiles] touched position of each tile
   unsigned char* fperm[2] = {nullptr, nullptr};  // [max_chunks][256] lane balance (fused.h); null: off
   bool lane_balance = true;               // GSMPM_LANE_BALANCE=0 turns it off (A/B)
   bool fuse_permute = true;               // GSMPM_FUSE_PERMUTE=0: separate k_permute (A/B)
+  bool cover_records = true;              // GSMPM_COVER_RECORDS=0: k_grid_f reads the tile tables only (A/B)
   int fused_wgs = 1024;                   // k_fused grid cap: the workgroups resident at once (init)
   float* planes_alt = nullptr;            // the other particle-plane buffer: every binning permutes
   int* orig_alt = nullptr;                //   storage into bin order, alternating planes / planes_alt
@@ -1453,6 +1504,8 @@ struct gsmpm_mpm {
   int* mig_tot = nullptr;                    // [3] leavers to lower, stayers, leavers to upper
   int* s_rec = nullptr;                      // [world][rec_ints_of(ng)] every rank's record (slab_records)
   std::vector<int> s_bounds;                 // every rank's planes: [world + 1] (from the records)
+  float* s_wdev = nullptr;                   // this rank's re-cut share weight (device: the record reads it)
+  float s_weight = 1.0f;
   bool s_rebal_on = true;                    // re-cut the slabs at call boundaries when unbalanced
   float s_rebal_tol = 0.05f;                 // ... by more than this (max count / mean - 1)
   bool s_rebal_pending = false;              // the next call starts with the migration to new bounds
@@ -1501,14 +1554,25 @@ static BinOut bin_out(gsmpm_mpm* h, int c) {
 static bool use_fused(const gsmpm_mpm* h) { return h->fused; }
 
 static ChunkIn chunk_in_f(gsmpm_mpm* h, int c) {
-  return ChunkIn{h->fcount[c], h->fcbase[c], h->fchunk[c], h->fnchunk[c], h->flist[c], h->ftouched[c]};
+  ChunkIn ci{h->fcount[c], h->fcbase[c], h->fchunk[c], h->fnchunk[c], h->flist[c], h->ftouched[c]};
+  if (h->cover_records) {
+    ci.rcov = h->frcov[c];
+    ci.rbox = h->frbox[c];
+  }
+  return ci;
 }
 static ChunkOut chunk_out_f(gsmpm_mpm* h, int c) {
-  return ChunkOut{h->fcstart[c], h->fcbase[c], h->fchunk[c], h->fnchunk[c], h->ftflag[c], h->ftouched[c]};
+  ChunkOut co{h->fcstart[c], h->fcbase[c], h->fchunk[c], h->fnchunk[c], h->ftflag[c], h->ftouched[c]};
+  co.rcov = h->frcov[c];
+  co.tpos = h->ftpos[c];
+  co.td1 = h->ftl.td1;
+  co.td2 = h->ftl.td2;
+  return co;
 }
 static Touch touch_f(gsmpm_mpm* h, int c) {
   return Touch{h->ftflag[c], h->ftouched[c], h->fnchunk[c], h->fchunk[c], h->fcbox[c], h->ftbox[c],
-               h->lane_balance ? h->fperm[c] : nullptr};
+               h->lane_balance ? h->fperm[c] : nullptr, h->frcov[c],
+               h->cover_records ? h->ftpos[c] : nullptr, h->frbox[c]};
 }
 static BinOutF bin_out_f(gsmpm_mpm* h, int c) { return BinOutF{h->fcount[c], h->ptile, h->pslot, h->ftflag[c], h->ftl}; }
 // k_finish_bins / the scan kernels only use ntiles and max_chunks of a Tiles
@@ -2113,6 +2177,7 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
   h->fused = !(prm->flags & (GSMPM_FLAG_PHASED | GSMPM_FLAG_KEEP_GRID));
   if (const char* lb = std::getenv("GSMPM_LANE_BALANCE")) h->lane_balance = lb[0] != '0';
   if (const char* fp = std::getenv("GSMPM_FUSE_PERMUTE")) h->fuse_permute = fp[0] != '0';
+  if (const char* cr = std::getenv("GSMPM_COVER_RECORDS")) h->cover_records = cr[0] != '0';
   {
     int dev = 0, ncu = 0, per_cu = 0;
     if (hipGetDevice(&dev) == hipSuccess &&
@@ -2153,6 +2218,15 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
         return fail(e, "hipMalloc boxes");
       if ((e = hipMalloc(&h->ftbox[c], sizeof(int) * (size_t)h->ftl.ntiles)) != hipSuccess)
         return fail(e, "hipMalloc boxes");
+      if ((e = hipMalloc(&h->frcov[c], sizeof(int2) * kRecStride * (size_t)h->ftl.ntiles)) != hipSuccess ||
+          (e = hipMemset(h->frcov[c], 0, sizeof(int2) * kRecStride * (size_t)h->ftl.ntiles)) != hipSuccess)
+        return fail(e, "hipMalloc cover records");
+      if ((e = hipMalloc(&h->frbox[c], sizeof(int) * kRecStride * (size_t)h->ftl.ntiles)) != hipSuccess ||
+          (e = hipMemset(h->frbox[c], 0, sizeof(int) * kRecStride * (size_t)h->ftl.ntiles)) != hipSuccess)
+        return fail(e, "hipMalloc cover boxes");
+      if ((e = hipMalloc(&h->ftpos[c], sizeof(int) * (size_t)h->ftl.ntiles)) != hipSuccess ||
+          (e = hipMemset(h->ftpos[c], 0xff, sizeof(int) * (size_t)h->ftl.ntiles)) != hipSuccess)
+        return fail(e, "hipMalloc touched positions");
       if ((e = hipMalloc(&h->fperm[c], (size_t)h->ftl.max_chunks * 256)) != hipSuccess)
         return fail(e, "hipMalloc lane balance");
       if ((e = hipMemset(h->fperm[c], 0, (size_t)h->ftl.max_chunks * 256)) != hipSuccess) return fail(e, "hipMemset");
@@ -2226,6 +2300,9 @@ int gsmpm_mpm_destroy(gsmpm_mpm* h) {
     (void)hipFree(h->fcbox[c]);
     (void)hipFree(h->ftbox[c]);
     (void)hipFree(h->fperm[c]);
+    (void)hipFree(h->frcov[c]);
+    (void)hipFree(h->frbox[c]);
+    (void)hipFree(h->ftpos[c]);
   }
   (void)hipFree(h->fslots);
   (void)hipFree(h->fesc);
@@ -2246,6 +2323,7 @@ int gsmpm_mpm_destroy(gsmpm_mpm* h) {
     (void)hipFree(h->mig_recv[w]);
   }
   (void)hipFree(h->s_drift);
+  (void)hipFree(h->s_wdev);
   (void)hipFree(h->d_n);
   (void)hipFree(h->gid);
   (void)hipFree(h->gid_alt);

@@ -151,4 +151,29 @@ __device__ __forceinline__ int wave_max(int v) {
   return v;
 }
 
+// Whole-wave reductions through DPP (no LDS crossbar: a __shfl_xor compiles to
+// ds_bpermute_b32): within each 16-lane row by quad swaps and the two row
+// mirrors, then the four rows' results read out as uniform values.  Every lane
+// of the wave must be active.
+template <typename Op>
+__device__ __forceinline__ int dpp_row_reduce(int v, Op op) {
+  v = op(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+  v = op(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+  v = op(v, __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+  v = op(v, __builtin_amdgcn_update_dpp(0, v, 0x140, 0xF, 0xF, false));  // row_mirror
+  return v;
+}
+__device__ __forceinline__ int wave_or_dpp(int v) {
+  v = dpp_row_reduce(v, [](int a, int b) { return a | b; });
+  return __builtin_amdgcn_readlane(v, 0) | __builtin_amdgcn_readlane(v, 16) | __builtin_amdgcn_readlane(v, 32) |
+         __builtin_amdgcn_readlane(v, 48);
+}
+// max of non-negative floats (their bit patterns order as integers)
+__device__ __forceinline__ float wave_max_nonneg_dpp(float x) {
+  int v = dpp_row_reduce(__float_as_int(x), [](int a, int b) { return max(a, b); });
+  v = max(max(__builtin_amdgcn_readlane(v, 0), __builtin_amdgcn_readlane(v, 16)),
+          max(__builtin_amdgcn_readlane(v, 32), __builtin_amdgcn_readlane(v, 48)));
+  return __int_as_float(v);
+}
+
 }  // namespace gsmpm

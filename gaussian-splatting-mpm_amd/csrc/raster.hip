@@ -776,6 +776,18 @@ __global__ void k_publish_count(const unsigned long long* __restrict__ src, cons
   __hip_atomic_store(dst, (unsigned)v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// the async form with no Gaussians: the background, and every count 0
+__global__ __launch_bounds__(256) void k_fill_bg(const float* __restrict__ bg, int npix, float* __restrict__ out,
+                                                 unsigned* counts) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < npix) {
+    out[i] = bg[0];
+    out[npix + i] = bg[1];
+    out[2 * npix + i] = bg[2];
+  }
+  if (i < 4) counts[i] = 0u;
+}
+
 // sorted emission index -> Gaussian id (the sort carries emission indices)
 __global__ __launch_bounds__(256) void k_ids(int K, const unsigned* __restrict__ pos, const unsigned* __restrict__ vals,
                                              unsigned* __restrict__ ids) {
@@ -864,24 +876,38 @@ __global__ __launch_bounds__(256) void k_emit_pairs(int K, int P, const unsigned
 constexpr int kEmitT = 256, kEmitMaxI = 16, kEmitG = GSMPM_EMIT_G;
 // starts[b] = the depth rank of the Gaussian holding pair b * E (E = pairs per
 // emission workgroup): each boundary lies in exactly one non-empty Gaussian
+// The async form (gsmpm_raster_forward_async: the pair count stays on the
+// device): at most bmax starts are written, and the lane of the last Gaussian
+// raises bit 1 of *flags when the frame bins more pairs than kcap (the pair
+// buffers were carved for kcap: the emission and the tile sort cut at kcap and
+// the caller renders the frame again with room for the count).
 __global__ __launch_bounds__(256) void k_emit_starts(int P, const unsigned long long* __restrict__ offr, unsigned E,
-                                                     unsigned* __restrict__ starts) {
+                                                     unsigned* __restrict__ starts, unsigned bmax, unsigned kcap,
+                                                     unsigned* flags) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= P) return;
   const unsigned s = r ? (unsigned)offr[r - 1] : 0u, t = (unsigned)offr[r];
-  for (unsigned b = (s + E - 1) / E; b * E < t; ++b) starts[b] = (unsigned)r;
+  for (unsigned b = (s + E - 1) / E; b * E < t && b < bmax; ++b) starts[b] = (unsigned)r;
+  if (flags && r == P - 1 && t > kcap) flags[0] |= 2u;
+}
+// K of the frame: the host's count, or (the async form) the device's, cut at the host's capacity
+__device__ __forceinline__ int pairs_of(int K, const unsigned long long* kdev) {
+  return kdev ? min(K, (int)min((unsigned)*kdev, 0x7fffffffu)) : K;
 }
 __global__ __launch_bounds__(kEmitT) void k_emit_wg(int K, int P, int items, const unsigned* __restrict__ starts,
                                                     const unsigned* __restrict__ order,
                                                     const unsigned long long* __restrict__ offr,
                                                     const float2* __restrict__ xy, const float4* __restrict__ conic_o,
                                                     const uint2* __restrict__ rect, int gx, int cull,
-                                                    unsigned* __restrict__ keys, unsigned* __restrict__ ids) {
+                                                    unsigned* __restrict__ keys, unsigned* __restrict__ ids,
+                                                    const unsigned long long* __restrict__ kdev) {
   __shared__ unsigned s_off[kEmitG + 1];  // [i]: first pair of staged Gaussian i, [i + 1]: one past its last
   __shared__ unsigned s_g[kEmitG];        // Gaussian id
   __shared__ uint2 s_rect[kEmitG];        // (x0 | y0 << 16, rect width) in tiles
   __shared__ float4 s_box[kEmitG];        // alpha-reach box (x lo, x hi, y lo, y hi) in pixels (culling)
+  K = pairs_of(K, kdev);
   const int e0 = blockIdx.x * kEmitT * items, e1 = min(K, e0 + kEmitT * items);
+  if (e0 >= K) return;  // the async form's workgroups past the frame's pairs (uniform)
   const int r0 = (int)starts[blockIdx.x];
   const int r1 = e1 < K ? (int)starts[blockIdx.x + 1] : P - 1;  // may stage one Gaussian past pair e1 - 1
   int rs = r0;        // first Gaussian of the span to stage
@@ -968,8 +994,10 @@ __device__ __forceinline__ void sorted_to_lds(const unsigned (&k)[kSortI], const
   __syncthreads();
 }
 __global__ __launch_bounds__(kSortT) void k_tile_hist(int K, int ntiles, int nch, int bits,
-                                                      const unsigned* __restrict__ keys, unsigned* __restrict__ H) {
+                                                      const unsigned* __restrict__ keys, unsigned* __restrict__ H,
+                                                      const unsigned long long* __restrict__ kdev) {
   __shared__ unsigned s_h[kMaxTiles + 1];
+  K = pairs_of(K, kdev);  // chunks past the frame's pairs store empty histograms
   const unsigned lowmask = (1u << bits) - 1u;
   for (int t = threadIdx.x; t <= ntiles; t += kSortT) s_h[t] = 0;
   __syncthreads();
@@ -992,8 +1020,10 @@ __global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int 
                                                          const unsigned* __restrict__ Hs,
                                                          const unsigned* __restrict__ tot,
                                                          unsigned* __restrict__ keys_out, unsigned* __restrict__ vals_out,
-                                                         uint2* __restrict__ ranges, int* __restrict__ dsort_counts) {
+                                                         uint2* __restrict__ ranges, int* __restrict__ dsort_counts,
+                                                         const unsigned long long* __restrict__ kdev) {
   if (dsort_counts && blockIdx.x == 0 && threadIdx.x < 2) dsort_counts[threadIdx.x] = 0;  // k_tile_dsort's lists
+  K = pairs_of(K, kdev);
   __shared__ unsigned s_k[kChunk], s_v[kChunk];
   __shared__ int s_start[kMaxTiles + 1];    // chunk-local start of each tile's run
   __shared__ unsigned s_ts[kMaxTiles + 2];  // exclusive scan of the tile totals: each tile's run start
@@ -1114,7 +1144,7 @@ __global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int 
       s_k[idx] = k[j];
       s_v[idx] = v[j];
     }
-  const int nv = min(kChunk, K - c * kChunk);
+  const int nv = max(0, min(kChunk, K - c * kChunk));  // 0: an async-form chunk past the frame's pairs
   for (int sp = nv + (int)threadIdx.x; sp < kChunk; sp += kSortT) s_v[sp] = kNoEntry;  // the tail: no pair
   __syncthreads();
 #endif
@@ -1761,6 +1791,10 @@ struct gsmpm_raster {
   unsigned long long* scan_bt = nullptr;  // [capP / 1024 + 1] block totals of the index-order scans (scan.h)
   unsigned* dl_h = nullptr;    // [2 * 256 * (capP / kDlChunk + 1) + 256] the LSD depth order's counts, prefixes, totals
   long dsort_fallbacks = 0;    // forwards whose depth order fell back to the library sort
+  // the async form (gsmpm_raster_forward_async): pair buffers carved for async_cap
+  // pairs, the counts published to async_counts, no host synchronisation
+  int64_t async_cap = 0;
+  unsigned* async_counts = nullptr;
   hipEvent_t count_ev = nullptr;  // recorded after the publishing kernels: surfaces a fault while the host spins
   // per pixel (backward)
   size_t capPix = 0;
@@ -2154,9 +2188,10 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     // surfaces at once instead of after a timeout; a completed event with no
     // count is an error.  The count needs the host, so a capturing stream is
     // refused.
+    const bool async = r->async_cap > 0;  // the pair count stays on the device (gsmpm_raster_forward_async)
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     GSMPM_HIP(hipStreamIsCapturing(st, &cap));
-    GSMPM_REQUIRE(cap == hipStreamCaptureStatusNone,
+    GSMPM_REQUIRE(async || cap == hipStreamCaptureStatusNone,
                   "gsmpm_raster_forward: the pair count is read on the host; the stream must not be capturing");
     volatile unsigned* hc = r->h_count;
     auto arm = [&]() {
@@ -2188,10 +2223,10 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     // kernel after its last launch, as rounds 1-3 did (A/B)
     const char* ec = std::getenv("GSMPM_RASTER_EARLY_COUNT");
     const bool early = own_dsort && !(ec && ec[0] == '0');
-    unsigned* pub = early ? r->h_count : nullptr;
+    unsigned* pub = async ? r->async_counts : early ? r->h_count : nullptr;
     // the depth order depends on P only: it runs before the count read-back,
     // queued behind whatever the stream is still doing
-    if (early) arm();  // before the kernels that publish
+    if (early && !async) arm();  // before the kernels that publish
     // the LSD form; from_state = 1: the bucket form's overflow fallback (lo from its state, all 4 passes)
     auto lsd_depth_order = [&](int from_state, unsigned* pubp) {
       const DlBufs b = dl_bufs(r, P);
@@ -2248,14 +2283,27 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       const int rc = lib_depth_order();
       if (rc) return rc;
     }
-    int rc = early ? wait_count() : publish(own_dsort && !lsd_dsort ? db.st + DS_OVERD : nullptr);
+    if (async) {
+      // no host read: the buckets above kDsSmall always get k_dsort_big (it exits
+      // at once without any), an overflowing bucket is the caller's flag (counts[2]:
+      // the frame is rendered again by the synchronous form), and the pair
+      // buffers hold async_cap pairs (counts[2] bit 1 when the frame needs more)
+      if (!lsd_dsort) {
+        hipLaunchKernelGGL(k_dsort_big, dim3(256), dim3(1024), 0, st, (const unsigned long long*)r->tiles, db,
+                           r->dorder, r->offr);
+        GSMPM_LAUNCH_CHECK();
+      }
+      K = (unsigned)r->async_cap;
+      K_full = 0;
+    }
+    int rc = async ? GSMPM_OK : early ? wait_count() : publish(own_dsort && !lsd_dsort ? db.st + DS_OVERD : nullptr);
     if (rc) return rc;
-    if (early && !lsd_dsort && hc[3]) {
+    if (!async && early && !lsd_dsort && hc[3]) {
       hipLaunchKernelGGL(k_dsort_big, dim3(256), dim3(1024), 0, st, (const unsigned long long*)r->tiles, db,
                          r->dorder, r->offr);
       GSMPM_LAUNCH_CHECK();
     }
-    if (own_dsort && !lsd_dsort && hc[2]) {
+    if (!async && own_dsort && !lsd_dsort && hc[2]) {
       // a depth bucket above kDsBig entries (a degenerate depth distribution): the
       // hand-written LSD form from the bucket form's state instead (dsort.h)
       r->dsort_fallbacks += 1;
@@ -2264,9 +2312,11 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       GSMPM_LAUNCH_CHECK();
       if ((rc = wait_count())) return rc;
     }
-    K = hc[0];
-    K_full = hc[1];
-    GSMPM_REQUIRE(K != kNoCount && K_full != kNoCount, "gsmpm_raster_forward: the pair count never arrived");
+    if (!async) {
+      K = hc[0];
+      K_full = hc[1];
+      GSMPM_REQUIRE(K != kNoCount && K_full != kNoCount, "gsmpm_raster_forward: the pair count never arrived");
+    }
   }
   if (K > 0 && r->ws) {
     const int rc = ws_carve_pairs(r, K, ntiles);
@@ -2290,6 +2340,8 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       r->capK = cap;
     }
     const int bits = msb_bits((unsigned)ntiles);
+    // the async form: the kernels cut at the device's count (offr's last entry)
+    const unsigned long long* kdev = r->async_cap > 0 ? (const unsigned long long*)(r->offr + (P - 1)) : nullptr;
     if (depth_ordered) {
       unsigned* tile_keys = reinterpret_cast<unsigned*>(r->keys);
       unsigned* tile_sorted = reinterpret_cast<unsigned*>(r->keys_sorted);
@@ -2345,26 +2397,27 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
         const int items = std::min(kEmitMaxI, std::max(1, div_up((long)K, (long)kEmitT * 1024)));
         const int nwg = div_up((long)K, (long)kEmitT * items);
         hipLaunchKernelGGL(k_emit_starts, dim3(div_up(P, 256)), dim3(256), 0, st, P, (const unsigned long long*)r->offr,
-                           (unsigned)(kEmitT * items), r->estart);
+                           (unsigned)(kEmitT * items), r->estart, (unsigned)(nwg + 1), K,
+                           r->async_cap > 0 ? r->async_counts + 2 : nullptr);
         GSMPM_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_emit_wg, dim3(nwg), dim3(kEmitT), 0, st, (int)K, P, items, (const unsigned*)r->estart,
                            tile_dsort ? nullptr : (const unsigned*)r->dorder, (const unsigned long long*)r->offr,
                            (const float2*)r->xy,
-                           (const float4*)r->conic, (const uint2*)r->rect, a.grid_x, cull, tile_keys, r->vals);
+                           (const float4*)r->conic, (const uint2*)r->rect, a.grid_x, cull, tile_keys, r->vals, kdev);
       }
       GSMPM_LAUNCH_CHECK();
       size_t bytes = r->sort_tmp_bytes;
       if (chunked) {
         unsigned* Hs = r->hist + r->capH;
         hipLaunchKernelGGL(k_tile_hist, dim3(nch), dim3(kSortT), 0, st, (int)K, (int)ntiles, nch, bits,
-                           (const unsigned*)tile_keys, r->hist);
+                           (const unsigned*)tile_keys, r->hist, kdev);
         GSMPM_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_tile_rows, dim3(div_up((long)ntiles + 1, 4)), dim3(256), 0, st, (int)ntiles, nch,
                            (const unsigned*)r->hist, Hs, r->ttot);
         hipLaunchKernelGGL(k_tile_scatter, dim3(nch), dim3(kSortT), 0, st, (int)K, (int)ntiles, nch, bits,
                            (const unsigned*)tile_keys, (const unsigned*)r->vals, (const unsigned*)Hs,
                            (const unsigned*)r->ttot, tile_sorted,
-                           r->ids_sorted, r->ranges, tile_dsort ? r->dsort_tl : nullptr);
+                           r->ids_sorted, r->ranges, tile_dsort ? r->dsort_tl : nullptr, kdev);
         GSMPM_LAUNCH_CHECK();
         if (tile_dsort) {  // depth order within each tile's list (the emission keys are dead: scratch)
           hipLaunchKernelGGL((k_tile_dsort<kDsortSmall, false>), dim3((unsigned)ntiles), dim3(256), 0, st,
@@ -2463,7 +2516,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
                        r->forward_only ? nullptr : r->n_contrib, tkeys, render_mode);
   r->has_pixel_state = !r->forward_only;
   GSMPM_LAUNCH_CHECK();
-  if (num_rendered) *num_rendered = (int32_t)K_full;
+  if (num_rendered) *num_rendered = r->async_cap > 0 ? -1 : (int32_t)K_full;
   r->P = P;
   r->W = a.W;
   r->H = a.H;
@@ -2621,6 +2674,61 @@ int gsmpm_raster_forward_ws(const gsmpm_raster_args* a, float* out_color, int32_
   rc = gsmpm_raster_forward(&r, a, out_color, out_radii, num_rendered, stream);
   if (rc == GSMPM_ESPACE && pairs_needed) *pairs_needed = r.pairs_needed;
   return rc;
+}
+
+int gsmpm_raster_forward_async(const gsmpm_raster_args* a, float* out_color, int32_t* out_radii, void* workspace,
+                               uint64_t ws_bytes, int64_t pairs_cap, uint32_t* counts, void* stream) {
+  GSMPM_REQUIRE(a && out_color && out_radii && counts && workspace && ((uintptr_t)workspace & 255u) == 0,
+                "gsmpm_raster_forward_async: null argument or workspace not 256-byte aligned");
+  GSMPM_REQUIRE(a->P >= 0 && a->W > 0 && a->H > 0 && pairs_cap > 0 && pairs_cap < (1LL << 31),
+                "gsmpm_raster_forward_async: bad sizes or pairs_cap");
+  const size_t ntiles = (size_t)div_up(a->W, kBX) * (size_t)div_up(a->H, kBY);
+  // the paths whose launch sizes do not depend on the pair count: the default
+  // depth-ordered forward with the chunked tile sort (<= kMaxTiles tiles)
+  auto env_is = [](const char* k, const char* v) {
+    const char* e = std::getenv(k);
+    return e && std::strcmp(e, v) == 0;
+  };
+  GSMPM_REQUIRE(ntiles <= (size_t)kMaxTiles, "gsmpm_raster_forward_async: more than 4,096 tiles (the digit sort "
+                "sizes its passes by the pair count): use gsmpm_raster_forward_ws");
+  GSMPM_REQUIRE(!env_is("GSMPM_RASTER_WIDE_KEYS", "1") && !env_is("GSMPM_RASTER_ONESWEEP", "1") &&
+                    !env_is("GSMPM_RASTER_CHUNKED", "0") && !env_is("GSMPM_RASTER_TILE_DSORT", "1") &&
+                    !env_is("GSMPM_RASTER_DSORT", "lib") && !env_is("GSMPM_RASTER_EMIT_LANE", "1"),
+                "gsmpm_raster_forward_async: an A/B switch selects a path the async form does not take");
+  hipStream_t st = (hipStream_t)stream;
+  if (a->P == 0) {  // the image is the background; every count is 0
+    hipLaunchKernelGGL(k_fill_bg, dim3(div_up((long)a->W * a->H, 256)), dim3(256), 0, st, a->bg, a->W * a->H,
+                       out_color, counts);
+    GSMPM_LAUNCH_CHECK();
+    return GSMPM_OK;
+  }
+  WsCount* c = nullptr;
+  int rc = ws_count(c);
+  if (rc) return rc;
+  gsmpm_raster r;  // a view of the workspace
+  r.forward_only = true;
+  r.h_count = c->h;
+  r.count_ev = c->ev;
+  r.ws = reinterpret_cast<char*>(workspace);
+  r.ws_bytes = (size_t)ws_bytes;
+  WsWalk w{r.ws, 0};
+  rc = ws_pre_walk(w, &r, (size_t)a->P, ntiles);
+  if (rc) return rc;
+  r.ws_pre = w.off;
+  {
+    WsWalk probe{nullptr, r.ws_pre};
+    gsmpm_raster tmp;
+    rc = ws_pairs_walk(probe, &tmp, (size_t)pairs_cap, ntiles);
+    if (rc) return rc;
+    if (probe.off > r.ws_bytes) {
+      set_error("gsmpm_raster_forward_async: the workspace is smaller than gsmpm_raster_workspace_size(P, H, W, "
+                "pairs_cap)");
+      return GSMPM_ESPACE;
+    }
+  }
+  r.async_cap = pairs_cap;
+  r.async_counts = reinterpret_cast<unsigned*>(counts);
+  return gsmpm_raster_forward(&r, a, out_color, out_radii, nullptr, stream);
 }
 
 int gsmpm_raster_mark_visible(const float* means3D, int32_t P, const float* vm, const float* pm, uint8_t* vis,

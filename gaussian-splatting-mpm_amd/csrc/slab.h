@@ -79,6 +79,7 @@ enum SlabRec : int {
   RF_CAP = 14,                                      // the slab's particle capacity
   RF_MMIN = 15,                                     // min particle mass (f32 bits; INT_MAX: no particle)
   RF_SLO = 16, RF_SHI = 17,                         // this rank's slab planes [lo, hi)
+  RF_WEIGHT = 18,                                   // this rank's share weight of the re-cut (f32 bits; 1: even)
   kRecHdr = 20                                      // then ng ints: the particles' base-plane histogram
 };
 // ints of one rank's record: the header and the base-plane histogram (the
@@ -97,7 +98,7 @@ struct MigGeom {
 };
 
 __global__ void k_rec_init(const int* __restrict__ flags, const int* __restrict__ nlive, int capacity, int lo, int hi,
-                           int nrec, int* __restrict__ rec) {
+                           int nrec, int* __restrict__ rec, const float* __restrict__ weight) {
   for (int i = kRecHdr + threadIdx.x; i < nrec; i += blockDim.x) rec[i] = 0;  // the histogram
   if (threadIdx.x != 0) return;
   rec[RF_FLAGS] = (flags[SF_DRIFT] ? 1 : 0) | (flags[SF_OOB] ? 2 : 0) | (flags[SF_NWANT_OVER] ? 8 : 0) |
@@ -119,7 +120,8 @@ __global__ void k_rec_init(const int* __restrict__ flags, const int* __restrict_
   rec[RF_MMIN] = INT_MAX;
   rec[RF_SLO] = lo;
   rec[RF_SHI] = hi;
-  for (int i = RF_SHI + 1; i < kRecHdr; ++i) rec[i] = 0;
+  rec[RF_WEIGHT] = __float_as_int(*weight);
+  for (int i = RF_WEIGHT + 1; i < kRecHdr; ++i) rec[i] = 0;
 }
 
 // yz box of the particles' base nodes (trunc(x * inv_dx - 0.5), utils.py:95),

@@ -93,6 +93,7 @@ _SIGS = {
     "gsmpm_mpm_slab_stats": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int64)]),
     "gsmpm_mpm_slab_rects": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int32)]),
     "gsmpm_mpm_slab_set_rebalance": (ctypes.c_int, [c_void_p, ctypes.c_int32, ctypes.c_float]),
+    "gsmpm_mpm_slab_set_weight": (ctypes.c_int, [c_void_p, ctypes.c_float]),
     "gsmpm_mpm_slab_bounds": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.c_int32,
                                              ctypes.POINTER(ctypes.c_int64)]),
     "gsmpm_mpm_resort": (ctypes.c_int, [c_void_p, ctypes.c_int32, c_void_p]),
@@ -151,6 +152,8 @@ _SIGS = {
     "gsmpm_raster_forward_ws": (ctypes.c_int, [ctypes.POINTER(RasterArgs), c_void_p, c_void_p,
                                                ctypes.POINTER(ctypes.c_int32), c_void_p, ctypes.c_uint64,
                                                ctypes.POINTER(ctypes.c_int64), c_void_p]),
+    "gsmpm_raster_forward_async": (ctypes.c_int, [ctypes.POINTER(RasterArgs), c_void_p, c_void_p, c_void_p,
+                                                  ctypes.c_uint64, ctypes.c_int64, c_void_p, c_void_p]),
 }
 GSMPM_OK, GSMPM_EINVAL, GSMPM_EHIP, GSMPM_ESTATE = 0, -1, -2, -3
 ESPACE = GSMPM_ESPACE = -4  # a caller-owned workspace is too small

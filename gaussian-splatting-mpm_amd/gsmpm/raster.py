@@ -248,6 +248,58 @@ def forward(means3D, opacities, viewmatrix, projmatrix, campos, bg, image_height
     return int(nr.value), color, radii
 
 
+class AsyncRender:
+    """One in-flight render of forward_async: the image and radii it writes and
+    its counts {K, num_rendered, flags, 1} in pinned host memory, valid once
+    the stream has passed the render (done())."""
+
+    def __init__(self, color, radii, counts, event, args):
+        self.color, self.radii, self.counts, self.event, self._args = color, radii, counts, event, args
+
+    def done(self) -> bool:
+        return self.event is None or self.event.query()
+
+    def result(self):
+        """(num_rendered, flags) after the stream reached it (waits for it)."""
+        if self.event is not None:
+            self.event.synchronize()
+        c = self.counts.tolist()
+        return int(c[1]), int(c[2])
+
+    @property
+    def valid(self) -> bool:
+        return self.result()[1] == 0
+
+
+def forward_async(means3D, opacities, viewmatrix, projmatrix, campos, bg, image_height, image_width, tanfovx, tanfovy,
+                  sh_degree=0, shs=None, colors_precomp=None, cov3D_precomp=None, scales=None, rotations=None,
+                  scale_modifier=1.0, pairs_cap=None, ws=None, counts=None, color=None, radii=None):
+    """gsmpm_raster_forward_async: the forward with no host synchronisation
+    (the pair count stays on the device; buffers carved for pairs_cap pairs,
+    default the workspace's).  Returns an AsyncRender; a frame whose flags
+    are set (a depth bucket overflow, or more pairs than pairs_cap) must be
+    rendered again by forward()."""
+    dev = means3D.device
+    a, keep = _args(means3D, opacities, viewmatrix, projmatrix, campos, bg, image_height, image_width, tanfovx,
+                    tanfovy, sh_degree, shs, colors_precomp, scales, rotations, cov3D_precomp, scale_modifier, False)
+    H, W = int(image_height), int(image_width)
+    color = torch.empty((3, H, W), dtype=torch.float32, device=dev) if color is None else color
+    radii = torch.empty(a.P, dtype=torch.int32, device=dev) if radii is None else radii
+    counts = torch.zeros(4, dtype=torch.int32, pin_memory=True) if counts is None else counts
+    w = ws if ws is not None else workspace(dev.index or 0, torch.cuda.current_stream(dev))
+    cap = int(pairs_cap) if pairs_cap else (w.key[3] if w.key else 8 * a.P + 4096)
+    w.ensure(a.P, H, W, cap)
+    with torch.cuda.device(dev):
+        check(LIB.gsmpm_raster_forward_async(ctypes.byref(a), ptr(color), ptr(radii), w.ptr(), w.nbytes(), cap,
+                                             ctypes.c_void_p(counts.data_ptr()), stream_of(dev)),
+              "rasterize_gaussians (async)")
+        ev = None
+        if not torch.cuda.is_current_stream_capturing():  # a graph replay is waited on by its caller
+            ev = torch.cuda.Event()
+            ev.record()
+    return AsyncRender(color, radii, counts, ev, (a, keep))
+
+
 def mark_visible(positions, viewmatrix, projmatrix):
     positions = _f32(positions)
     P = positions.shape[0]

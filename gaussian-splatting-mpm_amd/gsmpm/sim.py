@@ -162,6 +162,10 @@ class Simulator:
         check(LIB.gsmpm_mpm_slab_set_rebalance(self._h, 1 if on else 0, ctypes.c_float(tolerance)),
               "gsmpm_mpm_slab_set_rebalance")
 
+    def slab_set_weight(self, weight: float):
+        """This rank's share weight in the re-cut (gsmpm_mpm_slab_set_weight)."""
+        check(LIB.gsmpm_mpm_slab_set_weight(self._h, ctypes.c_float(weight)), "gsmpm_mpm_slab_set_weight")
+
     def slab_bounds(self, world: int):
         """(every slab's bounds [world + 1], re-cuts so far)."""
         b = (ctypes.c_int32 * (world + 1))()

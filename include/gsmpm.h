@@ -182,6 +182,16 @@ int gsmpm_mpm_slab_rects(gsmpm_mpm* h, int32_t out8[8]);
  * records on every rank: the same bounds), each bound staying inside its old
  * neighbouring slabs; the next call opens with the migration to them. */
 int gsmpm_mpm_slab_set_rebalance(gsmpm_mpm* h, int32_t on, float tolerance);
+/* This rank's weight in the re-cut (default 1; > 0): the bounds move to the
+ * quantiles that give rank r the share w_r / sum(w) of the particles, and a
+ * rank holding more than (1 + tolerance) x its share triggers the re-cut.  A
+ * rank with other work per frame takes a smaller share: the rank that renders
+ * the gathered frame (bench.py, SlabDomain.set_render_share) sets w = its
+ * simulation time / (its simulation + render time), so its sim + render
+ * matches the other ranks' sim (the round-4 verdict's render-aware re-cut).
+ * Carried in each rank's record (the next step call's), so every rank sees
+ * every weight.  No reference counterpart. */
+int gsmpm_mpm_slab_set_weight(gsmpm_mpm* h, float weight);
 /* The current bounds of every slab, out[world + 1] (before the first step call
  * only this rank's own two, the rest -1), and the re-cuts made so far. */
 int gsmpm_mpm_slab_bounds(gsmpm_mpm* h, int32_t* out, int32_t n, int64_t* rebalances);
@@ -432,6 +442,25 @@ int gsmpm_raster_workspace_size(int32_t P, int32_t H, int32_t W, int64_t pairs, 
 int gsmpm_raster_forward_ws(const gsmpm_raster_args* a, float* out_color, int32_t* out_radii,
                             int32_t* num_rendered, void* workspace, uint64_t ws_bytes, int64_t* pairs_needed,
                             void* stream);
+/* The forward with the pair count left on the device (the round-4 verdict's
+ * item 4: upstream and gsmpm_raster_forward_ws read it on the host to size
+ * the binning, main.py:148-156).  The pair buffers are carved for pairs_cap
+ * pairs (the workspace must hold gsmpm_raster_workspace_size(P, H, W,
+ * pairs_cap), else GSMPM_ESPACE before any launch); every launch size is
+ * fixed by P, H, W and pairs_cap, the kernels cut at the device's count, and
+ * nothing waits on the host: the call only enqueues on `stream`, and the
+ * sequence can be captured into a graph and replayed (the argument pointers
+ * are baked in).  When the stream reaches the end, counts (device-accessible:
+ * host-mapped pinned or device memory, 4 words) holds {K, num_rendered,
+ * flags, 1}: flags bit 0 = a depth bucket above 8,192 Gaussians (the hand-
+ * written order needs its LSD fallback, which this form does not take), bit 1
+ * = K > pairs_cap (the emission stopped at pairs_cap).  Either bit means
+ * out_color is not the frame: render it again with gsmpm_raster_forward_ws
+ * (or with pairs_cap >= K).  The default depth-ordered path with the chunked
+ * tile sort only (<= 4,096 tiles: the lego camera's 2,500); more tiles or an
+ * A/B switch that selects another path: GSMPM_EINVAL. */
+int gsmpm_raster_forward_async(const gsmpm_raster_args* a, float* out_color, int32_t* out_radii, void* workspace,
+                               uint64_t ws_bytes, int64_t pairs_cap, uint32_t* counts, void* stream);
 /* Diagnostics of the context's last forward: *binned = the (Gaussian, tile)
  * pairs actually sorted and listed (each Gaussian binned into the tiles its
  * alpha >= 1/255 box reaches, a subset of the 3-sigma rect), *rendered = its

@@ -28,16 +28,19 @@ def _line(p):
 
 
 def test_gpus_flag_starts_that_many_ranks():
+    """The default N > 1 headline: one lego scene per rank (weak scaling)."""
     out = _line(_run(["--gpus", "2", "--dry-run"]))
-    assert out["n_gpus"] == 2
-    assert out["config"]["parallelism"] == "slab2"
-    assert out["scaling"] == "strong"
-
-
-def test_gpus_flag_dp_mode():
-    out = _line(_run(["--gpus", "2", "--dp", "--dry-run"]))
     assert out["n_gpus"] == 2 and out["scaling"] == "weak"
     assert out["config"]["parallelism"].startswith("dp2")
+
+
+def test_gpus_flag_slab_mode():
+    for flag in (["--slab"], ["--multi", "slab"]):
+        out = _line(_run(["--gpus", "2", "--dry-run"] + flag))
+        assert out["n_gpus"] == 2 and out["scaling"] == "strong"
+        assert out["config"]["parallelism"] == "slab2"
+    out = _line(_run(["--gpus", "2", "--dp", "--dry-run"]))
+    assert out["scaling"] == "weak" and out["config"]["parallelism"].startswith("dp2")
 
 
 def test_default_is_one_rank():

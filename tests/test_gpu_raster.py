@@ -473,6 +473,67 @@ def test_depth_bucket_overflow_takes_lsd_fallback(dev, monkeypatch):
     assert Kb == Kl and torch.equal(rb, rl) and torch.equal(cb, cl)
 
 
+def test_async_forward_matches_workspace_forward(dev):
+    """gsmpm_raster_forward_async (the round-4 verdict's item 4: no host
+    round trip on the pair count): the image and radii bit-identical to the
+    workspace form's, counts = {K, num_rendered, 0, 1} once the stream is past
+    it; a capacity below K raises flag bit 1 (no fault, the caller re-renders);
+    a depth bucket above 8,192 raises bit 0; P = 0 gives the background and
+    zero counts; and the whole forward captured in a graph and replayed on new
+    means renders what the synchronous form renders."""
+    import torch
+    from gsmpm import raster
+    P, W, H = 20000, 800, 800
+    means, c6, opa, shs = _scene(P, seed=21)
+    view, full, campos, tx, ty = _camera(W, H, 0.9, yaw=0.3)
+    bgv = np.array([0.1, 0.2, 0.3], np.float32)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    args = [t(means), t(opa), t(view), t(full), t(campos), t(bgv), H, W, tx, ty]
+    kw = dict(sh_degree=3, shs=t(shs), cov3D_precomp=t(c6))
+    K, col, rad = raster.forward(*args, **kw)  # the workspace form (host count)
+    ctx = raster.RasterContext()
+    raster.forward(*args, **kw, context=ctx)
+    binned, _ = raster.pair_counts(ctx)
+    ws = raster.Workspace(dev)
+    ar = raster.forward_async(*args, **kw, pairs_cap=binned + binned // 4 + 64, ws=ws)
+    nr, flags = ar.result()
+    assert flags == 0 and nr == K and int(ar.counts[0]) == binned and int(ar.counts[3]) == 1
+    assert torch.equal(ar.radii, rad) and torch.equal(ar.color, col)
+    # too small a capacity: flagged, and the next full-capacity call is exact again (the state stays idle)
+    small = raster.forward_async(*args, **kw, pairs_cap=binned // 2, ws=ws)
+    assert small.result()[1] & 2
+    again = raster.forward_async(*args, **kw, pairs_cap=binned + 1, ws=ws)
+    assert again.result()[1] == 0 and torch.equal(again.color, col)
+    # a camera-facing plane: one depth bucket above 8,192 Gaussians -> flag bit 0
+    mflat = means.copy()
+    mflat[:, 2] = np.float32(0.1)
+    flat = raster.forward_async(t(mflat), *args[1:], **kw, pairs_cap=8 * P, ws=ws)
+    assert flat.result()[1] & 1
+    # no Gaussians: the background
+    empty = raster.forward_async(t(np.zeros((0, 3), np.float32)), t(np.zeros((0, 1), np.float32)), *args[2:],
+                                 sh_degree=3, shs=t(np.zeros((0, 16, 3), np.float32)),
+                                 cov3D_precomp=t(np.zeros((0, 6), np.float32)), ws=ws)
+    assert empty.result() == (0, 0) and torch.equal(empty.color, t(bgv).view(3, 1, 1).expand(3, H, W))
+    # captured once, replayed on new means (copied into the captured input buffer)
+    m_in = t(means).clone()
+    col_out = torch.empty((3, H, W), dtype=torch.float32, device=dev)
+    rad_out = torch.empty(P, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(4, dtype=torch.int32, pin_memory=True)
+    cap = 2 * binned
+    raster.forward_async(m_in, *args[1:], **kw, pairs_cap=cap, ws=ws, counts=cnt, color=col_out, radii=rad_out)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        raster.forward_async(m_in, *args[1:], **kw, pairs_cap=cap, ws=ws, counts=cnt, color=col_out, radii=rad_out)
+    m2 = means + np.float32(0.05)
+    K2, col2, rad2 = raster.forward(t(m2), *args[1:], **kw)
+    m_in.copy_(t(m2))
+    g.replay()
+    torch.cuda.synchronize()
+    assert int(cnt[2]) == 0 and int(cnt[1]) == K2
+    assert torch.equal(rad_out, rad2) and torch.equal(col_out, col2)
+
+
 @pytest.mark.parametrize("P,W,H", [(3000, 256, 192), (20000, 1100, 1000)])
 def test_workspace_forward_matches_context(dev, P, W, H):
     """SURVEY 8(b) b2's caller-owned workspace: gsmpm_raster_forward_ws into a

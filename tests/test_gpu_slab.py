@@ -204,7 +204,7 @@ def _drift_scene():
     return x, v, cov, vol
 
 
-def _rebalance_worker(rank, world, port, out, backend, rebalance):
+def _rebalance_worker(rank, world, port, out, backend, rebalance, weight0=None, drift=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     if backend == "nccl-shared":
         os.environ.update(shared_gpu_rccl_env(rank))
@@ -216,13 +216,16 @@ def _rebalance_worker(rank, world, port, out, backend, rebalance):
         dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from gsmpm.dist import SlabDomain, make_transport
-        x, v, cov, vol = _drift_scene()
+        x, v, cov, vol = _drift_scene() if drift else scene()
         xp = make_transport(rank, world, device=dev)
         dom = SlabDomain(x, cov, vol, v=v, rank=rank, world=world, transport=xp, n_grid=NG, grid_extent=EXT,
                          margin=2, interval=10, device=dev, jelly_fcr=True, rebalance=rebalance, **KW)
         dom.add_plane_collider([0, 0, 0.4], [0, 0, 1])
+        if weight0 is not None and rank == 0:
+            dom.set_weight(weight0)
         b0 = list(dom.bounds)
         imb = []
+        counts = []
         for _ in range(20):  # 20 calls of 10 substeps: a re-cut can follow every call
             dom.step(DT, [1] * 10)
             cnt = torch.tensor([dom.n], dtype=torch.int64, device=dev if backend != "gloo" else "cpu")
@@ -230,10 +233,12 @@ def _rebalance_worker(rank, world, port, out, backend, rebalance):
             dist.all_gather(allc, cnt)
             c = [int(t.item()) for t in allc]
             imb.append(max(c) / (sum(c) / world))
+            counts.append(c)
         got = {k: dom.gather_field(k) for k in ("x", "v", "C", "F_trial")}
         if rank == 0:
             np.savez(os.path.join(out, "rebal.npz"), imb=np.array(imb), b0=np.array(b0), b1=np.array(dom.bounds),
-                     rebalances=dom.rebalances, **{k: g.cpu().numpy() for k, g in got.items()})
+                     rebalances=dom.rebalances, counts=np.array(counts),
+                     **{k: g.cpu().numpy() for k, g in got.items()})
         dom.engine.close()
         xp.close()
     finally:
@@ -285,6 +290,41 @@ def test_gpu_slabs_no_rebalance_control(dev, tmp_path):
     r = np.load(os.path.join(tmp_path, "rebal.npz"))
     assert int(r["rebalances"]) == 0 and r["b1"].tolist() == r["b0"].tolist()
     assert float(r["imb"][-1]) > 1.3, r["imb"].tolist()
+
+
+@pytest.mark.parametrize("backend,world", [("gloo", 2), ("gloo", 3), ("nccl-shared", 2)])
+def test_gpu_slabs_weighted_recut(dev, tmp_path, backend, world):
+    """The render-aware re-cut (the round-4 verdict's item 2(a),
+    gsmpm_mpm_slab_set_weight): rank 0 -- the rank that renders the gathered
+    frame -- takes the share weight 0.5 (the others 1), so the library's
+    re-cut moves the bounds until rank 0 holds w0 / sum(w) of the particles
+    (1/3 at 2 ranks, 1/5 at 3).  The weights travel in the ranks' records, so
+    every rank computes the same bounds.  A static scene over 200 substeps in
+    20 calls: rank 0's count over the last 10 calls stays within 15 % of its
+    share (one plane holds several % of a slab of this 4,000-particle scene)
+    and the state matches the single-domain oracle."""
+    import oracle as O
+    mp.spawn(_rebalance_worker, args=(world, free_port(), str(tmp_path), backend, True, 0.5, False), nprocs=world,
+             join=True)
+    r = np.load(os.path.join(tmp_path, "rebal.npz"))
+    x, v, cov, vol = scene()
+    ref = O.OracleMPM(x, cov, vol, v=v, n_grid=NG, grid_extent=EXT, jelly_quirk=False, **KW)
+    ref.add_collider([0, 0, 0.4], [0, 0, 1])
+    for _ in range(200):
+        ref.substep(DT, op_active=[1])
+    counts = r["counts"]
+    share = 0.5 / (0.5 + (world - 1))
+    frac0 = counts[-10:, 0] / counts[-10:].sum(1)
+    rec = {"backend": backend, "world": world, "rebalances": int(r["rebalances"]), "bounds_init": r["b0"].tolist(),
+           "bounds_end": r["b1"].tolist(), "rank0_fraction_last10": [round(float(f), 4) for f in frac0],
+           "rank0_share": share}
+    print("weighted re-cut", rec)
+    assert counts[0, 0] / counts[0].sum() > 1.3 * share  # it starts far from the weighted share
+    assert int(r["rebalances"]) >= 1, rec
+    assert np.all(np.abs(frac0 / share - 1.0) < 0.15), rec
+    errs = {k: rel_err(r[k], getattr(ref, k)) for k in ("x", "v", "C", "F_trial")}
+    for k, e in errs.items():
+        assert e < TOL.get(k, 1e-4), (k, e, errs)
 
 
 IMPULSE = ([1.0, 1.0, 0.8], [0.4, 0.4, 0.4], [0.0, 300.0, 0.0])  # center, half-size, force (grid units)
