@@ -293,6 +293,9 @@ constexpr int kSimPrio = GSMPM_SIM_PRIO;
 __device__ __forceinline__ void sim_prio() {
   if constexpr (kSimPrio > 0) __builtin_amdgcn_s_setprio(kSimPrio);
 }
+#ifndef GSMPM_DPP_REDUCE
+#define GSMPM_DPP_REDUCE 1
+#endif
 // GSMPM_G2P_B128 (A/B, default 1): G2P's 27 LDS gathers as ds_read_b128
 #ifndef GSMPM_G2P_B128
 #define GSMPM_G2P_B128 1
@@ -573,10 +576,20 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
       int mxy = win ? (7 << (b[0] - o0)) | (7 << (16 + b[1] - o1)) : 0;
       int mz = win ? 7 << (b[2] - o2) : 0;
       // wave reductions by DPP (the bound is >= 0; a NaN bound -- non-finite
-      // inputs, flagged above -- orders above every finite one as integer bits)
-      bound = wave_max_nonneg_dpp(bound);
-      mxy = wave_or_dpp(mxy);
-      mz = wave_or_dpp(mz);
+      // inputs, flagged above -- orders above every finite one as integer bits);
+      // GSMPM_DPP_REDUCE=0 (A/B): shuffles (ds_bpermute_b32)
+      if constexpr (GSMPM_DPP_REDUCE != 0) {
+        bound = wave_max_nonneg_dpp(bound);
+        mxy = wave_or_dpp(mxy);
+        mz = wave_or_dpp(mz);
+      } else {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          bound = fmaxf(bound, __shfl_xor(bound, o));
+          mxy |= __shfl_xor(mxy, o);
+          mz |= __shfl_xor(mz, o);
+        }
+      }
       if ((k & 63) == 0) {
         s_max[k >> 6] = bound;
         s_mxy[k >> 6] = mxy;

@@ -248,7 +248,7 @@ def test_heterogeneous_masses(dev, pipe):
     vol = O.particle_volume(x, ng, ext).astype(np.float32)
     vol[nb] = vol[:nb].mean() * 1e-17
     kw = dict(n_grid=ng, grid_extent=ext, material="jelly", E=2e4, nu=0.3, density=200.0, gravity=(0.0, 0.0, 0.0))
-    ref = O.OracleMPM(x, cov, vol, v=v, jelly_quirk=False, **kw)
+    ref = O.OracleMPM(x, cov, vol, v=v, **kw)  # jelly as written, as Simulator runs it
     sim = Simulator(len(x), phased=pipe == "phased", **kw)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     sim.set_particles(t(x), t(cov), t(vol), t(v))
@@ -334,7 +334,7 @@ def test_particles_binned_outside_the_grid(dev):
     cov = np.tile(np.array([1e-4, 0, 0, 1e-4, 0, 1e-4], np.float32), (len(x), 1))
     vol = O.particle_volume(x, ng, ext)
     kw = dict(n_grid=ng, grid_extent=ext, material="jelly", E=2e4, nu=0.3, density=200.0, gravity=(0.0, -9.8, 0.0))
-    ref = O.OracleMPM(x, cov, vol, v=v, jelly_quirk=False, **kw)
+    ref = O.OracleMPM(x, cov, vol, v=v, **kw)  # jelly as written, as Simulator runs it
     sim = Simulator(len(x), **kw)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
     sim.set_particles(t(x), t(cov), t(vol), t(v))

