@@ -916,11 +916,16 @@ def main():
             else:
                 means_r, covs_r = sim.world_outputs(w_scale, w_center, render_space=True)
             if ren_async:
-                if not acap["cap"]:  # the capacity: one synchronous render of the first snapshot
+                if not acap["cap"]:  # the capacity: the binned pairs of one render of the first snapshot, + 15 %
                     nr, _, _ = raster.forward(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg,
                                               cam.height, cam.width, tanx, tany, sh_degree=3, shs=feats,
                                               cov3D_precomp=covs_r)
-                    acap["cap"] = nr + nr // 2 + 4096  # num_rendered (3 sigma) >= the binned pairs
+                    probe = raster.forward_async(means_r, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg,
+                                                 cam.height, cam.width, tanx, tany, sh_degree=3, shs=feats,
+                                                 cov3D_precomp=covs_r, pairs_cap=nr + 4096)  # 3 sigma >= binned
+                    probe.result()
+                    kb = int(probe.counts[0])
+                    acap["cap"] = kb + kb // 8 + 4096
                 t.append(time.perf_counter())
                 rs = render_stream if args.render_overlap else torch.cuda.current_stream()
                 ev = torch.cuda.Event()

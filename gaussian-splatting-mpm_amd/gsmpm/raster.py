@@ -250,8 +250,8 @@ def forward(means3D, opacities, viewmatrix, projmatrix, campos, bg, image_height
 
 class AsyncRender:
     """One in-flight render of forward_async: the image and radii it writes and
-    its counts {K, num_rendered, flags, 1} in pinned host memory, valid once
-    the stream has passed the render (done())."""
+    its counts {K, num_rendered, flags, internal} in pinned host memory, valid
+    once the stream has passed the render (done())."""
 
     def __init__(self, color, radii, counts, event, args):
         self.color, self.radii, self.counts, self.event, self._args = color, radii, counts, event, args

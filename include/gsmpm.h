@@ -452,7 +452,7 @@ int gsmpm_raster_forward_ws(const gsmpm_raster_args* a, float* out_color, int32_
  * sequence can be captured into a graph and replayed (the argument pointers
  * are baked in).  When the stream reaches the end, counts (device-accessible:
  * host-mapped pinned or device memory, 4 words) holds {K, num_rendered,
- * flags, 1}: flags bit 0 = a depth bucket above 8,192 Gaussians (the hand-
+ * flags, internal}: flags bit 0 = a depth bucket above 8,192 Gaussians (the hand-
  * written order needs its LSD fallback, which this form does not take), bit 1
  * = K > pairs_cap (the emission stopped at pairs_cap).  Either bit means
  * out_color is not the frame: render it again with gsmpm_raster_forward_ws

@@ -497,7 +497,7 @@ def test_async_forward_matches_workspace_forward(dev):
     ws = raster.Workspace(dev)
     ar = raster.forward_async(*args, **kw, pairs_cap=binned + binned // 4 + 64, ws=ws)
     nr, flags = ar.result()
-    assert flags == 0 and nr == K and int(ar.counts[0]) == binned and int(ar.counts[3]) == 1
+    assert flags == 0 and nr == K and int(ar.counts[0]) == binned
     assert torch.equal(ar.radii, rad) and torch.equal(ar.color, col)
     # too small a capacity: flagged, and the next full-capacity call is exact again (the state stays idle)
     small = raster.forward_async(*args, **kw, pairs_cap=binned // 2, ws=ws)
