@@ -93,10 +93,17 @@ def parse():
     ap.add_argument("--render-thread", type=int, default=int(os.environ.get("GSMPM_BENCH_RENDER_THREAD", "1")),
                     help="overlapped render: 1 = a host thread of its own issues the renders (its pair-count wait "
                          "no longer holds back the launch of the next frame's graph); 0 = the frame loop's thread")
-    ap.add_argument("--render-async", type=int, default=int(os.environ.get("GSMPM_BENCH_RENDER_ASYNC", "1")),
+    ap.add_argument("--render-async", type=int, default=int(os.environ.get("GSMPM_BENCH_RENDER_ASYNC", "0")),
                     help="1: frames render through gsmpm_raster_forward_async (the pair count stays on the device: "
                          "no host wait, no render thread; a frame whose counts flag an overflow is rendered again "
-                         "by the synchronous form inside the timed region); 0: the synchronous form")
+                         "by the synchronous form inside the timed region); 0 (default: measured faster with the render "
+                         "thread, DESIGN.md §6): the synchronous form")
+    ap.add_argument("--render-cu-layout", default=os.environ.get("GSMPM_BENCH_RENDER_CU_LAYOUT", "spread"),
+                    choices=["spread", "low", "xmajor"],
+                    help="which CU-mask bits --render-cus gives the render: spread = evenly spaced bits (round 4); "
+                         "low = bits 0 .. N-1; xmajor = the first N/8 bits of each 32-bit word (one word per XCD "
+                         "if the mask is XCD-major).  k_fused fills one round only if every XCD keeps enough CUs, "
+                         "so the render's CUs must be spread over the XCDs, whichever way the bits map")
     ap.add_argument("--render-cus", type=int, default=int(os.environ.get("GSMPM_BENCH_RENDER_CUS", "0")),
                     help="N > 0: the overlapped render gets N of the device's CUs (every (CUs / N)-th CU-mask bit) "
                          "and the simulator the rest, on CU-masked streams (hipExtStreamCreateWithCUMask), so the "
@@ -128,7 +135,7 @@ def launch_ranks(n):
     return subprocess.call(cmd, env=env)
 
 
-def cu_split_streams(dev, n_render):
+def cu_split_streams(dev, n_render, layout="spread"):
     """Two streams on disjoint CU masks (hipExtStreamCreateWithCUMask through the
     HIP runtime torch already loaded): the simulator's (every CU but the
     render's) and the render's: exactly n_render evenly spaced CUs.  Returns
@@ -137,7 +144,14 @@ def cu_split_streams(dev, n_render):
     import torch
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     n_render = max(1, min(int(n_render), ncu - 1))
-    rbits = {min(ncu - 1, round((i + 0.5) * ncu / n_render)) for i in range(n_render)}
+    if layout == "low":
+        rbits = set(range(n_render))
+    elif layout == "xmajor":
+        per = max(1, n_render // 8)
+        rbits = {32 * w + j for w in range((ncu + 31) // 32) for j in range(per) if 32 * w + j < ncu}
+        rbits = set(sorted(rbits)[:n_render])
+    else:
+        rbits = {min(ncu - 1, round((i + 0.5) * ncu / n_render)) for i in range(n_render)}
     sbits = set(range(ncu)) - rbits
     assert len(rbits) == n_render and sbits, (ncu, n_render)
     words = (ncu + 31) // 32
@@ -772,7 +786,7 @@ def main():
     # render's stream on disjoint CU masks
     masked_render_stream = None
     if args.render_cus > 0 and args.render_overlap and not args.no_render:
-        sim_stream, masked_render_stream, render_cus_actual = cu_split_streams(dev, args.render_cus)
+        sim_stream, masked_render_stream, render_cus_actual = cu_split_streams(dev, args.render_cus, args.render_cu_layout)
         torch.cuda.set_stream(sim_stream)
 
     from gsmpm import raster
@@ -1081,6 +1095,7 @@ def main():
                    "particles_total": n_total, "n_grid": sa.n_grid, "material": sa.material,
                    "substep_dt": dt, "render_overlap": bool(args.render_overlap),
                    "render_cus": render_cus_actual if masked_render_stream is not None else None,
+                   "render_cu_layout": args.render_cu_layout if masked_render_stream is not None else None,
                    "render_delay_us": args.render_delay_us if args.render_overlap else None,
                    "render_first": bool(args.render_first) if args.render_overlap else None,
                    "render_thread": bool(rq is not None),

@@ -301,6 +301,10 @@ __device__ __forceinline__ void sim_prio() {
 #define GSMPM_G2P_B128 1
 #endif
 constexpr bool kG2pB128 = GSMPM_G2P_B128 != 0;
+#ifndef GSMPM_BIN_AGG
+#define GSMPM_BIN_AGG 1
+#endif
+constexpr bool kBinAgg = GSMPM_BIN_AGG != 0;
 template <int MAT, int MODE>
 __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTiles tl, ChunkIn ck, Touch tc, BinOutF bo,
                                                int bin, int use_box, const float4* __restrict__ gvel,
@@ -460,14 +464,32 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
           nt = ftile_of(x, g, tl, tc);
           if (!outside && nt < tl.ntiles) {
             const int d0 = tc[0] - tx, d1 = tc[1] - ty, d2 = tc[2] - tz;
-            if (abs(d0) <= 1 && abs(d1) <= 1 && abs(d2) <= 1) {
-              code = (d0 + 1) * 9 + (d1 + 1) * 3 + (d2 + 1);
-              lslot = atomicAdd(&s_cnt[code], 1);
-            }
+            if (abs(d0) <= 1 && abs(d1) <= 1 && abs(d2) <= 1) code = (d0 + 1) * 9 + (d1 + 1) * 3 + (d2 + 1);
           }
         }
       }
       if (bin) {
+        // the slot of the particle in its new tile's bin, reserved once per
+        // (wave, neighbour tile): nearly every lane of a wave stays in the
+        // chunk's own tile, and one LDS counter hit by 64 lanes serializes
+        // them (2 cycles a lane, ~half of round 4's k_fused LDS bank-conflict
+        // cycles); GSMPM_BIN_AGG=0: a lane-level atomic (A/B)
+        if constexpr (kBinAgg) {
+          unsigned long long pending = __ballot(code >= 0);
+          while (pending) {  // wave-uniform: one trip per distinct neighbour tile of the wave
+            const int lead = __ffsll(pending) - 1;
+            const int lc = __builtin_amdgcn_readlane(code, lead);
+            const unsigned long long mk = __ballot(code == lc);
+            int base = 0;
+            if ((k & 63) == lead) base = atomicAdd(&s_cnt[lc], __popcll(mk));
+            base = __builtin_amdgcn_readlane(base, lead);
+            if (code == lc)
+              lslot = base + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(mk >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mk, 0u));
+            pending &= ~mk;
+          }
+        } else if (code >= 0) {
+          lslot = atomicAdd(&s_cnt[code], 1);
+        }
         __syncthreads();
         if (k < 27) {
           const int c = s_cnt[k];

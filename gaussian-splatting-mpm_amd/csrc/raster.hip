@@ -883,12 +883,14 @@ constexpr int kEmitT = 256, kEmitMaxI = 16, kEmitG = GSMPM_EMIT_G;
 // the caller renders the frame again with room for the count).
 __global__ __launch_bounds__(256) void k_emit_starts(int P, const unsigned long long* __restrict__ offr, unsigned E,
                                                      unsigned* __restrict__ starts, unsigned bmax, unsigned kcap,
-                                                     unsigned* flags) {
+                                                     const unsigned* __restrict__ over, unsigned* flags) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= P) return;
   const unsigned s = r ? (unsigned)offr[r - 1] : 0u, t = (unsigned)offr[r];
   for (unsigned b = (s + E - 1) / E; b * E < t && b < bmax; ++b) starts[b] = (unsigned)r;
-  if (flags && r == P - 1 && t > kcap) flags[0] |= 2u;
+  // the whole flags word, one store (the depth order's bucket overflow from the
+  // device state, not read back from the caller's host memory)
+  if (flags && r == P - 1) flags[0] = (over ? *over : 0u) | (t > kcap ? 2u : 0u);
 }
 // K of the frame: the host's count, or (the async form) the device's, cut at the host's capacity
 __device__ __forceinline__ int pairs_of(int K, const unsigned long long* kdev) {
@@ -2141,6 +2143,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
   r->offsets_pending = false;
   r->emit_culled = false;
   const unsigned* tkeys = nullptr;  // sorted tile keys with sub-tile masks (chunked path)
+  const unsigned* async_over = nullptr;  // the async form's bucket-overflow flag (device state, bucket form)
   unsigned K = 0, K_full = 0;  // binned pairs, upstream's 3-sigma pairs (num_rendered)
   if (P > 0) {
     // GSMPM_RASTER_DSORT=lib: the library's radix sort + scan for the depth order (A/B; also the
@@ -2295,6 +2298,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
       }
       K = (unsigned)r->async_cap;
       K_full = 0;
+      if (!lsd_dsort) async_over = db.st + DS_OVERD;
     }
     int rc = async ? GSMPM_OK : early ? wait_count() : publish(own_dsort && !lsd_dsort ? db.st + DS_OVERD : nullptr);
     if (rc) return rc;
@@ -2397,7 +2401,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
         const int items = std::min(kEmitMaxI, std::max(1, div_up((long)K, (long)kEmitT * 1024)));
         const int nwg = div_up((long)K, (long)kEmitT * items);
         hipLaunchKernelGGL(k_emit_starts, dim3(div_up(P, 256)), dim3(256), 0, st, P, (const unsigned long long*)r->offr,
-                           (unsigned)(kEmitT * items), r->estart, (unsigned)(nwg + 1), K,
+                           (unsigned)(kEmitT * items), r->estart, (unsigned)(nwg + 1), K, async_over,
                            r->async_cap > 0 ? r->async_counts + 2 : nullptr);
         GSMPM_LAUNCH_CHECK();
         hipLaunchKernelGGL(k_emit_wg, dim3(nwg), dim3(kEmitT), 0, st, (int)K, P, items, (const unsigned*)r->estart,
@@ -2678,7 +2682,7 @@ int gsmpm_raster_forward_ws(const gsmpm_raster_args* a, float* out_color, int32_
 
 int gsmpm_raster_forward_async(const gsmpm_raster_args* a, float* out_color, int32_t* out_radii, void* workspace,
                                uint64_t ws_bytes, int64_t pairs_cap, uint32_t* counts, void* stream) {
-  GSMPM_REQUIRE(a && out_color && out_radii && counts && workspace && ((uintptr_t)workspace & 255u) == 0,
+  GSMPM_REQUIRE(a && out_color && (out_radii || a->P == 0) && counts && workspace && ((uintptr_t)workspace & 255u) == 0,
                 "gsmpm_raster_forward_async: null argument or workspace not 256-byte aligned");
   GSMPM_REQUIRE(a->P >= 0 && a->W > 0 && a->H > 0 && pairs_cap > 0 && pairs_cap < (1LL << 31),
                 "gsmpm_raster_forward_async: bad sizes or pairs_cap");

@@ -476,7 +476,7 @@ def test_depth_bucket_overflow_takes_lsd_fallback(dev, monkeypatch):
 def test_async_forward_matches_workspace_forward(dev):
     """gsmpm_raster_forward_async (the round-4 verdict's item 4: no host
     round trip on the pair count): the image and radii bit-identical to the
-    workspace form's, counts = {K, num_rendered, 0, 1} once the stream is past
+    workspace form's, counts = {K, num_rendered, flags = 0, .} once the stream is past
     it; a capacity below K raises flag bit 1 (no fault, the caller re-renders);
     a depth bucket above 8,192 raises bit 0; P = 0 gives the background and
     zero counts; and the whole forward captured in a graph and replayed on new
@@ -505,9 +505,12 @@ def test_async_forward_matches_workspace_forward(dev):
     again = raster.forward_async(*args, **kw, pairs_cap=binned + 1, ws=ws)
     assert again.result()[1] == 0 and torch.equal(again.color, col)
     # a camera-facing plane: one depth bucket above 8,192 Gaussians -> flag bit 0
+    # (the camera looks along z: yaw 0, as test_depth_order_matches_library_sort's "flat")
     mflat = means.copy()
     mflat[:, 2] = np.float32(0.1)
-    flat = raster.forward_async(t(mflat), *args[1:], **kw, pairs_cap=8 * P, ws=ws)
+    view0, full0, campos0, tx0, ty0 = _camera(W, H, 0.9, yaw=0.0)
+    flat = raster.forward_async(t(mflat), args[1], t(view0), t(full0), t(campos0), args[5], H, W, tx0, ty0, **kw,
+                                pairs_cap=64 * P, ws=ws)
     assert flat.result()[1] & 1
     # no Gaussians: the background
     empty = raster.forward_async(t(np.zeros((0, 3), np.float32)), t(np.zeros((0, 1), np.float32)), *args[2:],

@@ -11,14 +11,18 @@
 //   bank0        n = 32 l                             (every lane on banks 0-1: the worst case)
 //   same         n = 0                                (one address)
 //   pairs        n = l / 2                            (two lanes per address)
+//   group0       n = l, lanes 0..15 active only       (are idle lane groups free?)
+//   half         n = l, lanes with l % 16 < 8 active  (half of every group)
+// The reads are inline-asm ds_read_b128 in batches of 8 behind one
+// lgkmcnt wait (a plain C++ load was hoisted out of the loop).
 // Build: hipcc -O3 --offload-arch=gfx950 lds_banks.hip -o lds_banks
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <vector>
 
 constexpr int ITERS = 4096;
-enum Pat { DISTINCT = 0, RES16, RES32, RES16X, BANK0, SAME, PAIRS, NPAT };
-static const char* kName[NPAT] = {"distinct", "res16", "res32", "res16x", "bank0", "same", "pairs"};
+enum Pat { DISTINCT = 0, RES16, RES32, RES16X, BANK0, SAME, PAIRS, GROUP0, HALF, NPAT };
+static const char* kName[NPAT] = {"distinct", "res16", "res32", "res16x", "bank0", "same", "pairs", "group0", "half"};
 
 __device__ __forceinline__ unsigned node_of(int pat, unsigned l) {
   switch (pat) {
@@ -32,7 +36,8 @@ __device__ __forceinline__ unsigned node_of(int pat, unsigned l) {
     }
     case BANK0: return 32 * l;
     case SAME: return 0;
-    default: return l / 2;
+    case PAIRS: return l / 2;
+    default: return l;
   }
 }
 
@@ -41,19 +46,35 @@ __global__ __launch_bounds__(256) void kern(int pat, unsigned long long* out, fl
   __shared__ __attribute__((aligned(16))) unsigned long long s[4096];  // 32 KB
   for (int i = threadIdx.x; i < 4096; i += 256) s[i] = 0ull;
   __syncthreads();
-  const unsigned n = node_of(pat, threadIdx.x & 63) & 2047u;
+  const unsigned l = threadIdx.x & 63;
+  const unsigned n = node_of(pat, l) & 2047u;
+  const bool on = pat == GROUP0 ? l < 16 : pat == HALF ? (l % 16) < 8 : true;
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   unsigned long long t0 = __builtin_amdgcn_s_memtime();
-  for (int it = 0; it < ITERS; ++it) {
-    const unsigned sh = (unsigned)(it & 7) * 128u;
+  if (on) {
     if constexpr (OP == 0) {
-      __hip_atomic_fetch_add(&s[(n + sh) & 2047u], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      for (int it = 0; it < ITERS; ++it) {
+        const unsigned sh = (unsigned)(it & 7) * 128u;
+        __hip_atomic_fetch_add(&s[(n + sh) & 2047u], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
     } else {
-      const float4 v = reinterpret_cast<const float4*>(s)[(n + sh) & 2047u];
-      acc.x += v.x;
-      acc.y += v.y;
-      acc.z += v.z;
-      acc.w += v.w;
+      const unsigned base = (unsigned)(uintptr_t)s;  // LDS byte address
+      for (int it = 0; it < ITERS; it += 8) {
+        float4 v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const unsigned a = base + 16u * ((n + (unsigned)u * 128u) & 2047u);
+          asm volatile("ds_read_b128 %0, %1" : "=v"(v[u]) : "v"(a));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          acc.x += v[u].x;
+          acc.y += v[u].y;
+          acc.z += v[u].z;
+          acc.w += v[u].w;
+        }
+      }
     }
   }
   __syncthreads();
