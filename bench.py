@@ -990,12 +990,26 @@ def main():
         frame()
     flush()
     barrier()
+    # k_render's and the whole forward's in-frame times: three events per
+    # forward on its own stream (gsmpm_raster_set_timing), read after the
+    # timed region; no host wait is added inside it
+    time_render = not args.no_render and rank == 0
+    if time_render:
+        raster.timing()
+        raster.set_timing(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         frame()
     flush()
     barrier()
     elapsed = time.perf_counter() - t0
+    render_in_frame = None
+    if time_render:
+        raster.set_timing(False)
+        kr_ms, fw_ms, n_fw = raster.timing()
+        if n_fw:
+            render_in_frame = {"forwards": n_fw, "k_render_ms": round(kr_ms / n_fw, 4),
+                               "forward_ms": round(fw_ms / n_fw, 4)}
     if rq is not None:  # the render worker's last frame is done (flush): stop it
         rq.put(None)
         worker.join()
@@ -1111,6 +1125,8 @@ def main():
         "render_ms_per_frame": render_ms,
         "render_host_ms_per_frame": render_host_ms,
         "render_default_stream_first_ms": render_cold_ms,
+        # per forward of the timed frames, on the render's stream beside the simulator
+        "render_in_frame": render_in_frame,
         "num_rendered": state["K"],
     }
     if kern is not None:

@@ -1465,6 +1465,15 @@ struct gsmpm_mpm {
   int fep = 0;                            // escape flag the next P2G raises
   int rebin_interval = 10;                // substeps between re-binnings (fused pipeline; set by material at create)
   std::map<std::vector<uint32_t>, hipGraphExec_t> graphs;
+  // a second instance of each (non-slab) graph, launched on alternate calls:
+  // a relaunch of the same hipGraphExec_t waits on the host until its previous
+  // launch has completed (its kernel arguments are rewritten), so with one
+  // instance the next frame's graph only reached the queue after the last
+  // frame's had drained (~100 us of idle GPU per lego frame in the bench's
+  // kernel trace); GSMPM_GRAPH_COPIES=1 keeps one (A/B)
+  std::map<std::vector<uint32_t>, hipGraphExec_t> graphs_alt;
+  std::map<std::vector<uint32_t>, int> graph_turn;
+  int graph_copies = 2;
   std::map<std::vector<uint32_t>, int> graph_box_parity;
   struct FState {
     int bpar, ep;
@@ -1884,7 +1893,10 @@ static int launch_substeps_f(gsmpm_mpm* h, float dt, int nsub, const uint32_t* b
 
 static void drop_graphs(gsmpm_mpm* h) {
   for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
+  for (auto& kv : h->graphs_alt) (void)hipGraphExecDestroy(kv.second);
   h->graphs.clear();
+  h->graphs_alt.clear();
+  h->graph_turn.clear();
   h->graph_box_parity.clear();
   h->graph_fstate.clear();
 }
@@ -2074,20 +2086,32 @@ static int graph_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc, 
       set_error(std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
       return GSMPM_EHIP;
     }
-    hipGraphExec_t exec;
+    hipGraphExec_t exec, exec2 = nullptr;
     e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
     gtrace(e == hipSuccess ? "instantiated" : "instantiate FAILED");
+    if (e == hipSuccess && !h->slab && h->graph_copies > 1) {
+      e = hipGraphInstantiate(&exec2, graph, nullptr, nullptr, 0);
+      if (e != hipSuccess) (void)hipGraphExecDestroy(exec);
+    }
     (void)hipGraphDestroy(graph);
     if (e != hipSuccess) {
       set_error(std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
       return GSMPM_EHIP;
     }
     it = h->graphs.emplace(key, exec).first;
+    if (exec2) h->graphs_alt.emplace(key, exec2);
     h->graph_box_parity[key] = parity;
     h->graph_fstate[key] = end;
   }
   gtrace("launch");
-  GSMPM_HIP(hipGraphLaunch(it->second, st));
+  hipGraphExec_t run = it->second;
+  auto alt = h->graphs_alt.find(key);
+  if (alt != h->graphs_alt.end()) {
+    int& turn = h->graph_turn[key];
+    if (turn) run = alt->second;
+    turn ^= 1;
+  }
+  GSMPM_HIP(hipGraphLaunch(run, st));
   gtrace("launched");
   h->cur_box = h->graph_box_parity[key];
   const gsmpm_mpm::FState& fs = h->graph_fstate[key];
@@ -2176,6 +2200,7 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
   // fused pipeline: 8 x 8 x 7-cell tiles (fused.h)
   h->fused = !(prm->flags & (GSMPM_FLAG_PHASED | GSMPM_FLAG_KEEP_GRID));
   if (const char* lb = std::getenv("GSMPM_LANE_BALANCE")) h->lane_balance = lb[0] != '0';
+  if (const char* gc = std::getenv("GSMPM_GRAPH_COPIES")) h->graph_copies = std::max(1, std::atoi(gc));
   if (const char* fp = std::getenv("GSMPM_FUSE_PERMUTE")) h->fuse_permute = fp[0] != '0';
   if (const char* cr = std::getenv("GSMPM_COVER_RECORDS")) h->cover_records = cr[0] != '0';
   {

@@ -48,6 +48,8 @@
 
 #include <chrono>
 #include <cstdlib>
+#include <mutex>
+#include <vector>
 #include <cstring>
 #include <string>
 
@@ -2020,6 +2022,85 @@ int gsmpm_raster_destroy(gsmpm_raster* r) {
   return GSMPM_OK;
 }
 
+// In-frame timing of the forwards (gsmpm_raster_set_timing): three events per
+// forward on its own stream -- at entry, before and after k_render -- so a
+// caller can read what k_render and the whole forward took inside a running
+// frame loop (beside the simulator) without a host wait in the loop.
+// Forwards issued while their stream is being captured are not timed.
+namespace {
+struct FwdTiming {
+  hipEvent_t e[3];
+};
+std::mutex g_tm_mu;
+bool g_tm_on = false;
+std::vector<FwdTiming> g_tm_pending, g_tm_free;
+struct TimingGuard {
+  FwdTiming t{};
+  bool on = false, done = false;
+  hipStream_t st = nullptr;
+  explicit TimingGuard(hipStream_t s) : st(s) {
+    {
+      std::lock_guard<std::mutex> lk(g_tm_mu);
+      if (!g_tm_on) return;
+      hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+      if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+      if (!g_tm_free.empty()) {
+        t = g_tm_free.back();
+        g_tm_free.pop_back();
+      } else {
+        for (auto& e : t.e)
+          if (hipEventCreate(&e) != hipSuccess) return;
+      }
+    }
+    on = hipEventRecord(t.e[0], st) == hipSuccess;
+  }
+  void mark(int i) {
+    if (on) on = hipEventRecord(t.e[i], st) == hipSuccess;
+    if (on && i == 2) done = true;
+  }
+  ~TimingGuard() {
+    if (t.e[0] == nullptr) return;
+    std::lock_guard<std::mutex> lk(g_tm_mu);
+    (done ? g_tm_pending : g_tm_free).push_back(t);
+  }
+};
+}  // namespace
+
+int gsmpm_raster_set_timing(int32_t on) {
+  std::lock_guard<std::mutex> lk(g_tm_mu);
+  g_tm_on = on != 0;
+  return GSMPM_OK;
+}
+
+int gsmpm_raster_timing(double* k_render_ms, double* forward_ms, int64_t* forwards) {
+  GSMPM_REQUIRE(k_render_ms && forward_ms && forwards, "gsmpm_raster_timing: null argument");
+  std::vector<FwdTiming> got;
+  {
+    std::lock_guard<std::mutex> lk(g_tm_mu);
+    got.swap(g_tm_pending);
+  }
+  double kr = 0.0, fw = 0.0;
+  int rc = GSMPM_OK;
+  for (auto& t : got) {
+    float a = 0.f, b = 0.f;
+    if (rc == GSMPM_OK && (hipEventSynchronize(t.e[2]) != hipSuccess || hipEventElapsedTime(&a, t.e[1], t.e[2]) != hipSuccess ||
+                           hipEventElapsedTime(&b, t.e[0], t.e[2]) != hipSuccess)) {
+      set_error("gsmpm_raster_timing: event query failed");
+      rc = GSMPM_EHIP;
+    }
+    kr += a;
+    fw += b;
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_tm_mu);
+    for (auto& t : got) g_tm_free.push_back(t);
+  }
+  *k_render_ms = kr;
+  *forward_ms = fw;
+  *forwards = (int64_t)got.size();
+  return rc;
+}
+
 int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* out_color, int32_t* out_radii,
                          int32_t* num_rendered, void* stream) {
   GSMPM_REQUIRE(r && in && out_color && out_radii, "gsmpm_raster_forward: null argument");
@@ -2035,6 +2116,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
                 "gsmpm_raster_forward: too few SH coefficients for sh_degree");
   GSMPM_REQUIRE(!in->prefiltered, "gsmpm_raster_forward: prefiltered=True is not supported (upstream traps too)");
   hipStream_t st = (hipStream_t)stream;
+  TimingGuard tmg(st);
   RasterDev a;
   a.P = in->P;
   a.D = in->D;
@@ -2510,6 +2592,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
   // (A/B: a render overlapping the simulator holds fewer of the CU slots its one-round launches need)
   if (const char* rw = std::getenv("GSMPM_RASTER_RENDER_WGS"))
     if (xcd && std::atoi(rw) >= 8) rgrid = dim3((unsigned)std::min(nq, std::atoi(rw) & ~7));
+  tmg.mark(1);
   if (!(ts && ts[0] == '1'))
     hipLaunchKernelGGL(k_render, rgrid, dim3(64), 0, st, r->ranges, r->ids_sorted, a.W, a.H, a.grid_x, r->xy, r->conic,
                        r->rgb, in->bg, out_color, r->forward_only ? nullptr : r->final_T,
@@ -2518,6 +2601,7 @@ int gsmpm_raster_forward(gsmpm_raster* r, const gsmpm_raster_args* in, float* ou
     hipLaunchKernelGGL(k_render4, dim3(a.grid_x, a.grid_y), dim3(256), 0, st, r->ranges, r->ids_sorted, a.W, a.H,
                        a.grid_x, r->xy, r->conic, r->rgb, in->bg, out_color, r->forward_only ? nullptr : r->final_T,
                        r->forward_only ? nullptr : r->n_contrib, tkeys, render_mode);
+  tmg.mark(2);
   r->has_pixel_state = !r->forward_only;
   GSMPM_LAUNCH_CHECK();
   if (num_rendered) *num_rendered = r->async_cap > 0 ? -1 : (int32_t)K_full;

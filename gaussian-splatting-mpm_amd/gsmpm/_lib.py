@@ -154,6 +154,9 @@ _SIGS = {
                                                ctypes.POINTER(ctypes.c_int64), c_void_p]),
     "gsmpm_raster_forward_async": (ctypes.c_int, [ctypes.POINTER(RasterArgs), c_void_p, c_void_p, c_void_p,
                                                   ctypes.c_uint64, ctypes.c_int64, c_void_p, c_void_p]),
+    "gsmpm_raster_set_timing": (ctypes.c_int, [ctypes.c_int32]),
+    "gsmpm_raster_timing": (ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(ctypes.c_int64)]),
 }
 GSMPM_OK, GSMPM_EINVAL, GSMPM_EHIP, GSMPM_ESTATE = 0, -1, -2, -3
 ESPACE = GSMPM_ESPACE = -4  # a caller-owned workspace is too small

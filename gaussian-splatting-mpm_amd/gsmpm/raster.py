@@ -300,6 +300,20 @@ def forward_async(means3D, opacities, viewmatrix, projmatrix, campos, bg, image_
     return AsyncRender(color, radii, counts, ev, (a, keep))
 
 
+def set_timing(on):
+    """gsmpm_raster_set_timing: record k_render's and each forward's in-stream
+    time from now on (process-wide; forwards under a stream capture excluded)."""
+    check(LIB.gsmpm_raster_set_timing(1 if on else 0), "set_timing")
+
+
+def timing():
+    """gsmpm_raster_timing: (k_render ms, whole forward ms, forwards) summed
+    over the forwards recorded since the last call (waits for them)."""
+    kr, fw, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+    check(LIB.gsmpm_raster_timing(ctypes.byref(kr), ctypes.byref(fw), ctypes.byref(n)), "timing")
+    return kr.value, fw.value, n.value
+
+
 def mark_visible(positions, viewmatrix, projmatrix):
     positions = _f32(positions)
     P = positions.shape[0]

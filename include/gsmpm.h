@@ -461,6 +461,16 @@ int gsmpm_raster_forward_ws(const gsmpm_raster_args* a, float* out_color, int32_
  * A/B switch that selects another path: GSMPM_EINVAL. */
 int gsmpm_raster_forward_async(const gsmpm_raster_args* a, float* out_color, int32_t* out_radii, void* workspace,
                                uint64_t ws_bytes, int64_t pairs_cap, uint32_t* counts, void* stream);
+
+/* In-frame timing of the forwards (diagnostics; process-wide).  With timing
+ * on, every forward not issued into a stream capture records three events on
+ * its stream (entry, before and after k_render); gsmpm_raster_timing waits
+ * for the forwards recorded since the last call and returns the sums of
+ * their k_render and whole-forward times (ms) and their count.  Replaces
+ * nothing in the reference (upstream has no timing); bench.py reports
+ * k_render's in-frame average with it. */
+int gsmpm_raster_set_timing(int32_t on);
+int gsmpm_raster_timing(double* k_render_ms, double* forward_ms, int64_t* forwards);
 /* Diagnostics of the context's last forward: *binned = the (Gaussian, tile)
  * pairs actually sorted and listed (each Gaussian binned into the tiles its
  * alpha >= 1/255 box reaches, a subset of the 3-sigma rect), *rendered = its

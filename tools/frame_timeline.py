@@ -48,6 +48,28 @@ def main(path):
     if ov and alone:
         print(f"k_fused<0,3>: {len(alone)} launches alone, mean {sum(alone) / len(alone) / 1e3:.2f} us; "
               f"{len(ov)} beside a render kernel, mean {sum(ov) / len(ov) / 1e3:.2f} us")
+        # per render kernel: the k_fused / k_grid_f launches it overlapped and their extra time
+        base = {"k_fused<0, 3>": sum(alone) / len(alone)}
+        g_alone = [b - a for a, b, n, k in win if "k_grid_f" in n and not any(c < b and d > a for c, d in rend)]
+        if g_alone:
+            base["k_grid_f"] = sum(g_alone) / len(g_alone)
+        short = lambda n: n.split("(")[0].replace("gsmpm::", "").replace("void ", "")
+        per = {}
+        for c, d, rn, rk in win:
+            if rk != "render":
+                continue
+            e = per.setdefault(short(rn), {"launches": 0, "us": 0.0, "sim_overlapped": 0, "sim_extra_us": 0.0})
+            e["launches"] += 1
+            e["us"] += (d - c) / 1e3
+            for a, b, n, k in win:
+                sn = next((x for x in base if x in n), None)
+                if sn and c < b and d > a:
+                    e["sim_overlapped"] += 1
+                    e["sim_extra_us"] += (b - a - base[sn]) / 1e3
+        print("per render kernel, 3 frames: launches, own time, sim launches beside it, their extra time "
+              "over the alone mean (a sim launch beside two render kernels counts for both)")
+        for nm, e in sorted(per.items(), key=lambda kv: -kv[1]["sim_extra_us"]):
+            print(f"  {nm:<22} {e['launches']:3d}  {e['us']:8.1f} us  {e['sim_overlapped']:4d}  {e['sim_extra_us']:8.1f} us")
     # idle: gaps in the union of all kernel intervals
     busy, cur_a, cur_b = 0, None, None
     for a, b, n, k in win:
