@@ -92,14 +92,10 @@ __device__ __forceinline__ bool slab_tile_in_window(const SlabWin& sw, int ti) {
 }
 
 // per-particle checks of k_fused: the slab drift check (base plane allowed in
-// [xlo, xhi)) and the non-finite check (a NaN / Inf position sets
-// *nonfin, which the step call reports as GSMPM_ESTATE; without it a
-// non-finite particle is silently binned "outside" and scatters nowhere)
-struct SlabK {
-  int xlo, xhi;
-  int* drift;
-  int* nonfin;
-};
+// [xlo, xhi), else *FusedRare::drift) and the non-finite check (a
+// NaN / Inf position sets *FusedRare::nonfin, which the step call reports as
+// GSMPM_ESTATE; without it a non-finite particle is silently binned
+// "outside" and scatters nowhere)
 __device__ __forceinline__ bool finite3(const float (&x)[3]) {
   return __builtin_isfinite(x[0]) && __builtin_isfinite(x[1]) && __builtin_isfinite(x[2]);
 }
@@ -116,6 +112,32 @@ struct BinOutF {
   int* pslot;  // [n]
   int* tflag;  // [ntiles] (zeroed with count)
   FTiles tl;
+};
+
+// Arguments of k_fused that only rare paths use -- the re-binning launches'
+// outputs, the escape path, impulses, tiles appended during the launch, the
+// error flags, the once-a-chunk box publishing -- read through one pointer
+// where they are used.  As kernel arguments they made ~150 dwords against
+// 102 SGPRs, and the compiler kept 89 SGPRs spilled to VGPR lanes (348
+// v_readlane restores in the code); now 38 (69).  k_fused's time did not
+// move (5 interleaved rounds: 16.07 against 16.11 us steady), the same
+// change to k_grid_f did (its slab-free form below).  One per (bins parity,
+// escape flag) in device memory (mpm.hip sync_rare).
+struct FusedRare {
+  BinOutF bo;          // re-binning outputs (bins parity c ^ 1)
+  float4* gacc;        // escape accumulator
+  int* esc;            // escape flag this launch raises
+  int* drift;          // slab: a particle past the margin (unused outside slabs)
+  int* nonfin;         // non-finite state word
+  const void* bct;     // const BcTable* (impulses)
+  int* tflag;          // Touch members of add_lower_tiles (bins parity c)
+  int* touched;
+  int* nchunk;
+  int4* chunk;
+  int2* rcov;
+  int* tbox;           // Touch's per-chunk box publishing (once a chunk: a scalar load, not a live SGPR)
+  const int* tpos;
+  int* rbox;
 };
 
 __device__ __forceinline__ void ftile_decode(const FTiles& tl, int t, int& tx, int& ty, int& tz) {
@@ -306,11 +328,10 @@ constexpr bool kG2pB128 = GSMPM_G2P_B128 != 0;
 #endif
 constexpr bool kBinAgg = GSMPM_BIN_AGG != 0;
 template <int MAT, int MODE>
-__global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTiles tl, ChunkIn ck, Touch tc, BinOutF bo,
-                                               int bin, int use_box, const float4* __restrict__ gvel,
-                                               const BcTable* __restrict__ bct, uint32_t mask, float dt, MatConsts mc,
-                                               float4* __restrict__ slots, float4* __restrict__ gacc,
-                                               int* __restrict__ esc, SlabK sk) {
+__global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTiles tl, ChunkIn ck, Touch tc, int bin,
+                                               int use_box, const float4* __restrict__ gvel, uint32_t mask, float dt,
+                                               MatConsts mc, float4* __restrict__ slots, int xlo, int xhi,
+                                               const FusedRare* __restrict__ rare) {
   constexpr bool G2P = (MODE & 1) != 0, P2G = (MODE & 2) != 0;
   // channel-planar u64 accumulators; the G2P v window aliases them (it is
   // consumed before the accumulators are zeroed)
@@ -353,10 +374,11 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
     // record takes this chunk's stencil box as its neighbour e (published after
     // the P2G below); requested now, used at the end
     int tpos_e = -1;
-    if (tc.tpos && !outside && k < 27) {
+    const int* __restrict__ tposp = rare->tpos;
+    if (tposp && !outside && k < 27) {
       const int x0 = tx - (k / 9 - 1), y0 = ty - ((k / 3) % 3 - 1), z0 = tz - (k % 3 - 1);
       if ((unsigned)x0 < (unsigned)tl.td0 && (unsigned)y0 < (unsigned)tl.td1 && (unsigned)z0 < (unsigned)tl.td2)
-        tpos_e = tc.tpos[(x0 * tl.td1 + y0) * tl.td2 + z0];
+        tpos_e = tposp[(x0 * tl.td1 + y0) * tl.td2 + z0];
     }
     int p = -1;
     float x[3] = {0.f, 0.f, 0.f}, v[3] = {0.f, 0.f, 0.f}, C[3][3], F[3][3], m = 0.f;
@@ -448,7 +470,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
           x[d] = x[d] + dt * v[d];
           ps.st(PX + d, p, x[d]);
         }
-        if (!finite3(x)) *sk.nonfin = 1;
+        if (!finite3(x)) *rare->nonfin = 1;
 #pragma unroll
         for (int i = 0; i < 9; ++i) {
           if (!P2G || GSMPM_STORE_VC) ps.st(PC + i, p, C[i / 3][i % 3]);
@@ -495,11 +517,12 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
           const int c = s_cnt[k];
           if (c > 0) {
             const int ntile = ((tx + k / 9 - 1) * tl.td1 + (ty + (k / 3) % 3 - 1)) * tl.td2 + (tz + k % 3 - 1);
-            s_base[k] = reserve_f(bo, ntile, c);
+            s_base[k] = reserve_f(rare->bo, ntile, c);
           }
         }
         __syncthreads();
         if (p >= 0) {
+          const BinOutF bo = rare->bo;
           bo.ptile[p] = nt;
           bo.pslot[p] = code >= 0 ? s_base[code] + lslot : reserve_f(bo, nt, 1);
         }
@@ -520,6 +543,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
       if (k < cnt) {
         // ImpulseBC.apply (boundary_conditions.py:41-45); the kicked v lives in registers only
         if (mask) {
+          const BcTable* __restrict__ bct = static_cast<const BcTable*>(rare->bct);
           const int ni = bct->n_imp;
           for (int b = 0; b < ni; ++b) {
             const Impulse& im = bct->imp[b];
@@ -564,7 +588,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
 #pragma unroll
             for (int i = 0; i < 9; ++i) chk += C[i / 3][i % 3];
           }
-          if (!__builtin_isfinite(chk)) *sk.nonfin = 1;
+          if (!__builtin_isfinite(chk)) *rare->nonfin = 1;
         }
         float vm = 0.f, cm = 0.f, sm = 0.f;
 #pragma unroll
@@ -580,8 +604,8 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
       }
       if (outside) {
         // chunk of particles binned outside the grid: bounds-checked global path
-        if (k < cnt) p2g_global<MAT>(x, v, C, m, nvt, g, dt, gacc);
-        if (k == 0 && cnt > 0) *esc = 1;
+        if (k < cnt) p2g_global<MAT>(x, v, C, m, nvt, g, dt, rare->gacc);
+        if (k == 0 && cnt > 0) *rare->esc = 1;
         // the next launch on these bins reads this chunk's lane order too: the
         // identity (round 4 left it unwritten, so a lane of the next G2P took a
         // stale row -- another chunk's particle, or one past the live rows)
@@ -593,7 +617,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
       base_of(x, g.inv_dx, b);
       const bool win = k < cnt && in_grid(x, g) && in_window(b, o0, o1, o2);
       // slab: a particle past the margin scatters where no window exchange reaches (slab.h)
-      if (k < cnt && (b[0] < sk.xlo || b[0] >= sk.xhi)) *sk.drift = 1;
+      if (k < cnt && (b[0] < xlo || b[0] >= xhi)) *rare->drift = 1;
       // window coordinates covered by this particle's stencil, as per-axis bit masks
       int mxy = win ? (7 << (b[0] - o0)) | (7 << (16 + b[1] - o1)) : 0;
       int mz = win ? 7 << (b[2] - o2) : 0;
@@ -627,8 +651,13 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
       // axes on which some stencil reaches below the tile (window coordinate 0)
       const int lo_all = (Mx & 1) | ((My & 1) << 1) | ((Mz & 1) << 2);
       if (lo_all & ~cr.w) {  // workgroup-uniform; rare (a new axis since the binning)
-        add_lower_tiles(tc, tl, tx, ty, tz, (lo_all | cr.w) & 7);
-        if (k == 0) tc.chunk[w].w = lo_all | cr.w;
+        Touch tr = tc;
+        tr.tflag = rare->tflag;
+        tr.touched = rare->touched;
+        tr.nchunk = rare->nchunk;
+        tr.rcov = rare->rcov;
+        add_lower_tiles(tr, tl, tx, ty, tz, (lo_all | cr.w) & 7);
+        if (k == 0) rare->chunk[w].w = lo_all | cr.w;
       }
       // stencil box of the chunk (empty chunk window: a 1-node box)
       int box = kFullBox;
@@ -639,9 +668,9 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
         box = 0;
       if (k == 0) {
         tc.cbox[w] = box;
-        tc.tbox[t] = (cr.w & 8) ? kFullBox : box;  // tiles with several chunks: whole windows
+        rare->tbox[t] = (cr.w & 8) ? kFullBox : box;  // tiles with several chunks: whole windows
       }
-      if (tpos_e >= 0) tc.rbox[(size_t)tpos_e * kRecStride + k] = (cr.w & 8) ? kFullBox : box;
+      if (tpos_e >= 0) rare->rbox[(size_t)tpos_e * kRecStride + k] = (cr.w & 8) ? kFullBox : box;
       if (cr.w & 8) box = kFullBox;
       if constexpr (kZeroBox) {  // only the nodes the scatter can reach and the store reads
         int lo[3], hi[3];
@@ -669,8 +698,8 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
           p2g_scatter<MAT, kFW1, kFW2, kFWin>(s_acc + ((b[0] - o0) * kFW1 + (b[1] - o1)) * kFW2 + (b[2] - o2), fx, ww,
                                               dw, v, C, m, nvt, g, dt, ldexp(1.0, S));
         } else {
-          p2g_global<MAT>(x, v, C, m, nvt, g, dt, gacc);
-          *esc = 1;
+          p2g_global<MAT>(x, v, C, m, nvt, g, dt, rare->gacc);
+          *rare->esc = 1;
         }
       }
       __syncthreads();
@@ -691,7 +720,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
           const int ix = o0 + wa, iy = o1 + wb, iz = o2 + wc;
           const float val = from_fixed32(s_acc[ch * kFWin + node], S);
           if (val != 0.f && (unsigned)ix < (unsigned)ng && (unsigned)iy < (unsigned)ng && (unsigned)iz < (unsigned)ng)
-            unsafeAtomicAdd(reinterpret_cast<float*>(gacc + (((size_t)ix * ng + iy) * ng + iz)) + ch, val);
+            unsafeAtomicAdd(reinterpret_cast<float*>(rare->gacc + (((size_t)ix * ng + iy) * ng + iz)) + ch, val);
         }
       } else {
         int lo[3], hi[3];
@@ -840,6 +869,13 @@ constexpr bool kGridSkip0 = GSMPM_GRID_SKIP0 != 0;
 #define GSMPM_GVEL_STORE 0
 #endif
 constexpr int kGvelStore = GSMPM_GVEL_STORE;
+// SLAB: a slab rank's grid pass (SlabWin hooks); the single-domain form is
+// compiled without them -- their ~20 argument dwords pushed the kernel past
+// the SGPR budget: 21 spilled SGPRs (21 v_writelane at the start, 26
+// v_readlane restores, ~13 % of the ~350 VALU instructions a wave issues)
+// against 4 now; k_grid_f 12.06 -> 11.67 us in the lego frame (5
+// interleaved rounds, profiles/r05/ab/ab_rare_args_pk_r05k.txt)
+template <bool SLAB>
 __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_grid_f(GridDims g, FTiles tl, ChunkIn ck, const int* __restrict__ tbox,
                                                     const float4* __restrict__ slots, float4* __restrict__ gacc,
                                                     float4* __restrict__ gvel, const BcTable* __restrict__ bct,
@@ -851,8 +887,9 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
   // a slab's grid update runs as two passes (window tiles first, so their
   // partials can travel while the rest updates): the flag and the zeroing go
   // with the second
-  if (blockIdx.x == 0 && threadIdx.x == 0 && sw.pass != 1) *esc_clear = 0;
-  if (zc && sw.pass != 1) {
+  const int pass = SLAB ? sw.pass : 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && pass != 1) *esc_clear = 0;
+  if (zc && pass != 1) {
     for (int t = blockIdx.x * blockDim.x + threadIdx.x; t <= tl.ntiles; t += gridDim.x * blockDim.x) {
       zc[t] = 0;
       if (t < tl.ntiles) zf[t] = 0;
@@ -884,7 +921,7 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     if ((unsigned)T >= (unsigned)tl.ntiles) continue;  // workgroup-uniform; never taken (wt < parts x count)
     int ti, tj, tk;
     ftile_decode(tl, T, ti, tj, tk);
-    if (sw.pass != 0 && slab_tile_in_window(sw, ti) != (sw.pass == 1)) continue;  // workgroup-uniform
+    if (SLAB && pass != 0 && slab_tile_in_window(sw, ti) != (pass == 1)) continue;  // workgroup-uniform
     if constexpr (!kAtomicGrid) {
       __syncthreads();  // readers of the previous tile's ranges are done
       if (wt == (int)blockIdx.x) stamp(3, 2);
@@ -935,7 +972,7 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
           gacc[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
       }
-      const int sww = sw.W ? slab_window_of(sw, i) : -1;
+      const int sww = (SLAB && sw.W) ? slab_window_of(sw, i) : -1;
       const bool inrect = sww >= 0 && (unsigned)(j - sw.y0[sww]) < (unsigned)sw.ny[sww] &&
                           (unsigned)(k - sw.z0[sww]) < (unsigned)sw.nz[sww];
       if (sww >= 0 && !inrect && a.w != 0.f) *sw.oob = 1;

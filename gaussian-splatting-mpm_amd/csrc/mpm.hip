@@ -289,11 +289,83 @@ __device__ __forceinline__ void lds_add(unsigned long long* a, unsigned long lon
 // per-axis weights, collapses to two FMAs per component per node.  Same
 // quantities as the reference's per-node expression, different rounding (a
 // few ulp).
+// GSMPM_P2G_PK=1 (A/B): components 0 and 1 of the momentum and stress terms
+// as packed f32 pairs (v_pk_fma_f32 / v_pk_mul_f32: the same IEEE operation
+// per element, two per instruction), component 2 scalar -- the same values
+// bit for bit as the scalar form.  Measured slower (5 interleaved rounds,
+// profiles/r05/ab/ab_rare_args_pk_r05k.txt): k_fused 16.68 against 16.07 us
+// steady, sim 3.095 against 3.075 ms/frame -- the pairs have to be built
+// (v_mov into aligned register pairs) and the scatter is not issue-bound
+#ifndef GSMPM_P2G_PK
+#define GSMPM_P2G_PK 0
+#endif
+typedef float pkf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pkf2 pk2(float a, float b) { return pkf2{a, b}; }
+__device__ __forceinline__ pkf2 pk_fma(pkf2 a, pkf2 b, pkf2 c) { return __builtin_elementwise_fma(a, b, c); }
+
 template <int MAT, int WY = kTW, int WZ = kTW, int WN = kWin>
 __device__ __forceinline__ void p2g_scatter(unsigned long long* cell0, const float (&fx)[3], const float (&w)[3][3],
                                             const float (&dw)[3][3], const float (&v)[3], const float (&C)[3][3],
                                             float m, const float (&nvt)[3][3], const GridDims& g, float dt,
                                             double scale) {
+#if GSMPM_P2G_PK
+  float dd[3][3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c)
+#pragma unroll
+    for (int o = 0; o < 3; ++o) dd[c][o] = ((float)o - fx[c]) * g.dx;
+  const pkf2 C0 = pk2(C[0][0], C[1][0]), C1 = pk2(C[0][1], C[1][1]), C2 = pk2(C[0][2], C[1][2]);
+  const pkf2 v01 = pk2(v[0], v[1]);
+  pkf2 G0 = pk2(0.f, 0.f), G1 = G0, G2 = G0;  // dt * inv_dx * nvt, rows 0 and 1
+  float g20 = 0.f, g21 = 0.f, g22 = 0.f;       // row 2
+  if constexpr (MAT != 0) {
+    const float f = dt * g.inv_dx;
+    G0 = pk2(f * nvt[0][0], f * nvt[1][0]);
+    G1 = pk2(f * nvt[0][1], f * nvt[1][1]);
+    G2 = pk2(f * nvt[0][2], f * nvt[1][2]);
+    g20 = f * nvt[2][0];
+    g21 = f * nvt[2][1];
+    g22 = f * nvt[2][2];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const pkf2 qi = pk_fma(C0, pk2(dd[0][i], dd[0][i]), v01);
+    const float qi2 = __builtin_fmaf(C[2][0], dd[0][i], v[2]);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const pkf2 qij = pk_fma(C1, pk2(dd[1][j], dd[1][j]), qi);
+      const float qij2 = __builtin_fmaf(C[2][1], dd[1][j], qi2);
+      const float wij = w[0][i] * w[1][j];
+      const float mij = wij * m;
+      pkf2 sa = pk2(0.f, 0.f), sc = sa;
+      float sa2 = 0.f, sc2 = 0.f;
+      if constexpr (MAT != 0) {
+        const float a0 = dw[0][i] * w[1][j], a1 = w[0][i] * dw[1][j];
+        sa = pk_fma(G0, pk2(a0, a0), G1 * pk2(a1, a1));
+        sc = G2 * pk2(wij, wij);
+        sa2 = __builtin_fmaf(g20, a0, g21 * a1);
+        sc2 = g22 * wij;
+      }
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const float wm = mij * w[2][k];
+        const pkf2 q = pk_fma(C2, pk2(dd[2][k], dd[2][k]), qij);
+        const float q2 = __builtin_fmaf(C[2][2], dd[2][k], qij2);
+        pkf2 add = pk2(wm, wm) * q;
+        float add2 = wm * q2;
+        if constexpr (MAT != 0) {
+          add = pk_fma(sa, pk2(w[2][k], w[2][k]), pk_fma(sc, pk2(dw[2][k], dw[2][k]), add));
+          add2 = __builtin_fmaf(sa2, w[2][k], __builtin_fmaf(sc2, dw[2][k], add2));
+        }
+        unsigned long long* cell = cell0 + (i * WY + j) * WZ + k;
+        lds_add(cell + 0 * WN, to_fixed(add.x, scale));
+        lds_add(cell + 1 * WN, to_fixed(add.y, scale));
+        lds_add(cell + 2 * WN, to_fixed(add2, scale));
+        lds_add(cell + 3 * WN, to_fixed(wm, scale));
+      }
+    }
+  }
+#else
   float dd[3][3];
 #pragma unroll
   for (int c = 0; c < 3; ++c)
@@ -344,6 +416,7 @@ __device__ __forceinline__ void p2g_scatter(unsigned long long* cell0, const flo
       }
     }
   }
+#endif
 }
 
 template <int MAT>
@@ -1465,15 +1538,16 @@ struct gsmpm_mpm {
   int fep = 0;                            // escape flag the next P2G raises
   int rebin_interval = 10;                // substeps between re-binnings (fused pipeline; set by material at create)
   std::map<std::vector<uint32_t>, hipGraphExec_t> graphs;
-  // a second instance of each (non-slab) graph, launched on alternate calls:
-  // a relaunch of the same hipGraphExec_t waits on the host until its previous
-  // launch has completed (its kernel arguments are rewritten), so with one
-  // instance the next frame's graph only reached the queue after the last
-  // frame's had drained (~100 us of idle GPU per lego frame in the bench's
-  // kernel trace); GSMPM_GRAPH_COPIES=1 keeps one (A/B)
+  // GSMPM_GRAPH_COPIES=2 (A/B): a second instance of each (non-slab) graph,
+  // launched on alternate calls.  Under rocprofv3's kernel trace the bench
+  // frame showed ~100 us of idle GPU before each frame's graph (the graph's
+  // launch reaching the queue only after the previous frame drained); two
+  // instances removed that idle in the trace (109 -> 15 us a frame) but
+  // changed nothing in the untraced bench (3 rounds: 2.978 vs 2.980e9), so
+  // one instance is the default
   std::map<std::vector<uint32_t>, hipGraphExec_t> graphs_alt;
   std::map<std::vector<uint32_t>, int> graph_turn;
-  int graph_copies = 2;
+  int graph_copies = 1;
   std::map<std::vector<uint32_t>, int> graph_box_parity;
   struct FState {
     int bpar, ep;
@@ -1522,6 +1596,8 @@ struct gsmpm_mpm {
   int* s_rec_host = nullptr;                 // pinned copy
   int* nonfin_host = nullptr;                // non-finite particle position seen (pinned, device-mapped; sticky)
   int* nonfin_dev = nullptr;                 // its device address
+  FusedRare* frare_dev = nullptr;            // [2 bins parities][2 escape flags] k_fused's rare arguments (fused.h)
+  FusedRare frare_host[4] = {};              // what frare_dev holds
   float* mig_send[2] = {nullptr, nullptr};   // fixed-size payloads: header + [NMIG][mig_cap]
   float* mig_recv[2] = {nullptr, nullptr};
   int mig_cap = 0;                           // leavers one migration may send one way (all ranks agree)
@@ -1770,24 +1846,58 @@ static int launch_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc,
 // rounds (config D) are spread evenly.
 static int fused_grid(gsmpm_mpm* h) { return std::min(h->ftl.max_chunks, h->fused_wgs); }
 
+static FusedRare rare_of(gsmpm_mpm* h, int c, int e) {
+  FusedRare r{};
+  r.bo = bin_out_f(h, c ^ 1);
+  r.gacc = h->gacc;
+  r.esc = h->fesc + e;
+  r.drift = h->slab ? h->s_drift : nullptr;
+  r.nonfin = h->slab ? h->s_drift + SF_NONFIN : h->nonfin_dev;
+  r.bct = h->dev_bc;
+  r.tflag = h->ftflag[c];
+  r.touched = h->ftouched[c];
+  r.nchunk = h->fnchunk[c];
+  r.chunk = h->fchunk[c];
+  r.rcov = h->frcov[c];
+  r.tbox = h->ftbox[c];
+  r.tpos = h->cover_records ? h->ftpos[c] : nullptr;
+  r.rbox = h->frbox[c];
+  return r;
+}
+// k_fused's rare arguments in device memory, rewritten (outside captures,
+// ordered on `st`) whenever one changes; graph_substeps calls it before it
+// captures, so a captured launch never finds them stale
+static int sync_rare(gsmpm_mpm* h, hipStream_t st) {
+  bool dirty = false;
+  for (int i = 0; i < 4; ++i) {
+    const FusedRare r = rare_of(h, i >> 1, i & 1);
+    if (std::memcmp(&r, &h->frare_host[i], sizeof(r)) != 0) {
+      h->frare_host[i] = r;
+      dirty = true;
+    }
+  }
+  if (!dirty) return GSMPM_OK;
+  GSMPM_REQUIRE(!h->capturing, "k_fused's rare arguments changed inside a capture");
+  GSMPM_HIP(hipMemcpyAsync(h->frare_dev, h->frare_host, sizeof(h->frare_host), hipMemcpyHostToDevice, st));
+  return GSMPM_OK;
+}
 template <int MAT, int MODE>
-static void launch_fused_t(gsmpm_mpm* h, int c, const BinOutF& bo, int bin, int use_box, uint32_t mask, float dt,
-                           int* esc, hipStream_t st, const hipEvent_t* ev) {
-  const SlabK sk = h->slab ? SlabK{h->s_lo - h->s_margin, h->s_hi + h->s_margin, h->s_drift, h->s_drift + SF_NONFIN}
-                          : SlabK{INT_MIN, INT_MAX, nullptr, h->nonfin_dev};
+static void launch_fused_t(gsmpm_mpm* h, int c, int bin, int use_box, uint32_t mask, float dt, int* esc,
+                           hipStream_t st, const hipEvent_t* ev) {
+  const int xlo = h->slab ? h->s_lo - h->s_margin : INT_MIN, xhi = h->slab ? h->s_hi + h->s_margin : INT_MAX;
   launch(ev, k_fused<MAT, MODE>, dim3(fused_grid(h)), dim3(256), st, particles_of(h), h->g, h->ftl, chunk_in_f(h, c),
-         touch_f(h, c), bo, bin, use_box, (const float4*)h->gvel, (const BcTable*)h->dev_bc, mask, dt, h->mc, h->fslots, h->gacc,
-         esc, sk);
+         touch_f(h, c), bin, use_box, (const float4*)h->gvel, mask, dt, h->mc, h->fslots, xlo, xhi,
+         (const FusedRare*)(h->frare_dev + c * 2 + (int)(esc - h->fesc)));
 }
 template <int MODE>
-static void launch_fused_m(gsmpm_mpm* h, int c, const BinOutF& bo, int bin, int ub, uint32_t mask, float dt, int* esc,
-                           hipStream_t st, const hipEvent_t* ev) {
+static void launch_fused_m(gsmpm_mpm* h, int c, int bin, int ub, uint32_t mask, float dt, int* esc, hipStream_t st,
+                           const hipEvent_t* ev) {
   switch (h->mat_kernel) {
-    case 0: launch_fused_t<0, MODE>(h, c, bo, bin, ub, mask, dt, esc, st, ev); break;
-    case 1: launch_fused_t<1, MODE>(h, c, bo, bin, ub, mask, dt, esc, st, ev); break;
-    case 2: launch_fused_t<2, MODE>(h, c, bo, bin, ub, mask, dt, esc, st, ev); break;
-    case 3: launch_fused_t<3, MODE>(h, c, bo, bin, ub, mask, dt, esc, st, ev); break;
-    default: launch_fused_t<4, MODE>(h, c, bo, bin, ub, mask, dt, esc, st, ev); break;
+    case 0: launch_fused_t<0, MODE>(h, c, bin, ub, mask, dt, esc, st, ev); break;
+    case 1: launch_fused_t<1, MODE>(h, c, bin, ub, mask, dt, esc, st, ev); break;
+    case 2: launch_fused_t<2, MODE>(h, c, bin, ub, mask, dt, esc, st, ev); break;
+    case 3: launch_fused_t<3, MODE>(h, c, bin, ub, mask, dt, esc, st, ev); break;
+    default: launch_fused_t<4, MODE>(h, c, bin, ub, mask, dt, esc, st, ev); break;
   }
 }
 // mode 1: G2P only, 2: P2G only, 3: G2P of the last grid update + P2G.
@@ -1795,14 +1905,17 @@ static void launch_fused_m(gsmpm_mpm* h, int c, const BinOutF& bo, int bin, int 
 // its per-chunk stencil boxes bound this launch's G2P gathers.
 static int launch_fused(gsmpm_mpm* h, int mode, int c, bool bin, bool use_box, uint32_t mask, float dt, int* esc,
                         hipStream_t st, const hipEvent_t* ev) {
-  const BinOutF bo = bin_out_f(h, c ^ 1);
+  if (!h->capturing) {
+    const int rc = sync_rare(h, st);
+    if (rc) return rc;
+  }
   const int ub = use_box ? 1 : 0;
   if (mode == 1)
-    launch_fused_t<0, 1>(h, c, bo, bin ? 1 : 0, ub, mask, dt, esc, st, ev);  // G2P does not depend on the material
+    launch_fused_t<0, 1>(h, c, bin ? 1 : 0, ub, mask, dt, esc, st, ev);  // G2P does not depend on the material
   else if (mode == 2)
-    launch_fused_m<2>(h, c, bo, bin ? 1 : 0, ub, mask, dt, esc, st, ev);
+    launch_fused_m<2>(h, c, bin ? 1 : 0, ub, mask, dt, esc, st, ev);
   else
-    launch_fused_m<3>(h, c, bo, bin ? 1 : 0, ub, mask, dt, esc, st, ev);
+    launch_fused_m<3>(h, c, bin ? 1 : 0, ub, mask, dt, esc, st, ev);
   GSMPM_LAUNCH_CHECK();
   return GSMPM_OK;
 }
@@ -1810,9 +1923,15 @@ static int launch_fused(gsmpm_mpm* h, int mode, int c, bool bin, bool use_box, u
 static int launch_grid_f(gsmpm_mpm* h, int wp, float dt, uint32_t mask, int ep, int* zc, int* zf, hipStream_t st,
                          const hipEvent_t* ev, const SlabWin* swp = nullptr) {
   const SlabWin sw = swp ? *swp : SlabWin{};
-  launch(ev, k_grid_f, dim3(std::min(kGridParts * h->ftl.ntiles, 1024 * kGridParts)), dim3(kGridT), st, h->g, h->ftl, chunk_in_f(h, wp),
-         (const int*)h->ftbox[wp], (const float4*)h->fslots, h->gacc, h->gvel, (const BcTable*)h->dev_bc, grid_step(h, dt, mask),
-         (const int*)(h->fesc + ep), h->fesc + (ep ^ 1), zc, zf, sw);
+  const dim3 grid(std::min(kGridParts * h->ftl.ntiles, 1024 * kGridParts));
+  if (swp)
+    launch(ev, k_grid_f<true>, grid, dim3(kGridT), st, h->g, h->ftl, chunk_in_f(h, wp), (const int*)h->ftbox[wp],
+           (const float4*)h->fslots, h->gacc, h->gvel, (const BcTable*)h->dev_bc, grid_step(h, dt, mask),
+           (const int*)(h->fesc + ep), h->fesc + (ep ^ 1), zc, zf, sw);
+  else
+    launch(ev, k_grid_f<false>, grid, dim3(kGridT), st, h->g, h->ftl, chunk_in_f(h, wp), (const int*)h->ftbox[wp],
+           (const float4*)h->fslots, h->gacc, h->gvel, (const BcTable*)h->dev_bc, grid_step(h, dt, mask),
+           (const int*)(h->fesc + ep), h->fesc + (ep ^ 1), zc, zf, sw);
   GSMPM_LAUNCH_CHECK();
   return GSMPM_OK;
 }
@@ -2054,6 +2173,11 @@ static int graph_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc, 
     hipGraph_t graph;
     int parity = h->cur_box, bp = h->fbpar, ep = h->fep;
     const gsmpm_mpm::FState start = fstate_of(h, bp, ep);
+    if (fz) {
+      const int rr = sync_rare(h, st);  // k_fused's rare arguments are current before the capture
+      if (rr) return rr;
+      GSMPM_HIP(hipStreamSynchronize(st));
+    }
     gtrace("begin capture");
     GSMPM_HIP(hipStreamBeginCapture(h->cap, hipStreamCaptureModeRelaxed));
     h->capturing = true;
@@ -2266,6 +2390,7 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
     if ((e = hipMalloc(&h->orig_alt, sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc orig");
     if ((e = hipMalloc(&h->fesc, sizeof(int) * 2)) != hipSuccess) return fail(e, "hipMalloc escape flags");
     if ((e = hipMemset(h->fesc, 0, sizeof(int) * 2)) != hipSuccess) return fail(e, "hipMemset");
+    if ((e = hipMalloc(&h->frare_dev, sizeof(h->frare_host))) != hipSuccess) return fail(e, "hipMalloc rare args");
   }
   const int scan_tiles = std::max(h->tl.ntiles, h->ftl.ntiles) + 1;
   if ((e = hipMalloc(&h->scan_part, sizeof(int4) * (size_t)div_up(scan_tiles, 1024))) != hipSuccess)
@@ -2331,6 +2456,7 @@ int gsmpm_mpm_destroy(gsmpm_mpm* h) {
   }
   (void)hipFree(h->fslots);
   (void)hipFree(h->fesc);
+  (void)hipFree(h->frare_dev);
   (void)hipFree(h->planes_alt);
   (void)hipFree(h->orig_alt);
   (void)hipFree(h->ptile);

@@ -24,12 +24,12 @@
 //    compacted (wave ballot + prefix sum, stable) into per-neighbour send
 //    buffers, stayers into a compacted storage; arrivals are appended.  A
 //    particle that drifts past the margin between migrations raises a flag
-//    (k_fused, SlabK) -- the window exchange would have missed its
+//    (k_fused's xlo / xhi check) -- the window exchange would have missed its
 //    contributions -- and the host reports it.
 
 constexpr int NMIG = NPLANES + NCOLD + 1;  // migration payload per particle: hot + cold planes + global id
 
-// SlabWin / SlabK (the hooks in k_fused and k_grid_f) are declared in fused.h.
+// SlabWin and k_fused's xlo / xhi / FusedRare::drift (the hooks in k_grid_f and k_fused) are declared in fused.h.
 
 // Window totals and their grid update.  One lane per window node; the lower
 // rank's partial is always the left operand, so both ranks of a bound compute

@@ -126,7 +126,9 @@ def test_impulse_window(dev, pipe):
 
 @pytest.mark.parametrize("pipe", PIPES)
 def test_eager_equals_graph(dev, pipe):
-    """Per-substep launches and the cached hipGraph replay give identical state."""
+    """Per-substep launches and the cached hipGraph replay give identical state,
+    over four step calls with the same key: the graph's two instances
+    (GSMPM_GRAPH_COPIES, launched in turn) both run."""
     import torch
     from gsmpm.sim import Simulator
     prob = lego_problem(3000, 48)
@@ -139,7 +141,8 @@ def test_eager_equals_graph(dev, pipe):
         sim.set_particles(t(prob["x"]), t(prob["cov"]), t(prob["vol"]))
         b = sim.add_fixed_cube([1.0, 1.2, 0.5], [1.0, 0.8, 0.3])
         sim.add_plane_collider([0, 0, 0.4], [0, 0, 1])
-        sim.step(1e-4, [1 << b] * 20)
+        for _ in range(4):
+            sim.step(1e-4, [1 << b] * 20)
         outs.append(sim.get("x").cpu().numpy())
     assert rel_err(outs[0], outs[1]) < 1e-6
 

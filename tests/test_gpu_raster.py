@@ -608,3 +608,32 @@ def test_tile_shared_render_matches_quarter_render(dev, monkeypatch, scene, ones
         out[quarters] = [x.detach().cpu().numpy() for x in (img, m3.grad, o1.grad, s1.grad, cv.grad)]
     for a, b in zip(out["0"], out["1"]):
         assert np.array_equal(a, b)
+
+
+def test_in_frame_timing(dev):
+    """gsmpm_raster_set_timing / gsmpm_raster_timing: with timing on, each
+    forward records its k_render and whole-forward times on its own stream;
+    the read returns their sums and count and clears them; off, nothing is
+    recorded."""
+    import torch
+    from gsmpm import raster
+    P, W, H = 5000, 320, 240
+    means, c6, opa, shs = _scene(P, seed=5)
+    view, full, campos, tx, ty = _camera(W, H, 0.9)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    args = [t(means), t(opa), t(view), t(full), t(campos), t(np.zeros(3, np.float32)), H, W, tx, ty]
+    kw = dict(sh_degree=3, shs=t(shs), cov3D_precomp=t(c6))
+    raster.timing()
+    raster.set_timing(True)
+    try:
+        s = torch.cuda.Stream(dev)
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                raster.forward(*args, **kw)
+        kr, fw, n = raster.timing()
+        assert n == 3 and 0 < kr <= fw, (kr, fw, n)
+        assert raster.timing()[2] == 0  # read once
+    finally:
+        raster.set_timing(False)
+    raster.forward(*args, **kw)
+    assert raster.timing()[2] == 0
