@@ -345,16 +345,35 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
   constexpr int SK = MODE == 3 ? 0 : 1;  // diagnostics slot (k_p2g's / k_g2p's in the per-phase pipeline)
   sim_prio();
   stamp(SK, 0);
-  const int nch = ck.nchunk[0];
   // the first chunk's record, box and lane order are requested with the chunk
   // count (clamped: a workgroup past the last chunk discards them), which
-  // takes one dependent round trip off every workgroup's chain
-  // (the same for every further chunk: its record, box and lane order are
-  // requested while the chunk before it is processed)
+  // takes dependent round trips off every workgroup's chain (the same for
+  // every further chunk: its record, box and lane order are requested while
+  // the chunk before it is processed).  The empty asm takes the pointers
+  // into SGPRs in the first argument batch and the loads go through the
+  // global address space as vector loads, so all four leave together: as
+  // plain scalar loads the compiler serialised them -- box, then count, then
+  // record, three memory round trips behind each other at the kernel start
+  // (one shared lgkmcnt, argument reloads between them)
+  // (all four unconditional, straight-line: an unused lane order reads
+  // cbox[0] instead, selected away below)
   const int w0 = min((int)blockIdx.x, tl.max_chunks - 1);
-  int4 cr_n = ck.chunk[w0];
-  int box_n = use_box ? tc.cbox[w0] : kFullBox;
-  int q_n = (use_box && tc.perm) ? (int)tc.perm[(size_t)w0 * 256 + threadIdx.x] : (int)threadIdx.x;
+  const bool perm0 = use_box && tc.perm;
+  const int* nch_p = ck.nchunk;
+  const int4* chk_p = ck.chunk;
+  const int* cbx_p = tc.cbox;
+  const unsigned char* prm_p = perm0 ? tc.perm : reinterpret_cast<const unsigned char*>(tc.cbox);
+  asm volatile("" : "+s"(nch_p), "+s"(chk_p), "+s"(cbx_p), "+s"(prm_p));
+  typedef const int __attribute__((address_space(1)))* gint_p;
+  typedef const unsigned char __attribute__((address_space(1)))* guc_p;
+  const gint_p c4 = (gint_p)chk_p + 4 * (size_t)w0;
+  const int r0 = c4[0], r1 = c4[1], r2 = c4[2], r3 = c4[3];
+  const int bx0 = ((gint_p)cbx_p)[w0];
+  const int qv0 = ((guc_p)prm_p)[perm0 ? (size_t)w0 * 256 + threadIdx.x : 0];
+  const int nch = *(gint_p)nch_p;
+  int4 cr_n = make_int4(r0, r1, r2, r3);
+  int box_n = use_box ? bx0 : kFullBox;
+  int q_n = perm0 ? qv0 : (int)threadIdx.x;
   for (int w = blockIdx.x; w < nch; w += gridDim.x) {
     const int4 cr = cr_n;
     const int cbox = box_n, q_lane = q_n;
@@ -888,22 +907,22 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
   // partials can travel while the rest updates): the flag and the zeroing go
   // with the second
   const int pass = SLAB ? sw.pass : 0;
-  if (blockIdx.x == 0 && threadIdx.x == 0 && pass != 1) *esc_clear = 0;
-  if (zc && pass != 1) {
-    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t <= tl.ntiles; t += gridDim.x * blockDim.x) {
-      zc[t] = 0;
-      if (t < tl.ntiles) zf[t] = 0;
-    }
-  }
-  const int ng = g.ng;
-  const bool all = *esc_in != 0;
-  const int ntouch = kGridParts * (all ? tl.ntiles : ck.nchunk[1]);
-  // the first touched tile requested with the count (clamped), one round trip
-  // less; and with it the tile's cover record -- its 27 neighbours' chunk
-  // ranges (from the binning) and stencil boxes (published by this substep's
-  // k_fused) -- so the slot addresses need no hop through the tile tables
+  // Every first load of the workgroup is issued here, together, before any
+  // store: the escape flag, the touched count, the first touched tile (its
+  // index clamped) and that tile's cover record -- its 27 neighbours' chunk
+  // ranges (from the binning) and stencil boxes (published by this
+  // substep's k_fused), so the slot addresses need no hop through the tile
+  // tables.  Round 5 first had the flag and count after the zeroing stores
+  // below, which the compiler may not hoist loads over (the pointers could
+  // alias): three dependent scalar round trips before the first record load.
   const int i0 = min((int)blockIdx.x / kGridParts, tl.ntiles - 1);
-  const int T0 = ck.touched[i0];
+  // (the empty asm takes the three pointers into SGPRs at once, so their
+  // kernel-argument loads come in the first batch and the three scalar loads
+  // below leave together: one round trip, not two behind each other)
+  const int* esc_p = esc_in;
+  const int* cnt_p = ck.nchunk;
+  const int* tch_p = ck.touched;
+  asm volatile("" : "+s"(esc_p), "+s"(cnt_p), "+s"(tch_p));
   const bool recs = ck.rcov != nullptr && !kAtomicGrid;
   const int le = threadIdx.x;  // lane: record entry
   int2 cov0 = make_int2(1, 0);
@@ -912,6 +931,20 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     cov0 = ck.rcov[(size_t)i0 * kRecStride + le];
     bx0 = ck.rbox[(size_t)i0 * kRecStride + le];
   }
+  typedef const int __attribute__((address_space(1)))* gint_p;  // global, not flat (flat loads count in lgkmcnt too)
+  const int esc0 = *(gint_p)esc_p;
+  const int cnt0 = ((gint_p)cnt_p)[1];
+  const int T0 = ((gint_p)tch_p)[i0];
+  if (blockIdx.x == 0 && threadIdx.x == 0 && pass != 1) *esc_clear = 0;
+  if (zc && pass != 1) {
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t <= tl.ntiles; t += gridDim.x * blockDim.x) {
+      zc[t] = 0;
+      if (t < tl.ntiles) zf[t] = 0;
+    }
+  }
+  const int ng = g.ng;
+  const bool all = esc0 != 0;
+  const int ntouch = kGridParts * (all ? tl.ntiles : cnt0);
   __shared__ int s_c0[27], s_nc[27], s_bx[27];
   __shared__ int s_none;
   for (int wt = blockIdx.x; wt < ntouch; wt += gridDim.x) {
@@ -972,13 +1005,17 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
           gacc[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
       }
-      const int sww = (SLAB && sw.W) ? slab_window_of(sw, i) : -1;
-      const bool inrect = sww >= 0 && (unsigned)(j - sw.y0[sww]) < (unsigned)sw.ny[sww] &&
-                          (unsigned)(k - sw.z0[sww]) < (unsigned)sw.nz[sww];
-      if (sww >= 0 && !inrect && a.w != 0.f) *sw.oob = 1;
-      if (inrect)  // a window node: this rank's partial, totalled after the exchange (k_win_update)
-        sw.part[sww][((size_t)(i - sw.a[sww]) * sw.ny[sww] + (j - sw.y0[sww])) * sw.nz[sww] + (k - sw.z0[sww])] = a;
-      else if (!kGridSkip0 || a.w != 0.f || (reach && !kAtomicGrid && GSMPM_GRID_SKIP0 == 1)) {
+      bool inrect = false;
+      if constexpr (SLAB) {
+        const int sww = sw.W ? slab_window_of(sw, i) : -1;
+        inrect = sww >= 0 && (unsigned)(j - sw.y0[sww]) < (unsigned)sw.ny[sww] &&
+                 (unsigned)(k - sw.z0[sww]) < (unsigned)sw.nz[sww];
+        if (sww >= 0 && !inrect && a.w != 0.f) *sw.oob = 1;
+        if (inrect)  // a window node: this rank's partial, totalled after the exchange (k_win_update)
+          sw.part[sww][((size_t)(i - sw.a[sww]) * sw.ny[sww] + (j - sw.y0[sww])) * sw.nz[sww] + (k - sw.z0[sww])] = a;
+      }
+      if (inrect) {
+      } else if (!kGridSkip0 || a.w != 0.f || (reach && !kAtomicGrid && GSMPM_GRID_SKIP0 == 1)) {
         if constexpr (kGvelStore == 1)
           nt_store4(gvel + idx, node_update(a, i, j, k, g, gs, bct));
         else if constexpr (kGvelStore == 2)
