@@ -817,19 +817,31 @@ __device__ __forceinline__ void node_reads(int max_chunks, const int* s_c0, cons
   const int sec2 = l2 < 3 ? -1 : (l2 == kFT2 - 1 ? 1 : 0);
   r.extra = 0;
   r.live = 0;
+  // every LDS read first, unconditionally (ci is a valid neighbour index for
+  // all e), then the tests as plain bit operations: with the reads behind
+  // short-circuit tests the compiler branched around each one and waited on
+  // each, 8 dependent LDS round trips in front of the slot loads
+  int nc[8], bx[8], c0[8], ci[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int a = (e >> 2) ? sec0 : 0, b = ((e >> 1) & 1) ? sec1 : 0, c = (e & 1) ? sec2 : 0;
+    ci[e] = (a + 1) * 9 + (b + 1) * 3 + (c + 1);
+    nc[e] = s_nc[ci[e]];
+    bx[e] = s_bx[ci[e]];
+    c0[e] = s_c0[ci[e]];
+  }
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int ax = e >> 2, ay = (e >> 1) & 1, az = e & 1;
     const int a = ax ? sec0 : 0, b = ay ? sec1 : 0, c = az ? sec2 : 0;
-    bool on = (!ax || sec0) && (!ay || sec1) && (!az || sec2);
-    const int ci = (a + 1) * 9 + (b + 1) * 3 + (c + 1);
-    const int nc = s_nc[ci], bx = s_bx[ci];
     const int w0 = l0 - a * kFT0 + 1, w1 = l1 - b * kFT1 + 1, w2 = l2 - c * kFT2 + 1;
-    on = on && nc > 0 && w0 >= (bx & 15) && w1 >= ((bx >> 4) & 15) && w2 >= ((bx >> 8) & 15) &&
-         w0 <= ((bx >> 12) & 15) && w1 <= ((bx >> 16) & 15) && w2 <= ((bx >> 20) & 15);
+    const int q = bx[e];
+    const bool on = ((!ax) | (sec0 != 0)) & ((!ay) | (sec1 != 0)) & ((!az) | (sec2 != 0)) & (nc[e] > 0) &
+                    (w0 >= (q & 15)) & (w1 >= ((q >> 4) & 15)) & (w2 >= ((q >> 8) & 15)) &
+                    (w0 <= ((q >> 12) & 15)) & (w1 <= ((q >> 16) & 15)) & (w2 <= ((q >> 20) & 15));
     const int loc = slot_loc(w0, w1, w2);
-    r.off[e] = on ? s_c0[ci] * kFWin + loc : max_chunks * kFWin;
-    r.extra |= (on && nc > 1) ? (1 << e) : 0;
+    r.off[e] = on ? c0[e] * kFWin + loc : max_chunks * kFWin;
+    r.extra |= (on & (nc[e] > 1)) ? (1 << e) : 0;
     r.live |= on ? (1 << e) : 0;
   }
 }
