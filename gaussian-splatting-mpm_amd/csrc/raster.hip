@@ -518,28 +518,32 @@ __global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges,
   // skipped; without, the quarter test runs on the gathered conic
   const unsigned* tk = tkeys ? tkeys + range.x : nullptr;
   const unsigned qbit = 1u << (kMaskShift + (((by & 1) << 1) | (bx & 1)));
+  // The ids and keys of a batch are loaded as raw words and tested only when
+  // used, a batch later: testing a key right after its load (a bool kept
+  // across the blend) made the compiler wait for each load where it was
+  // issued -- the "prefetch" of the next batch's ids and keys stalled the
+  // wave for kQ round trips in front of every blend.
   float2 g_xy[kQ];
   float4 g_co[kQ], g_rgb[kQ];
-  unsigned nid[kQ];
-  bool g_rel[kQ], n_rel[kQ];
+  unsigned gid[kQ], gkey[kQ], nid[kQ], nkey[kQ];
+  bool g_rel[kQ];
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) {  // batch 0's ids and keys, and batch 1's, all issued first
+    const bool v0 = 64 * q + lane < n, v1 = kBatch + 64 * q + lane < n;
+    gid[q] = v0 ? lst[64 * q + lane] : 0u;
+    gkey[q] = (v0 && tk) ? tk[64 * q + lane] : qbit;
+    nid[q] = v1 ? lst[kBatch + 64 * q + lane] : 0u;
+    nkey[q] = (v1 && tk) ? tk[kBatch + 64 * q + lane] : qbit;
+  }
 #pragma unroll
   for (int q = 0; q < kQ; ++q) {
     g_xy[q] = make_float2(0.f, 0.f);
     g_co[q] = g_rgb[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-    nid[q] = 0;
-    g_rel[q] = n_rel[q] = false;
-    if (64 * q + lane < n) {
-      g_rel[q] = !tk || (tk[64 * q + lane] & qbit);
-      if (g_rel[q]) {
-        const unsigned id = lst[64 * q + lane];
-        g_xy[q] = xy[id];
-        g_co[q] = conic_o[id];
-        g_rgb[q] = rgbo[id];
-      }
-    }
-    if (kBatch + 64 * q + lane < n) {
-      nid[q] = lst[kBatch + 64 * q + lane];
-      n_rel[q] = !tk || (tk[kBatch + 64 * q + lane] & qbit);
+    g_rel[q] = 64 * q + lane < n && (gkey[q] & qbit);
+    if (g_rel[q]) {
+      g_xy[q] = xy[gid[q]];
+      g_co[q] = conic_o[gid[q]];
+      g_rgb[q] = rgbo[gid[q]];
     }
   }
   for (int j0 = 0; j0 < n; j0 += kBatch) {
@@ -568,18 +572,32 @@ __global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges,
     }
     __syncthreads();
     // the next batch's gather and the one after's list ids fly while this one blends
+    // (every test first -- its words were loaded a batch ago -- then every
+    // gather: a test between two gathers is a wait for an older load, which
+    // the in-order counter turns into a wait for the gather just issued)
+    const float2* pxy[kQ];
+    const float4 *pco[kQ], *prgb[kQ];
 #pragma unroll
     for (int q = 0; q < kQ; ++q) {
-      g_rel[q] = j0 + kBatch + 64 * q + lane < n && n_rel[q];
+      g_rel[q] = j0 + kBatch + 64 * q + lane < n && (nkey[q] & qbit);
+      pxy[q] = xy + nid[q];
+      pco[q] = conic_o + nid[q];
+      prgb[q] = rgbo + nid[q];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
       if (g_rel[q]) {
-        g_xy[q] = xy[nid[q]];
-        g_co[q] = conic_o[nid[q]];
-        g_rgb[q] = rgbo[nid[q]];
+        g_xy[q] = *pxy[q];
+        g_co[q] = *pco[q];
+        g_rgb[q] = *prgb[q];
       }
-      if (j0 + 2 * kBatch + 64 * q + lane < n) {
-        nid[q] = lst[j0 + 2 * kBatch + 64 * q + lane];
-        n_rel[q] = !tk || (tk[j0 + 2 * kBatch + 64 * q + lane] & qbit);
-      }
+    }
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      const bool v = j0 + 2 * kBatch + 64 * q + lane < n;
+      nid[q] = v ? lst[j0 + 2 * kBatch + 64 * q + lane] : 0u;
+      nkey[q] = (v && tk) ? tk[j0 + 2 * kBatch + 64 * q + lane] : qbit;
     }
     for (int b = 0; b < cnt; b += kU) {
       if (__all(done)) break;
@@ -1006,10 +1024,16 @@ __global__ __launch_bounds__(kSortT) void k_tile_hist(int K, int ntiles, int nch
   for (int t = threadIdx.x; t <= ntiles; t += kSortT) s_h[t] = 0;
   __syncthreads();
   const int c = blockIdx.x;
-  for (int i = threadIdx.x; i < kChunk; i += kSortT) {
-    const int e = c * kChunk + i;
-    if (e < K) atomicAdd(&s_h[sort_tile(keys[e], lowmask, ntiles)], 1u);
-  }
+  // every key of the chunk loaded first (clamped indices), then the counts:
+  // a load then its atomic per element made the compiler wait on each load,
+  // kChunk / kSortT round trips in a row
+  constexpr int kPer = kChunk / kSortT;
+  unsigned kv[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) kv[u] = keys[min(c * kChunk + (int)threadIdx.x + u * kSortT, max(K - 1, 0))];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u)
+    if (c * kChunk + (int)threadIdx.x + u * kSortT < K) atomicAdd(&s_h[sort_tile(kv[u], lowmask, ntiles)], 1u);
   __syncthreads();
   for (int t = threadIdx.x; t <= ntiles; t += kSortT) H[(size_t)t * nch + c] = s_h[t];
 }
@@ -1035,9 +1059,17 @@ __global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int 
   const int c = blockIdx.x;
   const unsigned lowmask = (1u << bits) - 1u;  // >= ntiles
   {
+    // the thread's <= 17 tile totals loaded at once (clamped indices), kept in
+    // registers for the second pass: loaded in a loop with the sum, each load
+    // was waited for before the next
+    constexpr int kPerMax = (kMaxTiles + 1 + kSortT - 1) / kSortT;
     const int per = (ntiles + 1 + kSortT - 1) / kSortT, t0 = threadIdx.x * per;
+    unsigned tv[kPerMax];
+#pragma unroll
+    for (int q = 0; q < kPerMax; ++q) tv[q] = tot[min(t0 + q, ntiles)];
     unsigned sum = 0;
-    for (int q = 0; q < per; ++q) sum += t0 + q <= ntiles ? tot[t0 + q] : 0u;
+#pragma unroll
+    for (int q = 0; q < kPerMax; ++q) sum += (q < per && t0 + q <= ntiles) ? tv[q] : 0u;
     s_part[threadIdx.x] = sum;
     __syncthreads();
     for (int o = 1; o < kSortT; o <<= 1) {
@@ -1047,10 +1079,11 @@ __global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int 
       __syncthreads();
     }
     unsigned run = s_part[threadIdx.x] - sum;
-    for (int q = 0; q < per; ++q)
-      if (t0 + q <= ntiles) {
+#pragma unroll
+    for (int q = 0; q < kPerMax; ++q)
+      if (q < per && t0 + q <= ntiles) {
         s_ts[t0 + q] = run;
-        run += tot[t0 + q];
+        run += tv[q];
       }
     if (threadIdx.x == kSortT - 1) s_ts[ntiles + 1] = run;
   }
@@ -1090,10 +1123,16 @@ __global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int 
   const int e0 = c * kChunk + wv * kW;
   unsigned k[kSortI], v[kSortI], r[kSortI], tl[kSortI];
 #pragma unroll
+  for (int j = 0; j < kSortI; ++j) {  // unconditional loads (clamped), then the selects: no wait between them
+    const int ec = min(e0 + j * 64 + lane, max(K - 1, 0));
+    k[j] = keys[ec];
+    v[j] = vals[ec];
+  }
+#pragma unroll
   for (int j = 0; j < kSortI; ++j) {
     const int e = e0 + j * 64 + lane;
-    k[j] = e < K ? keys[e] : 0u;
-    v[j] = e < K ? vals[e] : 0u;
+    k[j] = e < K ? k[j] : 0u;
+    v[j] = e < K ? v[j] : 0u;
     tl[j] = e < K ? sort_tile(k[j], lowmask, ntiles) : 8191u;  // 8191: no pair (13 bits, > any tile)
   }
   const unsigned long long below = (1ull << lane) - 1ull;
@@ -1152,14 +1191,24 @@ __global__ __launch_bounds__(kSortT) void k_tile_scatter(int K, int ntiles, int 
   for (int sp = nv + (int)threadIdx.x; sp < kChunk; sp += kSortT) s_v[sp] = kNoEntry;  // the tail: no pair
   __syncthreads();
 #endif
+  // every chunk-offset load first (a no-pair slot reads tile 0's), then the
+  // stores: a load, its wait and its store per slot were kSortI round trips
+  unsigned hv[kSortI], tv[kSortI];
+#pragma unroll
+  for (int i = 0; i < kSortI; ++i) {
+    const int sp = i * kSortT + threadIdx.x;
+    const unsigned t = s_v[sp] == kNoEntry ? 0u : sort_tile(s_k[sp], lowmask, ntiles);
+    tv[i] = t;
+    hv[i] = Hs[(size_t)t * nch + c];
+  }
 #pragma unroll
   for (int i = 0; i < kSortI; ++i) {
     const int sp = i * kSortT + threadIdx.x;
     const unsigned vv = s_v[sp];
     if (vv == kNoEntry) continue;
-    const unsigned kk = s_k[sp], t = sort_tile(kk, lowmask, ntiles);
-    const unsigned pos = s_ts[t] + Hs[(size_t)t * nch + c] + (unsigned)(sp - s_start[t]);
-    keys_out[pos] = kk;
+    const unsigned t = tv[i];
+    const unsigned pos = s_ts[t] + hv[i] + (unsigned)(sp - s_start[t]);
+    keys_out[pos] = s_k[sp];
     vals_out[pos] = vv;
   }
   if (c == 0)
