@@ -429,8 +429,13 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
         const int nvol = (hi[0] - lo[0] + 1) * n12;
         const float r12 = 1.0f / (float)n12, r2 = 1.0f / (float)n2;  // exact floor for q < 2^11
         constexpr int kStageU = (kFWin + 255) / 256;  // window nodes per lane, at most
+        // all loads first, the out-of-grid zeroing as a select afterwards: a
+        // zeroing branch right after each load made the compiler wait for
+        // that load before issuing the next (the zeros and the in-flight load
+        // share the registers), 7 round trips in a row instead of one
         float4 gv[kStageU];
         int dst[kStageU];
+        bool gin[kStageU];
 #pragma unroll
         for (int u = 0; u < kStageU; ++u) {
           const int qn = min(k + u * 256, nvol - 1);
@@ -439,13 +444,16 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
           const int wa = lo[0] + a, wb = lo[1] + b, wc = lo[2] + c;
           dst[u] = (wa * kFW1 + wb) * kFW2 + wc;
           const int ix = o0 + wa, iy = o1 + wb, iz = o2 + wc;
-          const bool in = (unsigned)ix < (unsigned)ng && (unsigned)iy < (unsigned)ng && (unsigned)iz < (unsigned)ng;
-          gv[u] = gvel[in ? ((size_t)ix * ng + iy) * ng + iz : 0];
-          if (!in) gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+          gin[u] = (unsigned)ix < (unsigned)ng && (unsigned)iy < (unsigned)ng && (unsigned)iz < (unsigned)ng;
+          gv[u] = gvel[gin[u] ? ((size_t)ix * ng + iy) * ng + iz : 0];
         }
 #pragma unroll
-        for (int u = 0; u < kStageU; ++u)
-          if (k + u * 256 < nvol) s_win[dst[u]] = gv[u];
+        for (int u = 0; u < kStageU; ++u) {
+          const float4 z = gv[u];
+          const bool in = gin[u];
+          const float4 val = make_float4(in ? z.x : 0.f, in ? z.y : 0.f, in ? z.z : 0.f, in ? z.w : 0.f);
+          if (k + u * 256 < nvol) s_win[dst[u]] = val;
+        }
       }
       if (k < 27) s_cnt[k] = 0;
       __syncthreads();
