@@ -779,9 +779,10 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
 }
 
 // Chunk ranges and stencil boxes of the 27 tiles whose windows reach tile
-// (ti, tj, tk) -> LDS (lanes 0..26; caller syncs).
+// (ti, tj, tk) -> LDS (lanes 0..26; caller syncs), in a cover record's layout:
+// s_cov[2 e] = first chunk, s_cov[2 e + 1] = chunk count, s_bx[e] = box.
 __device__ __forceinline__ void load_cover27(const ChunkIn& ck, const int* __restrict__ tbox, const FTiles& tl, int ti,
-                                             int tj, int tk, int* s_c0, int* s_nc, int* s_bx) {
+                                             int tj, int tk, int* s_cov, int* s_bx) {
   const int e = threadIdx.x;
   if (e < 27) {
     const int x = ti + e / 9 - 1, y = tj + (e / 3) % 3 - 1, z = tk + e % 3 - 1;
@@ -793,8 +794,8 @@ __device__ __forceinline__ void load_cover27(const ChunkIn& ck, const int* __res
       bx = tbox[t];
       nc = (cnt + kChunk - 1) / kChunk;
     }
-    s_c0[e] = c0;
-    s_nc[e] = nc;
+    s_cov[2 * e] = c0;
+    s_cov[2 * e + 1] = nc;
     s_bx[e] = bx;
   }
 }
@@ -818,7 +819,7 @@ __device__ __forceinline__ void node_cover(int l0, int l1, int l2, int e, int& c
   ci = (a + 1) * 9 + (b + 1) * 3 + (c + 1);
   loc = slot_loc(l0 - a * kFT0 + 1, l1 - b * kFT1 + 1, l2 - c * kFT2 + 1);
 }
-__device__ __forceinline__ void node_reads(int max_chunks, const int* s_c0, const int* s_nc, const int* s_bx, int l0,
+__device__ __forceinline__ void node_reads(int max_chunks, const int* s_cov, const int* s_bx, int l0,
                                            int l1, int l2, NodeReads& r) {
   const int sec0 = l0 < 3 ? -1 : (l0 == kFT0 - 1 ? 1 : 0);
   const int sec1 = l1 < 3 ? -1 : (l1 == kFT1 - 1 ? 1 : 0);
@@ -834,9 +835,9 @@ __device__ __forceinline__ void node_reads(int max_chunks, const int* s_c0, cons
   for (int e = 0; e < 8; ++e) {
     const int a = (e >> 2) ? sec0 : 0, b = ((e >> 1) & 1) ? sec1 : 0, c = (e & 1) ? sec2 : 0;
     ci[e] = (a + 1) * 9 + (b + 1) * 3 + (c + 1);
-    nc[e] = s_nc[ci[e]];
+    nc[e] = s_cov[2 * ci[e] + 1];
     bx[e] = s_bx[ci[e]];
-    c0[e] = s_c0[ci[e]];
+    c0[e] = s_cov[2 * ci[e]];
   }
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
@@ -859,15 +860,55 @@ __device__ __forceinline__ void add4(float4& a, const float4& b) {
   a.z += b.z;
   a.w += b.w;
 }
-// the further chunks of covering tiles with several (rare: tiles of > 256 particles)
-__device__ __forceinline__ void node_extra(const float4* __restrict__ slots, const int* s_c0, const int* s_nc, int l0,
-                                           int l1, int l2, int extra, float4& acc) {
+// the further chunks of covering tiles with several (tiles of > 256
+// particles: a few in the 100k lego frame, most of the 240k one's).  The
+// second chunks of the 8 covering tiles are read in batches of 4 (a batch's
+// loads in flight together, the zero slot for a tile without one), then the third and
+// later ones (tiles of > 512 particles) one by one.  Until round 5 every extra
+// chunk was a load and its wait inside the loop: one round trip each.
+// one dword a lane, global -> LDS (LDS-DMA): lane l's word lands at
+// lds_base + 4 l (lds_base wave-uniform), tracked by vmcnt like a load
+__device__ __forceinline__ void glds4(const int* src, int* lds_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_base, 4, 0, 0);
+}
+// a window slot by its float4 offset, addressed as the slots' SGPR base plus a
+// 32-bit byte offset (global_load saddr form: one VGPR per address, not a
+// 64-bit pair; the slot array is < 4 GiB, checked where it is sized)
+__device__ __forceinline__ float4 ld_slot(const float4* __restrict__ slots, int off) {
+  return *(const float4*)((const char*)slots + (unsigned)off * 16u);
+}
+#ifndef GSMPM_EXTRA_BATCH
+#define GSMPM_EXTRA_BATCH 4
+#endif
+constexpr int kExtraBatch = GSMPM_EXTRA_BATCH;  // second-chunk loads in flight (8: VGPR spills)
+__device__ __forceinline__ void node_extra(const float4* __restrict__ slots, const int* s_cov, int l0,
+                                           int l1, int l2, int extra2, int zero, float4& acc) {
+  // (the offsets recomputed from the LDS cover table: keeping node_reads'
+  // 8 offsets live across the first batch spilled VGPRs)
+  int o2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    int ci, loc;
+    node_cover(l0, l1, l2, e, ci, loc);
+    o2[e] = ((extra2 >> e) & 1) ? (s_cov[2 * ci] + 1) * kFWin + loc : zero;
+  }
+#pragma unroll
+  for (int h = 0; h < 8; h += kExtraBatch) {
+    float4 u[kExtraBatch];
+#pragma unroll
+    for (int e = 0; e < kExtraBatch; ++e) u[e] = ld_slot(slots, o2[h + e]);
+#pragma unroll
+    for (int e = 0; e < kExtraBatch; ++e) add4(acc, u[e]);
+    __builtin_amdgcn_sched_barrier(0);  // (else the batches merge: 8 in flight, and spills)
+  }
+  int extra = extra2;  // (a tile of <= 512 particles: no iteration)
   while (extra) {
     const int e = __builtin_ctz(extra);
     extra &= extra - 1;
     int ci, loc;
     node_cover(l0, l1, l2, e, ci, loc);
-    for (int w = s_c0[ci] + 1; w < s_c0[ci] + s_nc[ci]; ++w) add4(acc, slots[(size_t)w * kFWin + loc]);
+    for (int w = s_cov[2 * ci] + 2; w < s_cov[2 * ci] + s_cov[2 * ci + 1]; ++w) add4(acc, ld_slot(slots, w * kFWin + loc));
   }
 }
 
@@ -945,59 +986,65 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
   asm volatile("" : "+s"(esc_p), "+s"(cnt_p), "+s"(tch_p));
   const bool recs = ck.rcov != nullptr && !kAtomicGrid;
   const int le = threadIdx.x;  // lane: record entry
-  int2 cov0 = make_int2(1, 0);
-  int bx0 = 0;
-  if (recs && le < 28) {
-    cov0 = ck.rcov[(size_t)i0 * kRecStride + le];
-    bx0 = ck.rbox[(size_t)i0 * kRecStride + le];
+  // Cover records reach LDS by LDS-DMA (global_load_lds: no VGPR holds
+  // them): buffer b of s_rec / s_box holds the tile being updated, and at the
+  // top of each iteration the NEXT tile's record and id are requested into
+  // the other buffer, so a workgroup owning several tiles (config D: ~27 a
+  // launch) pays one round trip a tile (its slot loads) instead of two.  A
+  // record is 64 dwords (27 {first chunk, count} pairs + the "none" flag at
+  // dword 54) and its boxes 32; lane le moves dword le of each (the boxes'
+  // upper half a harmless copy of the lower).
+  __shared__ int s_rec[2][64];
+  __shared__ int s_box[2][64];
+  __shared__ int s_tn[2];
+  // (wave 0's lanes only: the DMA writes lds_base + 4 x lane-in-wave)
+  if (recs && threadIdx.x < 64) {
+    glds4(reinterpret_cast<const int*>(ck.rcov) + (size_t)i0 * 2 * kRecStride + le, &s_rec[0][0]);
+    glds4(ck.rbox + (size_t)i0 * kRecStride + (le & 31), &s_box[0][0]);
   }
   typedef const int __attribute__((address_space(1)))* gint_p;  // global, not flat (flat loads count in lgkmcnt too)
-  const int esc0 = *(gint_p)esc_p;
-  const int cnt0 = ((gint_p)cnt_p)[1];
-  const int T0 = ((gint_p)tch_p)[i0];
-  if (blockIdx.x == 0 && threadIdx.x == 0 && pass != 1) *esc_clear = 0;
-  if (zc && pass != 1) {
-    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t <= tl.ntiles; t += gridDim.x * blockDim.x) {
-      zc[t] = 0;
-      if (t < tl.ntiles) zf[t] = 0;
-    }
-  }
+  // (uniform words: readfirstlane keeps them in SGPRs, not three VGPRs live across the tile loop)
+  const int esc0 = __builtin_amdgcn_readfirstlane(*(gint_p)esc_p);
+  const int cnt0 = __builtin_amdgcn_readfirstlane(((gint_p)cnt_p)[1]);
+  const int T0 = __builtin_amdgcn_readfirstlane(((gint_p)tch_p)[i0]);
   const int ng = g.ng;
   const bool all = esc0 != 0;
   const int ntouch = kGridParts * (all ? tl.ntiles : cnt0);
-  __shared__ int s_c0[27], s_nc[27], s_bx[27];
-  __shared__ int s_none;
-  for (int wt = blockIdx.x; wt < ntouch; wt += gridDim.x) {
+  const bool pre = recs && !all;  // workgroup-uniform: records in LDS, the next one prefetched
+  int b = 0;
+  for (int wt = blockIdx.x; wt < ntouch; wt += gridDim.x, b ^= 1) {
+    if constexpr (!kAtomicGrid) {
+      // this tile's DMA (issued a tile ago, or in the prologue) has landed;
+      // readers of the other buffer are done.  The wait is explicit: the
+      // compiler's own waits for LDS-DMA did not cover every read of these
+      // arrays (the slab test caught stale records), and a one-wave
+      // workgroup's barrier compiles to nothing.  What else it waits for is
+      // the previous tile's v_out stores (L2 write acks, not an HBM trip).
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const int wn = wt + (int)gridDim.x;
+      if (pre && wn < ntouch && threadIdx.x < 64) {  // workgroup-uniform (kGridT = 64: one wave)
+        const int pn = wn / kGridParts;
+        glds4(reinterpret_cast<const int*>(ck.rcov) + (size_t)pn * 2 * kRecStride + le, &s_rec[b ^ 1][0]);
+        glds4(ck.rbox + (size_t)pn * kRecStride + (le & 31), &s_box[b ^ 1][0]);
+        if (le == 0) glds4(ck.touched + pn, &s_tn[b ^ 1]);
+      }
+    }
+    int* s_cov = s_rec[b];
+    int* s_bx = s_box[b];
     const int q = threadIdx.x + (wt % kGridParts) * kGridT;
     const int l0 = q / (kFT1 * kFT2), l1 = (q / kFT2) % kFT1, l2 = q % kFT2;
-    const int T = all ? wt / kGridParts : wt == (int)blockIdx.x ? T0 : ck.touched[wt / kGridParts];
+    const int T = all ? wt / kGridParts : wt == (int)blockIdx.x ? T0 : pre ? s_tn[b] : ck.touched[wt / kGridParts];
     if ((unsigned)T >= (unsigned)tl.ntiles) continue;  // workgroup-uniform; never taken (wt < parts x count)
     int ti, tj, tk;
     ftile_decode(tl, T, ti, tj, tk);
     if (SLAB && pass != 0 && slab_tile_in_window(sw, ti) != (pass == 1)) continue;  // workgroup-uniform
     if constexpr (!kAtomicGrid) {
-      __syncthreads();  // readers of the previous tile's ranges are done
       if (wt == (int)blockIdx.x) stamp(3, 2);
-      bool tables = all || !recs;  // workgroup-uniform
-      if (!tables) {
-        int2 cv = cov0;
-        int bx = bx0;
-        if (wt != (int)blockIdx.x && le < 28) {
-          const size_t r = (size_t)(wt / kGridParts) * kRecStride + le;
-          cv = ck.rcov[r];
-          bx = ck.rbox[r];
-        }
-        if (le < 27) {
-          s_c0[le] = cv.x;
-          s_nc[le] = cv.y;
-          s_bx[le] = bx;
-        }
-        if (le == 27) s_none = cv.x;
-        __syncthreads();
-        tables = s_none != 0;  // a tile k_fused appended (add_lower_tiles): no record
-      }
+      // a tile k_fused appended (add_lower_tiles) has no record: "none" flag
+      const bool tables = !pre || s_cov[54] != 0;  // workgroup-uniform
       if (tables) {
-        load_cover27(ck, tbox, tl, ti, tj, tk, s_c0, s_nc, s_bx);
+        load_cover27(ck, tbox, tl, ti, tj, tk, s_cov, s_bx);
         __syncthreads();
       }
     }
@@ -1012,14 +1059,14 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
         if (a.x != 0.f || a.y != 0.f || a.z != 0.f || a.w != 0.f) gacc[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
       } else {
         NodeReads r;
-        node_reads(tl.max_chunks, s_c0, s_nc, s_bx, l0, l1, l2, r);
+        node_reads(tl.max_chunks, s_cov, s_bx, l0, l1, l2, r);
         reach = r.live != 0;
         float4 v[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = slots[r.off[e]];
+        for (int e = 0; e < 8; ++e) v[e] = ld_slot(slots, r.off[e]);
 #pragma unroll
         for (int e = 0; e < 8; ++e) add4(a, v[e]);
-        node_extra(slots, s_c0, s_nc, l0, l1, l2, r.extra, a);
+        if (r.extra) node_extra(slots, s_cov, l0, l1, l2, r.extra, tl.max_chunks * kFWin, a);
         if (all) {
           add4(a, gacc[idx]);
           gacc[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1045,6 +1092,15 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
       }
     }
     if (wt == (int)blockIdx.x) stamp(3, 4);
+  }
+  // the zeroing for the next launches, after the tiles: its stores are not
+  // in front of any wait above
+  if (blockIdx.x == 0 && threadIdx.x == 0 && pass != 1) *esc_clear = 0;
+  if (zc && pass != 1) {
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t <= tl.ntiles; t += gridDim.x * blockDim.x) {
+      zc[t] = 0;
+      if (t < tl.ntiles) zf[t] = 0;
+    }
   }
   stamp(3, 1);
 }

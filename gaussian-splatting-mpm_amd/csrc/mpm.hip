@@ -510,7 +510,10 @@ __global__ __launch_bounds__(256) void k_p2g(Particles ps, GridDims g, Tiles tl,
 // (boundary_conditions.py:23-27) / MPM_Collider.collide (collider.py:13-44),
 // pointwise, in list order.
 struct GridStep {
-  float dt, gx, gy, gz;
+  // dgx..dgz: dt * gravity, the f32 product formed on the host (the same
+  // rounding as the device multiply; as three uniform VALU products hoisted
+  // out of k_grid_f's tile loop they held three VGPRs it needs)
+  float dt, dgx, dgy, dgz;
   uint32_t mask;
   int keep;
 };
@@ -522,9 +525,9 @@ __device__ __forceinline__ float4 node_update(const float4& a, int i, int j, int
                                               const GridStep& gs, const BcTable* __restrict__ bct) {
   float v[3] = {0.f, 0.f, 0.f};
   if (a.w > 1e-15f) {
-    v[0] = a.x / a.w + gs.dt * gs.gx;
-    v[1] = a.y / a.w + gs.dt * gs.gy;
-    v[2] = a.z / a.w + gs.dt * gs.gz;
+    v[0] = a.x / a.w + gs.dgx;
+    v[1] = a.y / a.w + gs.dgy;
+    v[2] = a.z / a.w + gs.dgz;
     const int nops = bct->n_ops;
     for (int o = 0; o < nops; ++o) {
       const GridOp& op = bct->op[o];
@@ -1774,9 +1777,9 @@ static int rebin(gsmpm_mpm* h, hipStream_t st) { return use_fused(h) ? rebin_f(h
 static GridStep grid_step(gsmpm_mpm* h, float dt, uint32_t mask) {
   GridStep gs;
   gs.dt = dt;
-  gs.gx = (float)h->prm.gravity[0];
-  gs.gy = (float)h->prm.gravity[1];
-  gs.gz = (float)h->prm.gravity[2];
+  gs.dgx = dt * (float)h->prm.gravity[0];
+  gs.dgy = dt * (float)h->prm.gravity[1];
+  gs.dgz = dt * (float)h->prm.gravity[2];
   gs.keep = (h->prm.flags & GSMPM_FLAG_KEEP_GRID) ? 1 : 0;
   gs.mask = mask;
   return gs;
@@ -2341,6 +2344,10 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
   h->ftl.td2 = (h->g.ng + kFT2 - 1) / kFT2;
   h->ftl.ntiles = h->ftl.td0 * h->ftl.td1 * h->ftl.td2;
   h->ftl.max_chunks = h->n / kChunk + std::min(h->ftl.ntiles + 1, h->n) + 1;
+  // k_grid_f addresses the window slots with 32-bit byte offsets (fused.h
+  // ld_slot): a rank whose slot array would pass 4 GiB (~40M particles) runs
+  // the per-phase pipeline instead
+  if (h->fused && sizeof(float4) * (size_t)(h->ftl.max_chunks + 1) * kFWin > 0xffffffffull) h->fused = false;
   if (h->fused) {
     const size_t E = (size_t)h->ftl.ntiles + 1;
     if ((e = hipMalloc(&h->fslots, sizeof(float4) * (size_t)(h->ftl.max_chunks + 1) * kFWin)) != hipSuccess)
