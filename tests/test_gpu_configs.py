@@ -299,6 +299,45 @@ def test_dense_tiles_multi_chunk(dev, material, fcr):
     _dump(f"dense_tiles_{material}", {"errs": errs, "max_per_tile": stats["max_per_tile"]})
 
 
+def test_spread_scene_grid_update_loops(dev):
+    """More touched tiles than k_grid_f's grid covers in one round (7 x 1,024
+    one-wave workgroups): particles spread over a whole 128^3 grid touch
+    ~4,800 tiles, so every grid workgroup updates several tiles in turn --
+    the cover records' LDS-DMA path with the next tile's record prefetched
+    into the second buffer (fused.h k_grid_f), on a grid small enough for
+    k_finish_bins' records.  FCR jelly with gravity and the ground collider,
+    30 substeps with re-binning, against the oracle at 1e-4."""
+    import oracle as O
+    import torch
+    from gsmpm.sim import Simulator
+    rng = np.random.default_rng(11)
+    n, ng, ext = 60_000, 128, 2.0
+    x = rng.uniform(0.1, 1.9, size=(n, 3)).astype(np.float32)
+    x[:, 2] = np.maximum(x[:, 2], np.float32(0.45))
+    cov = np.tile(np.array([4e-5, 0, 0, 4e-5, 0, 4e-5], np.float32), (n, 1))
+    vol = O.particle_volume(x, ng, ext)
+    kw = dict(n_grid=ng, grid_extent=ext, material="jelly", E=2e5, nu=0.3, density=200.0, gravity=(0, 0, -9.8))
+    ref = O.OracleMPM(x, cov, vol, jelly_quirk=False, threaded=True, **kw)
+    ref.add_collider([0.0, 0.0, 0.4], [0.0, 0.0, 1.0], 0.0)
+    sim = Simulator(n, jelly_fcr=True, **kw)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    sim.set_particles(t(x), t(cov), t(vol))
+    sim.add_plane_collider([0.0, 0.0, 0.4], [0.0, 0.0, 1.0], 0.0)
+    assert sim.pipeline == "fused"
+    dt = 1e-4
+    for _ in range(30):
+        ref.substep(dt, [], [1])
+    sim.step(dt, [0xFFFFFFFF] * 30)
+    stats = sim.debug_stats()
+    assert stats["touched_tiles"] > 2 * 1024, stats
+    got = {"x": sim.get("x"), "v": sim.get("v"), "C": sim.get("C"), "F_trial": sim.get("F_trial")}
+    exp = {"x": ref.x, "v": ref.v, "C": ref.C, "F_trial": ref.F_trial}
+    errs = {k: rel_err(got[k].cpu().numpy().reshape(exp[k].shape), exp[k]) for k in got}
+    errs["C"] = _c_err(got["C"].cpu().numpy(), ref.C, ref.v, ng / ext)
+    _check(errs, "spread scene", {"F_trial": 1e-4}, stress=True)
+    _dump("spread_scene_grid_loops", {"errs": errs, "touched_tiles": stats["touched_tiles"]})
+
+
 # ------------------------------------------------------------------ (a4) --
 @pytest.mark.parametrize("n,ng,box", [(100_000, 128, "lego"), (1_000_000, 256, "bicycle"), (5000, 64, "lego"),
                                       (3000, 48, "grid")])
