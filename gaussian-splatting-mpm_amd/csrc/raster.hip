@@ -458,6 +458,12 @@ __global__ __launch_bounds__(256) void k_ranges(int L, const unsigned long long*
 constexpr int kU = 8;
 constexpr int kQ = 4;            // list entries per lane per batch
 constexpr int kBatch = 64 * kQ;  // entries staged per batch
+// k_render's own batch (A/B: GSMPM_RENDER_Q; k_render4 stages kBatch, one entry a lane)
+#ifndef GSMPM_RENDER_Q
+#define GSMPM_RENDER_Q 4
+#endif
+constexpr int kQR = GSMPM_RENDER_Q;
+constexpr int kBatchR = 64 * kQR;
 
 
 // Tile keys of the depth-ordered path carry, above the tile index, a mask of
@@ -493,9 +499,9 @@ __global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges,
                                                float* __restrict__ final_T, int* __restrict__ n_contrib,
                                                const unsigned* __restrict__ tkeys, int mode, int xcd, int ntiles,
                                                int nq) {
-  __shared__ float2 s_xy[kBatch];
-  __shared__ float4 s_co[kBatch];
-  __shared__ float4 s_rgb[kBatch];  // .w: the entry's tile-list index (as int bits)
+  __shared__ float2 s_xy[kBatchR];
+  __shared__ float4 s_co[kBatchR];
+  __shared__ float4 s_rgb[kBatchR];  // .w: the entry's tile-list index (as int bits)
   // one quarter per workgroup, or (a grid of fewer workgroups, a multiple of 8
   // so a quarter keeps its XCD) quarters L, L + grid, ...
   for (int L = blockIdx.x; L < nq; L += gridDim.x) {
@@ -512,7 +518,7 @@ __global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges,
   float T = 1.0f, C0 = 0.f, C1 = 0.f, C2 = 0.f;
   int last = 0;
   bool done = !inside;
-  // lane holds entries j0 + 64 q + lane, q < kQ
+  // lane holds entries j0 + 64 q + lane, q < kQR
   // with tkeys (the depth-ordered sort's keys), an entry's sub-tile mask says
   // whether it reaches this quarter: the gather of one that does not is
   // skipped; without, the quarter test runs on the gathered conic
@@ -522,21 +528,21 @@ __global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges,
   // used, a batch later: testing a key right after its load (a bool kept
   // across the blend) made the compiler wait for each load where it was
   // issued -- the "prefetch" of the next batch's ids and keys stalled the
-  // wave for kQ round trips in front of every blend.
-  float2 g_xy[kQ];
-  float4 g_co[kQ], g_rgb[kQ];
-  unsigned gid[kQ], gkey[kQ], nid[kQ], nkey[kQ];
-  bool g_rel[kQ];
+  // wave for kQR round trips in front of every blend.
+  float2 g_xy[kQR];
+  float4 g_co[kQR], g_rgb[kQR];
+  unsigned gid[kQR], gkey[kQR], nid[kQR], nkey[kQR];
+  bool g_rel[kQR];
 #pragma unroll
-  for (int q = 0; q < kQ; ++q) {  // batch 0's ids and keys, and batch 1's, all issued first
-    const bool v0 = 64 * q + lane < n, v1 = kBatch + 64 * q + lane < n;
+  for (int q = 0; q < kQR; ++q) {  // batch 0's ids and keys, and batch 1's, all issued first
+    const bool v0 = 64 * q + lane < n, v1 = kBatchR + 64 * q + lane < n;
     gid[q] = v0 ? lst[64 * q + lane] : 0u;
     gkey[q] = (v0 && tk) ? tk[64 * q + lane] : qbit;
-    nid[q] = v1 ? lst[kBatch + 64 * q + lane] : 0u;
-    nkey[q] = (v1 && tk) ? tk[kBatch + 64 * q + lane] : qbit;
+    nid[q] = v1 ? lst[kBatchR + 64 * q + lane] : 0u;
+    nkey[q] = (v1 && tk) ? tk[kBatchR + 64 * q + lane] : qbit;
   }
 #pragma unroll
-  for (int q = 0; q < kQ; ++q) {
+  for (int q = 0; q < kQR; ++q) {
     g_xy[q] = make_float2(0.f, 0.f);
     g_co[q] = g_rgb[q] = make_float4(0.f, 0.f, 0.f, 0.f);
     g_rel[q] = 64 * q + lane < n && (gkey[q] & qbit);
@@ -546,13 +552,13 @@ __global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges,
       g_rgb[q] = rgbo[gid[q]];
     }
   }
-  for (int j0 = 0; j0 < n; j0 += kBatch) {
+  for (int j0 = 0; j0 < n; j0 += kBatchR) {
     if (__all(done)) break;
     // stage the batch's survivors in list order; slots up to the next
     // multiple of kU are zero (opacity 0: alpha 0, and fma(0, 0, C) = C)
     int cnt = 0;
 #pragma unroll
-    for (int q = 0; q < kQ; ++q) {
+    for (int q = 0; q < kQR; ++q) {
       const int j = j0 + 64 * q + lane;
       const bool keep = j < n && g_rel[q] && (tk || (mode & 1) || reaches_subtile(g_xy[q], g_co[q], fx0, fy0));
       const unsigned long long m = __ballot(keep);
@@ -575,18 +581,18 @@ __global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges,
     // (every test first -- its words were loaded a batch ago -- then every
     // gather: a test between two gathers is a wait for an older load, which
     // the in-order counter turns into a wait for the gather just issued)
-    const float2* pxy[kQ];
-    const float4 *pco[kQ], *prgb[kQ];
+    const float2* pxy[kQR];
+    const float4 *pco[kQR], *prgb[kQR];
 #pragma unroll
-    for (int q = 0; q < kQ; ++q) {
-      g_rel[q] = j0 + kBatch + 64 * q + lane < n && (nkey[q] & qbit);
+    for (int q = 0; q < kQR; ++q) {
+      g_rel[q] = j0 + kBatchR + 64 * q + lane < n && (nkey[q] & qbit);
       pxy[q] = xy + nid[q];
       pco[q] = conic_o + nid[q];
       prgb[q] = rgbo + nid[q];
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int q = 0; q < kQ; ++q) {
+    for (int q = 0; q < kQR; ++q) {
       if (g_rel[q]) {
         g_xy[q] = *pxy[q];
         g_co[q] = *pco[q];
@@ -594,10 +600,10 @@ __global__ __launch_bounds__(64) void k_render(const uint2* __restrict__ ranges,
       }
     }
 #pragma unroll
-    for (int q = 0; q < kQ; ++q) {
-      const bool v = j0 + 2 * kBatch + 64 * q + lane < n;
-      nid[q] = v ? lst[j0 + 2 * kBatch + 64 * q + lane] : 0u;
-      nkey[q] = (v && tk) ? tk[j0 + 2 * kBatch + 64 * q + lane] : qbit;
+    for (int q = 0; q < kQR; ++q) {
+      const bool v = j0 + 2 * kBatchR + 64 * q + lane < n;
+      nid[q] = v ? lst[j0 + 2 * kBatchR + 64 * q + lane] : 0u;
+      nkey[q] = (v && tk) ? tk[j0 + 2 * kBatchR + 64 * q + lane] : qbit;
     }
     for (int b = 0; b < cnt; b += kU) {
       if (__all(done)) break;
