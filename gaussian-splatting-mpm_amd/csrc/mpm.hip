@@ -1534,7 +1534,7 @@ struct gsmpm_mpm {
   bool lane_balance = true;               // GSMPM_LANE_BALANCE=0 turns it off (A/B)
   bool fuse_permute = true;               // GSMPM_FUSE_PERMUTE=0: separate k_permute (A/B)
   bool cover_records = true;              // GSMPM_COVER_RECORDS=0: k_grid_f reads the tile tables only (A/B)
-  int fused_wgs = 1024;                   // k_fused grid cap: the workgroups resident at once (init)
+  int fused_wgs = 1024;                   // k_fused grid cap: the workgroups resident at once x rounds of full chunks, <= 6 (init)
   float* planes_alt = nullptr;            // the other particle-plane buffer: every binning permutes
   int* orig_alt = nullptr;                //   storage into bin order, alternating planes / planes_alt
   int fbpar = 0;                          // parity of the bins the next k_fused reads
@@ -2335,8 +2335,18 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
     if (hipGetDevice(&dev) == hipSuccess &&
         hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_fused<0, 3>, 256, 0) == hipSuccess && ncu > 0 &&
-        per_cu > 0)
-      h->fused_wgs = ncu * per_cu;
+        per_cu > 0) {
+      // one round of resident workgroups, or -- a scene of several rounds of
+      // full chunks (bicycle's 1M: ~30,000 chunks of ~33 particles) -- up to
+      // 6 rounds' worth, so workgroups own fewer chunks each and the
+      // dispatcher refills CUs as chunks finish.  Bicycle's k_fused (A/B,
+      // GSMPM_FUSED_WGS): 100.8 us at 1 round, 99.2 at 2, 96.7 at 3, 94.4 at 6,
+      // 98.5 at one workgroup a chunk; B' (240,549, 1.2 rounds) lost frame
+      // time at 2 rounds, so the factor is the floor of the rounds
+      const int resident = ncu * per_cu;
+      const int rounds = (int)std::min<long long>(6, std::max<long long>(1, (long long)h->n / ((long long)resident * kChunk)));
+      h->fused_wgs = resident * rounds;
+    }
     if (const char* fw = std::getenv("GSMPM_FUSED_WGS")) h->fused_wgs = std::max(1, std::atoi(fw));
   }
   h->ftl.td0 = (h->g.ng + kFT0 - 1) / kFT0;
