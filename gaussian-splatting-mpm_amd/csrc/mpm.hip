@@ -48,7 +48,13 @@ namespace gsmpm {
 #define GSMPM_REBIN_SF 20
 #endif
 constexpr int kRebinStressFree = GSMPM_REBIN_SF;  // default re-binning interval, stress-free materials
-constexpr int kRebinStress = 10;                  // ... stress-bearing ones
+// ... stress-bearing ones: 20 as well since round 5 (lego-fracture metal, 3
+// rounds: value 2.628 -> 2.672e9, frame 3.80 -> 3.74 ms against 10;
+// profiles/r05/ab/ab_rebin_interval_metal_r05ax.txt)
+#ifndef GSMPM_REBIN_STRESS
+#define GSMPM_REBIN_STRESS 20
+#endif
+constexpr int kRebinStress = GSMPM_REBIN_STRESS;
 constexpr int kChunk = 256;  // particles per work chunk (one per lane of a 256-lane workgroup)
 
 // Workgroup timeline stamps (diagnostics): [kernel][wg][start, end] in
