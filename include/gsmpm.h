@@ -203,7 +203,7 @@ int gsmpm_mpm_slab_bounds(gsmpm_mpm* h, int32_t* out, int32_t n, int64_t* rebala
 int gsmpm_mpm_resort(gsmpm_mpm* h, int32_t interval, void* stream);
 
 /* Fused pipeline: substeps between re-binnings of the particles into tiles
- * (at most; default 20 for stress-free jelly, 10 for stress-bearing materials; any
+ * (at most; default 20 for every material since round 5; any
  * value is correct -- particles that moved more than one cell
  * since their binning take a slower global path).  No counterpart in the
  * reference (its p2g2p has no binning, solver.py:27-52). */
