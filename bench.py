@@ -68,16 +68,18 @@ def parse():
     ap.add_argument("--no-extra-configs", action="store_true",
                     help="skip the driver-timed config C (metal) / D (bicycle 1M, 256^3) side runs")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--multi", choices=("dp", "slab"), default="dp",
-                    help="N > 1 headline: dp = independent lego scenes per rank (default, weak scaling); slab = one "
-                         "lego scene sharded by spatial slab over RCCL (strong scaling)")
+    ap.add_argument("--multi", choices=("dp", "slab"), default="slab",
+                    help="N > 1 headline: slab = one lego scene sharded by spatial slab over RCCL (default, "
+                         "north_star's design, strong scaling); dp = independent lego scenes per rank (weak scaling)")
     ap.add_argument("--dp", action="store_const", const="dp", dest="multi", help="= --multi dp")
     ap.add_argument("--slab", action="store_const", const="slab", dest="multi", help="= --multi slab")
     ap.add_argument("--no-multi-configs", action="store_true",
-                    help="N > 1: skip the slab / sim-render-split side measurements (multi_gpu)")
-    ap.add_argument("--multi-configs", default="lego,bicycle,split",
-                    help="N > 1: which side measurements multi_gpu holds (lego slab, bicycle slab, lego sim/render "
-                         "split)")
+                    help="N > 1: skip the side measurements (multi_gpu)")
+    ap.add_argument("--multi-configs", default=None,
+                    help="N > 1: which side measurements multi_gpu holds: bicycle (config D through the slabs), "
+                         "dp (one lego scene per rank), lego (the lego slab form, when the headline is dp), split "
+                         "(lego's sim / render split); default: bicycle,dp under the slab headline, "
+                         "bicycle,lego under --dp")
     ap.add_argument("--rebin", type=int, default=0, help="fused pipeline: substeps between re-binnings (0: library default)")
     ap.add_argument("--render-overlap", type=int, default=int(os.environ.get("GSMPM_BENCH_RENDER_OVERLAP", "1")),
                     help="1: frame f-1 renders on a second stream while frame f simulates; 0: each frame renders "
@@ -324,12 +326,16 @@ def measured_traffic(kernel, workload):
 
 
 def kernel_roofline(n, n_grid, material, live_nodes, us_per_launch, workload):
-    """Per-kernel roofline figures of the fused pipeline: the live-node bytes
-    and their fraction of the HBM peak, the PMC-measured HBM traffic (when it
-    matches the workload and sources) and its fraction, and the SURVEY 8(d)
-    dense bytes as a rate only: the dense grid is what the reference sweeps,
-    not what this kernel moves, so its "fraction" can exceed 1 (config D's
-    k_grid_f) and is not reported as one."""
+    """Per-kernel roofline figures of the fused pipeline, on the live-byte
+    basis: `bytes` = the bytes the kernel must move at least (208 N particle
+    planes (+ 8 N plastic) + 28 B per live node for k_fused, 28 B per live node
+    for k_grid_f; live nodes = touched tiles x 448), `frac` = bytes / launch
+    time / HBM peak (<= 1 by construction), and beside it the PMC-measured HBM
+    traffic (when it matches the workload and sources) with its fraction.  The
+    SURVEY 8(d) dense n^3 figure is what the reference sweeps, not what these
+    kernels move, so it is given as bytes only (`dense_contract_bytes`), never
+    as a rate or fraction.  `substep` = both kernels' bytes over their summed
+    time: the whole-substep fraction."""
     dense = algorithmic_bytes(n, n_grid, material)
     live = algorithmic_bytes_live(n, live_nodes, material)
     out = {}
@@ -338,10 +344,17 @@ def kernel_roofline(n, n_grid, material, live_nodes, us_per_launch, workload):
             continue
         t = us * 1e-6
         tr = measured_traffic(k, workload)
-        out[k] = {"us_per_launch": round(us, 2),
-                  "dense_bytes": dense[k], "dense_rate_GBps": round(dense[k] / t / 1e9, 1),
-                  "live_bytes": live[k], "frac_sparse": round(live[k] / t / 1e9 / HBM_PEAK_GBS, 4),
-                  "traffic": tr, "traffic_frac": None if tr is None else round(tr / t / 1e9 / HBM_PEAK_GBS, 4)}
+        out[k] = {"us_per_launch": round(us, 2), "bytes": live[k],
+                  "achieved_GBps": round(live[k] / t / 1e9, 1),
+                  "frac": round(live[k] / t / 1e9 / HBM_PEAK_GBS, 4),
+                  "traffic": tr, "traffic_frac": None if tr is None else round(tr / t / 1e9 / HBM_PEAK_GBS, 4),
+                  "dense_contract_bytes": dense[k]}
+    if all(k in out for k in ("k_fused", "k_grid_f")):
+        b = live["k_fused"] + live["k_grid_f"]
+        t = (us_per_launch["k_fused"] + us_per_launch["k_grid_f"]) * 1e-6
+        out["substep"] = {"kernels": ["k_fused", "k_grid_f"], "bytes": b,
+                          "us": round(t * 1e6, 2), "achieved_GBps": round(b / t / 1e9, 1),
+                          "frac": round(b / t / 1e9 / HBM_PEAK_GBS, 4)}
     return out
 
 
@@ -498,17 +511,29 @@ def other_configs(args, dev, frames=3, rank=0, world=1, xp=None, sync=None):
     return res
 
 
-def slab_frames(args, dev, rank, world, xp, barrier, red_dev, cfg, n, ng, frames=3, settle=4, weighted=True):
+def slab_exchange_bytes(sim):
+    """Bytes this rank sends per substep in the grid-window exchange (the same
+    count arrives): float4 (m v, m) partials over the window planes x the
+    exchanged yz rect of each window that has a neighbour (slab_host.inc,
+    slab_grid_phase)."""
+    st = sim.stats()
+    w = int(st["window_planes"])
+    return sum(16 * w * ny * nz for (_, ny, _, nz) in sim.engine.slab_rects() if ny > 0 and nz > 0)
+
+
+def slab_frames(args, dev, rank, world, xp, barrier, red_dev, cfg, n, ng, frames=3, warmup=6, weighted=True):
     """One scene sharded by slab over the N ranks, frame by frame as main.py
     runs it (step, postprocess, gather to rank 0, rank 0 renders), with the
     render-aware re-cut: rank 0 measures its simulation and render times and
-    takes the particle share sim / (sim + render) (SlabDomain.set_render_share,
-    gsmpm_mpm_slab_set_weight), `settle` frames let the library's re-cut move
-    the bounds, then `frames` frames are timed barrier to barrier (max over
-    ranks).  Per-rank fields: each rank's simulation device time per frame
-    (hipEvents around its step call), its particle count, and rank 0's render
-    and gather host times (the gather includes the wait for the slowest
-    rank's simulation)."""
+    takes the particle share given by SlabDomain.set_render_share
+    (gsmpm_mpm_slab_set_weight); `warmup` untimed frames (the graph capture,
+    the share measurement, and frames that let the library's re-cut move the
+    bounds), then `frames` frames timed barrier to barrier (max over ranks).
+    Per-rank fields: each rank's simulation device time per frame (hipEvents
+    around its step call), its particle count, the bytes it sends per substep
+    in the window exchange, its migrations, and rank 0's render and gather
+    host times (the gather includes the wait for the slowest rank's
+    simulation)."""
     import copy
     import torch
     import torch.distributed as dist
@@ -557,37 +582,94 @@ def slab_frames(args, dev, rank, world, xp, barrier, red_dev, cfg, n, ng, frames
     sim_ms, render_ms = acc["sim"], acc["render"]
     weight = 1.0
     if weighted and rank == 0:
-        weight = sim.set_render_share(sim_ms, render_ms)
-    for _ in range(settle):
+        weight = sim.set_render_share(sim_ms, render_ms, world)
+    for _ in range(max(0, warmup - 2)):
         frame(False)
     barrier()
     acc.update(sim=0.0, render=0.0, gather=0.0)
+    st0 = sim.stats()
     t0 = time.perf_counter()
     for _ in range(frames):
         frame(True)
     barrier()
     el = time.perf_counter() - t0
+    st1 = sim.stats()
     tt = torch.tensor([el], dtype=torch.float64, device=red_dev)
     dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     el = float(tt.item())
-    mine = torch.tensor([acc["sim"] / frames, float(sim.n)], dtype=torch.float64, device=red_dev)
+    mine = torch.tensor([acc["sim"] / frames, float(sim.n), float(slab_exchange_bytes(sim)),
+                         float(st1["migrations"] - st0["migrations"]), float(st1["migrated"] - st0["migrated"])],
+                        dtype=torch.float64, device=red_dev)
     allr = [torch.zeros_like(mine) for _ in range(world)]
     dist.all_gather(allr, mine)
     nsim = sc["xg"].shape[0]
     r = {"config": cfg, "particles": nsim, "n_grid": sa.n_grid, "parallelism": f"slab{world}", "scaling": "strong",
-         "frame_ms": round(el / frames * 1e3, 4), "particle_substeps_per_s": nsim * spf * frames / el,
+         "frames": frames, "substeps_per_frame": spf, "frame_ms": round(el / frames * 1e3, 4),
+         "particle_substeps_per_s": nsim * spf * frames / el,
          "per_rank_sim_ms": [round(float(x[0]), 4) for x in allr],
          "per_rank_particles": [int(x[1]) for x in allr],
+         "per_rank_exchange_bytes_per_substep": [int(x[2]) for x in allr],
+         "per_rank_migrations_per_frame": [round(float(x[3]) / frames, 2) for x in allr],
+         "per_rank_migrated_per_frame": [round(float(x[4]) / frames, 1) for x in allr],
          "rank0_render_ms": round(acc["render"] / frames, 4), "rank0_gather_ms": round(acc["gather"] / frames, 4),
          "rank0_weight": round(weight, 4), "rank0_first_frame": {"sim_ms": round(sim_ms, 4),
                                                                  "render_ms": round(render_ms, 4)},
          "render": f"{cam.width}x{cam.height} SH3", "num_rendered": acc["K"] if rank == 0 else None,
-         "slab_bounds": sim.bounds, "slab_recuts": sim.rebalances}
+         "slab_bounds": sim.bounds, "slab_recuts": sim.rebalances, "cut_axis": sim.cut_axis}
     sim.engine.close()
     barrier()
     del sim, sc
     torch.cuda.empty_cache()
     return r
+
+
+def dp_frames(args, dev, rank, world, barrier, red_dev, frames=5, warmup=2):
+    """N independent lego scenes, one per rank (synthetic seed = rank), each
+    simulated and rendered in main.py's order on its own GPU with no
+    collective in the data path: the replicas form of the N > 1 job, kept
+    beside north_star's slab sharding (weak scaling: value = all ranks'
+    particle-substeps / the slowest rank's time)."""
+    import torch
+    import torch.distributed as dist
+    from gsmpm import raster
+    from gsmpm.bc import substep_masks
+    sc = build_scene(args, dev, rank=rank)
+    sim, specs = make_sim(sc, dev)
+    sa = sc["sargs"]
+    dt, spf = sa.substep_dt, sa.steps_per_frame
+    cam, g, mask = sc["cam"], sc["g"], sc["mask"]
+    feats, opac = g.get_features[mask].contiguous(), g.get_opacity[mask].reshape(-1).contiguous()
+    tx, ty = math.tan(cam.FovX * 0.5), math.tan(cam.FovY * 0.5)
+    bg = torch.zeros(3, device=dev)
+    w_args = (float(sc["s"]), [float(v) for v in sc["c"].reshape(-1).tolist()])
+    st = {"t": 0.0}
+
+    def frame():
+        masks, st["t"] = substep_masks(specs, st["t"], dt, spf)
+        sim.step(dt, masks)
+        sim.postprocess()
+        m, c = sim.world_outputs(*w_args, render_space=True)
+        raster.forward(m, opac, cam.view_mat, cam.full_proj_mat, cam.cam_center, bg, cam.height, cam.width, tx, ty,
+                       sh_degree=3, shs=feats, cov3D_precomp=c)
+
+    for _ in range(warmup):
+        frame()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(frames):
+        frame()
+    barrier()
+    el = time.perf_counter() - t0
+    tt = torch.tensor([el, float(sim.n)], dtype=torch.float64, device=red_dev)
+    nt = tt.clone()
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    dist.all_reduce(nt)
+    el, n_total = float(tt[0].item()), int(nt[1].item())
+    del sim, sc
+    torch.cuda.empty_cache()
+    return {"config": args.config, "parallelism": f"dp{world} independent scenes", "scaling": "weak",
+            "particles_total": n_total, "frames": frames, "frame_ms": round(el / frames * 1e3, 4),
+            "particle_substeps_per_s": n_total * spf * frames / el}
 
 
 def sim_render_split(args, dev, rank, world, barrier, red_dev, frames=5):
@@ -668,19 +750,20 @@ def sim_render_split(args, dev, rank, world, barrier, red_dev, frames=5):
 
 
 def multi_gpu_configs(args, dev, rank, world, xp, barrier, red_dev):
-    """N > 1 side measurements (north_star's slab sharding; the round-4
-    verdict's items 2 and 3): lego and config D through the slab path with the
-    render-aware re-cut, and lego's sim / render split."""
+    """N > 1 side measurements beside the slab headline: config D (bicycle 1M,
+    256^3) through the slab path with the render-aware re-cut, the replicas
+    form (one lego scene per rank), and lego's sim / render split."""
     import torch
     res = {}
-    which = set(args.multi_configs.split(","))
+    which = set((args.multi_configs or ("bicycle,dp" if args.multi == "slab" else "bicycle,lego")).split(","))
     torch.cuda.empty_cache()
-    if "lego" in which:
-        res["B_lego_slab"] = slab_frames(args, dev, rank, world, xp, barrier, red_dev, args.config, args.particles,
-                                         args.n_grid)
     if "bicycle" in which:
         res["D_bicycle_slab"] = slab_frames(args, dev, rank, world, xp, barrier, red_dev, "bicycle.json", 1_000_000,
-                                            256, frames=2, settle=3)
+                                            256, frames=3, warmup=5)
+    if "lego" in which:  # the headline's own form at the bench's default size (when the headline was changed)
+        res["B_lego_slab"] = slab_frames(args, dev, rank, world, xp, barrier, red_dev, "lego.json", 100_000, 128)
+    if "dp" in which:
+        res["B_lego_dp"] = dp_frames(args, dev, rank, world, barrier, red_dev)
     if "split" in which:
         res["B_lego_sim_render_split"] = sim_render_split(args, dev, rank, world, barrier, red_dev)
     return res
@@ -733,6 +816,47 @@ def config_e(dev, iters=5):
             "particle_substeps_per_s_fwd_bwd": 2 * bf.NSUB * n / (ms * 1e-3)}
 
 
+def slab_main(args, dev, rank, world, red_dev):
+    """The N > 1 headline (north_star): ONE lego scene sharded by spatial slab
+    over the N ranks (gsmpm.dist.SlabDomain, csrc/slab.h: every substep each
+    pair of neighbouring ranks swaps the partial (m v, m) sums of the window
+    planes around their shared bound over RCCL, the pairwise all-reduce of
+    boundary grid nodes; particles migrate every 10 substeps), rank 0 renders
+    the gathered frame and takes the render-aware particle share.  W untimed
+    warm-up frames, K frames timed barrier + synchronize to barrier +
+    synchronize, max over ranks; value = the scene's particles x substeps /
+    that time (strong scaling).  Side fields: config D (bicycle 1M, 256^3)
+    through the same slabs, and the replicas form (one scene per rank)."""
+    import torch
+    import torch.distributed as dist
+    from gsmpm.dist import make_transport
+    xp = make_transport(rank, world, device=dev)
+
+    def barrier():
+        dist.barrier()
+        torch.cuda.synchronize()
+
+    r = slab_frames(args, dev, rank, world, xp, barrier, red_dev, args.config, args.particles, args.n_grid,
+                    frames=args.steps, warmup=max(2, args.warmup))
+    spf = r["substeps_per_frame"]
+    out = {"metric": METRIC, "value": r["particle_substeps_per_s"], "unit": "particle-substeps/s",
+           "n_gpus": world, "steps": args.steps, "warmup": max(2, args.warmup), "ms_per_step": r["frame_ms"],
+           "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f32",
+           "data": "synthetic (lego-like Gaussians, seed 0; lego PLY is an LFS pointer in the reference)",
+           "config": {"workload": f"{args.config} frame: {spf} substeps + postprocess + gather to rank 0 + render "
+                                  f"{r['render']}", "particles_total": r["particles"], "n_grid": r["n_grid"],
+                      "material": "jelly", "parallelism": f"slab{world}"},
+           "substeps_per_s": spf * 1e3 / r["frame_ms"], "frames_per_s": 1e3 / r["frame_ms"],
+           "num_rendered": r["num_rendered"], "slab": r}
+    if not args.no_multi_configs and not args.no_extra_configs:
+        out["multi_gpu"] = multi_gpu_configs(args, dev, rank, world, xp, barrier, red_dev)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    barrier()
+    xp.close()
+    dist.destroy_process_group()
+
+
 def dry_run(args, rank, world):
     """--dry-run: the launch bookkeeping of the real run on the CPU (gloo), so
     tests can check that --gpus N starts N ranks that agree on N."""
@@ -782,6 +906,8 @@ def main():
         else:
             dist.init_process_group(backend)
     red_dev = dev if backend == "nccl" else torch.device("cpu")
+    if world > 1 and args.multi == "slab":
+        return slab_main(args, dev, rank, world, red_dev)
     # --render-cus: the simulator's stream (made current: everything below runs on it) and the
     # render's stream on disjoint CU masks
     masked_render_stream = None
@@ -1134,11 +1260,16 @@ def main():
         # carry the reference's work
         dom = max(abytes, key=lambda k: frame_prof[k])
         frame_s = frame_prof[dom] * 1e-3
-        ach = abytes[dom] * spf / frame_s / 1e9  # one substep's algorithmic bytes per substep
         avg_launch_s = frame_s / nl[dom]
-        lbytes = algorithmic_bytes_live(n_local, live, sa.material).get(dom) if fused else None
-        traffic = measured_traffic(dom, {"config": args.config, "particles": args.particles, "n_grid": sa.n_grid,
-                                         "material": sa.material})
+        wl = {"config": args.config, "particles": args.particles, "n_grid": sa.n_grid, "material": sa.material}
+        us = {k: frame_prof[k] / nl[k] * 1e3 for k in ("k_fused", "k_grid_f") if k in frame_prof}
+        kr = kernel_roofline(n_local, sa.n_grid, sa.material, live, us, wl) if fused else {}
+        # headline: the live-byte basis (bytes the kernel must move at least), not
+        # SURVEY 8(d)'s dense n^3 sweep; the dense figure stays only as the
+        # labelled contract fraction
+        lbytes = algorithmic_bytes_live(n_local, live, sa.material)[dom] if fused else abytes[dom]
+        ach = lbytes / avg_launch_s / 1e9
+        traffic = measured_traffic(dom, wl)
         out["kernels_ms_per_launch"] = {k: round(frame_prof[k] / nl[k], 5) for k in frame_prof if k in nl}
         out["kernels_ms_per_frame"] = {k: round(v, 4) for k, v in frame_prof.items()}
         out["kernels_ms_per_launch_steady"] = {k: round(v, 5) for k, v in kern.items()}
@@ -1147,23 +1278,21 @@ def main():
                            "traffic_frac": None if traffic is None else
                            round(traffic / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4),
                            "avg_launch_us": round(avg_launch_s * 1e6, 2), "launches_per_frame": nl[dom],
-                           "algorithmic_bytes_per_substep": abytes[dom],
-                           "basis": "SURVEY.md 8(d) B_sub = 208 N + 56 n^3 split per kernel (dense grid); "
-                                    "achieved = spf x bytes / the kernel's summed packet-stamped time over one "
-                                    "eager frame (= rocprofv3 avg x launches)",
+                           "algorithmic_bytes_per_launch": lbytes,
+                           "basis": "live bytes: 208 N particle-plane bytes (+ 8 N plastic) + 28 B x live nodes "
+                                    "(touched 8x8x7 tiles x 448) per launch; achieved = bytes / the kernel's average "
+                                    "packet-stamped launch time over one eager frame (= rocprofv3's per-launch "
+                                    "duration); traffic = PMC FETCH_SIZE + WRITE_SIZE per launch",
                            "pipeline": sim.pipeline,
                            "live_nodes": live,
-                           # the same kernel time over the live-node bytes (208 N + 28 x touched-tile
-                           # nodes for k_fused): the bandwidth fraction of what the kernel must move
-                           "live_bytes_per_substep": lbytes,
-                           "achieved_sparse": None if lbytes is None else round(lbytes * spf / frame_s / 1e9, 1),
-                           "frac_sparse": None if lbytes is None else
-                           round(lbytes * spf / frame_s / 1e9 / HBM_PEAK_GBS, 4),
+                           "substep": kr.get("substep"),
+                           # SURVEY 8(d)'s B_sub split per kernel with the dense n^3 grid the reference sweeps
+                           # (utils.py:177-183, model.py:124-127): bytes this kernel never moves, kept only as
+                           # the labelled contract figure
+                           "frac_dense_contract": round(abytes[dom] / avg_launch_s / 1e9 / HBM_PEAK_GBS, 4),
+                           "dense_contract_bytes_per_launch": abytes[dom],
                            "traffic_source_sha": source_sha()}
-        out["kernels_roofline"] = kernel_roofline(
-            n_local, sa.n_grid, sa.material, live,
-            {k: frame_prof[k] / nl[k] * 1e3 for k in ("k_fused", "k_grid_f") if k in frame_prof},
-            {"config": args.config, "particles": args.particles, "n_grid": sa.n_grid, "material": sa.material})
+        out["kernels_roofline"] = kr
     if not args.no_extra_configs and world == 1:
         out["other_configs"] = other_configs(args, dev)
     if world > 1 and xp is not None and not args.no_multi_configs and not args.no_extra_configs:

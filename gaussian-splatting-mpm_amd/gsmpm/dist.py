@@ -323,12 +323,22 @@ class SlabDomain:
         if hasattr(self.engine, "slab_set_weight"):
             self.engine.slab_set_weight(float(weight))
 
-    def set_render_share(self, sim_ms: float, render_ms: float, floor: float = 0.1) -> float:
-        """The render-aware re-cut (the round-4 verdict's item 2(a)): the rank
-        that renders the gathered frame takes the particle share
-        sim / (sim + render) of an even one, so that its simulation plus the
-        render matches the other ranks' simulation.  Returns the weight set."""
-        w = max(float(floor), min(1.0, float(sim_ms) / max(float(sim_ms) + float(render_ms), 1e-9)))
+    def set_render_share(self, sim_ms: float, render_ms: float, world: int | None = None,
+                         floor: float = 0.1) -> float:
+        """The render-aware re-cut: the rank that renders the gathered frame
+        takes a smaller particle share so that its simulation plus the render
+        matches the other ranks' simulation.  `sim_ms` must be this rank's
+        simulation time at an EVEN share (weight 1, i.e. before any call to
+        this), `render_ms` its render time.  The library's re-cut gives this
+        rank the share w / (w + W - 1) of the particles (W = world), so with a
+        simulation time linear in the particle count the balancing weight is
+            w = (W s - (W - 1) r) / (W s + r)
+        (rank 0: W s w / (w + W - 1) + r = the others' W s / (w + W - 1)),
+        clamped to [floor, 1].  Returns the weight set."""
+        W = self.world if world is None else int(world)
+        s, r = float(sim_ms), float(render_ms)
+        w = (W * s - (W - 1) * r) / max(W * s + r, 1e-9)
+        w = max(float(floor), min(1.0, w))
         self.set_weight(w)
         return w
 

@@ -186,9 +186,10 @@ int gsmpm_mpm_slab_set_rebalance(gsmpm_mpm* h, int32_t on, float tolerance);
  * quantiles that give rank r the share w_r / sum(w) of the particles, and a
  * rank holding more than (1 + tolerance) x its share triggers the re-cut.  A
  * rank with other work per frame takes a smaller share: the rank that renders
- * the gathered frame (bench.py, SlabDomain.set_render_share) sets w = its
- * simulation time / (its simulation + render time), so its sim + render
- * matches the other ranks' sim (the round-4 verdict's render-aware re-cut).
+ * the gathered frame (bench.py, SlabDomain.set_render_share) sets
+ * w = (W s - (W - 1) r) / (W s + r) from its simulation time s at an even
+ * share and its render time r (W = world size), so its sim + render matches
+ * the other ranks' sim when the sim time is linear in the particle count.
  * Carried in each rank's record (the next step call's), so every rank sees
  * every weight.  No reference counterpart. */
 int gsmpm_mpm_slab_set_weight(gsmpm_mpm* h, float weight);

@@ -49,7 +49,22 @@ static void bsp(const float x[3], float inv_dx, int base[3], float fx[3], float 
 }
 static const float kDDW[3] = {1.0f, -2.0f, 1.0f}; /* d(dw)/dfx */
 
+/* The reference's _opt kernels index the grid without a range check
+ * (utils.py:57-76, Taichi debug=False, main.py:28): an index outside the grid
+ * is undefined behaviour there.  The debug build (-DOM_DEBUG: make asan /
+ * make debug) stops at one, as Taichi's debug mode would. */
+#ifdef OM_DEBUG
+#include <stdio.h>
+static inline size_t node(int ng, int ix, int iy, int iz) {
+  if (ix < 0 || iy < 0 || iz < 0 || ix >= ng || iy >= ng || iz >= ng) {
+    fprintf(stderr, "diff oracle: grid node (%d, %d, %d) outside the %d^3 grid\n", ix, iy, iz, ng);
+    abort();
+  }
+  return ((size_t)ix * ng + iy) * ng + iz;
+}
+#else
 static inline size_t node(int ng, int ix, int iy, int iz) { return ((size_t)ix * ng + iy) * ng + iz; }
+#endif
 
 /* compute_mu_lam_from_E_nu, utils.py:349-362 */
 void od_mu_lam(od_state* s) {

@@ -18,6 +18,48 @@
 static inline float fmaxf_(float a, float b) { return a > b ? a : b; }
 static inline float fminf_(float a, float b) { return a < b ? a : b; }
 
+/* Host debug build (make asan / make debug: -DOM_DEBUG).  The
+ * reference runs Taichi without debug=True (main.py:28), so an out-of-range
+ * grid index there is undefined behaviour that nothing reports; Taichi's
+ * debug mode would stop at it.  Here every grid access goes through OM_NODE,
+ * which in the debug build aborts on an index outside [0, ng)^3, and every
+ * stencil node that the restatement skips because it lies outside the grid
+ * (the documented choice above) is counted (om_debug_skipped); with the
+ * environment variable GSMPM_ORACLE_STRICT=1 a skip aborts too, as Taichi's
+ * debug mode would. */
+#ifdef OM_DEBUG
+#include <stdio.h>
+static long om_dbg_skipped = 0;
+static int om_dbg_strict = -1;
+static size_t om_node_checked(int ng, int ix, int iy, int iz, const char* where) {
+  if (ix < 0 || iy < 0 || iz < 0 || ix >= ng || iy >= ng || iz >= ng) {
+    fprintf(stderr, "oracle %s: grid node (%d, %d, %d) outside the %d^3 grid\n", where, ix, iy, iz, ng);
+    abort();
+  }
+  return ((size_t)ix * ng + iy) * ng + iz;
+}
+static void om_skip(int ng, int ix, int iy, int iz, const char* where) {
+  __atomic_add_fetch(&om_dbg_skipped, 1, __ATOMIC_RELAXED);
+  if (om_dbg_strict < 0) {
+    const char* e = getenv("GSMPM_ORACLE_STRICT");
+    om_dbg_strict = e && e[0] == '1';
+  }
+  if (om_dbg_strict) {
+    fprintf(stderr, "oracle %s: stencil node (%d, %d, %d) outside the %d^3 grid (strict)\n", where, ix, iy, iz, ng);
+    abort();
+  }
+}
+#define OM_NODE(ng, ix, iy, iz, where) om_node_checked((ng), (ix), (iy), (iz), (where))
+#define OM_SKIP(ng, ix, iy, iz, where) om_skip((ng), (ix), (iy), (iz), (where))
+long om_debug_skipped(void) { return __atomic_load_n(&om_dbg_skipped, __ATOMIC_RELAXED); }
+int om_debug_build(void) { return 1; }
+#else
+#define OM_NODE(ng, ix, iy, iz, where) (((size_t)(ix) * (ng) + (iy)) * (ng) + (iz))
+#define OM_SKIP(ng, ix, iy, iz, where) ((void)0)
+long om_debug_skipped(void) { return -1; }
+int om_debug_build(void) { return 0; }
+#endif
+
 /* ------------------------------------------------------------------ 3x3 -- */
 static void mm3(const float A[9], const float B[9], float C[9]) {
   float T[9];
@@ -174,15 +216,18 @@ void om_particle_volume(int n, const float* x, int ng, float grid_dx, int32_t* c
   for (int p = 0; p < n; ++p) {
     int c[3];
     for (int d = 0; d < 3; ++d) c[d] = (int)floorf(x[p * 3 + d] / grid_dx);
-    if (c[0] < 0 || c[1] < 0 || c[2] < 0 || c[0] >= ng || c[1] >= ng || c[2] >= ng) continue;
-    cnt[((size_t)c[0] * ng + c[1]) * ng + c[2]] += 1;
+    if (c[0] < 0 || c[1] < 0 || c[2] < 0 || c[0] >= ng || c[1] >= ng || c[2] >= ng) {
+      OM_SKIP(ng, c[0], c[1], c[2], "particle_volume");
+      continue;
+    }
+    cnt[OM_NODE(ng, c[0], c[1], c[2], "particle_volume")] += 1;
   }
   float dx3 = grid_dx * grid_dx * grid_dx; /* Taichi lowers `grid_dx ** 3` (int exponent) to products */
   for (int p = 0; p < n; ++p) {
     int c[3];
     for (int d = 0; d < 3; ++d) c[d] = (int)floorf(x[p * 3 + d] / grid_dx);
     if (c[0] < 0 || c[1] < 0 || c[2] < 0 || c[0] >= ng || c[1] >= ng || c[2] >= ng) { vol[p] = 0.f; continue; }
-    vol[p] = dx3 / (float)cnt[((size_t)c[0] * ng + c[1]) * ng + c[2]];
+    vol[p] = dx3 / (float)cnt[OM_NODE(ng, c[0], c[1], c[2], "particle_volume")];
   }
 }
 
@@ -436,8 +481,11 @@ static void p2g_particle(om_state* s, int p, float dt) {
             float cd = C[r * 3 + 0] * dpos[0] + C[r * 3 + 1] * dpos[1] + C[r * 3 + 2] * dpos[2];
             add[r] = weight * m * (vp[r] + cd) + dt * ef[r];
           }
-          if (ix < 0 || iy < 0 || iz < 0 || ix >= ng || iy >= ng || iz >= ng) continue;
-          size_t g = ((size_t)ix * ng + iy) * ng + iz;
+          if (ix < 0 || iy < 0 || iz < 0 || ix >= ng || iy >= ng || iz >= ng) {
+            OM_SKIP(ng, ix, iy, iz, "p2g");
+            continue;
+          }
+          size_t g = OM_NODE(ng, ix, iy, iz, "p2g");
           s->gv_in[g * 3 + 0] += add[0];
           s->gv_in[g * 3 + 1] += add[1];
           s->gv_in[g * 3 + 2] += add[2];
@@ -504,7 +552,7 @@ void om_grid_ops(om_state* s, int n_ops, const om_gridop* ops, const int32_t* ac
     for (int i = 0; i < ng; ++i)
       for (int j = 0; j < ng; ++j)
         for (int k = 0; k < ng; ++k) {
-          size_t g = ((size_t)i * ng + j) * ng + k;
+          size_t g = OM_NODE(ng, i, j, k, "grid_ops");
           float* v = s->gv_out + g * 3;
           if (op->kind == 0) {
             float px[3] = {(float)i * dx, (float)j * dx, (float)k * dx};
@@ -551,8 +599,10 @@ void om_g2p(om_state* s, float dt) {
           int ix = base[0] + i, iy = base[1] + j, iz = base[2] + k;
           float weight = w[0][i] * w[1][j] * w[2][k];
           float gv[3] = {0, 0, 0};
-          if (!(ix < 0 || iy < 0 || iz < 0 || ix >= ng || iy >= ng || iz >= ng)) {
-            size_t g = ((size_t)ix * ng + iy) * ng + iz;
+          if (ix < 0 || iy < 0 || iz < 0 || ix >= ng || iy >= ng || iz >= ng) {
+            OM_SKIP(ng, ix, iy, iz, "g2p");
+          } else {
+            size_t g = OM_NODE(ng, ix, iy, iz, "g2p");
             gv[0] = s->gv_out[g * 3]; gv[1] = s->gv_out[g * 3 + 1]; gv[2] = s->gv_out[g * 3 + 2];
           }
           for (int d = 0; d < 3; ++d) nv[d] += gv[d] * weight;

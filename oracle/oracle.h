@@ -61,6 +61,11 @@ typedef struct {
 void om_svd3(const float A[9], float U[9], float sig[3], float V[9]);
 void om_mu_lam(int n, const float* logE, const float* y, float* mu, float* lam);
 void om_particle_volume(int n, const float* x, int ng, float grid_dx, int32_t* count_grid, float* vol);
+/* host debug build (-DOM_DEBUG; make asan / make debug): 1 in it, else 0; the
+ * number of stencil / cell accesses skipped because they lie outside the grid
+ * (-1 outside the debug build) */
+int om_debug_build(void);
+long om_debug_skipped(void);
 void om_stress(om_state* s, float dt);
 void om_fluid(int n, const float* F_trial, const float* mu, const float* lam, const float* yield, float pvisc, float dt,
               float* F_out, float* tau_out);

@@ -77,6 +77,11 @@ def lib(threaded=False):
     bench.py's timed CPU baseline, and in the long-horizon parity tests one
     member of the spread of valid reference outputs -- never the checker)."""
     name = "liboracle_fast.so" if threaded == "fast" else ("liboracle_omp.so" if threaded else "liboracle.so")
+    variant = os.environ.get("GSMPM_ORACLE_VARIANT", "")
+    if variant in ("asan", "debug"):  # the host sanitizer / bounds-checked builds (oracle/Makefile)
+        name = name.replace(".so", f"_{variant}.so")
+    elif variant:
+        raise ValueError(f"GSMPM_ORACLE_VARIANT={variant!r}: expected asan or debug")
     if name not in _LIBS:
         path = os.path.join(_HERE, name)
         if not os.path.exists(path):

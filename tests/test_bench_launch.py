@@ -28,10 +28,11 @@ def _line(p):
 
 
 def test_gpus_flag_starts_that_many_ranks():
-    """The default N > 1 headline: one lego scene per rank (weak scaling)."""
+    """The default N > 1 headline is north_star's design: one lego scene
+    sharded by spatial slab over the N ranks (strong scaling)."""
     out = _line(_run(["--gpus", "2", "--dry-run"]))
-    assert out["n_gpus"] == 2 and out["scaling"] == "weak"
-    assert out["config"]["parallelism"].startswith("dp2")
+    assert out["n_gpus"] == 2 and out["scaling"] == "strong"
+    assert out["config"]["parallelism"] == "slab2"
 
 
 def test_gpus_flag_slab_mode():
