@@ -259,14 +259,16 @@ def make_sim(scene, dev, use_graph=True, slab=None):
     return sim, specs
 
 
-def algorithmic_bytes_live(n, live_nodes, material):
+def algorithmic_bytes_live(n, live_nodes, material, fold=False):
     """The same split with the grid counted as the nodes the kernels own: the
     touched tiles' nodes (live_nodes = touched tiles x 448 of the fused
     pipeline's 8x8x7 tiles) instead of the dense n^3 the reference sweeps --
     the bytes a sparse implementation must move at least, so the fraction it
-    gives is a bandwidth fraction (<= 1)."""
+    gives is a bandwidth fraction (<= 1).  fold: k_fused also does the grid
+    update of the substep before (fused.h FOLD), so its launch carries the
+    whole substep's 208 N + 56 B per live node."""
     plastic = 8 * n if material in ("metal",) else 0
-    return {"k_fused": 208 * n + 28 * live_nodes + plastic, "k_grid_f": 28 * live_nodes}
+    return {"k_fused": 208 * n + (56 if fold else 28) * live_nodes + plastic, "k_grid_f": 28 * live_nodes}
 
 
 # translation units whose kernels are not the simulator's (the rasterizer, the
@@ -325,33 +327,36 @@ def measured_traffic(kernel, workload):
     return None
 
 
-def kernel_roofline(n, n_grid, material, live_nodes, us_per_launch, workload):
+def kernel_roofline(n, n_grid, material, live_nodes, us_per_launch, workload, launches=None, spf=100, fold=False):
     """Per-kernel roofline figures of the fused pipeline, on the live-byte
     basis: `bytes` = the bytes the kernel must move at least (208 N particle
-    planes (+ 8 N plastic) + 28 B per live node for k_fused, 28 B per live node
-    for k_grid_f; live nodes = touched tiles x 448), `frac` = bytes / launch
-    time / HBM peak (<= 1 by construction), and beside it the PMC-measured HBM
-    traffic (when it matches the workload and sources) with its fraction.  The
-    SURVEY 8(d) dense n^3 figure is what the reference sweeps, not what these
-    kernels move, so it is given as bytes only (`dense_contract_bytes`), never
-    as a rate or fraction.  `substep` = both kernels' bytes over their summed
-    time: the whole-substep fraction."""
+    planes (+ 8 N plastic) + 28 B per live node for k_fused -- 56 when it
+    folds the grid update in --, 28 B per live node for k_grid_f; live nodes =
+    touched tiles x 448), `frac` = bytes / launch time / HBM peak (<= 1 by
+    construction), and beside it the PMC-measured HBM traffic (when it
+    matches the workload and sources) with its fraction.  The SURVEY 8(d)
+    dense n^3 figure is what the reference sweeps, not what these kernels
+    move, so it is given as bytes only (`dense_contract_bytes`), never as a
+    rate or fraction.  `substep` = one substep's live bytes (208 N + 56 B per
+    live node) over the time both kernels spend per substep (launches x
+    per-launch time / substeps): the whole-substep fraction."""
     dense = algorithmic_bytes(n, n_grid, material)
-    live = algorithmic_bytes_live(n, live_nodes, material)
+    live = algorithmic_bytes_live(n, live_nodes, material, fold)
+    launches = launches or {"k_fused": spf + 1, "k_grid_f": spf}
     out = {}
     for k, us in us_per_launch.items():
         if k not in live or not us:
             continue
         t = us * 1e-6
         tr = measured_traffic(k, workload)
-        out[k] = {"us_per_launch": round(us, 2), "bytes": live[k],
+        out[k] = {"us_per_launch": round(us, 2), "launches_per_frame": launches.get(k), "bytes": live[k],
                   "achieved_GBps": round(live[k] / t / 1e9, 1),
                   "frac": round(live[k] / t / 1e9 / HBM_PEAK_GBS, 4),
                   "traffic": tr, "traffic_frac": None if tr is None else round(tr / t / 1e9 / HBM_PEAK_GBS, 4),
                   "dense_contract_bytes": dense[k]}
     if all(k in out for k in ("k_fused", "k_grid_f")):
-        b = live["k_fused"] + live["k_grid_f"]
-        t = (us_per_launch["k_fused"] + us_per_launch["k_grid_f"]) * 1e-6
+        b = algorithmic_bytes_live(n, live_nodes, material, True)["k_fused"]
+        t = sum(us_per_launch[k] * launches[k] for k in ("k_fused", "k_grid_f")) / spf * 1e-6
         out["substep"] = {"kernels": ["k_fused", "k_grid_f"], "bytes": b,
                           "us": round(t * 1e6, 2), "achieved_GBps": round(b / t / 1e9, 1),
                           "frac": round(b / t / 1e9 / HBM_PEAK_GBS, 4)}
@@ -471,13 +476,17 @@ def other_configs(args, dev, frames=3, rank=0, world=1, xp=None, sync=None):
             masks, t = substep_masks(specs, t, dt, spf)
             prof = sim.profile(dt, masks)
             r["k_fused_us_per_launch"] = round(prof[0] / (spf + 1) * 1e3, 2)
-            r["k_grid_f_us_per_launch"] = round(prof[1] / spf * 1e3, 2)
+            ngrid = int(prof[3]) if prof[3] > 0 else spf  # k_grid_f launches (folded: one per re-binning)
+            r["k_grid_f_launches_per_frame"] = ngrid
+            r["k_grid_f_us_per_launch"] = round(prof[1] / ngrid * 1e3, 2)
             live = sim.debug_stats()["touched_tiles"] * 448
             r["live_nodes"] = live
+            r["folded"] = sim.folded
             r["roofline"] = kernel_roofline(
                 nsim, sa.n_grid, sa.material, live,
                 {"k_fused": r["k_fused_us_per_launch"], "k_grid_f": r["k_grid_f_us_per_launch"]},
-                {"config": cfg, "particles": n, "n_grid": ng, "material": sa.material})
+                {"config": cfg, "particles": n, "n_grid": ng, "material": sa.material},
+                launches={"k_fused": spf + 1, "k_grid_f": ngrid}, spf=spf, fold=sim.folded)
         else:
             st = sim.stats()
             r["rank0_slab_planes"] = [st["lo"], st["hi"]]
@@ -1209,7 +1218,8 @@ def main():
         names = ("k_fused", "k_grid_f", "binning") if fused else ("k_p2g", "k_grid", "k_g2p", "binning")
         # the fused pipeline runs spf + 1 k_fused launches per frame (the first is
         # P2G only, the last G2P only: together one substep's work)
-        nl = {"k_fused": spf + 1, "k_grid_f": spf, "k_p2g": spf, "k_grid": spf, "k_g2p": spf}
+        nl = {"k_fused": spf + 1, "k_grid_f": int(prof[3]) if fused and prof[3] > 0 else spf,
+              "k_p2g": spf, "k_grid": spf, "k_g2p": spf}
         frame_prof = {k: prof[i] for i, k in enumerate(names)}
         # (2) steady state: hipEvents around 20 back-to-back launches of each kernel
         # on the current frame's inputs (no re-binning launches)
@@ -1263,11 +1273,13 @@ def main():
         avg_launch_s = frame_s / nl[dom]
         wl = {"config": args.config, "particles": args.particles, "n_grid": sa.n_grid, "material": sa.material}
         us = {k: frame_prof[k] / nl[k] * 1e3 for k in ("k_fused", "k_grid_f") if k in frame_prof}
-        kr = kernel_roofline(n_local, sa.n_grid, sa.material, live, us, wl) if fused else {}
+        folded = fused and sim.folded
+        kr = kernel_roofline(n_local, sa.n_grid, sa.material, live, us, wl, launches=nl, spf=spf,
+                             fold=folded) if fused else {}
         # headline: the live-byte basis (bytes the kernel must move at least), not
         # SURVEY 8(d)'s dense n^3 sweep; the dense figure stays only as the
         # labelled contract fraction
-        lbytes = algorithmic_bytes_live(n_local, live, sa.material)[dom] if fused else abytes[dom]
+        lbytes = algorithmic_bytes_live(n_local, live, sa.material, folded)[dom] if fused else abytes[dom]
         ach = lbytes / avg_launch_s / 1e9
         traffic = measured_traffic(dom, wl)
         out["kernels_ms_per_launch"] = {k: round(frame_prof[k] / nl[k], 5) for k in frame_prof if k in nl}
@@ -1280,10 +1292,11 @@ def main():
                            "avg_launch_us": round(avg_launch_s * 1e6, 2), "launches_per_frame": nl[dom],
                            "algorithmic_bytes_per_launch": lbytes,
                            "basis": "live bytes: 208 N particle-plane bytes (+ 8 N plastic) + 28 B x live nodes "
-                                    "(touched 8x8x7 tiles x 448) per launch; achieved = bytes / the kernel's average "
+                                    "(56 B when k_fused folds the grid update in) (touched 8x8x7 tiles x 448) per "
+                                    "launch; achieved = bytes / the kernel's average "
                                     "packet-stamped launch time over one eager frame (= rocprofv3's per-launch "
                                     "duration); traffic = PMC FETCH_SIZE + WRITE_SIZE per launch",
-                           "pipeline": sim.pipeline,
+                           "pipeline": sim.pipeline + (" (grid update folded into k_fused)" if folded else ""),
                            "live_nodes": live,
                            "substep": kr.get("substep"),
                            # SURVEY 8(d)'s B_sub split per kernel with the dense n^3 grid the reference sweeps

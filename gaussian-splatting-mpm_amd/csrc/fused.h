@@ -138,7 +138,168 @@ struct FusedRare {
   int* tbox;           // Touch's per-chunk box publishing (once a chunk: a scalar load, not a live SGPR)
   const int* tpos;
   int* rbox;
+  // ---- the folded grid update (FOLD launches, below; null / unused otherwise) ----
+  // Launch r of a step call (phase r mod 12) writes its chunk windows to the
+  // slot buffer r mod 2, its tile boxes to tbox buffer r mod 2, its escapes to
+  // gacc buffer r mod 3 and raises escape flag r mod 12.  The previous
+  // launch's outputs are what a FOLD launch's staging reads:
+  const float4* slots_prev;  // chunk windows of launch r - 1
+  const int* tbox_prev;      // tile boxes of launch r - 1
+  const float4* gacc_prev;   // escapes of launch r - 1 (read when *esc_prev)
+  const int* esc_prev;       // escape flag of launch r - 1
+  // launch r's housekeeping at its end: the escapes of launch r - 2 (read by
+  // launch r - 1, written next by launch r + 1) are zeroed when *esc_old, and
+  // flag r - 3 (read by launches r - 2 and r - 1) is cleared
+  const int* esc_old;
+  float4* gacc_old;
+  int* esc_clr;
+  float grav[3];  // gravity (f32): a FOLD launch forms dt * gravity as the host's grid_step does
+  unsigned* esc_count;  // particle scatters that escaped their chunk window, summed (gsmpm_mpm_escapes)
 };
+
+// ---------------------------------------------------------------- the fold --
+// FOLD launches (MODE bit 4) take the grid update of the previous substep
+// into their own G2P staging instead of reading the dense v_out that a
+// k_grid_f launch would have written: every node of the chunk's stencil box
+// is summed from the chunk windows that cover it (the previous P2G's slots,
+// in k_grid_f's fixed order: the node's owner tile's window first, then the
+// covering neighbours by k_grid_f's e order, the second and further chunks
+// after, the escape accumulator last), then normalised, gravity and the BC
+// list applied (node_update, utils.py:177-183 + solver.py:41-46).  The staged
+// value is bit-identical to k_grid_f's, so a step runs one launch per substep
+// (k_grid_f only after a re-binning, whose next launch reads chunk windows of
+// the old bins).  A node lies in up to 8 chunk windows (3.5 on average), so
+// the slot bytes a launch reads grow by that factor over k_grid_f's; they come
+// from L2 / MALL, written by the launch before.
+constexpr int kFT[3] = {kFT0, kFT1, kFT2};
+#ifndef GSMPM_FOLD_BATCH
+#define GSMPM_FOLD_BATCH 2
+#endif
+constexpr int kFoldB = GSMPM_FOLD_BATCH;  // nodes a lane stages at once (their loads in flight together)
+// per axis: window coordinate w (node o + w of tile t's window, o = t T - 1) ->
+// the node's owner tile offset d in {-1, 0, 1} and k_grid_f's section sec of
+// its owner-local coordinate l = w - 1 - d T (sec -1: l < 3, +1: l = T - 1)
+__device__ __forceinline__ void fold_axis(int w, int T, int& d, int& sec) {
+  d = w == 0 ? -1 : (w <= T ? 0 : 1);
+  const int l = w - 1 - d * T;
+  sec = l < 3 ? -1 : (l == T - 1 ? 1 : 0);
+}
+// (global address space: the loads may move across the staging's LDS stores)
+__device__ __forceinline__ float4 ld_slot4(const float4* __restrict__ slots, int off) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  typedef const f4v __attribute__((address_space(1)))* gf4_p;
+  const f4v r = *(gf4_p)((const char*)slots + (unsigned)off * 16u);
+  return make_float4(r.x, r.y, r.z, r.w);
+}
+__device__ __forceinline__ void add4f(float4& a, const float4& b) {
+  a.x += b.x;
+  a.y += b.y;
+  a.z += b.z;
+  a.w += b.w;
+}
+// The summed window value of one node from per-neighbour tables: covering
+// tile e of the node is t + a_e (a_e per axis = d + (bit e ? sec : 0)), its
+// {first chunk, chunks, box} read through `tab(ci, c0, nc, bx)` for the
+// 27-neighbour index ci of a_e, and the node's coordinate in that window is
+// w - a_e T.  Loads of covers outside the window's box (nothing was scattered
+// there) are not issued.  Order of the sum: k_grid_f's (node_reads,
+// node_extra).  fold_prep computes the 8 covers' slot offsets, fold_load
+// issues their loads, fold_acc sums them (+ further chunks): split so a
+// caller can have several nodes' loads in flight at once.
+struct FoldNode {
+  int off[8];   // first chunk's slot offset of each cover (valid where on)
+  int c0[8];    // first chunk (further chunks: c0 + 1 ...)
+  int nc[8];    // chunks
+  int loc[8];   // the node's offset inside each cover's window
+  int on;       // bit e: cover e exists and its box holds the node
+};
+template <typename Tab>
+__device__ __forceinline__ void fold_prep(const int (&w)[3], Tab tab, FoldNode& f) {
+  int d[3], sec[3];
+#pragma unroll
+  for (int ax = 0; ax < 3; ++ax) fold_axis(w[ax], kFT[ax], d[ax], sec[ax]);
+  f.on = 0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int b0 = e >> 2, b1 = (e >> 1) & 1, b2 = e & 1;
+    const int a0 = d[0] + (b0 ? sec[0] : 0), a1 = d[1] + (b1 ? sec[1] : 0), a2 = d[2] + (b2 ? sec[2] : 0);
+    const int ci = (a0 + 1) * 9 + (a1 + 1) * 3 + (a2 + 1);
+    int c0, nc, q;
+    tab(ci, c0, nc, q);
+    const int wn0 = w[0] - a0 * kFT0, wn1 = w[1] - a1 * kFT1, wn2 = w[2] - a2 * kFT2;
+    const bool on = ((!b0) | (sec[0] != 0)) & ((!b1) | (sec[1] != 0)) & ((!b2) | (sec[2] != 0)) & (nc > 0) &
+                    (wn0 >= (q & 15)) & (wn1 >= ((q >> 4) & 15)) & (wn2 >= ((q >> 8) & 15)) &
+                    (wn0 <= ((q >> 12) & 15)) & (wn1 <= ((q >> 16) & 15)) & (wn2 <= ((q >> 20) & 15));
+    f.on |= on ? (1 << e) : 0;
+    f.loc[e] = slot_loc(wn0, wn1, wn2);
+    f.c0[e] = c0;
+    f.nc[e] = nc;
+    f.off[e] = c0 * kFWin + f.loc[e];
+  }
+}
+__device__ __forceinline__ void fold_load(const float4* __restrict__ slots, const FoldNode& f, float4 (&v)[8]) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = ((f.on >> e) & 1) ? ld_slot4(slots, f.off[e]) : make_float4(0.f, 0.f, 0.f, 0.f);
+}
+__device__ __forceinline__ float4 fold_acc(const float4* __restrict__ slots, const FoldNode& f, const float4 (&v)[8]) {
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) add4f(a, v[e]);
+  int extra = 0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) extra |= (((f.on >> e) & 1) && f.nc[e] > 1) ? (1 << e) : 0;
+  if (extra) {  // the second chunks of the covering tiles (e order), then the third and later ones
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float4 u = ((extra >> e) & 1) ? ld_slot4(slots, (f.c0[e] + 1) * kFWin + f.loc[e])
+                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+      add4f(a, u);
+    }
+    while (extra) {
+      const int e = __builtin_ctz(extra);
+      extra &= extra - 1;
+      for (int c = f.c0[e] + 2; c < f.c0[e] + f.nc[e]; ++c) add4f(a, ld_slot4(slots, c * kFWin + f.loc[e]));
+    }
+  }
+  return a;
+}
+template <typename Tab>
+__device__ __forceinline__ float4 fold_sum(const float4* __restrict__ slots, const int (&w)[3], Tab tab) {
+  FoldNode f;
+  fold_prep(w, tab, f);
+  float4 v[8];
+  fold_load(slots, f, v);
+  return fold_acc(slots, f, v);
+}
+
+// The slow path: the updated velocity of any grid node (i, j, k) from the
+// previous P2G's windows, through the tile tables of the node's owner tile
+// (a particle of a FOLD launch that left its chunk's window, or one binned
+// outside the grid).  0 outside the grid.
+__device__ __noinline__ float4 fold_node(int i, int j, int k, const GridDims& g, const FTiles& tl, const ChunkIn& ck,
+                                         const FusedRare* __restrict__ rare, const GridStep& gs,
+                                         const BcTable* __restrict__ bct, bool esc) {
+  const int ng = g.ng;
+  if ((unsigned)i >= (unsigned)ng || (unsigned)j >= (unsigned)ng || (unsigned)k >= (unsigned)ng)
+    return make_float4(0.f, 0.f, 0.f, 0.f);
+  const int ti = i / kFT0, tj = j / kFT1, tk = k / kFT2;
+  // window coordinates of the node in its owner tile's window (owner offset d = 0)
+  const int w[3] = {i - ti * kFT0 + 1, j - tj * kFT1 + 1, k - tk * kFT2 + 1};
+  float4 a = fold_sum(rare->slots_prev, w, [&](int ci, int& c0, int& nc, int& q) {
+    const int x = ti + ci / 9 - 1, y = tj + (ci / 3) % 3 - 1, z = tk + ci % 3 - 1;
+    c0 = 0;
+    nc = 0;
+    q = 0;
+    if ((unsigned)x < (unsigned)tl.td0 && (unsigned)y < (unsigned)tl.td1 && (unsigned)z < (unsigned)tl.td2) {
+      const int u = (x * tl.td1 + y) * tl.td2 + z;
+      c0 = ck.cbase[u];
+      nc = (ck.count[u] + kChunk - 1) / kChunk;
+      q = rare->tbox_prev[u];
+    }
+  });
+  if (esc) add4f(a, rare->gacc_prev[((size_t)i * ng + j) * ng + k]);
+  return node_update(a, i, j, k, g, gs, bct);
+}
 
 __device__ __forceinline__ void ftile_decode(const FTiles& tl, int t, int& tx, int& ty, int& tz) {
   tz = t % tl.td2;
@@ -327,12 +488,28 @@ constexpr bool kG2pB128 = GSMPM_G2P_B128 != 0;
 #define GSMPM_BIN_AGG 1
 #endif
 constexpr bool kBinAgg = GSMPM_BIN_AGG != 0;
+// bin: 1 = re-bin the particles by their new x into rare->bo; 2 = zero
+// rare->bo's counts and flags for the next launch's re-binning (at the end)
 template <int MAT, int MODE>
 __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTiles tl, ChunkIn ck, Touch tc, int bin,
                                                int use_box, const float4* __restrict__ gvel, uint32_t mask, float dt,
                                                MatConsts mc, float4* __restrict__ slots, int xlo, int xhi,
-                                               const FusedRare* __restrict__ rare) {
+                                               const FusedRare* __restrict__ rare, uint32_t mask_prev) {
   constexpr bool G2P = (MODE & 1) != 0, P2G = (MODE & 2) != 0;
+  constexpr bool FOLD = G2P && (MODE & 4) != 0;  // the previous substep's grid update staged from its chunk windows
+  __shared__ int s_fc0[27], s_fnc[27], s_fbx[27];  // FOLD: the 27 neighbour tiles' tables
+  // FOLD: the previous substep's grid step, and whether its P2G had escapes (uniform)
+  GridStep fgs{};
+  bool fesc = false;
+  if constexpr (FOLD) {
+    fgs.dt = dt;
+    fgs.dgx = dt * rare->grav[0];
+    fgs.dgy = dt * rare->grav[1];
+    fgs.dgz = dt * rare->grav[2];
+    fgs.mask = mask_prev;
+    fgs.keep = 0;
+    fesc = __builtin_amdgcn_readfirstlane(*rare->esc_prev) != 0;
+  }
   // channel-planar u64 accumulators; the G2P v window aliases them (it is
   // consumed before the accumulators are zeroed)
   __shared__ unsigned long long s_acc[4 * kFWin];
@@ -421,7 +598,69 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
       }
     }
     if constexpr (G2P) {
-      if (!outside) {
+      if (FOLD && !outside) {
+        // the 27 neighbour tiles' first chunk, chunk count and stencil box of the previous P2G (lanes 0..26)
+        if (k < 27) {
+          const int x0 = tx + k / 9 - 1, y0 = ty + (k / 3) % 3 - 1, z0 = tz + k % 3 - 1;
+          int c0 = 0, nc = 0, bx = 0;
+          if ((unsigned)x0 < (unsigned)tl.td0 && (unsigned)y0 < (unsigned)tl.td1 && (unsigned)z0 < (unsigned)tl.td2) {
+            const int u = (x0 * tl.td1 + y0) * tl.td2 + z0;
+            c0 = ck.cbase[u];
+            nc = (ck.count[u] + kChunk - 1) / kChunk;
+            bx = rare->tbox_prev[u];
+          }
+          s_fc0[k] = c0;
+          s_fnc[k] = nc;
+          s_fbx[k] = bx;
+        }
+        __syncthreads();
+        int lo[3], hi[3];
+        box_unpack(cbox, lo, hi);
+        const int n1 = hi[1] - lo[1] + 1, n2 = hi[2] - lo[2] + 1, n12 = n1 * n2;
+        const int nvol = (hi[0] - lo[0] + 1) * n12;
+        const float r12 = 1.0f / (float)n12, r2 = 1.0f / (float)n2;
+        const float4* __restrict__ sp = rare->slots_prev;
+        const BcTable* __restrict__ fbct = static_cast<const BcTable*>(rare->bct);
+        auto tab = [&](int ci, int& c0, int& nc, int& q) {
+          c0 = s_fc0[ci];
+          nc = s_fnc[ci];
+          q = s_fbx[ci];
+        };
+        // kFoldB nodes a lane at a time: all their cover loads in flight together
+        for (int q0 = k; q0 < nvol; q0 += 256 * kFoldB) {
+          FoldNode fn[kFoldB];
+          int w3[kFoldB][3];
+          bool gin[kFoldB], live[kFoldB];
+#pragma unroll
+          for (int u = 0; u < kFoldB; ++u) {
+            const int qn = min(q0 + u * 256, nvol - 1);
+            live[u] = q0 + u * 256 < nvol;
+            const int a = (int)(((float)qn + 0.5f) * r12), rem = qn - a * n12;
+            const int b = (int)(((float)rem + 0.5f) * r2), c = rem - b * n2;
+            w3[u][0] = lo[0] + a;
+            w3[u][1] = lo[1] + b;
+            w3[u][2] = lo[2] + c;
+            const int ix = o0 + w3[u][0], iy = o1 + w3[u][1], iz = o2 + w3[u][2];
+            gin[u] = live[u] && (unsigned)ix < (unsigned)ng && (unsigned)iy < (unsigned)ng && (unsigned)iz < (unsigned)ng;
+            fold_prep(w3[u], tab, fn[u]);
+            if (!gin[u]) fn[u].on = 0;
+          }
+          float4 vv[kFoldB][8];
+#pragma unroll
+          for (int u = 0; u < kFoldB; ++u) fold_load(sp, fn[u], vv[u]);
+#pragma unroll
+          for (int u = 0; u < kFoldB; ++u) {
+            const int ix = o0 + w3[u][0], iy = o1 + w3[u][1], iz = o2 + w3[u][2];
+            float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (gin[u]) {
+              float4 sum = fold_acc(sp, fn[u], vv[u]);
+              if (fesc) add4f(sum, rare->gacc_prev[((size_t)ix * ng + iy) * ng + iz]);
+              val = node_update(sum, ix, iy, iz, g, fgs, fbct);
+            }
+            if (live[u]) s_win[(w3[u][0] * kFW1 + w3[u][1]) * kFW2 + w3[u][2]] = val;
+          }
+        }
+      } else if (!outside) {
         // the chunk's stencil box from its last P2G (particles unmoved since), else the whole window
         int lo[3], hi[3];
         box_unpack(cbox, lo, hi);
@@ -480,8 +719,12 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
                      [&](const int (&base)[3], int i, int j, int kk) {
                        const int ix = base[0] + i, iy = base[1] + j, iz = base[2] + kk;
                        float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
-                       if ((unsigned)ix < (unsigned)ng && (unsigned)iy < (unsigned)ng && (unsigned)iz < (unsigned)ng)
-                         r = gvel[((size_t)ix * ng + iy) * ng + iz];
+                       if constexpr (FOLD) {
+                         r = fold_node(ix, iy, iz, g, tl, ck, rare, fgs, static_cast<const BcTable*>(rare->bct), fesc);
+                       } else {
+                         if ((unsigned)ix < (unsigned)ng && (unsigned)iy < (unsigned)ng && (unsigned)iz < (unsigned)ng)
+                           r = gvel[((size_t)ix * ng + iy) * ng + iz];
+                       }
                        return r;
                      },
                      v, C, gvd);
@@ -508,7 +751,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
 #pragma unroll
           for (int i = 0; i < 9; ++i) ps.st(PF + i, p, F[i / 3][i % 3]);
         }
-        if (bin) {
+        if (bin == 1) {
           int tc[3];
           nt = ftile_of(x, g, tl, tc);
           if (!outside && nt < tl.ntiles) {
@@ -517,7 +760,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
           }
         }
       }
-      if (bin) {
+      if (bin == 1) {
         // the slot of the particle in its new tile's bin, reserved once per
         // (wave, neighbour tile): nearly every lane of a wave stays in the
         // chunk's own tile, and one LDS counter hit by 64 lanes serializes
@@ -632,7 +875,10 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
       if (outside) {
         // chunk of particles binned outside the grid: bounds-checked global path
         if (k < cnt) p2g_global<MAT>(x, v, C, m, nvt, g, dt, rare->gacc);
-        if (k == 0 && cnt > 0) *rare->esc = 1;
+        if (k == 0 && cnt > 0) {
+          *rare->esc = 1;
+          atomicAdd(rare->esc_count, (unsigned)cnt);
+        }
         // the next launch on these bins reads this chunk's lane order too: the
         // identity (round 4 left it unwritten, so a lane of the next G2P took a
         // stale row -- another chunk's particle, or one past the live rows)
@@ -729,6 +975,10 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
           *rare->esc = 1;
         }
       }
+      {  // escape statistics (gsmpm_mpm_escapes): one atomic a wave with escapes
+        const unsigned long long eb = __ballot(k < cnt && !win);
+        if (eb && (k & 63) == 0) atomicAdd(rare->esc_count, (unsigned)__popcll(eb));
+      }
       __syncthreads();
       if (w == (int)blockIdx.x) stamp(SK, 4);
       if (tc.perm && k < cnt) tc.perm[(size_t)w * 256 + balanced_lane(s_rcnt, cnt, res, rrank)] = (unsigned char)q;
@@ -775,7 +1025,44 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
       __syncthreads();  // LDS reuse by the next chunk
     }
   }
+  // end-of-launch housekeeping (no load of this launch depends on it)
+  if (bin == 2) {  // the next launch re-bins into rare->bo: its counts and flags start at zero
+    const BinOutF bo = rare->bo;
+    for (int t = blockIdx.x * 256 + threadIdx.x; t <= tl.ntiles; t += gridDim.x * 256) {
+      bo.count[t] = 0;
+      if (t < tl.ntiles) bo.tflag[t] = 0;
+    }
+  }
+  if (rare->esc_clr) {  // FOLD rotation (null outside it): escapes of launch r - 2, flag r - 3
+    if (__builtin_amdgcn_readfirstlane(*rare->esc_old) != 0) {
+      const size_t nn = (size_t)ng * ng * ng;
+      for (size_t q = (size_t)blockIdx.x * 256 + threadIdx.x; q < nn; q += (size_t)gridDim.x * 256)
+        rare->gacc_old[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *rare->esc_clr = 0;
+  }
   stamp(SK, 1);
+}
+
+// The end of a FOLD step call: the escape accumulators that the call's last
+// launches left dirty are zeroed and every rotation flag cleared, so the next
+// call starts from clean buffers.  One workgroup (no flag is cleared while
+// another workgroup could still test it); nothing to do in a call without
+// escapes.
+__global__ __launch_bounds__(1024) void k_fold_tail(int* __restrict__ flags, float4* __restrict__ g0,
+                                                    float4* __restrict__ g1, float4* __restrict__ g2, int ng) {
+  __shared__ int s_f[12];
+  if (threadIdx.x < 12) s_f[threadIdx.x] = flags[threadIdx.x];
+  __syncthreads();
+  const size_t nn = (size_t)ng * ng * ng;
+  bool dirty[3] = {false, false, false};
+  for (int r = 0; r < 12; ++r) dirty[r % 3] = dirty[r % 3] || s_f[r] != 0;
+  float4* gb[3] = {g0, g1, g2};
+  for (int b = 0; b < 3; ++b)
+    if (dirty[b])
+      for (size_t q = threadIdx.x; q < nn; q += 1024) gb[b][q] = make_float4(0.f, 0.f, 0.f, 0.f);
+  __syncthreads();
+  if (threadIdx.x < 12 && s_f[threadIdx.x]) flags[threadIdx.x] = 0;
 }
 
 // Chunk ranges and stencil boxes of the 27 tiles whose windows reach tile

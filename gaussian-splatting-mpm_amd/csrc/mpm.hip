@@ -1530,7 +1530,14 @@ struct gsmpm_mpm {
   int* ftouched[2] = {nullptr, nullptr};
   int* ftflag[2] = {nullptr, nullptr};
   int* flist[2] = {nullptr, nullptr};
-  int* fesc = nullptr;                    // [2] escape flags (alternating per grid update)
+  int* fesc = nullptr;                    // [2] escape flags (alternating per grid update), then the FOLD
+                                          // rotation's [12] (one per phase) and one scratch word
+  // the folded grid update (fused.h FOLD): launch r of a step call writes slot
+  // buffer r % 2, tile-box buffer r % 2 and escape accumulator r % 3
+  bool fold = true;                       // GSMPM_FOLD=0: a k_grid_f launch after every k_fused (A/B)
+  float4* fslots2 = nullptr;              // the second slot buffer [max_chunks + 1][kFWin]
+  float4* gacc_f[3] = {nullptr, nullptr, nullptr};  // escape accumulators ([0] = gacc)
+  int* ftbox2[2] = {nullptr, nullptr};    // the second tile-box buffer per bins parity
   int* fcbox[2] = {nullptr, nullptr};     // [max_chunks] per-chunk stencil boxes (fused.h)
   int* ftbox[2] = {nullptr, nullptr};     // [ntiles] per-tile stencil boxes
   int2* frcov[2] = {nullptr, nullptr};    // [ntiles][kRecStride] cover records per touched position (k_grid_f)
@@ -1603,10 +1610,13 @@ struct gsmpm_mpm {
   bool s_rebal_pending = false;              // the next call starts with the migration to new bounds
   long s_rebalances = 0;
   int* s_rec_host = nullptr;                 // pinned copy
-  int* nonfin_host = nullptr;                // non-finite particle position seen (pinned, device-mapped; sticky)
+  int* nonfin_host = nullptr;                // non-finite particle state seen: x, or P2G's m / v / C / stress
+                                             // (pinned, device-mapped; sticky)
   int* nonfin_dev = nullptr;                 // its device address
-  FusedRare* frare_dev = nullptr;            // [2 bins parities][2 escape flags] k_fused's rare arguments (fused.h)
-  FusedRare frare_host[4] = {};              // what frare_dev holds
+  // k_fused's rare arguments (fused.h): [2 bins parities][kRareSlots], slots
+  // 0 / 1 the escape flags of the unfolded pipeline, 2 + r the FOLD phase r
+  FusedRare* frare_dev = nullptr;
+  FusedRare frare_host[2 * 14] = {};         // what frare_dev holds
   float* mig_send[2] = {nullptr, nullptr};   // fixed-size payloads: header + [NMIG][mig_cap]
   float* mig_recv[2] = {nullptr, nullptr};
   int mig_cap = 0;                           // leavers one migration may send one way (all ranks agree)
@@ -1855,11 +1865,23 @@ static int launch_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc,
 // rounds (config D) are spread evenly.
 static int fused_grid(gsmpm_mpm* h) { return std::min(h->ftl.max_chunks, h->fused_wgs); }
 
-static FusedRare rare_of(gsmpm_mpm* h, int c, int e) {
+constexpr int kRareSlots = 14;  // per bins parity: 2 unfolded escape flags + 12 FOLD phases
+constexpr int kFoldPhases = 12;
+// FOLD phase r's buffers (launch r of a step call, fused.h FusedRare)
+static float4* fold_slots(gsmpm_mpm* h, int r) { return (r & 1) ? h->fslots2 : h->fslots; }
+static int* fold_tbox(gsmpm_mpm* h, int c, int r) { return (r & 1) ? h->ftbox2[c] : h->ftbox[c]; }
+static int* fold_flag(gsmpm_mpm* h, int r) { return h->fesc + 2 + ((r % kFoldPhases) + kFoldPhases) % kFoldPhases; }
+static float4* fold_gacc(gsmpm_mpm* h, int r) { return h->gacc_f[((r % 3) + 3) % 3]; }
+static int* fold_scratch(gsmpm_mpm* h) { return h->fesc + 2 + kFoldPhases; }
+
+// rare slot: 0 / 1 the unfolded pipeline's escape flag e; 2 + r the FOLD phase r
+static FusedRare rare_of(gsmpm_mpm* h, int c, int slot) {
   FusedRare r{};
+  const bool fold = slot >= 2;
+  const int ph = slot - 2;
   r.bo = bin_out_f(h, c ^ 1);
-  r.gacc = h->gacc;
-  r.esc = h->fesc + e;
+  r.gacc = fold ? fold_gacc(h, ph) : h->gacc;
+  r.esc = fold ? fold_flag(h, ph) : h->fesc + slot;
   r.drift = h->slab ? h->s_drift : nullptr;
   r.nonfin = h->slab ? h->s_drift + SF_NONFIN : h->nonfin_dev;
   r.bct = h->dev_bc;
@@ -1868,9 +1890,20 @@ static FusedRare rare_of(gsmpm_mpm* h, int c, int e) {
   r.nchunk = h->fnchunk[c];
   r.chunk = h->fchunk[c];
   r.rcov = h->frcov[c];
-  r.tbox = h->ftbox[c];
+  r.tbox = fold ? fold_tbox(h, c, ph) : h->ftbox[c];
   r.tpos = h->cover_records ? h->ftpos[c] : nullptr;
   r.rbox = h->frbox[c];
+  if (fold) {
+    r.slots_prev = fold_slots(h, ph + 1);  // (r - 1) mod 2
+    r.tbox_prev = fold_tbox(h, c, ph + 1);
+    r.gacc_prev = fold_gacc(h, ph - 1);
+    r.esc_prev = fold_flag(h, ph - 1);
+    r.esc_old = fold_flag(h, ph - 2);
+    r.gacc_old = fold_gacc(h, ph - 2);
+    r.esc_clr = fold_flag(h, ph - 3);
+  }
+  for (int d = 0; d < 3; ++d) r.grav[d] = (float)h->prm.gravity[d];
+  r.esc_count = reinterpret_cast<unsigned*>(h->fesc + 3 + kFoldPhases);
   return r;
 }
 // k_fused's rare arguments in device memory, rewritten (outside captures,
@@ -1878,8 +1911,8 @@ static FusedRare rare_of(gsmpm_mpm* h, int c, int e) {
 // captures, so a captured launch never finds them stale
 static int sync_rare(gsmpm_mpm* h, hipStream_t st) {
   bool dirty = false;
-  for (int i = 0; i < 4; ++i) {
-    const FusedRare r = rare_of(h, i >> 1, i & 1);
+  for (int i = 0; i < 2 * kRareSlots; ++i) {
+    const FusedRare r = rare_of(h, i / kRareSlots, i % kRareSlots);
     if (std::memcmp(&r, &h->frare_host[i], sizeof(r)) != 0) {
       h->frare_host[i] = r;
       dirty = true;
@@ -1890,59 +1923,90 @@ static int sync_rare(gsmpm_mpm* h, hipStream_t st) {
   GSMPM_HIP(hipMemcpyAsync(h->frare_dev, h->frare_host, sizeof(h->frare_host), hipMemcpyHostToDevice, st));
   return GSMPM_OK;
 }
+// one k_fused launch: bins parity c, rare slot `slot`, chunk windows stored to
+// `slots`; mask_prev: the BC mask of the previous substep (a FOLD launch's grid step)
+struct FusedLaunch {
+  int c, bin, use_box, slot;
+  uint32_t mask, mask_prev;
+  float dt;
+  float4* slots;
+};
 template <int MAT, int MODE>
-static void launch_fused_t(gsmpm_mpm* h, int c, int bin, int use_box, uint32_t mask, float dt, int* esc,
-                           hipStream_t st, const hipEvent_t* ev) {
+static void launch_fused_t(gsmpm_mpm* h, const FusedLaunch& f, hipStream_t st, const hipEvent_t* ev) {
   const int xlo = h->slab ? h->s_lo - h->s_margin : INT_MIN, xhi = h->slab ? h->s_hi + h->s_margin : INT_MAX;
-  launch(ev, k_fused<MAT, MODE>, dim3(fused_grid(h)), dim3(256), st, particles_of(h), h->g, h->ftl, chunk_in_f(h, c),
-         touch_f(h, c), bin, use_box, (const float4*)h->gvel, mask, dt, h->mc, h->fslots, xlo, xhi,
-         (const FusedRare*)(h->frare_dev + c * 2 + (int)(esc - h->fesc)));
+  launch(ev, k_fused<MAT, MODE>, dim3(fused_grid(h)), dim3(256), st, particles_of(h), h->g, h->ftl, chunk_in_f(h, f.c),
+         touch_f(h, f.c), f.bin, f.use_box, (const float4*)h->gvel, f.mask, f.dt, h->mc, f.slots, xlo, xhi,
+         (const FusedRare*)(h->frare_dev + f.c * kRareSlots + f.slot), f.mask_prev);
 }
 template <int MODE>
-static void launch_fused_m(gsmpm_mpm* h, int c, int bin, int ub, uint32_t mask, float dt, int* esc, hipStream_t st,
-                           const hipEvent_t* ev) {
+static void launch_fused_m(gsmpm_mpm* h, const FusedLaunch& f, hipStream_t st, const hipEvent_t* ev) {
   switch (h->mat_kernel) {
-    case 0: launch_fused_t<0, MODE>(h, c, bin, ub, mask, dt, esc, st, ev); break;
-    case 1: launch_fused_t<1, MODE>(h, c, bin, ub, mask, dt, esc, st, ev); break;
-    case 2: launch_fused_t<2, MODE>(h, c, bin, ub, mask, dt, esc, st, ev); break;
-    case 3: launch_fused_t<3, MODE>(h, c, bin, ub, mask, dt, esc, st, ev); break;
-    default: launch_fused_t<4, MODE>(h, c, bin, ub, mask, dt, esc, st, ev); break;
+    case 0: launch_fused_t<0, MODE>(h, f, st, ev); break;
+    case 1: launch_fused_t<1, MODE>(h, f, st, ev); break;
+    case 2: launch_fused_t<2, MODE>(h, f, st, ev); break;
+    case 3: launch_fused_t<3, MODE>(h, f, st, ev); break;
+    default: launch_fused_t<4, MODE>(h, f, st, ev); break;
   }
 }
-// mode 1: G2P only, 2: P2G only, 3: G2P of the last grid update + P2G.
-// use_box: the previous k_fused launch did the P2G of these same bins, so
-// its per-chunk stencil boxes bound this launch's G2P gathers.
-static int launch_fused(gsmpm_mpm* h, int mode, int c, bool bin, bool use_box, uint32_t mask, float dt, int* esc,
-                        hipStream_t st, const hipEvent_t* ev) {
+// mode 1: G2P only, 2: P2G only, 3: G2P of the last grid update + P2G; + 4:
+// FOLD (the G2P stages the previous substep's grid update from its chunk
+// windows, fused.h).  use_box: the previous k_fused launch did the P2G of
+// these same bins, so its per-chunk stencil boxes bound this launch's G2P.
+static int launch_fused(gsmpm_mpm* h, int mode, const FusedLaunch& f, hipStream_t st, const hipEvent_t* ev) {
   if (!h->capturing) {
     const int rc = sync_rare(h, st);
     if (rc) return rc;
   }
-  const int ub = use_box ? 1 : 0;
-  if (mode == 1)
-    launch_fused_t<0, 1>(h, c, bin ? 1 : 0, ub, mask, dt, esc, st, ev);  // G2P does not depend on the material
-  else if (mode == 2)
-    launch_fused_m<2>(h, c, bin ? 1 : 0, ub, mask, dt, esc, st, ev);
-  else
-    launch_fused_m<3>(h, c, bin ? 1 : 0, ub, mask, dt, esc, st, ev);
+  switch (mode) {
+    case 1: launch_fused_t<0, 1>(h, f, st, ev); break;  // G2P does not depend on the material
+    case 5: launch_fused_t<0, 5>(h, f, st, ev); break;
+    case 2: launch_fused_m<2>(h, f, st, ev); break;
+    case 7: launch_fused_m<7>(h, f, st, ev); break;
+    default: launch_fused_m<3>(h, f, st, ev); break;
+  }
   GSMPM_LAUNCH_CHECK();
   return GSMPM_OK;
 }
+// the unfolded pipeline's launch: escape flag ep, slot buffer fslots
+static int launch_fused(gsmpm_mpm* h, int mode, int c, bool bin, bool use_box, uint32_t mask, float dt, int ep,
+                        hipStream_t st, const hipEvent_t* ev) {
+  const FusedLaunch f{c, bin ? 1 : 0, use_box ? 1 : 0, ep, mask, mask, dt, h->fslots};
+  return launch_fused(h, mode, f, st, ev);
+}
 
-static int launch_grid_f(gsmpm_mpm* h, int wp, float dt, uint32_t mask, int ep, int* zc, int* zf, hipStream_t st,
-                         const hipEvent_t* ev, const SlabWin* swp = nullptr) {
+// k_grid_f's buffers: the unfolded pipeline's (fslots, ftbox[wp], gacc, escape
+// flag ep read, ep ^ 1 cleared), or a FOLD phase's (fold_grid_bufs)
+struct GridBufs {
+  const float4* slots;
+  const int* tbox;
+  float4* gacc;
+  const int* esc_in;
+  int* esc_clear;
+};
+static GridBufs grid_bufs(gsmpm_mpm* h, int wp, int ep) {
+  return GridBufs{h->fslots, h->ftbox[wp], h->gacc, h->fesc + ep, h->fesc + (ep ^ 1)};
+}
+// after FOLD launch r (the re-binning one): its windows, boxes and escapes; the
+// rotation clears the flags, so the grid's own clear goes to a scratch word
+static GridBufs fold_grid_bufs(gsmpm_mpm* h, int wp, int r) {
+  return GridBufs{fold_slots(h, r), fold_tbox(h, wp, r), fold_gacc(h, r), fold_flag(h, r), fold_scratch(h)};
+}
+static int launch_grid_f(gsmpm_mpm* h, int wp, float dt, uint32_t mask, const GridBufs& gb, int* zc, int* zf,
+                         hipStream_t st, const hipEvent_t* ev, const SlabWin* swp = nullptr) {
   const SlabWin sw = swp ? *swp : SlabWin{};
   const dim3 grid(std::min(kGridParts * h->ftl.ntiles, 1024 * kGridParts));
   if (swp)
-    launch(ev, k_grid_f<true>, grid, dim3(kGridT), st, h->g, h->ftl, chunk_in_f(h, wp), (const int*)h->ftbox[wp],
-           (const float4*)h->fslots, h->gacc, h->gvel, (const BcTable*)h->dev_bc, grid_step(h, dt, mask),
-           (const int*)(h->fesc + ep), h->fesc + (ep ^ 1), zc, zf, sw);
+    launch(ev, k_grid_f<true>, grid, dim3(kGridT), st, h->g, h->ftl, chunk_in_f(h, wp), gb.tbox, gb.slots, gb.gacc,
+           h->gvel, (const BcTable*)h->dev_bc, grid_step(h, dt, mask), gb.esc_in, gb.esc_clear, zc, zf, sw);
   else
-    launch(ev, k_grid_f<false>, grid, dim3(kGridT), st, h->g, h->ftl, chunk_in_f(h, wp), (const int*)h->ftbox[wp],
-           (const float4*)h->fslots, h->gacc, h->gvel, (const BcTable*)h->dev_bc, grid_step(h, dt, mask),
-           (const int*)(h->fesc + ep), h->fesc + (ep ^ 1), zc, zf, sw);
+    launch(ev, k_grid_f<false>, grid, dim3(kGridT), st, h->g, h->ftl, chunk_in_f(h, wp), gb.tbox, gb.slots, gb.gacc,
+           h->gvel, (const BcTable*)h->dev_bc, grid_step(h, dt, mask), gb.esc_in, gb.esc_clear, zc, zf, sw);
   GSMPM_LAUNCH_CHECK();
   return GSMPM_OK;
+}
+static int launch_grid_f(gsmpm_mpm* h, int wp, float dt, uint32_t mask, int ep, int* zc, int* zf, hipStream_t st,
+                         const hipEvent_t* ev, const SlabWin* swp = nullptr) {
+  return launch_grid_f(h, wp, dt, mask, grid_bufs(h, wp, ep), zc, zf, st, ev, swp);
 }
 
 // nsub substeps = nsub + 1 k_fused launches (P2G, nsub - 1 x G2P+P2G, G2P)
@@ -1952,6 +2016,7 @@ static int launch_grid_f(gsmpm_mpm* h, int wp, float dt, uint32_t mask, int ep, 
 // k_fused launch ({K, grid, binning} pairs), summed into kernel_ms[0..2].
 static int slab_grid_phase(gsmpm_mpm* h, int wp, float dt, uint32_t mask, int ep, int* zc, int* zf, hipStream_t st,
                            const gsmpm_transport* xp);  // slab_host.inc
+static bool fold_on(const gsmpm_mpm* h) { return h->fold && !h->slab; }
 static int launch_substeps_f(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc, hipStream_t st, int& bp, int& ep,
                              hipEvent_t* ev = nullptr, float* kernel_ms = nullptr,
                              const gsmpm_transport* xp = nullptr) {
@@ -1968,6 +2033,11 @@ static int launch_substeps_f(gsmpm_mpm* h, float dt, int nsub, const uint32_t* b
     if (s <= 0) return false;
     return h->slab ? s % R == 0 : (long)s * m / nsub > (long)(s - 1) * m / nsub;
   };
+  // FOLD (fused.h): launch s stages the grid update of substep s - 1 itself
+  // whenever launch s - 1 did its P2G on the same bins; a k_grid_f launch
+  // remains only after a re-binning launch (the next launch's chunks are new)
+  const bool fold = fold_on(h);
+  std::vector<char> grid_at(nsub + 1, 0);
   int wp = bp;
   bool zeroed = false;  // counts / flags of parity bp ^ 1 zeroed by a grid launch since the last binning
   bool boxed = false;   // the last k_fused launch did P2G on the bins parity bp
@@ -1975,13 +2045,20 @@ static int launch_substeps_f(gsmpm_mpm* h, float dt, int nsub, const uint32_t* b
     const int mode = s == 0 ? 2 : (s == nsub ? 1 : 3);
     const bool bin = bin_at(s);
     const uint32_t mask = s < nsub ? (bc ? bc[s] : 0xffffffffu) : 0u;
+    const uint32_t mask_prev = s > 0 ? (bc ? bc[s - 1] : 0xffffffffu) : 0u;
     hipEvent_t* e8 = ev ? ev + 8 * s : nullptr;
     if (bin && !zeroed) {
       GSMPM_HIP(hipMemsetAsync(h->fcount[bp ^ 1], 0, sizeof(int) * (h->ftl.ntiles + 1), st));
       GSMPM_HIP(hipMemsetAsync(h->ftflag[bp ^ 1], 0, sizeof(int) * h->ftl.ntiles, st));
     }
-    int rc = launch_fused(h, mode, bp, bin, boxed, mask, dt, h->fesc + ep, st, e8);
+    // FOLD: the launch before a re-binning one zeroes its counts (no grid launch between them)
+    const bool zero_next = fold && !bin && s < nsub && bin_at(s + 1);
+    const bool fl = fold && boxed && (mode & 1);
+    const FusedLaunch f{bp, bin ? 1 : (zero_next ? 2 : 0), boxed ? 1 : 0, fold ? 2 + s % kFoldPhases : ep,
+                        mask, mask_prev, dt, fold ? fold_slots(h, s) : h->fslots};
+    int rc = launch_fused(h, fl ? mode + 4 : mode, f, st, e8);
     if (rc) return rc;
+    if (zero_next) zeroed = true;
     if (mode & 2) wp = bp;
     boxed = (mode & 2) && !bin;
     if (bin) {
@@ -1990,7 +2067,7 @@ static int launch_substeps_f(gsmpm_mpm* h, float dt, int nsub, const uint32_t* b
       bp ^= 1;
       zeroed = false;
     }
-    if (s < nsub) {
+    if (s < nsub && (!fold || bin)) {
       const bool next_bin = bin_at(s + 1);
       int *zc = nullptr, *zf = nullptr;
       if (next_bin && wp == bp) {  // this grid launch does not read parity bp ^ 1
@@ -1999,21 +2076,30 @@ static int launch_substeps_f(gsmpm_mpm* h, float dt, int nsub, const uint32_t* b
         zeroed = true;
       }
       rc = h->slab ? slab_grid_phase(h, wp, dt, mask, ep, zc, zf, st, xp)
-                   : launch_grid_f(h, wp, dt, mask, ep, zc, zf, st, e8 ? e8 + 2 : nullptr);
+                   : launch_grid_f(h, wp, dt, mask, fold ? fold_grid_bufs(h, wp, s) : grid_bufs(h, wp, ep), zc, zf, st,
+                                   e8 ? e8 + 2 : nullptr);
       if (rc) return rc;
-      ep ^= 1;
+      if (!fold) ep ^= 1;
+      grid_at[s] = 1;
     }
   }
+  if (fold) {  // escape accumulators the call's last launches left dirty, and the rotation's flags
+    hipLaunchKernelGGL(k_fold_tail, dim3(1), dim3(1024), 0, st, h->fesc + 2, h->gacc_f[0], h->gacc_f[1], h->gacc_f[2],
+                       h->g.ng);
+    GSMPM_LAUNCH_CHECK();
+  }
   if (ev) {
+    // kernel_ms: {k_fused, k_grid_f, binning (+ permute), grid launches}
     GSMPM_HIP(hipStreamSynchronize(st));
     for (int s = 0; s <= nsub; ++s) {
       const bool bin = bin_at(s);
       for (int k = 0; k < 4; ++k) {
-        if ((k == 1 && s == nsub) || (k >= 2 && !bin)) continue;
+        if ((k == 1 && !grid_at[s]) || (k >= 2 && !bin)) continue;
         float ms = 0.f;
         GSMPM_HIP(hipEventElapsedTime(&ms, ev[8 * s + 2 * k], ev[8 * s + 2 * k + 1]));
-        kernel_ms[k] += ms;
+        kernel_ms[k < 3 ? k : 2] += ms;
       }
+      if (grid_at[s]) kernel_ms[3] += 1.f;
     }
   }
   return GSMPM_OK;
@@ -2166,6 +2252,7 @@ static int graph_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc, 
   key.push_back((uint32_t)h->fbpar);
   key.push_back((uint32_t)h->fep);
   key.push_back((uint32_t)h->rebin_interval);
+  key.push_back(fold_on(h) ? 1u : 0u);
   key.push_back(h->planes_alt && h->planes > h->planes_alt ? 1u : 0u);  // which particle buffer is current
   key.push_back(xp ? (uint32_t)(((uintptr_t)xp->comm >> 4) ^ (uint32_t)xp->kind) : 0u);
   if (h->slab) {  // where the migrations fall, and the buffers they swap (rects / capacity changes drop graphs)
@@ -2411,8 +2498,24 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
     if ((e = hipMemset(h->planes_alt, 0, sizeof(float) * (size_t)NPLANES * h->np)) != hipSuccess)
       return fail(e, "hipMemset");
     if ((e = hipMalloc(&h->orig_alt, sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc orig");
-    if ((e = hipMalloc(&h->fesc, sizeof(int) * 2)) != hipSuccess) return fail(e, "hipMalloc escape flags");
-    if ((e = hipMemset(h->fesc, 0, sizeof(int) * 2)) != hipSuccess) return fail(e, "hipMemset");
+    if ((e = hipMalloc(&h->fesc, sizeof(int) * (4 + kFoldPhases))) != hipSuccess) return fail(e, "hipMalloc escape flags");
+    if ((e = hipMemset(h->fesc, 0, sizeof(int) * (4 + kFoldPhases))) != hipSuccess) return fail(e, "hipMemset");
+    // FOLD (fused.h): the second slot and tile-box buffers, two more escape accumulators
+    if (const char* fo = std::getenv("GSMPM_FOLD")) h->fold = fo[0] != '0';
+    if ((e = hipMalloc(&h->fslots2, sizeof(float4) * (size_t)(h->ftl.max_chunks + 1) * kFWin)) != hipSuccess)
+      return fail(e, "hipMalloc fused slots");
+    if ((e = hipMemset(h->fslots2 + (size_t)h->ftl.max_chunks * kFWin, 0, sizeof(float4) * kFWin)) != hipSuccess)
+      return fail(e, "hipMemset");
+    h->gacc_f[0] = h->gacc;
+    for (int b = 1; b < 3; ++b) {
+      if ((e = hipMalloc(&h->gacc_f[b], sizeof(float4) * nn)) != hipSuccess) return fail(e, "hipMalloc grid acc");
+      if ((e = hipMemset(h->gacc_f[b], 0, sizeof(float4) * nn)) != hipSuccess) return fail(e, "hipMemset");
+    }
+    for (int c = 0; c < 2; ++c) {
+      if ((e = hipMalloc(&h->ftbox2[c], sizeof(int) * (size_t)h->ftl.ntiles)) != hipSuccess)
+        return fail(e, "hipMalloc boxes");
+      if ((e = hipMemset(h->ftbox2[c], 0, sizeof(int) * (size_t)h->ftl.ntiles)) != hipSuccess) return fail(e, "hipMemset");
+    }
     if ((e = hipMalloc(&h->frare_dev, sizeof(h->frare_host))) != hipSuccess) return fail(e, "hipMalloc rare args");
   }
   const int scan_tiles = std::max(h->tl.ntiles, h->ftl.ntiles) + 1;
@@ -2478,6 +2581,10 @@ int gsmpm_mpm_destroy(gsmpm_mpm* h) {
     (void)hipFree(h->ftpos[c]);
   }
   (void)hipFree(h->fslots);
+  (void)hipFree(h->fslots2);
+  (void)hipFree(h->gacc_f[1]);
+  (void)hipFree(h->gacc_f[2]);
+  for (int c = 0; c < 2; ++c) (void)hipFree(h->ftbox2[c]);
   (void)hipFree(h->fesc);
   (void)hipFree(h->frare_dev);
   (void)hipFree(h->planes_alt);
@@ -2556,6 +2663,10 @@ int gsmpm_mpm_set_particles(gsmpm_mpm* h, const float* x, const float* cov6, con
   const size_t nn = (size_t)h->g.ng * h->g.ng * h->g.ng;
   GSMPM_HIP(hipMemsetAsync(h->gacc, 0, nn * sizeof(float4), st));
   GSMPM_HIP(hipMemsetAsync(h->gvel, 0, nn * sizeof(float4), st));
+  if (h->fesc) {  // the fused pipeline's escape flags and the FOLD accumulators: a new state
+    GSMPM_HIP(hipMemsetAsync(h->fesc, 0, sizeof(int) * (4 + kFoldPhases), st));
+    for (int b = 1; b < 3; ++b) GSMPM_HIP(hipMemsetAsync(h->gacc_f[b], 0, nn * sizeof(float4), st));
+  }
   int rc = rebin(h, st);
   if (rc) return rc;
   GSMPM_HIP(hipStreamSynchronize(st));
@@ -2635,8 +2746,8 @@ int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t nsub, const uint32_t* bc, voi
     return GSMPM_ESTATE;
   }
   if (*(volatile int*)h->nonfin_host) {
-    set_error("gsmpm_mpm_step: a particle position became non-finite (NaN / Inf) in an earlier step; the state is "
-              "invalid");
+    set_error("gsmpm_mpm_step: particle state (position, mass, velocity, C or stress) became non-finite (NaN / Inf) "
+              "in an earlier step; the state is invalid");
     return GSMPM_ESTATE;
   }
   if (nsub == 0) return GSMPM_OK;
@@ -2673,7 +2784,7 @@ int gsmpm_mpm_check_finite(gsmpm_mpm* h, int32_t clear, void* stream) {
     if (h->slab && h->s_drift) GSMPM_HIP(hipMemset(h->s_drift + SF_NONFIN, 0, sizeof(int)));
   }
   if (f) {
-    set_error("non-finite (NaN / Inf) particle position");
+    set_error("non-finite (NaN / Inf) particle state (position, mass, velocity, C or stress)");
     return GSMPM_ESTATE;
   }
   return GSMPM_OK;
@@ -2689,6 +2800,25 @@ int gsmpm_mpm_set_rebin_interval(gsmpm_mpm* h, int32_t substeps) {
 int gsmpm_mpm_pipeline(gsmpm_mpm* h) {
   GSMPM_REQUIRE(h, "gsmpm_mpm_pipeline: null handle");
   return use_fused(h) ? GSMPM_PIPE_FUSED : GSMPM_PIPE_PHASED;
+}
+
+int gsmpm_mpm_escapes(gsmpm_mpm* h, int32_t clear, int64_t* out, void* stream) {
+  GSMPM_REQUIRE(h && out, "gsmpm_mpm_escapes: null argument");
+  *out = 0;
+  if (!use_fused(h)) return GSMPM_OK;
+  hipStream_t st = (hipStream_t)stream;
+  unsigned v = 0;
+  unsigned* d = reinterpret_cast<unsigned*>(h->fesc + 3 + kFoldPhases);
+  GSMPM_HIP(hipMemcpyAsync(&v, d, sizeof(v), hipMemcpyDeviceToHost, st));
+  GSMPM_HIP(hipStreamSynchronize(st));
+  if (clear) GSMPM_HIP(hipMemsetAsync(d, 0, sizeof(unsigned), st));
+  *out = (int64_t)v;
+  return GSMPM_OK;
+}
+
+int gsmpm_mpm_folded(gsmpm_mpm* h) {
+  GSMPM_REQUIRE(h, "gsmpm_mpm_folded: null handle");
+  return use_fused(h) && fold_on(h) ? 1 : 0;
 }
 
 int gsmpm_mpm_resort(gsmpm_mpm* h, int32_t interval, void* stream) {
@@ -2808,9 +2938,9 @@ static int time_kernels_f(gsmpm_mpm* h, float dt, uint32_t mask, int reps, float
     return GSMPM_OK;
   };
   ms4[3] = 0.f;
-  int rc = launch_fused(h, 2, c, false, false, mask, dt, h->fesc + ep, st, nullptr);  // windows of the current x
+  int rc = launch_fused(h, 2, c, false, false, mask, dt, ep, st, nullptr);  // windows of the current x
   if (!rc) rc = launch_grid_f(h, c, dt, mask, ep, nullptr, nullptr, st, nullptr);
-  if (!rc) rc = timed(0, [&]() { return launch_fused(h, 3, c, false, true, mask, dt, h->fesc + ep, st, nullptr); });
+  if (!rc) rc = timed(0, [&]() { return launch_fused(h, 3, c, false, true, mask, dt, ep, st, nullptr); });
   if (!rc) {
     GSMPM_HIP(hipMemsetAsync(h->fesc, 0, 2 * sizeof(int), st));  // time the touched-tile update
     rc = timed(1, [&]() { return launch_grid_f(h, c, dt, mask, ep, nullptr, nullptr, st, nullptr); });
@@ -2818,7 +2948,7 @@ static int time_kernels_f(gsmpm_mpm* h, float dt, uint32_t mask, int reps, float
   if (!rc) {
     GSMPM_HIP(hipMemsetAsync(h->fcount[c ^ 1], 0, sizeof(int) * (h->ftl.ntiles + 1), st));
     GSMPM_HIP(hipMemsetAsync(h->ftflag[c ^ 1], 0, sizeof(int) * h->ftl.ntiles, st));
-    rc = launch_fused(h, 1, c, true, true, mask, dt, h->fesc + ep, st, nullptr);
+    rc = launch_fused(h, 1, c, true, true, mask, dt, ep, st, nullptr);
     if (!rc) rc = timed(2, [&]() { return finish_binning_f(h, c ^ 1, st); });
   }
   (void)hipEventDestroy(e[0]);

@@ -49,6 +49,7 @@
 #include <chrono>
 #include <cstdlib>
 #include <mutex>
+#include <atomic>
 #include <vector>
 #include <cstring>
 #include <string>
@@ -2082,21 +2083,45 @@ int gsmpm_raster_destroy(gsmpm_raster* r) {
 // caller can read what k_render and the whole forward took inside a running
 // frame loop (beside the simulator) without a host wait in the loop.
 // Forwards issued while their stream is being captured are not timed.
+// The pending list is bounded: past kTmCap entries a new one first folds the
+// oldest completed entries into running sums (a hipEventQuery, never a wait),
+// so a caller that turns timing on and never reads it holds at most kTmCap
+// forwards' events.  Timing off costs one relaxed atomic load per forward.
 namespace {
 struct FwdTiming {
   hipEvent_t e[3];
 };
+constexpr size_t kTmCap = 256;
 std::mutex g_tm_mu;
-bool g_tm_on = false;
+std::atomic<bool> g_tm_on{false};
 std::vector<FwdTiming> g_tm_pending, g_tm_free;
+double g_tm_kr = 0.0, g_tm_fw = 0.0;  // folded entries' sums (under g_tm_mu)
+int64_t g_tm_n = 0;
+// fold the oldest completed pending entries (caller holds g_tm_mu)
+void tm_fold_locked() {
+  size_t k = 0;
+  while (k < g_tm_pending.size() && g_tm_pending.size() - k > kTmCap / 2) {
+    FwdTiming& t = g_tm_pending[k];
+    if (hipEventQuery(t.e[2]) != hipSuccess) break;  // not done yet (in order on one stream)
+    float a = 0.f, b = 0.f;
+    if (hipEventElapsedTime(&a, t.e[1], t.e[2]) == hipSuccess && hipEventElapsedTime(&b, t.e[0], t.e[2]) == hipSuccess) {
+      g_tm_kr += a;
+      g_tm_fw += b;
+      ++g_tm_n;
+    }
+    g_tm_free.push_back(t);
+    ++k;
+  }
+  g_tm_pending.erase(g_tm_pending.begin(), g_tm_pending.begin() + (long)k);
+}
 struct TimingGuard {
   FwdTiming t{};
   bool on = false, done = false;
   hipStream_t st = nullptr;
   explicit TimingGuard(hipStream_t s) : st(s) {
+    if (!g_tm_on.load(std::memory_order_relaxed)) return;
     {
       std::lock_guard<std::mutex> lk(g_tm_mu);
-      if (!g_tm_on) return;
       hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
       if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
       if (!g_tm_free.empty()) {
@@ -2116,25 +2141,31 @@ struct TimingGuard {
   ~TimingGuard() {
     if (t.e[0] == nullptr) return;
     std::lock_guard<std::mutex> lk(g_tm_mu);
+    if (done && g_tm_pending.size() >= kTmCap) tm_fold_locked();
     (done ? g_tm_pending : g_tm_free).push_back(t);
   }
 };
 }  // namespace
 
 int gsmpm_raster_set_timing(int32_t on) {
-  std::lock_guard<std::mutex> lk(g_tm_mu);
-  g_tm_on = on != 0;
+  g_tm_on.store(on != 0, std::memory_order_relaxed);
   return GSMPM_OK;
 }
 
 int gsmpm_raster_timing(double* k_render_ms, double* forward_ms, int64_t* forwards) {
   GSMPM_REQUIRE(k_render_ms && forward_ms && forwards, "gsmpm_raster_timing: null argument");
   std::vector<FwdTiming> got;
+  double kr = 0.0, fw = 0.0;
+  int64_t n0 = 0;
   {
     std::lock_guard<std::mutex> lk(g_tm_mu);
     got.swap(g_tm_pending);
+    kr = g_tm_kr;
+    fw = g_tm_fw;
+    n0 = g_tm_n;
+    g_tm_kr = g_tm_fw = 0.0;
+    g_tm_n = 0;
   }
-  double kr = 0.0, fw = 0.0;
   int rc = GSMPM_OK;
   for (auto& t : got) {
     float a = 0.f, b = 0.f;
@@ -2152,7 +2183,7 @@ int gsmpm_raster_timing(double* k_render_ms, double* forward_ms, int64_t* forwar
   }
   *k_render_ms = kr;
   *forward_ms = fw;
-  *forwards = (int64_t)got.size();
+  *forwards = n0 + (int64_t)got.size();
   return rc;
 }
 

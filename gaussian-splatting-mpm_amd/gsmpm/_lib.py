@@ -100,6 +100,8 @@ _SIGS = {
     "gsmpm_mpm_set_rebin_interval": (ctypes.c_int, [c_void_p, ctypes.c_int32]),
     "gsmpm_mpm_check_finite": (ctypes.c_int, [c_void_p, ctypes.c_int32, c_void_p]),
     "gsmpm_mpm_pipeline": (ctypes.c_int, [c_void_p]),
+    "gsmpm_mpm_folded": (ctypes.c_int, [c_void_p]),
+    "gsmpm_mpm_escapes": (ctypes.c_int, [c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64), c_void_p]),
     "gsmpm_mpm_postprocess": (ctypes.c_int, [c_void_p, c_void_p]),
     "gsmpm_mpm_field_width": (ctypes.c_int, [ctypes.c_int32]),
     "gsmpm_mpm_get": (ctypes.c_int, [c_void_p, ctypes.c_int32, c_void_p, c_void_p]),

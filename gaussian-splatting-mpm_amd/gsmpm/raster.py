@@ -86,8 +86,15 @@ class Workspace:
         return self.buf.numel() - (self.ptr() - self.buf.data_ptr())
 
 
-_WS = {}
+_WS = __import__("collections").OrderedDict()  # (device, stream handle) -> Workspace, least recently used first
 _WS_LOCK = __import__("threading").Lock()
+_WS_KEEP = 8  # default workspaces kept; a process cycling through more streams evicts the oldest
+
+
+def _drop_workspace(device_index: int):
+    # the evicted workspace may still be in use by a forward queued on its stream:
+    # let the device drain before its buffer goes back to the allocator
+    torch.cuda.synchronize(torch.device("cuda", device_index))
 
 
 def workspace(device_index: int = 0, stream=None) -> Workspace:
@@ -95,15 +102,38 @@ def workspace(device_index: int = 0, stream=None) -> Workspace:
     keeps the workspace's depth-order state zero between forwards
     (csrc/dsort.h), which holds only while its forwards are ordered, so two
     streams (e.g. bench's render worker and the default stream) never share
-    one."""
+    one.  At most _WS_KEEP are kept (least recently used evicted, after a
+    device sync), so short-lived streams do not leak workspaces;
+    release_workspace(stream) drops one explicitly."""
     if stream is None:
         stream = torch.cuda.current_stream(torch.device("cuda", device_index))
     key = (device_index, int(stream.cuda_stream))
+    evict = []
     with _WS_LOCK:
         w = _WS.get(key)
         if w is None:
             w = _WS[key] = Workspace(torch.device("cuda", device_index))
+            while len(_WS) > _WS_KEEP:
+                evict.append(_WS.popitem(last=False))
+        else:
+            _WS.move_to_end(key)
+    for (dev, _), _w in evict:
+        _drop_workspace(dev)
     return w
+
+
+def release_workspace(stream=None, device_index: int = 0) -> bool:
+    """Drop the default workspace of (device, stream), e.g. before the stream
+    is destroyed (a later stream could otherwise get the same handle and with
+    it this workspace).  Returns whether one was held."""
+    if stream is None:
+        stream = torch.cuda.current_stream(torch.device("cuda", device_index))
+    key = (device_index, int(stream.cuda_stream))
+    with _WS_LOCK:
+        w = _WS.pop(key, None)
+    if w is not None:
+        _drop_workspace(device_index)
+    return w is not None
 
 
 class RasterContext:

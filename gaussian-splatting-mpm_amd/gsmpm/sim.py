@@ -95,9 +95,10 @@ class Simulator:
         check(LIB.gsmpm_mpm_step(self._h, ctypes.c_float(dt), n, arr, stream_of(self.device)), "gsmpm_mpm_step")
 
     def check_finite(self, clear: bool = False):
-        """SURVEY 5's per-frame NaN / Inf check on x: waits for the stream and
-        raises RuntimeError if any substep so far produced a non-finite
-        particle position (``step`` also raises, at the call after)."""
+        """SURVEY 5's per-frame NaN / Inf check: waits for the stream and
+        raises RuntimeError if any substep so far produced non-finite particle
+        state -- a position, or a P2G scatter input (mass, velocity, C,
+        stress) -- (``step`` also raises, at the call after)."""
         check(LIB.gsmpm_mpm_check_finite(self._h, int(bool(clear)), stream_of(self.device)), "check_finite")
 
     # ---------------------------------------------------------- slab mode --
@@ -208,6 +209,20 @@ class Simulator:
         """'fused' (k_fused + k_grid_f per substep) or 'phased' (k_p2g, k_grid, k_g2p, binning)."""
         code = check(LIB.gsmpm_mpm_pipeline(self._h), "gsmpm_mpm_pipeline")
         return "fused" if code == _lib.PIPE_FUSED else "phased"
+
+    @property
+    def folded(self) -> bool:
+        """True when each substep's grid update is folded into the next k_fused
+        launch (gsmpm_mpm_folded; one launch per substep)."""
+        return bool(check(LIB.gsmpm_mpm_folded(self._h), "gsmpm_mpm_folded"))
+
+    def escapes(self, clear: bool = False) -> int:
+        """Particle scatters that left their chunk window since set_particles or
+        the last clear (gsmpm_mpm_escapes; syncs the stream)."""
+        out = ctypes.c_int64(0)
+        check(LIB.gsmpm_mpm_escapes(self._h, int(bool(clear)), ctypes.byref(out), stream_of(self.device)),
+              "gsmpm_mpm_escapes")
+        return int(out.value)
 
     def set_rebin_interval(self, substeps: int):
         """Fused pipeline: substeps between particle re-binnings (any value >= 1 is correct)."""

@@ -90,14 +90,17 @@ int gsmpm_mpm_add_plane_collider(gsmpm_mpm* h, const double point[3], const doub
  * the activity bits of substep s, decided by the caller from the f64 host
  * clock exactly as BasicBC.isActive (boundary_conditions.py:30-31); NULL =
  * all active.  Asynchronous on `stream`.  Returns GSMPM_ESTATE (and launches
- * nothing) once an earlier call's substeps produced a non-finite (NaN / Inf)
- * particle position (SURVEY 5's per-frame check on x; the kernels set a
- * sticky host-mapped word, read here without a sync: the error surfaces at
- * the call after the frame that produced it, or at gsmpm_mpm_check_finite). */
+ * nothing) once an earlier call's substeps produced non-finite (NaN / Inf)
+ * particle state: a position, or a scatter input of P2G -- mass, velocity
+ * (after an impulse), C or the stress term -- while x may still be finite
+ * (SURVEY 5's per-frame check; the kernels set a sticky host-mapped word,
+ * read here without a sync: the error surfaces at the call after the frame
+ * that produced it, or at gsmpm_mpm_check_finite). */
 int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t n_substeps, const uint32_t* bc_active, void* stream);
 /* Synchronizes `stream`, then GSMPM_ESTATE if any substep so far produced a
- * non-finite particle position (clear != 0 resets the word; set_particles
- * does too), else GSMPM_OK.  No reference counterpart. */
+ * non-finite particle state (position, mass, velocity, C or stress; clear
+ * != 0 resets the word; set_particles does too), else GSMPM_OK.  No
+ * reference counterpart. */
 int gsmpm_mpm_check_finite(gsmpm_mpm* h, int32_t clear, void* stream);
 
 /* ------------------------------------------------- multi-GPU slabs ---
@@ -211,6 +214,20 @@ int gsmpm_mpm_resort(gsmpm_mpm* h, int32_t interval, void* stream);
 int gsmpm_mpm_set_rebin_interval(gsmpm_mpm* h, int32_t substeps);
 /* GSMPM_PIPE_FUSED or GSMPM_PIPE_PHASED: the pipeline gsmpm_mpm_step runs now. */
 int gsmpm_mpm_pipeline(gsmpm_mpm* h);
+/* 1 when the fused pipeline folds each substep's grid update into the next
+ * k_fused launch (one launch per substep; a k_grid_f launch only after a
+ * re-binning), 0 otherwise (the per-phase pipeline, slabs, or GSMPM_FOLD=0
+ * at create).  The grid update it folds is utils.py:177-183 +
+ * solver.py:41-46; results are bit-identical either way. */
+int gsmpm_mpm_folded(gsmpm_mpm* h);
+/* Fused pipeline diagnostics: the particle scatters since set_particles (or
+ * the last clear) that left their chunk's window -- they took the global
+ * float-atomic path, and the next grid update evaluates every node they may
+ * reach -- (particles binned outside the grid count every substep).
+ * Synchronizes `stream`.  0 on the per-phase pipeline.  No reference
+ * counterpart (the reference scatters every particle with atomics,
+ * utils.py:89-134). */
+int gsmpm_mpm_escapes(gsmpm_mpm* h, int32_t clear, int64_t* out, void* stream);
 
 /* MPM_Simulator.postprocess (solver.py:135-137): compute_cov_from_F and
  * compute_R_from_F (utils.py:376-433). */

@@ -215,6 +215,40 @@ def test_config_B_lego_full_frame(dev):
     assert rec["end_to_end"]["pixels_over_1e-3"] <= 1e-4 * d.size, rec["end_to_end"]
 
 
+def test_config_B_prime_lego_240549(dev):
+    """SURVEY 8(d) config B's "also report 240,549": lego.json with the real lego
+    model's Gaussian count (models/lego/point_cloud/iteration_7000),
+    128^3, ONE frame as main.py runs it (main.py:303-313: 100 p2g2p calls, one
+    step call of 100 substeps through the captured graph, then postprocess).
+    Most tiles hold several 256-particle chunks (the multi-chunk path of the
+    fused pipeline).  x and cov are checked PER ELEMENT against the OpenMP
+    oracle: every element within 1e-4 of itself (floored at 1e-3 of the
+    field's max); F_trial, R at 1e-4 of the field's max; v, C at the derived
+    bounds."""
+    from gpu_helpers import dropin_sim
+    prob = lego_problem(240_549, 128)
+    assert len(prob["x"]) == 240_549
+    ref, imps, ops = build_oracle_sim(prob, threaded=True)
+    dt = prob["cfg"]["substep_dt"]
+    s, args = dropin_sim(prob, dev)
+    assert args.steps_per_frame == 100
+    for _ in range(args.steps_per_frame):
+        s.p2g2p(dt)
+    t = oracle_run(ref, imps, ops, dt, args.steps_per_frame)
+    assert abs(s.time - t) == 0.0
+    got = _state(s)
+    stats = s._sim.debug_stats()
+    assert stats["max_per_tile"] > 256, stats  # multi-chunk tiles
+    rec = {"config": "lego.json", "N": 240_549, "n_grid": 128, "max_per_tile": stats["max_per_tile"],
+           "folded": s._sim.folded}
+    rec["errs"] = _errs(s, ref)
+    _check(rec["errs"], "B' substep 100")
+    rec["x_elem"] = rel_err_elem(got["x"], ref.x)
+    assert rec["x_elem"] < TOL, rec
+    rec["post"] = _post(s, ref, per_element=True)
+    _dump("config_B_prime", rec)
+
+
 @pytest.mark.parametrize("material", ["jelly", "metal"])
 def test_config_C_lego_fracture(dev, material):
     """configs[2]: lego-fracture.json as written (jelly, impulse on substeps 0-9,

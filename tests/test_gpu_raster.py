@@ -637,3 +637,19 @@ def test_in_frame_timing(dev):
         raster.set_timing(False)
     raster.forward(*args, **kw)
     assert raster.timing()[2] == 0
+
+
+def test_default_workspaces_bounded_and_released(dev):
+    """The default workspace cache (gsmpm.raster.workspace) keeps at most
+    _WS_KEEP per process -- short-lived streams evict the least recently used
+    one after a device sync instead of leaking a workspace each -- and
+    release_workspace drops one explicitly."""
+    import torch
+    from gsmpm import raster
+    streams = [torch.cuda.Stream(dev) for _ in range(raster._WS_KEEP + 4)]
+    for st in streams:
+        raster.workspace(dev.index or 0, st)
+    assert len(raster._WS) <= raster._WS_KEEP
+    last = streams[-1]
+    assert raster.release_workspace(last, dev.index or 0) is True
+    assert raster.release_workspace(last, dev.index or 0) is False
