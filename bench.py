@@ -1132,6 +1132,7 @@ def main():
     if time_render:
         raster.timing()
         raster.set_timing(True)
+    esc0 = sim.escapes() if hasattr(sim, "escapes") else None  # (a sync, outside the timed region)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         frame()
@@ -1145,6 +1146,10 @@ def main():
         if n_fw:
             render_in_frame = {"forwards": n_fw, "k_render_ms": round(kr_ms / n_fw, 4),
                                "forward_ms": round(fw_ms / n_fw, 4)}
+    # particle scatters that left their chunk window so far (fused pipeline; a diagnostic of the
+    # re-binning interval: gsmpm_mpm_escapes)
+    escapes = sim.escapes() if (world == 1 and hasattr(sim, "escapes")) else None
+    escapes_timed = None if escapes is None or esc0 is None else escapes - esc0
     if rq is not None:  # the render worker's last frame is done (flush): stop it
         rq.put(None)
         worker.join()
@@ -1264,6 +1269,11 @@ def main():
         # per forward of the timed frames, on the render's stream beside the simulator
         "render_in_frame": render_in_frame,
         "num_rendered": state["K"],
+        # particle scatters that left their chunk window (each makes the next k_grid_f sweep every tile):
+        # since set_particles, and in the timed frames
+        "escapes_since_start": escapes,
+        "escapes_timed": escapes_timed,
+        "rebin_interval": args.rebin or None,
     }
     if kern is not None:
         # dominant kernel: the one with the most time per frame among those that

@@ -155,6 +155,7 @@ struct FusedRare {
   int* esc_clr;
   float grav[3];  // gravity (f32): a FOLD launch forms dt * gravity as the host's grid_step does
   unsigned* esc_count;  // particle scatters that escaped their chunk window, summed (gsmpm_mpm_escapes)
+  float4* esc_nodes;    // FOLD: [np][27] the stencil node values of a particle outside its chunk's window
 };
 
 // ---------------------------------------------------------------- the fold --
@@ -173,7 +174,7 @@ struct FusedRare {
 // from L2 / MALL, written by the launch before.
 constexpr int kFT[3] = {kFT0, kFT1, kFT2};
 #ifndef GSMPM_FOLD_BATCH
-#define GSMPM_FOLD_BATCH 2
+#define GSMPM_FOLD_BATCH 1
 #endif
 constexpr int kFoldB = GSMPM_FOLD_BATCH;  // nodes a lane stages at once (their loads in flight together)
 // per axis: window coordinate w (node o + w of tile t's window, o = t T - 1) ->
@@ -207,59 +208,79 @@ __device__ __forceinline__ void add4f(float4& a, const float4& b) {
 // issues their loads, fold_acc sums them (+ further chunks): split so a
 // caller can have several nodes' loads in flight at once.
 struct FoldNode {
-  int off[8];   // first chunk's slot offset of each cover (valid where on)
-  int c0[8];    // first chunk (further chunks: c0 + 1 ...)
-  int nc[8];    // chunks
-  int loc[8];   // the node's offset inside each cover's window
-  int on;       // bit e: cover e exists and its box holds the node
+  int off[8];  // first chunk's slot offset of each cover (valid where on)
+  int on;      // bit e: cover e exists and its box holds the node
+  int extra;   // bit e: ... and that cover's tile has further chunks
 };
-template <typename Tab>
-__device__ __forceinline__ void fold_prep(const int (&w)[3], Tab tab, FoldNode& f) {
+// cover e of window node w: its 27-neighbour index and the node's offset in its window
+__device__ __forceinline__ void fold_cover(const int (&w)[3], int e, int& ci, int (&wn)[3], bool& valid) {
   int d[3], sec[3];
 #pragma unroll
   for (int ax = 0; ax < 3; ++ax) fold_axis(w[ax], kFT[ax], d[ax], sec[ax]);
+  const int b0 = e >> 2, b1 = (e >> 1) & 1, b2 = e & 1;
+  const int a0 = d[0] + (b0 ? sec[0] : 0), a1 = d[1] + (b1 ? sec[1] : 0), a2 = d[2] + (b2 ? sec[2] : 0);
+  ci = (a0 + 1) * 9 + (a1 + 1) * 3 + (a2 + 1);
+  wn[0] = w[0] - a0 * kFT0;
+  wn[1] = w[1] - a1 * kFT1;
+  wn[2] = w[2] - a2 * kFT2;
+  valid = ((!b0) | (sec[0] != 0)) & ((!b1) | (sec[1] != 0)) & ((!b2) | (sec[2] != 0));
+}
+__device__ __forceinline__ bool in_box(const int (&wn)[3], int q) {
+  return (wn[0] >= (q & 15)) & (wn[1] >= ((q >> 4) & 15)) & (wn[2] >= ((q >> 8) & 15)) & (wn[0] <= ((q >> 12) & 15)) &
+         (wn[1] <= ((q >> 16) & 15)) & (wn[2] <= ((q >> 20) & 15));
+}
+template <typename Tab>
+__device__ __forceinline__ void fold_prep(const int (&w)[3], Tab tab, FoldNode& f) {
   f.on = 0;
+  f.extra = 0;
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    const int b0 = e >> 2, b1 = (e >> 1) & 1, b2 = e & 1;
-    const int a0 = d[0] + (b0 ? sec[0] : 0), a1 = d[1] + (b1 ? sec[1] : 0), a2 = d[2] + (b2 ? sec[2] : 0);
-    const int ci = (a0 + 1) * 9 + (a1 + 1) * 3 + (a2 + 1);
+    int ci, wn[3];
+    bool valid;
+    fold_cover(w, e, ci, wn, valid);
     int c0, nc, q;
     tab(ci, c0, nc, q);
-    const int wn0 = w[0] - a0 * kFT0, wn1 = w[1] - a1 * kFT1, wn2 = w[2] - a2 * kFT2;
-    const bool on = ((!b0) | (sec[0] != 0)) & ((!b1) | (sec[1] != 0)) & ((!b2) | (sec[2] != 0)) & (nc > 0) &
-                    (wn0 >= (q & 15)) & (wn1 >= ((q >> 4) & 15)) & (wn2 >= ((q >> 8) & 15)) &
-                    (wn0 <= ((q >> 12) & 15)) & (wn1 <= ((q >> 16) & 15)) & (wn2 <= ((q >> 20) & 15));
+    const bool on = valid & (nc > 0) & in_box(wn, q);
     f.on |= on ? (1 << e) : 0;
-    f.loc[e] = slot_loc(wn0, wn1, wn2);
-    f.c0[e] = c0;
-    f.nc[e] = nc;
-    f.off[e] = c0 * kFWin + f.loc[e];
+    f.extra |= (on & (nc > 1)) ? (1 << e) : 0;
+    f.off[e] = c0 * kFWin + slot_loc(wn[0], wn[1], wn[2]);
   }
 }
 __device__ __forceinline__ void fold_load(const float4* __restrict__ slots, const FoldNode& f, float4 (&v)[8]) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) v[e] = ((f.on >> e) & 1) ? ld_slot4(slots, f.off[e]) : make_float4(0.f, 0.f, 0.f, 0.f);
 }
-__device__ __forceinline__ float4 fold_acc(const float4* __restrict__ slots, const FoldNode& f, const float4 (&v)[8]) {
+// the sum: the first chunks in e order, then (rare: tiles of > 256 particles)
+// the second chunks in e order and the third and later ones, their offsets
+// recomputed from the tables (not kept live across the loads)
+template <typename Tab>
+__device__ __forceinline__ float4 fold_acc(const float4* __restrict__ slots, const int (&w)[3], Tab tab,
+                                           const FoldNode& f, const float4 (&v)[8]) {
   float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
   for (int e = 0; e < 8; ++e) add4f(a, v[e]);
-  int extra = 0;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) extra |= (((f.on >> e) & 1) && f.nc[e] > 1) ? (1 << e) : 0;
-  if (extra) {  // the second chunks of the covering tiles (e order), then the third and later ones
+  if (f.extra) {
+    int c0s[8], ncs[8], locs[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float4 u = ((extra >> e) & 1) ? ld_slot4(slots, (f.c0[e] + 1) * kFWin + f.loc[e])
-                                          : make_float4(0.f, 0.f, 0.f, 0.f);
+      int ci, wn[3];
+      bool valid;
+      fold_cover(w, e, ci, wn, valid);
+      int q;
+      tab(ci, c0s[e], ncs[e], q);
+      locs[e] = slot_loc(wn[0], wn[1], wn[2]);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float4 u = ((f.extra >> e) & 1) ? ld_slot4(slots, (c0s[e] + 1) * kFWin + locs[e])
+                                            : make_float4(0.f, 0.f, 0.f, 0.f);
       add4f(a, u);
     }
-    while (extra) {
-      const int e = __builtin_ctz(extra);
-      extra &= extra - 1;
-      for (int c = f.c0[e] + 2; c < f.c0[e] + f.nc[e]; ++c) add4f(a, ld_slot4(slots, c * kFWin + f.loc[e]));
-    }
+    // (an unrolled scan, not a ctz loop: a dynamic index would put the arrays in scratch)
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if ((f.extra >> e) & 1)
+        for (int c = c0s[e] + 2; c < c0s[e] + ncs[e]; ++c) add4f(a, ld_slot4(slots, c * kFWin + locs[e]));
   }
   return a;
 }
@@ -269,16 +290,16 @@ __device__ __forceinline__ float4 fold_sum(const float4* __restrict__ slots, con
   fold_prep(w, tab, f);
   float4 v[8];
   fold_load(slots, f, v);
-  return fold_acc(slots, f, v);
+  return fold_acc(slots, w, tab, f, v);
 }
 
 // The slow path: the updated velocity of any grid node (i, j, k) from the
 // previous P2G's windows, through the tile tables of the node's owner tile
 // (a particle of a FOLD launch that left its chunk's window, or one binned
 // outside the grid).  0 outside the grid.
-__device__ __noinline__ float4 fold_node(int i, int j, int k, const GridDims& g, const FTiles& tl, const ChunkIn& ck,
-                                         const FusedRare* __restrict__ rare, const GridStep& gs,
-                                         const BcTable* __restrict__ bct, bool esc) {
+__device__ __forceinline__ float4 fold_node(int i, int j, int k, const GridDims& g, const FTiles& tl, const ChunkIn& ck,
+                                            const FusedRare* __restrict__ rare, const GridStep& gs,
+                                            const BcTable* __restrict__ bct, bool esc) {
   const int ng = g.ng;
   if ((unsigned)i >= (unsigned)ng || (unsigned)j >= (unsigned)ng || (unsigned)k >= (unsigned)ng)
     return make_float4(0.f, 0.f, 0.f, 0.f);
@@ -498,6 +519,12 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
   constexpr bool G2P = (MODE & 1) != 0, P2G = (MODE & 2) != 0;
   constexpr bool FOLD = G2P && (MODE & 4) != 0;  // the previous substep's grid update staged from its chunk windows
   __shared__ int s_fc0[27], s_fnc[27], s_fbx[27];  // FOLD: the 27 neighbour tiles' tables
+  // FOLD: particles outside their chunk's window (escapes; rare): their stencil
+  // nodes are evaluated by the whole workgroup into the upper half of s_acc
+  // (free while G2P runs: the v window uses the lower half), kEscMax at a time
+  constexpr int kEscMax = kFWin / 27;
+  __shared__ int s_nesc;
+  __shared__ int s_eb[3][kEscMax];
   // FOLD: the previous substep's grid step, and whether its P2G had escapes (uniform)
   GridStep fgs{};
   bool fesc = false;
@@ -519,7 +546,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
   __shared__ int s_rcnt[16];
   float4* s_win = reinterpret_cast<float4*>(s_acc);
   const int ng = g.ng;
-  constexpr int SK = MODE == 3 ? 0 : 1;  // diagnostics slot (k_p2g's / k_g2p's in the per-phase pipeline)
+  constexpr int SK = (MODE & 3) == 3 ? 0 : 1;  // diagnostics slot (k_p2g's / k_g2p's in the per-phase pipeline)
   sim_prio();
   stamp(SK, 0);
   // the first chunk's record, box and lane order are requested with the chunk
@@ -597,6 +624,7 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
         for (int i = 0; i < 9; ++i) C[i / 3][i % 3] = ps.ld(PC + i, p);
       }
     }
+    int eslot = -1;  // FOLD: this lane's escape slot (its stencil nodes at s_win[kFWin + 27 eslot ...])
     if constexpr (G2P) {
       if (FOLD && !outside) {
         // the 27 neighbour tiles' first chunk, chunk count and stencil box of the previous P2G (lanes 0..26)
@@ -613,7 +641,21 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
           s_fnc[k] = nc;
           s_fbx[k] = bx;
         }
+        if (k == 0) s_nesc = 0;
         __syncthreads();
+        // a lane whose particle left the window takes an escape slot (its base in s_eb)
+        if (k < cnt) {
+          int bq[3];
+          base_of(x, g.inv_dx, bq);
+          if (!(in_grid(x, g) && in_window(bq, o0, o1, o2))) {
+            eslot = atomicAdd(&s_nesc, 1);
+            if (eslot < kEscMax) {
+              s_eb[0][eslot] = bq[0];
+              s_eb[1][eslot] = bq[1];
+              s_eb[2][eslot] = bq[2];
+            }
+          }
+        }
         int lo[3], hi[3];
         box_unpack(cbox, lo, hi);
         const int n1 = hi[1] - lo[1] + 1, n2 = hi[2] - lo[2] + 1, n12 = n1 * n2;
@@ -653,12 +695,20 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
             const int ix = o0 + w3[u][0], iy = o1 + w3[u][1], iz = o2 + w3[u][2];
             float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
             if (gin[u]) {
-              float4 sum = fold_acc(sp, fn[u], vv[u]);
+              float4 sum = fold_acc(sp, w3[u], tab, fn[u], vv[u]);
               if (fesc) add4f(sum, rare->gacc_prev[((size_t)ix * ng + iy) * ng + iz]);
               val = node_update(sum, ix, iy, iz, g, fgs, fbct);
             }
             if (live[u]) s_win[(w3[u][0] * kFW1 + w3[u][1]) * kFW2 + w3[u][2]] = val;
           }
+        }
+        // the escaped particles' stencil nodes, one node a lane (workgroup-uniform skip when none)
+        __syncthreads();
+        const int ne = min(s_nesc, kEscMax);
+        for (int t = k; t < ne * 27; t += 256) {
+          const int sl = t / 27, qn = t - sl * 27;
+          s_win[kFWin + t] = fold_node(s_eb[0][sl] + qn / 9, s_eb[1][sl] + (qn / 3) % 3, s_eb[2][sl] + qn % 3, g, tl,
+                                       ck, rare, fgs, fbct, fesc);
         }
       } else if (!outside) {
         // the chunk's stencil box from its last P2G (particles unmoved since), else the whole window
@@ -707,7 +757,19 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
         int b[3];
         base_of(x, g.inv_dx, b);
         float gvd[3][3];
-        if (!outside && in_grid(x, g) && in_window(b, o0, o1, o2)) {
+        const bool inwin = !outside && in_grid(x, g) && in_window(b, o0, o1, o2);
+        const bool eslds = eslot >= 0 && eslot < kEscMax;  // nodes evaluated by the workgroup (LDS)
+        if (FOLD && !inwin && !eslds) {
+          // the outside chunk, or more escapes than LDS slots (rarer still): this
+          // lane's 27 stencil nodes one at a time through the owner tiles' tables,
+          // into its rows of esc_nodes (a rolled loop: no call, no stack)
+          float4* en = rare->esc_nodes + (size_t)p * 27;
+#pragma unroll 1
+          for (int qn = 0; qn < 27; ++qn)
+            en[qn] = fold_node(b[0] + qn / 9, b[1] + (qn / 3) % 3, b[2] + qn % 3, g, tl, ck, rare, fgs,
+                               static_cast<const BcTable*>(rare->bct), fesc);
+        }
+        if (inwin) {
           g2p_gather<kG2pB128>(x, g,
                      [&](const int (&base)[3], int i, int j, int kk) {
                        const int q = ((base[0] - o0 + i) * kFW1 + (base[1] - o1 + j)) * kFW2 + (base[2] - o2 + kk);
@@ -720,7 +782,8 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
                        const int ix = base[0] + i, iy = base[1] + j, iz = base[2] + kk;
                        float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
                        if constexpr (FOLD) {
-                         r = fold_node(ix, iy, iz, g, tl, ck, rare, fgs, static_cast<const BcTable*>(rare->bct), fesc);
+                         const int qn = i * 9 + j * 3 + kk;
+                         r = eslds ? s_win[kFWin + eslot * 27 + qn] : rare->esc_nodes[(size_t)p * 27 + qn];
                        } else {
                          if ((unsigned)ix < (unsigned)ng && (unsigned)iy < (unsigned)ng && (unsigned)iz < (unsigned)ng)
                            r = gvel[((size_t)ix * ng + iy) * ng + iz];

@@ -1534,10 +1534,14 @@ struct gsmpm_mpm {
                                           // rotation's [12] (one per phase) and one scratch word
   // the folded grid update (fused.h FOLD): launch r of a step call writes slot
   // buffer r % 2, tile-box buffer r % 2 and escape accumulator r % 3
-  bool fold = true;                       // GSMPM_FOLD=0: a k_grid_f launch after every k_fused (A/B)
+  // GSMPM_FOLD=1 at create (A/B, off by default): measured and rejected in
+  // round 6 -- the folded staging costs k_fused more than k_grid_f + its
+  // boundary
+  bool fold = false;
   float4* fslots2 = nullptr;              // the second slot buffer [max_chunks + 1][kFWin]
   float4* gacc_f[3] = {nullptr, nullptr, nullptr};  // escape accumulators ([0] = gacc)
   int* ftbox2[2] = {nullptr, nullptr};    // the second tile-box buffer per bins parity
+  float4* fesc_nodes = nullptr;           // [np][27] stencil values of particles outside their window
   int* fcbox[2] = {nullptr, nullptr};     // [max_chunks] per-chunk stencil boxes (fused.h)
   int* ftbox[2] = {nullptr, nullptr};     // [ntiles] per-tile stencil boxes
   int2* frcov[2] = {nullptr, nullptr};    // [ntiles][kRecStride] cover records per touched position (k_grid_f)
@@ -1904,6 +1908,7 @@ static FusedRare rare_of(gsmpm_mpm* h, int c, int slot) {
   }
   for (int d = 0; d < 3; ++d) r.grav[d] = (float)h->prm.gravity[d];
   r.esc_count = reinterpret_cast<unsigned*>(h->fesc + 3 + kFoldPhases);
+  r.esc_nodes = h->fesc_nodes;
   return r;
 }
 // k_fused's rare arguments in device memory, rewritten (outside captures,
@@ -2511,6 +2516,8 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
       if ((e = hipMalloc(&h->gacc_f[b], sizeof(float4) * nn)) != hipSuccess) return fail(e, "hipMalloc grid acc");
       if ((e = hipMemset(h->gacc_f[b], 0, sizeof(float4) * nn)) != hipSuccess) return fail(e, "hipMemset");
     }
+    if ((e = hipMalloc(&h->fesc_nodes, sizeof(float4) * 27 * (size_t)h->np)) != hipSuccess)
+      return fail(e, "hipMalloc escape nodes");
     for (int c = 0; c < 2; ++c) {
       if ((e = hipMalloc(&h->ftbox2[c], sizeof(int) * (size_t)h->ftl.ntiles)) != hipSuccess)
         return fail(e, "hipMalloc boxes");
@@ -2585,6 +2592,7 @@ int gsmpm_mpm_destroy(gsmpm_mpm* h) {
   (void)hipFree(h->gacc_f[1]);
   (void)hipFree(h->gacc_f[2]);
   for (int c = 0; c < 2; ++c) (void)hipFree(h->ftbox2[c]);
+  (void)hipFree(h->fesc_nodes);
   (void)hipFree(h->fesc);
   (void)hipFree(h->frare_dev);
   (void)hipFree(h->planes_alt);

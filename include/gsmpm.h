@@ -216,9 +216,10 @@ int gsmpm_mpm_set_rebin_interval(gsmpm_mpm* h, int32_t substeps);
 int gsmpm_mpm_pipeline(gsmpm_mpm* h);
 /* 1 when the fused pipeline folds each substep's grid update into the next
  * k_fused launch (one launch per substep; a k_grid_f launch only after a
- * re-binning), 0 otherwise (the per-phase pipeline, slabs, or GSMPM_FOLD=0
- * at create).  The grid update it folds is utils.py:177-183 +
- * solver.py:41-46; results are bit-identical either way. */
+ * re-binning): GSMPM_FOLD=1 in the environment at create, off by default
+ * (measured slower); 0 otherwise (the default, the per-phase
+ * pipeline, slabs).  The grid update it folds is utils.py:177-183 +
+ * solver.py:41-46; without escapes the results are bit-identical either way. */
 int gsmpm_mpm_folded(gsmpm_mpm* h);
 /* Fused pipeline diagnostics: the particle scatters since set_particles (or
  * the last clear) that left their chunk's window -- they took the global
