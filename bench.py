@@ -1273,7 +1273,7 @@ def main():
         # since set_particles, and in the timed frames
         "escapes_since_start": escapes,
         "escapes_timed": escapes_timed,
-        "rebin_interval": args.rebin or None,
+        "rebin": sim.rebin_state() if hasattr(sim, "rebin_state") else None,
     }
     if kern is not None:
         # dominant kernel: the one with the most time per frame among those that

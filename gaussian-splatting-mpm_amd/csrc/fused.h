@@ -156,6 +156,8 @@ struct FusedRare {
   float grav[3];  // gravity (f32): a FOLD launch forms dt * gravity as the host's grid_step does
   unsigned* esc_count;  // particle scatters that escaped their chunk window, summed (gsmpm_mpm_escapes)
   float4* esc_nodes;    // FOLD: [np][27] the stencil node values of a particle outside its chunk's window
+  unsigned* vmax;       // G2P-only launches (a step call's last): max |v| component over the particles, as
+                        // f32 bits (atomicMax), for the next call's re-binning count (mpm.hip choose_rebins)
 };
 
 // ---------------------------------------------------------------- the fold --
@@ -859,6 +861,13 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
           bo.ptile[p] = nt;
           bo.pslot[p] = code >= 0 ? s_base[code] + lslot : reserve_f(bo, nt, 1);
         }
+      }
+      if constexpr (!P2G) {  // the call's last launch: the particles' fastest velocity component
+        float vm = 0.f;
+        if (k < cnt) vm = fmaxf(fabsf(v[0]), fmaxf(fabsf(v[1]), fabsf(v[2])));
+        if (!(vm <= 3.0e38f)) vm = 3.0e38f;  // NaN / Inf (flagged elsewhere): keep the bits ordered
+        vm = wave_max_nonneg_dpp(vm);
+        if ((k & 63) == 0 && vm > 0.f && rare->vmax) atomicMax(rare->vmax, __float_as_uint(vm));
       }
       __syncthreads();  // the window is consumed (and s_cnt / s_base read) before LDS is reused
       if (w == (int)blockIdx.x) stamp(SK, 3);

@@ -48,11 +48,13 @@ namespace gsmpm {
 #define GSMPM_REBIN_SF 20
 #endif
 constexpr int kRebinStressFree = GSMPM_REBIN_SF;  // default re-binning interval, stress-free materials
-// ... stress-bearing ones: 20 as well since round 5 (lego-fracture metal, 3
-// rounds: value 2.628 -> 2.672e9, frame 3.80 -> 3.74 ms against 10;
-// profiles/r05/ab/ab_rebin_interval_metal_r05ax.txt)
+// ... stress-bearing ones: 25 since round 6 (lego-fracture metal has no
+// escapes at 20-40 and the frame is 0.8 % shorter at 25-40 than at 20,
+// profiles/r06/rebin_sweep_r06i.txt; round 5 took 10 -> 20, frame 3.80 ->
+// 3.74 ms, profiles/r05/ab/ab_rebin_interval_metal_r05ax.txt); a call of
+// 100 substeps re-bins 4 times
 #ifndef GSMPM_REBIN_STRESS
-#define GSMPM_REBIN_STRESS 20
+#define GSMPM_REBIN_STRESS 25
 #endif
 constexpr int kRebinStress = GSMPM_REBIN_STRESS;
 constexpr int kChunk = 256;  // particles per work chunk (one per lane of a 256-lane workgroup)
@@ -1542,6 +1544,20 @@ struct gsmpm_mpm {
   float4* gacc_f[3] = {nullptr, nullptr, nullptr};  // escape accumulators ([0] = gacc)
   int* ftbox2[2] = {nullptr, nullptr};    // the second tile-box buffer per bins parity
   float4* fesc_nodes = nullptr;           // [np][27] stencil values of particles outside their window
+  // adaptive re-binning (round 6): the re-binnings of a step call are chosen
+  // from the particles' fastest velocity at the end of the call before
+  // (vmax_dev, copied to vmax_host without a sync), so that no particle
+  // moves more than ~0.8 of a cell between two re-binnings -- the moves that
+  // leave a chunk's window and make the next grid update sweep every tile
+  // (DESIGN.md §3.4).  rebin_interval is then the longest spacing allowed.
+  // GSMPM_REBIN_AUTO=1 at create (A/B, off by default): it removes the
+  // escape storms of long intervals (lego R = 50: 3.95 -> 3.26 ms/frame) but
+  // at the default interval the extra re-binnings of the fall cost the
+  // 20-frame bench 2-3 %
+  bool rebin_auto = false;
+  unsigned* vmax_dev = nullptr;           // [1] max |v| component of the last G2P-only launch (f32 bits)
+  float* vmax_host = nullptr;             // pinned copy, read by the next call
+  int rebin_m = 0;                        // re-binnings of the current call (0: from rebin_interval)
   int* fcbox[2] = {nullptr, nullptr};     // [max_chunks] per-chunk stencil boxes (fused.h)
   int* ftbox[2] = {nullptr, nullptr};     // [ntiles] per-tile stencil boxes
   int2* frcov[2] = {nullptr, nullptr};    // [ntiles][kRecStride] cover records per touched position (k_grid_f)
@@ -1909,6 +1925,7 @@ static FusedRare rare_of(gsmpm_mpm* h, int c, int slot) {
   for (int d = 0; d < 3; ++d) r.grav[d] = (float)h->prm.gravity[d];
   r.esc_count = reinterpret_cast<unsigned*>(h->fesc + 3 + kFoldPhases);
   r.esc_nodes = h->fesc_nodes;
+  r.vmax = h->slab ? nullptr : h->vmax_dev;
   return r;
 }
 // k_fused's rare arguments in device memory, rewritten (outside captures,
@@ -2032,6 +2049,7 @@ static int launch_substeps_f(gsmpm_mpm* h, float dt, int nsub, const uint32_t* b
   // per BC-mask sequence from call to call (a capture inside a timed frame).
   // Slabs re-bin every R substeps, in step with their migrations.
   int m = std::max(1, (nsub + R - 1) / R);
+  if (!h->slab && h->rebin_m > 0) m = std::min(std::max(m, h->rebin_m), nsub);  // the call's chosen count
   if (!h->slab && (m & 1) && m < nsub) ++m;
   auto bin_at = [&](int s) {
     if (s == nsub) return true;
@@ -2056,6 +2074,7 @@ static int launch_substeps_f(gsmpm_mpm* h, float dt, int nsub, const uint32_t* b
       GSMPM_HIP(hipMemsetAsync(h->fcount[bp ^ 1], 0, sizeof(int) * (h->ftl.ntiles + 1), st));
       GSMPM_HIP(hipMemsetAsync(h->ftflag[bp ^ 1], 0, sizeof(int) * h->ftl.ntiles, st));
     }
+    if (mode == 1 && !h->slab && h->vmax_dev) GSMPM_HIP(hipMemsetAsync(h->vmax_dev, 0, sizeof(unsigned), st));
     // FOLD: the launch before a re-binning one zeroes its counts (no grid launch between them)
     const bool zero_next = fold && !bin && s < nsub && bin_at(s + 1);
     const bool fl = fold && boxed && (mode & 1);
@@ -2258,6 +2277,7 @@ static int graph_substeps(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc, 
   key.push_back((uint32_t)h->fep);
   key.push_back((uint32_t)h->rebin_interval);
   key.push_back(fold_on(h) ? 1u : 0u);
+  key.push_back((uint32_t)h->rebin_m);
   key.push_back(h->planes_alt && h->planes > h->planes_alt ? 1u : 0u);  // which particle buffer is current
   key.push_back(xp ? (uint32_t)(((uintptr_t)xp->comm >> 4) ^ (uint32_t)xp->kind) : 0u);
   if (h->slab) {  // where the migrations fall, and the buffers they swap (rects / capacity changes drop graphs)
@@ -2518,6 +2538,13 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
     }
     if ((e = hipMalloc(&h->fesc_nodes, sizeof(float4) * 27 * (size_t)h->np)) != hipSuccess)
       return fail(e, "hipMalloc escape nodes");
+    if ((e = hipMalloc(&h->vmax_dev, sizeof(unsigned))) != hipSuccess ||
+        (e = hipMemset(h->vmax_dev, 0, sizeof(unsigned))) != hipSuccess)
+      return fail(e, "hipMalloc vmax");
+    if ((e = hipHostMalloc((void**)&h->vmax_host, sizeof(float), hipHostMallocDefault)) != hipSuccess)
+      return fail(e, "hipHostMalloc vmax");
+    *h->vmax_host = 0.f;
+    if (const char* ra = std::getenv("GSMPM_REBIN_AUTO")) h->rebin_auto = ra[0] != '0';
     for (int c = 0; c < 2; ++c) {
       if ((e = hipMalloc(&h->ftbox2[c], sizeof(int) * (size_t)h->ftl.ntiles)) != hipSuccess)
         return fail(e, "hipMalloc boxes");
@@ -2593,6 +2620,8 @@ int gsmpm_mpm_destroy(gsmpm_mpm* h) {
   (void)hipFree(h->gacc_f[2]);
   for (int c = 0; c < 2; ++c) (void)hipFree(h->ftbox2[c]);
   (void)hipFree(h->fesc_nodes);
+  (void)hipFree(h->vmax_dev);
+  if (h->vmax_host) (void)hipHostFree(h->vmax_host);
   (void)hipFree(h->fesc);
   (void)hipFree(h->frare_dev);
   (void)hipFree(h->planes_alt);
@@ -2742,6 +2771,32 @@ int gsmpm_mpm_add_plane_collider(gsmpm_mpm* h, const double p[3], const double n
   return rc ? rc : id;
 }
 
+namespace gsmpm {
+// The re-binnings of the next step call (fused pipeline, one domain): enough
+// that no particle moves more than 0.8 cell between two of them, from the
+// fastest velocity component the previous call ended with (read from pinned
+// memory without a sync: one or two calls old) plus the velocity gravity can
+// add over two calls; at least the count rebin_interval asks for; a call with
+// an active impulse (boundary_conditions.py:41-45: an unbounded kick)
+// re-bins every 5 substeps.  A spacing that turns out too long only costs
+// time: the particles that leave their window take the escape path.
+static void choose_rebins(gsmpm_mpm* h, float dt, int nsub, const uint32_t* bc) {
+  h->rebin_m = 0;
+  if (!h->rebin_auto || h->slab || !h->vmax_host || nsub < 2) return;
+  const float vprev = *(volatile float*)h->vmax_host;
+  const double g = std::sqrt(h->prm.gravity[0] * h->prm.gravity[0] + h->prm.gravity[1] * h->prm.gravity[1] +
+                             h->prm.gravity[2] * h->prm.gravity[2]);
+  const double v = (std::isfinite(vprev) ? (double)vprev : 0.0) + 2.0 * g * (double)nsub * dt;
+  const double cells = v * (double)nsub * dt * h->g.inv_dx;  // cells the fastest particle crosses in the call
+  int m = (int)std::ceil(cells / 0.8);
+  bool imp = false;
+  for (int b = 0; b < h->host_bc.n_imp && !imp; ++b)
+    for (int s = 0; s < nsub && !imp; ++s) imp = !bc || ((bc[s] >> h->host_bc.imp[b].bit) & 1u);
+  if (imp) m = std::max(m, (nsub + 4) / 5);
+  h->rebin_m = std::min(std::max(m, 0), nsub);
+}
+}  // namespace gsmpm
+
 int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t nsub, const uint32_t* bc, void* stream) {
   GSMPM_REQUIRE(h, "gsmpm_mpm_step: null handle");
   if (!h->has_particles) {
@@ -2767,15 +2822,21 @@ int gsmpm_mpm_step(gsmpm_mpm* h, float dt, int32_t nsub, const uint32_t* bc, voi
     if (rc) return rc;
   }
   h->since_sort += nsub;
+  if (use_fused(h)) choose_rebins(h, dt, nsub, bc);
   const bool use_graph = !(h->prm.flags & GSMPM_FLAG_NO_GRAPH) && nsub >= 2;
+  int rc;
   if (!use_graph) {
     int parity = h->cur_box;
-    int rc = use_fused(h) ? launch_substeps_f(h, dt, nsub, bc, st, h->fbpar, h->fep)
-                          : launch_substeps(h, dt, nsub, bc, st, parity);
+    rc = use_fused(h) ? launch_substeps_f(h, dt, nsub, bc, st, h->fbpar, h->fep)
+                      : launch_substeps(h, dt, nsub, bc, st, parity);
     h->cur_box = parity;
-    return rc;
+  } else {
+    rc = graph_substeps(h, dt, nsub, bc, st, nullptr);
   }
-  return graph_substeps(h, dt, nsub, bc, st, nullptr);
+  // the call's fastest velocity, for the next call's re-binnings (no sync)
+  if (!rc && use_fused(h) && h->vmax_host && h->rebin_auto)
+    GSMPM_HIP(hipMemcpyAsync(h->vmax_host, h->vmax_dev, sizeof(unsigned), hipMemcpyDeviceToHost, st));
+  return rc;
 }
 
 int gsmpm_mpm_check_finite(gsmpm_mpm* h, int32_t clear, void* stream) {
@@ -2802,6 +2863,8 @@ int gsmpm_mpm_set_rebin_interval(gsmpm_mpm* h, int32_t substeps) {
   GSMPM_REQUIRE(h, "gsmpm_mpm_set_rebin_interval: null handle");
   GSMPM_REQUIRE(substeps >= 1, "gsmpm_mpm_set_rebin_interval: substeps must be >= 1");
   h->rebin_interval = substeps;
+  h->rebin_auto = false;  // a fixed spacing, as asked
+  h->rebin_m = 0;
   return GSMPM_OK;
 }
 
@@ -2821,6 +2884,15 @@ int gsmpm_mpm_escapes(gsmpm_mpm* h, int32_t clear, int64_t* out, void* stream) {
   GSMPM_HIP(hipStreamSynchronize(st));
   if (clear) GSMPM_HIP(hipMemsetAsync(d, 0, sizeof(unsigned), st));
   *out = (int64_t)v;
+  return GSMPM_OK;
+}
+
+int gsmpm_mpm_rebin_state(gsmpm_mpm* h, int32_t* out3, float* vmax) {
+  GSMPM_REQUIRE(h && out3, "gsmpm_mpm_rebin_state: null argument");
+  out3[0] = h->rebin_interval;
+  out3[1] = h->rebin_auto ? 1 : 0;
+  out3[2] = h->rebin_m;
+  if (vmax) *vmax = h->vmax_host ? *(volatile float*)h->vmax_host : 0.f;
   return GSMPM_OK;
 }
 

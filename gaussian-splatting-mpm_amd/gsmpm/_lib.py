@@ -101,6 +101,7 @@ _SIGS = {
     "gsmpm_mpm_check_finite": (ctypes.c_int, [c_void_p, ctypes.c_int32, c_void_p]),
     "gsmpm_mpm_pipeline": (ctypes.c_int, [c_void_p]),
     "gsmpm_mpm_folded": (ctypes.c_int, [c_void_p]),
+    "gsmpm_mpm_rebin_state": (ctypes.c_int, [c_void_p, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_float)]),
     "gsmpm_mpm_escapes": (ctypes.c_int, [c_void_p, ctypes.c_int32, ctypes.POINTER(ctypes.c_int64), c_void_p]),
     "gsmpm_mpm_postprocess": (ctypes.c_int, [c_void_p, c_void_p]),
     "gsmpm_mpm_field_width": (ctypes.c_int, [ctypes.c_int32]),

@@ -224,6 +224,16 @@ class Simulator:
               "gsmpm_mpm_escapes")
         return int(out.value)
 
+    def rebin_state(self):
+        """{interval, auto, rebins_last_call, vmax} (gsmpm_mpm_rebin_state): the
+        longest spacing, whether the re-binnings adapt to the particles' speed,
+        how many the last step call ran (0: from the interval) and the fastest
+        velocity component seen."""
+        b = (ctypes.c_int32 * 3)()
+        v = ctypes.c_float(0.0)
+        check(LIB.gsmpm_mpm_rebin_state(self._h, b, ctypes.byref(v)), "gsmpm_mpm_rebin_state")
+        return {"interval": int(b[0]), "auto": bool(b[1]), "rebins_last_call": int(b[2]), "vmax": float(v.value)}
+
     def set_rebin_interval(self, substeps: int):
         """Fused pipeline: substeps between particle re-binnings (any value >= 1 is correct)."""
         check(LIB.gsmpm_mpm_set_rebin_interval(self._h, int(substeps)), "gsmpm_mpm_set_rebin_interval")

@@ -207,11 +207,25 @@ int gsmpm_mpm_slab_bounds(gsmpm_mpm* h, int32_t* out, int32_t n, int64_t* rebala
 int gsmpm_mpm_resort(gsmpm_mpm* h, int32_t interval, void* stream);
 
 /* Fused pipeline: substeps between re-binnings of the particles into tiles
- * (at most; default 20 for every material since round 5; any
+ * (at most; default 20 for stress-free materials, 25 for stress-bearing ones; any
  * value is correct -- particles that moved more than one cell
- * since their binning take a slower global path).  No counterpart in the
- * reference (its p2g2p has no binning, solver.py:27-52). */
+ * since their binning take a slower global path).  Fixes the spacing: the
+ * adaptive choice (gsmpm_mpm_rebin_state) is turned off.  No counterpart in
+ * the reference (its p2g2p has no binning, solver.py:27-52). */
 int gsmpm_mpm_set_rebin_interval(gsmpm_mpm* h, int32_t substeps);
+/* Fused pipeline, one domain: with GSMPM_REBIN_AUTO=1 in the environment at
+ * create (off by default: DESIGN.md §3.4), the re-binnings of each step call
+ * adapt to the particles' speed (gsmpm_mpm_set_rebin_interval fixes the
+ * spacing again): from the fastest
+ * velocity component the previous call ended with (copied to pinned memory
+ * without a sync) plus what gravity adds, enough re-binnings that no
+ * particle moves more than 0.8 cell between two -- a particle that leaves
+ * its chunk's window makes the next grid update sweep every tile -- and at
+ * least one per rebin_interval substeps.  out3 = {rebin_interval, auto
+ * (0/1), re-binnings chosen for the last call (0: from rebin_interval)};
+ * *vmax (may be null) = the last fastest velocity component seen.  No
+ * reference counterpart (the reference does not bin, solver.py:27-52). */
+int gsmpm_mpm_rebin_state(gsmpm_mpm* h, int32_t* out3, float* vmax);
 /* GSMPM_PIPE_FUSED or GSMPM_PIPE_PHASED: the pipeline gsmpm_mpm_step runs now. */
 int gsmpm_mpm_pipeline(gsmpm_mpm* h);
 /* 1 when the fused pipeline folds each substep's grid update into the next
