@@ -26,11 +26,21 @@ namespace gsmpm {
 #ifndef GSMPM_SVD_REUSE
 #define GSMPM_SVD_REUSE 1
 #endif
+// GSMPM_LOG_REUSE=0 (A/B): metal's stress takes its three logs again even
+// where the return map kept F
+#ifndef GSMPM_LOG_REUSE
+#define GSMPM_LOG_REUSE 1
+#endif
 template <int MAT>
 __device__ __forceinline__ void return_map_and_stress(float (&F)[3][3], float mu, float lam, float& yld, float dt,
                                                       const MatConsts& mc, float (&tau)[3][3]) {
   float U[3][3], V[3][3], s[3];
   bool fresh = false;  // F changed in a way U, s, V do not describe: take its SVD
+  // metal whose F the return map left unchanged: the stress's log(max(s, 0.01))
+  // and its StVK diagonal are the return map's eps and t3 (the same f32
+  // operations on the same s, utils.py:23-38 vs constitutive_models.py:62-75)
+  bool kept = false;
+  float t3_k[3] = {0.f, 0.f, 0.f};
   constexpr bool kFast = MAT != 3;  // foam's plastic F depends on the SVD basis (svd3.h)
   if constexpr (MAT == 1) {
     // von_mises_return_mapping, constitutive_models.py:62-103
@@ -48,6 +58,9 @@ __device__ __forceinline__ void return_map_and_stress(float (&F)[3][3], float mu
 #pragma unroll
     for (int d = 0; d < 3; ++d) cond[d] = t3[d] - st / 3.0f;
     const float cn = sqrtf(cond[0] * cond[0] + cond[1] * cond[1] + cond[2] * cond[2]);
+    kept = !(cn > yld);
+#pragma unroll
+    for (int d = 0; d < 3; ++d) t3_k[d] = t3[d];
     if (cn > yld) {
       float eh[3];
 #pragma unroll
@@ -153,12 +166,17 @@ __device__ __forceinline__ void return_map_and_stress(float (&F)[3][3], float mu
     if constexpr (MAT == 1 || MAT == 3 || MAT == 5) {
       // kirchoff_stress_StVK, constitutive_models.py:23-38
       float tv[3];
-      float ls[3];
+      if (MAT == 1 && GSMPM_SVD_REUSE && GSMPM_LOG_REUSE && kept) {
 #pragma unroll
-      for (int d = 0; d < 3; ++d) ls[d] = logf(fmaxf(s[d], 0.01f));
-      const float lss = ls[0] + ls[1] + ls[2];
+        for (int d = 0; d < 3; ++d) tv[d] = t3_k[d];
+      } else {
+        float ls[3];
 #pragma unroll
-      for (int d = 0; d < 3; ++d) tv[d] = 2.0f * mu * ls[d] + lam * lss * 1.0f;
+        for (int d = 0; d < 3; ++d) ls[d] = logf(fmaxf(s[d], 0.01f));
+        const float lss = ls[0] + ls[1] + ls[2];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) tv[d] = 2.0f * mu * ls[d] + lam * lss * 1.0f;
+      }
       float W[3][3];
       usv(U, tv, V, W);
       mmT(W, F, T);

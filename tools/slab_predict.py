@@ -1,6 +1,7 @@
-"""Predicted N-GPU frame time of config D (bicycle 1M, 256^3) through the slab
-path, from pieces measured on ONE GPU (the round-5 verdict's
-item 2).  Run on the GPU box:
+"""Predicted N-GPU frame time of a scene through the slab path -- config D
+(bicycle 1M, 256^3) by default, or the lego headline (--config lego.json
+--particles 100000 --n_grid 128) -- from pieces measured on ONE GPU (SURVEY
+8(e); the round-5 verdict's item 2).  Run on the GPU box:
 
     python3 tools/slab_predict.py [--gpus 2,4,8] [--out profiles/r06/slab_prediction_D.json]
 
@@ -44,6 +45,9 @@ def main():
     ap.add_argument("--gpus", default="1,2,4,8")
     ap.add_argument("--frames", type=int, default=3)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--config", default="bicycle.json")
+    ap.add_argument("--particles", type=int, default=1_000_000)
+    ap.add_argument("--n_grid", type=int, default=256)
     a = ap.parse_args()
     # a slab rank runs the unfolded pipeline (k_grid_f every substep, split around the exchange):
     # measure the rank's kernels in that form
@@ -56,7 +60,7 @@ def main():
     from gsmpm import raster
 
     dev = torch.device("cuda", 0)
-    ns = argparse.Namespace(config="bicycle.json", material=None, particles=1_000_000, n_grid=256)
+    ns = argparse.Namespace(config=a.config, material=None, particles=a.particles, n_grid=a.n_grid)
     sc = B.build_scene(ns, dev)
     sa = sc["sargs"]
     ng, ext = sa.n_grid, sa.grid_extent
@@ -92,7 +96,7 @@ def main():
     del full, m_r, c_r
     torch.cuda.empty_cache()
 
-    res = {"config": "bicycle.json 1M, 256^3 (BASELINE configs[3])", "cut_axis": axis, "window_planes": W,
+    res = {"config": f"{a.config} {ntot} particles, {ng}^3", "cut_axis": axis, "window_planes": W,
            "constants": {"xgmi_link_GBps": LINK_GBPS, "rccl_round_latency_us": RCCL_LAT_US,
                          "gather_bytes_per_particle": 36, "migration_rounds_per_frame": 2 * spf // INTERVAL},
            "render_ms_rank0": round(render_ms, 3), "per_n": {}}
