@@ -15,8 +15,8 @@ forms agree to the run-to-run spread (multi-chunk tiles: 1e-6) or within
 the parity bar (a swirl leaving the windows -- the slow path that evaluates
 a particle's stencil nodes on demand -- and particles outside the grid,
 where every launch escapes).  Parity with
-the CPU oracle is the rest of the GPU suite, which runs the folded pipeline
-(the default).
+the CPU oracle is the rest of the GPU suite, which runs the default
+two-launch pipeline that these tests compare against.
 
 Reference: the substep being folded is /root/reference/mpm_solver/solver.py:27-52
 (p2g -> grid_normalization_and_gravity -> grid_postprocess -> g2p),
