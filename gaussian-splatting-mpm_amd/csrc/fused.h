@@ -444,6 +444,37 @@ __device__ __forceinline__ void base_of(const float (&x)[3], float inv_dx, int (
 #pragma unroll
   for (int d = 0; d < 3; ++d) b[d] = (int)(x[d] * inv_dx - 0.5f);
 }
+
+// Escapes and the grid update.  A particle that scatters through the dense
+// accumulator (p2g_global: it left its chunk's window, or its chunk lies
+// outside the grid) adds the tiles owning its in-grid stencil nodes to the
+// touched list, as add_lower_tiles does for a new lower neighbour, so the
+// next k_grid_f -- which adds the accumulator to the nodes it owns and zeroes
+// it -- finds every node an escape wrote among the touched tiles.  Round 5
+// swept every tile of the grid after any escape (4,864 tiles at 128^3 against
+// ~900 touched); GSMPM_ESC_SWEEP=1 restores that (A/B).
+#ifndef GSMPM_ESC_SWEEP
+#define GSMPM_ESC_SWEEP 0
+#endif
+constexpr bool kEscSweepAll = GSMPM_ESC_SWEEP != 0;
+__device__ __forceinline__ void mark_escape_tiles(int* __restrict__ tflag, int* __restrict__ touched,
+                                               int* __restrict__ ntouch, int2* __restrict__ rcov, const FTiles& tl,
+                                               int ng, int b0, int b1, int b2) {
+  const int lo0 = max(b0, 0), lo1 = max(b1, 0), lo2 = max(b2, 0);
+  const int hi0 = min(b0 + 2, ng - 1), hi1 = min(b1 + 2, ng - 1), hi2 = min(b2 + 2, ng - 1);
+  if (lo0 > hi0 || lo1 > hi1 || lo2 > hi2) return;  // no stencil node in the grid
+  for (int a = lo0 / kFT0; a <= hi0 / kFT0; ++a)
+    for (int c = lo1 / kFT1; c <= hi1 / kFT1; ++c)
+      for (int e = lo2 / kFT2; e <= hi2 / kFT2; ++e) {
+        const int t = (a * tl.td1 + c) * tl.td2 + e;
+        if (__hip_atomic_load(&tflag[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 &&
+            atomicCAS(&tflag[t], 0, 1) == 0) {
+          const int pos = atomicAdd(ntouch, 1);
+          touched[pos] = t;
+          if (rcov) rcov[(size_t)pos * kRecStride + 27] = make_int2(1, 0);  // no cover record: the tile tables
+        }
+      }
+}
 // stencil inside the chunk window whose first node is o
 __device__ __forceinline__ bool in_window(const int (&b)[3], int o0, int o1, int o2) {
   return (unsigned)(b[0] - o0) <= (unsigned)(kFW0 - 3) && (unsigned)(b[1] - o1) <= (unsigned)(kFW1 - 3) &&
@@ -946,7 +977,12 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
       }
       if (outside) {
         // chunk of particles binned outside the grid: bounds-checked global path
-        if (k < cnt) p2g_global<MAT>(x, v, C, m, nvt, g, dt, rare->gacc);
+        if (k < cnt) {
+          p2g_global<MAT>(x, v, C, m, nvt, g, dt, rare->gacc);
+          int bq[3];
+          base_of(x, g.inv_dx, bq);
+          if (!kEscSweepAll) mark_escape_tiles(rare->tflag, rare->touched, rare->nchunk + 1, rare->rcov, tl, ng, bq[0], bq[1], bq[2]);
+        }
         if (k == 0 && cnt > 0) {
           *rare->esc = 1;
           atomicAdd(rare->esc_count, (unsigned)cnt);
@@ -1047,9 +1083,14 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
           *rare->esc = 1;
         }
       }
-      {  // escape statistics (gsmpm_mpm_escapes): one atomic a wave with escapes
+      {  // escape statistics (gsmpm_mpm_escapes): one atomic a wave with escapes; their tiles
         const unsigned long long eb = __ballot(k < cnt && !win);
-        if (eb && (k & 63) == 0) atomicAdd(rare->esc_count, (unsigned)__popcll(eb));
+        if (eb) {  // wave-uniform; rare.  (The tiles are marked here, after the scatter, not in its branch:
+                   // there the code cost k_fused<metal> 1 % with no escape, profiles/r06/ab_esc_r06o.txt)
+          if ((k & 63) == 0) atomicAdd(rare->esc_count, (unsigned)__popcll(eb));
+          if (!kEscSweepAll && k < cnt && !win)
+            mark_escape_tiles(rare->tflag, rare->touched, rare->nchunk + 1, rare->rcov, tl, ng, b[0], b[1], b[2]);
+        }
       }
       __syncthreads();
       if (w == (int)blockIdx.x) stamp(SK, 4);
@@ -1077,7 +1118,9 @@ __global__ __launch_bounds__(256, 3) void k_fused(Particles ps, GridDims g, FTil
         const int n1 = hi[1] - lo[1] + 1, n2 = hi[2] - lo[2] + 1, n12 = n1 * n2;
         const int nvol = (hi[0] - lo[0] + 1) * n12;
         const float r12 = 1.0f / (float)n12, r2 = 1.0f / (float)n2;
-        float4* dst = slots + (size_t)w * kFWin;
+        // the window's slot: the chunk's tile-order id (an ordered record carries it, k_chunk_order)
+        const int cid = (cr.w & 16) ? (int)((unsigned)cr.w >> 5) : w;
+        float4* dst = slots + (size_t)cid * kFWin;
         for (int qn = k; qn < nvol; qn += 256) {
           const int a = (int)(((float)qn + 0.5f) * r12), rem = qn - a * n12;
           const int bq = (int)(((float)rem + 0.5f) * r2), c = rem - bq * n2;
@@ -1367,7 +1410,8 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
   const int cnt0 = __builtin_amdgcn_readfirstlane(((gint_p)cnt_p)[1]);
   const int T0 = __builtin_amdgcn_readfirstlane(((gint_p)tch_p)[i0]);
   const int ng = g.ng;
-  const bool all = esc0 != 0;
+  const bool esc = esc0 != 0;            // the escape accumulator holds sums: add it to the owned nodes
+  const bool all = esc && kEscSweepAll;  // (A/B) every tile, not the touched ones
   const int ntouch = kGridParts * (all ? tl.ntiles : cnt0);
   const bool pre = recs && !all;  // workgroup-uniform: records in LDS, the next one prefetched
   int b = 0;
@@ -1426,9 +1470,10 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
 #pragma unroll
         for (int e = 0; e < 8; ++e) add4(a, v[e]);
         if (r.extra) node_extra(slots, s_cov, l0, l1, l2, r.extra, tl.max_chunks * kFWin, a);
-        if (all) {
-          add4(a, gacc[idx]);
-          gacc[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (esc) {  // the nodes an escape wrote lie in touched tiles (mark_escape_tiles); zero what was written
+          const float4 e = gacc[idx];
+          add4(a, e);
+          if (all || e.x != 0.f || e.y != 0.f || e.z != 0.f || e.w != 0.f) gacc[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
         }
       }
       bool inrect = false;

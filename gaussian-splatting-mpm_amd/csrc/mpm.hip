@@ -1568,6 +1568,14 @@ struct gsmpm_mpm {
   bool fuse_permute = true;               // GSMPM_FUSE_PERMUTE=0: separate k_permute (A/B)
   bool cover_records = true;              // GSMPM_COVER_RECORDS=0: k_grid_f reads the tile tables only (A/B)
   int fused_wgs = 1024;                   // k_fused grid cap: the workgroups resident at once x rounds of full chunks, <= 6 (init)
+  // Chunk order (k_chunk_order): k_fused's workgroup b takes the chunk at
+  // position b of a size-balanced order instead of chunk b, so the
+  // workgroups that share a CU carry about equal particle counts.
+  // On for one resident round of workgroups (init); GSMPM_CHUNK_ORDER=0 / 1
+  // forces tile order / the balanced order (A/B)
+  bool chunk_order = true;
+  int ncu = 256;                          // CUs of the device (the order's tier width)
+  int4* fpchunk[2] = {nullptr, nullptr};  // [max_chunks] chunk records in that order (k_fused reads these)
   float* planes_alt = nullptr;            // the other particle-plane buffer: every binning permutes
   int* orig_alt = nullptr;                //   storage into bin order, alternating planes / planes_alt
   int fbpar = 0;                          // parity of the bins the next k_fused reads
@@ -1677,8 +1685,10 @@ static BinOut bin_out(gsmpm_mpm* h, int c) {
 
 static bool use_fused(const gsmpm_mpm* h) { return h->fused; }
 
+// the chunk records k_fused walks: the balanced order (k_chunk_order) or tile order
+static int4* fused_records(gsmpm_mpm* h, int c) { return h->chunk_order ? h->fpchunk[c] : h->fchunk[c]; }
 static ChunkIn chunk_in_f(gsmpm_mpm* h, int c) {
-  ChunkIn ci{h->fcount[c], h->fcbase[c], h->fchunk[c], h->fnchunk[c], h->flist[c], h->ftouched[c]};
+  ChunkIn ci{h->fcount[c], h->fcbase[c], fused_records(h, c), h->fnchunk[c], h->flist[c], h->ftouched[c]};
   if (h->cover_records) {
     ci.rcov = h->frcov[c];
     ci.rbox = h->frbox[c];
@@ -1747,8 +1757,63 @@ static int finish_bins_on(gsmpm_mpm* h, const Tiles& tl, const int* count, const
 static int finish_binning(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t* ev = nullptr) {
   return finish_bins_on(h, h->tl, h->count[c], chunk_out(h, c), h->list[c], st, ev);
 }
+// Chunk order (the fused bins of parity c): one workgroup ranks the chunks by
+// particle count, largest first, and lays the ranks out in tiers of ncu
+// positions, every other complete tier reversed.  The k_fused grid is a
+// multiple of the CU count, and the dispatcher puts workgroups b, b + ncu,
+// b + 2 ncu, ... on one CU (tools/wg_timeline_f.py: "WG sets sharing a CU"),
+// so a CU that gets one of the largest chunks gets one of the smallest of the
+// next tier.  In tile order (round 5) the lego frame's CUs carried 392
+// particles at the median and up to 667, and the launch ended with the
+// most loaded CU's workgroups (profiles/r06/k_fused_wg_timeline_nofold_r06h.txt:
+// max workgroup 13.7 us on CUs under 300 particles, 17.2 us over 600).  The
+// order changes no arithmetic: a chunk's work is the same on any workgroup.
+// Records keep their tile-order id in .w (bit 4 set, id << 5), which indexes
+// the chunk's window slot (k_grid_f finds slots by tile chunk ranges); the
+// per-chunk state k_fused keeps between launches (stencil box, lane order)
+// is indexed by position.
+__global__ __launch_bounds__(1024) void k_chunk_order(const int4* __restrict__ chunk, const int* __restrict__ nchunk,
+                                                      int4* __restrict__ pchunk, int ncu) {
+  __shared__ int s_h[kChunk];  // chunks of kChunk - b particles, then the first rank of each
+  const int nch = *nchunk;
+  for (int i = threadIdx.x; i < kChunk; i += blockDim.x) s_h[i] = 0;
+  __syncthreads();
+  for (int c = threadIdx.x; c < nch; c += blockDim.x) atomicAdd(&s_h[kChunk - chunk[c].z], 1);
+  __syncthreads();
+  if (threadIdx.x < 64) {  // exclusive scan of the 256 bins: 4 a lane
+    int v[kChunk / 64], t = 0;
+#pragma unroll
+    for (int u = 0; u < kChunk / 64; ++u) {
+      v[u] = s_h[threadIdx.x * (kChunk / 64) + u];
+      t += v[u];
+    }
+    int o = wave_incl_scan(t) - t;
+#pragma unroll
+    for (int u = 0; u < kChunk / 64; ++u) {
+      s_h[threadIdx.x * (kChunk / 64) + u] = o;
+      o += v[u];
+    }
+  }
+  __syncthreads();
+  const int full = nch / ncu;  // complete tiers (the last, partial tier runs forward)
+  for (int c = threadIdx.x; c < nch; c += blockDim.x) {
+    const int4 r = chunk[c];
+    const int rank = atomicAdd(&s_h[kChunk - r.z], 1);
+    const int tier = rank / ncu, i = rank - tier * ncu;
+    const int pos = tier * ncu + (((tier & 1) && tier < full) ? ncu - 1 - i : i);
+    pchunk[pos] = make_int4(r.x, r.y, r.z, r.w | 16 | (c << 5));
+  }
+}
+static int order_chunks_f(gsmpm_mpm* h, int c, hipStream_t st) {
+  if (!h->chunk_order) return GSMPM_OK;
+  launch(nullptr, k_chunk_order, dim3(1), dim3(1024), st, (const int4*)h->fchunk[c], (const int*)h->fnchunk[c],
+         h->fpchunk[c], h->ncu);
+  GSMPM_LAUNCH_CHECK();
+  return GSMPM_OK;
+}
 static int finish_binning_f(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t* ev = nullptr) {
-  return finish_bins_on(h, ftiles_flat(h), h->fcount[c], chunk_out_f(h, c), h->flist[c], st, ev);
+  const int rc = finish_bins_on(h, ftiles_flat(h), h->fcount[c], chunk_out_f(h, c), h->flist[c], st, ev);
+  return rc ? rc : order_chunks_f(h, c, st);
 }
 // the binning of parity c and the storage permutation into its order: one
 // launch on the fused path (k_finish_bins moves the particles), else the
@@ -1758,6 +1823,7 @@ static int rebin_permute_f(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t
   if (bins_fused(ftiles_flat(h)) && h->fuse_permute) {
     const BinPermute bp{h->planes, h->planes_alt, h->np, h->orig, h->orig_alt, (vc_live || GSMPM_STORE_VC) ? 0 : 1};
     int rc = finish_bins_on(h, ftiles_flat(h), h->fcount[c], chunk_out_f(h, c), h->flist[c], st, ev, bp);
+    if (!rc) rc = order_chunks_f(h, c, st);
     if (rc) return rc;
     if (ev) {  // the permute's timing pair: nothing left to time
       GSMPM_HIP(hipEventRecord(ev[2], st));
@@ -1908,7 +1974,7 @@ static FusedRare rare_of(gsmpm_mpm* h, int c, int slot) {
   r.tflag = h->ftflag[c];
   r.touched = h->ftouched[c];
   r.nchunk = h->fnchunk[c];
-  r.chunk = h->fchunk[c];
+  r.chunk = fused_records(h, c);
   r.rcov = h->frcov[c];
   r.tbox = fold ? fold_tbox(h, c, ph) : h->ftbox[c];
   r.tpos = h->cover_records ? h->ftpos[c] : nullptr;
@@ -2461,11 +2527,17 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
       // GSMPM_FUSED_WGS): 100.8 us at 1 round, 99.2 at 2, 96.7 at 3, 94.4 at 6,
       // 98.5 at one workgroup a chunk; B' (240,549, 1.2 rounds) lost frame
       // time at 2 rounds, so the factor is the floor of the rounds
+      h->ncu = ncu;
       const int resident = ncu * per_cu;
       const int rounds = (int)std::min<long long>(6, std::max<long long>(1, (long long)h->n / ((long long)resident * kChunk)));
       h->fused_wgs = resident * rounds;
+      // the balanced order only where the workgroups are one resident round
+      // (later rounds are placed as CUs free up, not by position): lego and B'
+      // gain, bicycle's 5 rounds lost 1 % (profiles/r06/ab_chunk_order_r06n.txt)
+      h->chunk_order = rounds == 1;
     }
     if (const char* fw = std::getenv("GSMPM_FUSED_WGS")) h->fused_wgs = std::max(1, std::atoi(fw));
+    if (const char* co = std::getenv("GSMPM_CHUNK_ORDER")) h->chunk_order = co[0] != '0';
   }
   h->ftl.td0 = (h->g.ng + kFT0 - 1) / kFT0;
   h->ftl.td1 = (h->g.ng + kFT1 - 1) / kFT1;
@@ -2500,6 +2572,9 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
       if ((e = hipMalloc(&h->flist[c], sizeof(int) * (size_t)h->np)) != hipSuccess) return fail(e, "hipMalloc list");
       if ((e = hipMalloc(&h->fcbox[c], sizeof(int) * (size_t)h->ftl.max_chunks)) != hipSuccess)
         return fail(e, "hipMalloc boxes");
+      if ((e = hipMalloc(&h->fpchunk[c], sizeof(int4) * (size_t)h->ftl.max_chunks)) != hipSuccess ||
+          (e = hipMemset(h->fpchunk[c], 0, sizeof(int4) * (size_t)h->ftl.max_chunks)) != hipSuccess)
+        return fail(e, "hipMalloc ordered chunks");
       if ((e = hipMalloc(&h->ftbox[c], sizeof(int) * (size_t)h->ftl.ntiles)) != hipSuccess)
         return fail(e, "hipMalloc boxes");
       if ((e = hipMalloc(&h->frcov[c], sizeof(int2) * kRecStride * (size_t)h->ftl.ntiles)) != hipSuccess ||
@@ -2608,6 +2683,7 @@ int gsmpm_mpm_destroy(gsmpm_mpm* h) {
     (void)hipFree(h->fnchunk[c]);
     (void)hipFree(h->flist[c]);
     (void)hipFree(h->fcbox[c]);
+    (void)hipFree(h->fpchunk[c]);
     (void)hipFree(h->ftbox[c]);
     (void)hipFree(h->fperm[c]);
     (void)hipFree(h->frcov[c]);
