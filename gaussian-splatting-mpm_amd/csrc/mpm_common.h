@@ -59,6 +59,9 @@ struct BcTable {
   GridOp op[kMaxBC];
 };
 
+#ifndef GSMPM_PSTORE
+#define GSMPM_PSTORE 2
+#endif
 struct Particles {
   float* P;
   int n, np;
@@ -77,8 +80,10 @@ struct Particles {
   __device__ __forceinline__ float ld(int plane, int i) const {
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc(), i * 4, plane * np * 4, 0));
   }
+  // GSMPM_PSTORE: the hot-plane stores' cache policy (buffer aux bits: 2 nt,
+  // 16 sc1 write-through, 18 both)
   __device__ __forceinline__ void st(int plane, int i, float v) const {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rsrc(), i * 4, plane * np * 4, 2);  // nt
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rsrc(), i * 4, plane * np * 4, GSMPM_PSTORE);
   }
   // cold planes, by caller row
   __device__ __forceinline__ float ldc(int plane, int row) const { return cold[(size_t)plane * np + row]; }
