@@ -75,12 +75,20 @@ __device__ __forceinline__ float svd_sqrt(float x) {
   return sqrtf(x);
 }
 
+// GSMPM_SVD_TRIM (default 1, round 6): the quaternion and U updates skip the
+// products with the zeros of their rotation or of the identity they start
+// from.  Same operands and order for every non-zero term, so the same f32
+// results for finite input (0: the plain forms, A/B).
+#ifndef GSMPM_SVD_TRIM
+#define GSMPM_SVD_TRIM 1
+#endif
+
 struct M3 {
   float m[3][3];
 };
 
 template <bool FAST>
-__device__ __forceinline__ void svd_jacobi(float (&S)[3][3], float (&q)[4], int p, int r) {
+__device__ __forceinline__ void svd_jacobi(float (&S)[3][3], float (&q)[4], int p, int r, bool first = false) {
   constexpr float kGamma = 5.828427124746190f;  // 3 + 2 sqrt(2)
   constexpr float kCStar = 0.923879532511287f;  // cos(pi/8)
   constexpr float kSStar = 0.382683432365090f;  // sin(pi/8)
@@ -104,9 +112,38 @@ __device__ __forceinline__ void svd_jacobi(float (&S)[3][3], float (&q)[4], int 
   S[p][k] = npk; S[k][p] = npk;
   S[r][k] = nrk; S[k][r] = nrk;
   // q <- q * (ch, sh e_k)
+  const float a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
+  if constexpr (GSMPM_SVD_TRIM) {
+    // The Hamilton product with the two zero components of (ch, sh e_k)
+    // dropped: the full form's a * 0 terms are +-0, and x +- 0 = x, so for
+    // finite q each component is the same two products and one add, rounded
+    // identically.  The full form spends 16 mul + 12 add a rotation, the
+    // compiler cannot fold a * 0 under IEEE semantics; this one 8 + 4.
+    if (first) {  // q = (1, 0, 0, 0): the product is (ch, sh e_k) exactly
+      q[0] = ch;
+      q[1] = k == 0 ? sh : 0.f;
+      q[2] = k == 1 ? sh : 0.f;
+      q[3] = k == 2 ? sh : 0.f;
+    } else if (k == 0) {
+      q[0] = a0 * ch - a1 * sh;
+      q[1] = a0 * sh + a1 * ch;
+      q[2] = a2 * ch + a3 * sh;
+      q[3] = -(a2 * sh) + a3 * ch;
+    } else if (k == 1) {
+      q[0] = a0 * ch - a2 * sh;
+      q[1] = a1 * ch - a3 * sh;
+      q[2] = a0 * sh + a2 * ch;
+      q[3] = a1 * sh + a3 * ch;
+    } else {
+      q[0] = a0 * ch - a3 * sh;
+      q[1] = a1 * ch + a2 * sh;
+      q[2] = -(a1 * sh) + a2 * ch;
+      q[3] = a0 * sh + a3 * ch;
+    }
+    return;
+  }
   float rq[4] = {ch, 0.f, 0.f, 0.f};
   rq[1 + k] = sh;
-  const float a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
   q[0] = a0 * rq[0] - a1 * rq[1] - a2 * rq[2] - a3 * rq[3];
   q[1] = a0 * rq[1] + a1 * rq[0] + a2 * rq[3] - a3 * rq[2];
   q[2] = a0 * rq[2] - a1 * rq[3] + a2 * rq[0] + a3 * rq[1];
@@ -128,8 +165,9 @@ __device__ __forceinline__ void svd_cond_swap(bool c, float (&B)[3][3], float (&
   rho[j] = c ? ri : rj;
 }
 
+// one Givens step of the QR: rotates B's rows p, r and returns the rotation
 template <bool FAST>
-__device__ __forceinline__ void svd_qr_givens(float (&B)[3][3], float (&U)[3][3], int p, int r) {
+__device__ __forceinline__ void svd_qr_rot(float (&B)[3][3], int p, int r, float& c, float& s) {
   constexpr float kEps = 1.0e-12f;
   const float a1 = B[p][p], a2 = B[r][p];
   const float rho = svd_sqrt<FAST>(a1 * a1 + a2 * a2);
@@ -142,13 +180,17 @@ __device__ __forceinline__ void svd_qr_givens(float (&B)[3][3], float (&U)[3][3]
   const float w = svd_rsqrt<FAST>(ch * ch + sh * sh);
   ch *= w;
   sh *= w;
-  const float c = ch * ch - sh * sh, s = 2.0f * sh * ch;
+  c = ch * ch - sh * sh;
+  s = 2.0f * sh * ch;
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const float bp = B[p][j], br = B[r][j];
     B[p][j] = c * bp + s * br;
     B[r][j] = -s * bp + c * br;
   }
+}
+// U <- U G(p, r)
+__device__ __forceinline__ void svd_qr_acc(float (&U)[3][3], int p, int r, float c, float s) {
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const float up = U[i][p], ur = U[i][r];
@@ -168,7 +210,7 @@ __device__ __forceinline__ void svd3(const float (&A)[3][3], float (&U)[3][3], f
   float q[4] = {1.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int it = 0; it < 5; ++it) {
-    svd_jacobi<FAST>(S, q, 0, 1);
+    svd_jacobi<FAST>(S, q, 0, 1, it == 0);
     svd_jacobi<FAST>(S, q, 1, 2);
     svd_jacobi<FAST>(S, q, 2, 0);
   }
@@ -188,13 +230,34 @@ __device__ __forceinline__ void svd3(const float (&A)[3][3], float (&U)[3][3], f
   svd_cond_swap(rho[0] < rho[1], B, V, rho, 0, 1);
   svd_cond_swap(rho[0] < rho[2], B, V, rho, 0, 2);
   svd_cond_swap(rho[1] < rho[2], B, V, rho, 1, 2);
+  float c1, s1, c2, s2, c3, s3;
+  svd_qr_rot<FAST>(B, 0, 1, c1, s1);
+  svd_qr_rot<FAST>(B, 0, 2, c2, s2);
+  svd_qr_rot<FAST>(B, 1, 2, c3, s3);
+  if constexpr (GSMPM_SVD_TRIM) {
+    // U = I G(0,1) G(0,2) with the identity's zeros and ones folded (each
+    // entry the one product the plain form rounds; the rest are +-0 or x*1)
+    U[0][0] = c2 * c1;  U[0][1] = -s1;  U[0][2] = -s2 * c1;
+    U[1][0] = c2 * s1;  U[1][1] = c1;   U[1][2] = -s2 * s1;
+    U[2][0] = s2;
+    // G(1,2) on the rows with U[i][1] = -s1, c1 and row 2's (s2, 0, c2)
 #pragma unroll
-  for (int i = 0; i < 3; ++i)
+    for (int i = 0; i < 2; ++i) {
+      const float up = U[i][1], ur = U[i][2];
+      U[i][1] = c3 * up + s3 * ur;
+      U[i][2] = -s3 * up + c3 * ur;
+    }
+    U[2][1] = s3 * c2;
+    U[2][2] = c3 * c2;
+  } else {
 #pragma unroll
-    for (int j = 0; j < 3; ++j) U[i][j] = (i == j) ? 1.f : 0.f;
-  svd_qr_givens<FAST>(B, U, 0, 1);
-  svd_qr_givens<FAST>(B, U, 0, 2);
-  svd_qr_givens<FAST>(B, U, 1, 2);
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) U[i][j] = (i == j) ? 1.f : 0.f;
+    svd_qr_acc(U, 0, 1, c1, s1);
+    svd_qr_acc(U, 0, 2, c2, s2);
+    svd_qr_acc(U, 1, 2, c3, s3);
+  }
   sig[0] = B[0][0];
   sig[1] = B[1][1];
   sig[2] = B[2][2];
