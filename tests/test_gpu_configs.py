@@ -17,7 +17,9 @@ The oracle side is the OpenMP build of the C restatement (same arithmetic as
 the serial checker, different P2G summation order) so a 1M-particle run
 finishes in seconds on the box's cores.
 
-Tolerances (north_star): x, F_trial, cov, R 1e-4 relative to the field's max;
+Tolerances (north_star): x, F_trial, cov, R 1e-4 relative to the field's max,
+and x and cov also per element (1e-4 of each element, floored at 1e-3 of the
+field's max);
 pixels 1e-3; num_rendered and radii exact on identical inputs.  v and C carry
 the documented derived-field bounds of test_gpu_mpm.py.  The error of every
 field is recorded at substeps 1/10/50/100 (SURVEY §4's error-vs-substep
@@ -62,6 +64,9 @@ def _errs(s, ref):
     exp = {"x": ref.x, "v": ref.v, "C": ref.C, "F_trial": ref.F_trial}
     e = {k: rel_err(got[k], exp[k]) for k in FIELDS}
     e["C"] = _c_err(got["C"], ref.C, ref.v, s._sim.n_grid / s._sim.grid_extent)
+    # positions per element as well (north_star's 1e-4 on particle positions):
+    # every coordinate within 1e-4 of itself, floored at 1e-3 of the field's max
+    e["x_elem"] = rel_err_elem(got["x"], ref.x)
     return e
 
 
@@ -236,15 +241,12 @@ def test_config_B_prime_lego_240549(dev):
         s.p2g2p(dt)
     t = oracle_run(ref, imps, ops, dt, args.steps_per_frame)
     assert abs(s.time - t) == 0.0
-    got = _state(s)
     stats = s._sim.debug_stats()
     assert stats["max_per_tile"] > 256, stats  # multi-chunk tiles
     rec = {"config": "lego.json", "N": 240_549, "n_grid": 128, "max_per_tile": stats["max_per_tile"],
            "folded": s._sim.folded}
     rec["errs"] = _errs(s, ref)
-    _check(rec["errs"], "B' substep 100")
-    rec["x_elem"] = rel_err_elem(got["x"], ref.x)
-    assert rec["x_elem"] < TOL, rec
+    _check(rec["errs"], "B' substep 100")  # x per element included (x_elem)
     rec["post"] = _post(s, ref, per_element=True)
     _dump("config_B_prime", rec)
 
