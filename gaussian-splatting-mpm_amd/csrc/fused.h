@@ -1357,6 +1357,37 @@ constexpr int kGvelStore = GSMPM_GVEL_STORE;
 // v_readlane restores, ~13 % of the ~350 VALU instructions a wave issues)
 // against 4 now; k_grid_f 12.06 -> 11.67 us in the lego frame (5
 // interleaved rounds, profiles/r05/ab/ab_rare_args_pk_r05k.txt)
+// XCD-grouped work order (round 6).  Workgroup b runs on XCD b % 8, and each
+// XCD has its own L2.  A window slot is read by the grid update of its own
+// tile and of the upper neighbours whose low nodes it covers, and a tile's
+// seven parts read one cover record; in the plain order (work item b: tile
+// b / 7, part b % 7) the seven parts of a tile land on seven XCDs and
+// neighbouring tiles on others, so each line is fetched once per XCD that
+// reads it.  Here a tile's parts run on one XCD, and kGridGroup consecutive
+// touched tiles (the touched list is in tile order: z-neighbours, whose
+// windows share lines, are adjacent) go to one XCD before the next XCD's
+// group.  tools/grid_f_bytes.py models the lego launch at 20.5 MB fetched in
+// the plain order (FETCH_SIZE: 21.3 MB) and 10.9 MB grouped by 16.  The grid
+// is a multiple of 8 workgroups (launch_grid_f).  GSMPM_GRID_GROUP=0: the
+// plain order (A/B).
+#ifndef GSMPM_GRID_GROUP
+#define GSMPM_GRID_GROUP 16
+#endif
+constexpr int kGridGroup = GSMPM_GRID_GROUP;
+// work item it of workgroup b (grid stride S): touched position P, part
+// (P never decreases with it, so a workgroup stops at the first P past the count)
+__device__ __forceinline__ void grid_work(int b, int it, int S, int& P, int& part) {
+  if constexpr (kGridGroup == 0) {
+    const int wt = b + it * S;
+    P = wt / kGridParts;
+    part = wt - P * kGridParts;
+  } else {
+    const int x = b & 7, m = (b >> 3) + it * (S >> 3);
+    const int u = m / kGridParts, k = u / kGridGroup;
+    part = m - u * kGridParts;
+    P = (k * 8 + x) * kGridGroup + (u - k * kGridGroup);
+  }
+}
 template <bool SLAB>
 __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) void k_grid_f(GridDims g, FTiles tl, ChunkIn ck, const int* __restrict__ tbox,
                                                     const float4* __restrict__ slots, float4* __restrict__ gacc,
@@ -1378,7 +1409,9 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
   // tables.  Round 5 first had the flag and count after the zeroing stores
   // below, which the compiler may not hoist loads over (the pointers could
   // alias): three dependent scalar round trips before the first record load.
-  const int i0 = min((int)blockIdx.x / kGridParts, tl.ntiles - 1);
+  int P0, part0;
+  grid_work(blockIdx.x, 0, gridDim.x, P0, part0);
+  const int i0 = min(P0, tl.ntiles - 1);
   // (the empty asm takes the three pointers into SGPRs at once, so their
   // kernel-argument loads come in the first batch and the three scalar loads
   // below leave together: one round trip, not two behind each other)
@@ -1412,10 +1445,13 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
   const int ng = g.ng;
   const bool esc = esc0 != 0;            // the escape accumulator holds sums: add it to the owned nodes
   const bool all = esc && kEscSweepAll;  // (A/B) every tile, not the touched ones
-  const int ntouch = kGridParts * (all ? tl.ntiles : cnt0);
+  const int ntouch = all ? tl.ntiles : cnt0;  // tiles to update
   const bool pre = recs && !all;  // workgroup-uniform: records in LDS, the next one prefetched
   int b = 0;
-  for (int wt = blockIdx.x; wt < ntouch; wt += gridDim.x, b ^= 1) {
+  for (int it = 0;; ++it, b ^= 1) {
+    int P, part;
+    grid_work(blockIdx.x, it, gridDim.x, P, part);
+    if (P >= ntouch) break;  // workgroup-uniform
     if constexpr (!kAtomicGrid) {
       // this tile's DMA (issued a tile ago, or in the prologue) has landed;
       // readers of the other buffer are done.  The wait is explicit: the
@@ -1425,9 +1461,9 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
       // the previous tile's v_out stores (L2 write acks, not an HBM trip).
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      const int wn = wt + (int)gridDim.x;
-      if (pre && wn < ntouch && threadIdx.x < 64) {  // workgroup-uniform (kGridT = 64: one wave)
-        const int pn = wn / kGridParts;
+      int pn, partn;
+      grid_work(blockIdx.x, it + 1, gridDim.x, pn, partn);
+      if (pre && pn < ntouch && threadIdx.x < 64) {  // workgroup-uniform (kGridT = 64: one wave)
         glds4(reinterpret_cast<const int*>(ck.rcov) + (size_t)pn * 2 * kRecStride + le, &s_rec[b ^ 1][0]);
         glds4(ck.rbox + (size_t)pn * kRecStride + (le & 31), &s_box[b ^ 1][0]);
         if (le == 0) glds4(ck.touched + pn, &s_tn[b ^ 1]);
@@ -1435,15 +1471,15 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     }
     int* s_cov = s_rec[b];
     int* s_bx = s_box[b];
-    const int q = threadIdx.x + (wt % kGridParts) * kGridT;
+    const int q = threadIdx.x + part * kGridT;
     const int l0 = q / (kFT1 * kFT2), l1 = (q / kFT2) % kFT1, l2 = q % kFT2;
-    const int T = all ? wt / kGridParts : wt == (int)blockIdx.x ? T0 : pre ? s_tn[b] : ck.touched[wt / kGridParts];
-    if ((unsigned)T >= (unsigned)tl.ntiles) continue;  // workgroup-uniform; never taken (wt < parts x count)
+    const int T = all ? P : it == 0 ? T0 : pre ? s_tn[b] : ck.touched[P];
+    if ((unsigned)T >= (unsigned)tl.ntiles) continue;  // workgroup-uniform; never taken (P < count)
     int ti, tj, tk;
     ftile_decode(tl, T, ti, tj, tk);
     if (SLAB && pass != 0 && slab_tile_in_window(sw, ti) != (pass == 1)) continue;  // workgroup-uniform
     if constexpr (!kAtomicGrid) {
-      if (wt == (int)blockIdx.x) stamp(3, 2);
+      if (it == 0) stamp(3, 2);
       // a tile k_fused appended (add_lower_tiles) has no record: "none" flag
       const bool tables = !pre || s_cov[54] != 0;  // workgroup-uniform
       if (tables) {
@@ -1451,7 +1487,7 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
         __syncthreads();
       }
     }
-    if (wt == (int)blockIdx.x) stamp(3, 3);
+    if (it == 0) stamp(3, 3);
     const int i = ti * kFT0 + l0, j = tj * kFT1 + l1, k = tk * kFT2 + l2;
     if ((unsigned)i < (unsigned)ng && (unsigned)j < (unsigned)ng && (unsigned)k < (unsigned)ng) {
       const size_t idx = ((size_t)i * ng + j) * ng + k;
@@ -1495,7 +1531,7 @@ __global__ __launch_bounds__(kGridT) __attribute__((amdgpu_waves_per_eu(7, 8))) 
           gvel[idx] = node_update(a, i, j, k, g, gs, bct);
       }
     }
-    if (wt == (int)blockIdx.x) stamp(3, 4);
+    if (it == 0) stamp(3, 4);
   }
   // the zeroing for the next launches, after the tiles: its stores are not
   // in front of any wait above

@@ -2082,7 +2082,8 @@ static GridBufs fold_grid_bufs(gsmpm_mpm* h, int wp, int r) {
 static int launch_grid_f(gsmpm_mpm* h, int wp, float dt, uint32_t mask, const GridBufs& gb, int* zc, int* zf,
                          hipStream_t st, const hipEvent_t* ev, const SlabWin* swp = nullptr) {
   const SlabWin sw = swp ? *swp : SlabWin{};
-  const dim3 grid(std::min(kGridParts * h->ftl.ntiles, 1024 * kGridParts));
+  // a multiple of 8 workgroups: grid_work's XCD grouping takes b % 8 as the XCD
+  const dim3 grid((std::min(kGridParts * h->ftl.ntiles, 1024 * kGridParts) + 7) / 8 * 8);
   if (swp)
     launch(ev, k_grid_f<true>, grid, dim3(kGridT), st, h->g, h->ftl, chunk_in_f(h, wp), gb.tbox, gb.slots, gb.gacc,
            h->gvel, (const BcTable*)h->dev_bc, grid_step(h, dt, mask), gb.esc_in, gb.esc_clear, zc, zf, sw);
