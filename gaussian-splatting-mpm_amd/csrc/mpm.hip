@@ -1772,10 +1772,9 @@ static int finish_binning(gsmpm_mpm* h, int c, hipStream_t st, const hipEvent_t*
 // the chunk's window slot (k_grid_f finds slots by tile chunk ranges); the
 // per-chunk state k_fused keeps between launches (stencil box, lane order)
 // is indexed by position.
-__global__ __launch_bounds__(1024) void k_chunk_order(const int4* __restrict__ chunk, const int* __restrict__ nchunk,
-                                                      int4* __restrict__ pchunk, int ncu) {
+__device__ __forceinline__ void order_by_size(const int4* __restrict__ chunk, int nch, int4* __restrict__ pchunk,
+                                              int ncu) {
   __shared__ int s_h[kChunk];  // chunks of kChunk - b particles, then the first rank of each
-  const int nch = *nchunk;
   for (int i = threadIdx.x; i < kChunk; i += blockDim.x) s_h[i] = 0;
   __syncthreads();
   for (int c = threadIdx.x; c < nch; c += blockDim.x) atomicAdd(&s_h[kChunk - chunk[c].z], 1);
@@ -1804,10 +1803,104 @@ __global__ __launch_bounds__(1024) void k_chunk_order(const int4* __restrict__ c
     pchunk[pos] = make_int4(r.x, r.y, r.z, r.w | 16 | (c << 5));
   }
 }
+__global__ __launch_bounds__(1024) void k_chunk_order(const int4* __restrict__ chunk, const int* __restrict__ nchunk,
+                                                      int4* __restrict__ pchunk, int ncu) {
+  order_by_size(chunk, *nchunk, pchunk, ncu);
+}
+// The same order made XCD-affine (round 6): k_fused's workgroup b runs on XCD
+// b % 8 (its grid is a multiple of 8), and k_grid_f updates touched tile P on
+// XCD (P / kGridGroup) % 8 (fused.h grid_work).  Here chunk c goes to a
+// position on the XCD that updates its tile, so the v_out box it stages was
+// stored from that XCD's L2 and its neighbour chunks' boxes share lines there.
+// Each XCD takes exactly its share of positions (cap: ceil or floor of nch /
+// 8, positions 0..nch-1 all filled): chunks past their XCD's share move to
+// XCDs short of theirs.  Within an XCD the size tiers of k_chunk_order, 32
+// positions (its CUs) a tier.  GSMPM_CHUNK_XCD=0: the size order alone (A/B).
+constexpr int kOrdMax = 4096;  // chunks the XCD order handles (one-round grids: <= 3 x 256 workgroups' worth)
+__global__ __launch_bounds__(1024) void k_chunk_order_xcd(const int4* __restrict__ chunk, const int* __restrict__ nchunk,
+                                                          const int* __restrict__ tpos, int ntiles,
+                                                          int4* __restrict__ pchunk, int ncu) {
+  __shared__ int s_h[8][kChunk];      // per XCD: chunks of kChunk - b particles, then the first rank of each
+  __shared__ unsigned char s_x[kOrdMax];
+  __shared__ unsigned short s_r[kOrdMax];
+  __shared__ int s_n[8], s_cap[8], s_def[9], s_ovf;
+  const int nch = *nchunk;
+  if (nch > kOrdMax) {  // more chunks than the tables hold: the size order alone
+    order_by_size(chunk, nch, pchunk, ncu);
+    return;
+  }
+  for (int i = threadIdx.x; i < 8 * kChunk; i += blockDim.x) (&s_h[0][0])[i] = 0;
+  if (threadIdx.x < 8) s_n[threadIdx.x] = 0;
+  if (threadIdx.x == 0) s_ovf = 0;
+  __syncthreads();
+  const int T = (nch + 7) / 8, rem = nch - 8 * (T - 1);  // XCD x takes T positions if x < rem, else T - 1
+  for (int c = threadIdx.x; c < nch; c += blockDim.x) {
+    const int t = chunk[c].x;
+    const int P = t < ntiles ? tpos[t] : -1;
+    const int x = P >= 0 ? (P / kGridGroup) & 7 : c & 7;
+    s_x[c] = (unsigned char)x;
+    s_r[c] = (unsigned short)atomicAdd(&s_n[x], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int d = 0;
+    for (int x = 0; x < 8; ++x) {
+      s_cap[x] = x < rem ? T : T - 1;
+      s_def[x] = d;
+      d += max(0, s_cap[x] - s_n[x]);
+    }
+    s_def[8] = d;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < nch; c += blockDim.x) {
+    if (s_r[c] >= s_cap[s_x[c]]) {  // past its XCD's share: to the next free place of an XCD short of its share
+      const int k = atomicAdd(&s_ovf, 1);
+      int x = 0;
+      while (x < 7 && s_def[x + 1] <= k) ++x;
+      s_x[c] = (unsigned char)x;
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < nch; c += blockDim.x) atomicAdd(&s_h[s_x[c]][kChunk - chunk[c].z], 1);
+  __syncthreads();
+  if (threadIdx.x < 8 * 64) {  // one wave per XCD: exclusive scan of its 256 bins, 4 a lane
+    const int x = threadIdx.x >> 6, l = threadIdx.x & 63;
+    int v[kChunk / 64], t = 0;
+#pragma unroll
+    for (int u = 0; u < kChunk / 64; ++u) {
+      v[u] = s_h[x][l * (kChunk / 64) + u];
+      t += v[u];
+    }
+    int o = wave_incl_scan(t) - t;
+#pragma unroll
+    for (int u = 0; u < kChunk / 64; ++u) {
+      s_h[x][l * (kChunk / 64) + u] = o;
+      o += v[u];
+    }
+  }
+  __syncthreads();
+  const int cpx = max(1, ncu / 8);  // CUs an XCD
+  for (int c = threadIdx.x; c < nch; c += blockDim.x) {
+    const int4 r = chunk[c];
+    const int x = s_x[c];
+    const int rank = atomicAdd(&s_h[x][kChunk - r.z], 1);
+    const int tier = rank / cpx, i = rank - tier * cpx, full = s_cap[x] / cpx;
+    const int j = tier * cpx + (((tier & 1) && tier < full) ? cpx - 1 - i : i);
+    pchunk[j * 8 + x] = make_int4(r.x, r.y, r.z, r.w | 16 | (c << 5));
+  }
+}
+#ifndef GSMPM_CHUNK_XCD
+#define GSMPM_CHUNK_XCD 1
+#endif
 static int order_chunks_f(gsmpm_mpm* h, int c, hipStream_t st) {
   if (!h->chunk_order) return GSMPM_OK;
-  launch(nullptr, k_chunk_order, dim3(1), dim3(1024), st, (const int4*)h->fchunk[c], (const int*)h->fnchunk[c],
-         h->fpchunk[c], h->ncu);
+  // the XCD form where k_fused's grid is a multiple of 8 and the chunks fit its LDS tables
+  if (GSMPM_CHUNK_XCD && kGridGroup > 0 && std::min(h->ftl.max_chunks, h->fused_wgs) % 8 == 0)
+    launch(nullptr, k_chunk_order_xcd, dim3(1), dim3(1024), st, (const int4*)h->fchunk[c], (const int*)h->fnchunk[c],
+           (const int*)h->ftpos[c], h->ftl.ntiles, h->fpchunk[c], h->ncu);
+  else
+    launch(nullptr, k_chunk_order, dim3(1), dim3(1024), st, (const int4*)h->fchunk[c], (const int*)h->fnchunk[c],
+           h->fpchunk[c], h->ncu);
   GSMPM_LAUNCH_CHECK();
   return GSMPM_OK;
 }
