@@ -1574,6 +1574,7 @@ struct gsmpm_mpm {
   // On for one resident round of workgroups (init); GSMPM_CHUNK_ORDER=0 / 1
   // forces tile order / the balanced order (A/B)
   bool chunk_order = true;
+  bool chunk_xcd_seq = false;             // multi-round grids: k_chunk_order_xcd_seq (XCD placement, tile order)
   int ncu = 256;                          // CUs of the device (the order's tier width)
   int4* fpchunk[2] = {nullptr, nullptr};  // [max_chunks] chunk records in that order (k_fused reads these)
   float* planes_alt = nullptr;            // the other particle-plane buffer: every binning permutes
@@ -1686,7 +1687,13 @@ static BinOut bin_out(gsmpm_mpm* h, int c) {
 static bool use_fused(const gsmpm_mpm* h) { return h->fused; }
 
 // the chunk records k_fused walks: the balanced order (k_chunk_order) or tile order
-static int4* fused_records(gsmpm_mpm* h, int c) { return h->chunk_order ? h->fpchunk[c] : h->fchunk[c]; }
+// the multi-round XCD placement (k_chunk_order_xcd_seq): its grid must be a multiple of 8
+static bool xcd_seq_on(const gsmpm_mpm* h) {
+  return !h->chunk_order && h->chunk_xcd_seq && std::min(h->ftl.max_chunks, h->fused_wgs) % 8 == 0;
+}
+static int4* fused_records(gsmpm_mpm* h, int c) {
+  return (h->chunk_order || xcd_seq_on(h)) ? h->fpchunk[c] : h->fchunk[c];
+}
 static ChunkIn chunk_in_f(gsmpm_mpm* h, int c) {
   ChunkIn ci{h->fcount[c], h->fcbase[c], fused_records(h, c), h->fnchunk[c], h->flist[c], h->ftouched[c]};
   if (h->cover_records) {
@@ -1889,11 +1896,113 @@ __global__ __launch_bounds__(1024) void k_chunk_order_xcd(const int4* __restrict
     pchunk[j * 8 + x] = make_int4(r.x, r.y, r.z, r.w | 16 | (c << 5));
   }
 }
+// Multi-round grids (bicycle's 1M: ~30,000 chunks over 6 rounds): no size
+// tiers (later rounds are placed as CUs free up), only the XCD: each XCD's
+// chunks in tile order at positions 8 j + x, so a round's workgroups on one
+// XCD take consecutive groups of its tiles; the same equal shares as above.
+// One workgroup, each lane a contiguous run of chunks; block scans of the 8
+// per-XCD counts give every chunk its rank.
+__device__ __forceinline__ void block_scan_n(int (&v)[8], int (&o)[8], int (&tot)[8], int nv) {
+  __shared__ int s_ws[8][16];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int r = 0; r < nv; ++r) {
+    const int inc = wave_incl_scan(v[r]);
+    if (lane == 63) s_ws[r][wave] = inc;
+    o[r] = inc - v[r];
+  }
+  __syncthreads();
+  for (int r = 0; r < nv; ++r) {
+    tot[r] = 0;
+    for (int w = 0; w < nw; ++w) {
+      if (w < wave) o[r] += s_ws[r][w];
+      tot[r] += s_ws[r][w];
+    }
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ int chunk_xcd(const int4* __restrict__ chunk, const int* __restrict__ tpos, int ntiles, int c) {
+  const int t = chunk[c].x;
+  const int P = t < ntiles ? tpos[t] : -1;
+  return P >= 0 ? (P / kGridGroup) & 7 : c & 7;
+}
+__global__ __launch_bounds__(1024) void k_chunk_order_xcd_seq(const int4* __restrict__ chunk,
+                                                              const int* __restrict__ nchunk,
+                                                              const int* __restrict__ tpos, int ntiles,
+                                                              int4* __restrict__ pchunk) {
+  __shared__ int s_def[9], s_n[8];
+  const int nch = *nchunk;
+  const int S = (nch + (int)blockDim.x - 1) / (int)blockDim.x;
+  const int c0 = min(nch, (int)threadIdx.x * S), c1 = min(nch, c0 + S);
+  int v[8], o[8], tot[8];
+#pragma unroll
+  for (int x = 0; x < 8; ++x) v[x] = 0;
+  for (int c = c0; c < c1; ++c) {
+    const int x = chunk_xcd(chunk, tpos, ntiles, c);
+#pragma unroll
+    for (int y = 0; y < 8; ++y) v[y] += x == y;
+  }
+  block_scan_n(v, o, tot, 8);
+  const int T = (nch + 7) / 8, rem = nch - 8 * (T - 1);
+  int cap[8];
+#pragma unroll
+  for (int x = 0; x < 8; ++x) cap[x] = x < rem ? T : T - 1;
+  if (threadIdx.x == 0) {
+    int d = 0;
+    for (int x = 0; x < 8; ++x) {
+      s_def[x] = d;
+      s_n[x] = tot[x];
+      d += max(0, cap[x] - tot[x]);
+    }
+    s_def[8] = d;
+  }
+  // overflow chunks (past their XCD's share) of this lane's run, in tile order
+  int ov[8] = {0, 0, 0, 0, 0, 0, 0, 0}, oo[8], ot[8];
+  {
+    int r[8];
+#pragma unroll
+    for (int x = 0; x < 8; ++x) r[x] = o[x];
+    for (int c = c0; c < c1; ++c) {
+      const int x = chunk_xcd(chunk, tpos, ntiles, c);
+      int rk = 0;
+#pragma unroll
+      for (int y = 0; y < 8; ++y)
+        if (x == y) rk = r[y]++;
+      ov[0] += rk >= cap[x];
+    }
+  }
+  block_scan_n(ov, oo, ot, 1);  // (also orders s_def / s_n before their reads)
+  int k = oo[0];
+  for (int c = c0; c < c1; ++c) {
+    const int x = chunk_xcd(chunk, tpos, ntiles, c);
+    int rk = 0;
+#pragma unroll
+    for (int y = 0; y < 8; ++y)
+      if (x == y) rk = o[y]++;
+    int px = x, pr = rk;
+    if (rk >= cap[x]) {  // the k-th overflow chunk: the next free rank of an XCD short of its share
+      int y = 0;
+      while (y < 7 && s_def[y + 1] <= k) ++y;
+      px = y;
+      pr = s_n[y] + (k - s_def[y]);
+      ++k;
+    }
+    const int4 rc = chunk[c];
+    pchunk[pr * 8 + px] = make_int4(rc.x, rc.y, rc.z, rc.w | 16 | (c << 5));
+  }
+}
 #ifndef GSMPM_CHUNK_XCD
 #define GSMPM_CHUNK_XCD 1
 #endif
 static int order_chunks_f(gsmpm_mpm* h, int c, hipStream_t st) {
-  if (!h->chunk_order) return GSMPM_OK;
+  if (!h->chunk_order) {
+    // multi-round grids: the XCD placement alone (tile order within each XCD)
+    if (xcd_seq_on(h)) {
+      launch(nullptr, k_chunk_order_xcd_seq, dim3(1), dim3(1024), st, (const int4*)h->fchunk[c],
+             (const int*)h->fnchunk[c], (const int*)h->ftpos[c], h->ftl.ntiles, h->fpchunk[c]);
+      GSMPM_LAUNCH_CHECK();
+    }
+    return GSMPM_OK;
+  }
   // the XCD form where k_fused's grid is a multiple of 8 and the chunks fit its LDS tables
   if (GSMPM_CHUNK_XCD && kGridGroup > 0 && std::min(h->ftl.max_chunks, h->fused_wgs) % 8 == 0)
     launch(nullptr, k_chunk_order_xcd, dim3(1), dim3(1024), st, (const int4*)h->fchunk[c], (const int*)h->fnchunk[c],
@@ -2629,9 +2738,11 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
       // (later rounds are placed as CUs free up, not by position): lego and B'
       // gain, bicycle's 5 rounds lost 1 % (profiles/r06/ab_chunk_order_r06n.txt)
       h->chunk_order = rounds == 1;
+      h->chunk_xcd_seq = rounds > 1 && GSMPM_CHUNK_XCD && kGridGroup > 0 && h->fused_wgs % 8 == 0;
     }
     if (const char* fw = std::getenv("GSMPM_FUSED_WGS")) h->fused_wgs = std::max(1, std::atoi(fw));
     if (const char* co = std::getenv("GSMPM_CHUNK_ORDER")) h->chunk_order = co[0] != '0';
+    if (h->chunk_order) h->chunk_xcd_seq = false;
   }
   h->ftl.td0 = (h->g.ng + kFT0 - 1) / kFT0;
   h->ftl.td1 = (h->g.ng + kFT1 - 1) / kFT1;

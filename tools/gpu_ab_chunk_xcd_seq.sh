@@ -1,0 +1,9 @@
+# Multi-round XCD placement of chunks (k_chunk_order_xcd_seq, bicycle D): the
+# config/slab/mpm tests on the new default, then an interleaved A/B against
+# GSMPM_CHUNK_XCD=0 (cx0) on D, B' and B.
+set -o pipefail
+O=gpurun_out/${1:-r06cxs}; mkdir -p $O
+timeout -k 10 700 python3 -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_configs.py tests/test_gpu_slab.py tests/test_gpu_mpm.py > $O/tests.txt 2>&1 || { tail -30 $O/tests.txt; exit 1; }
+tail -1 $O/tests.txt
+VARIANTS="base cx0" CONFIGS="D Bp B" REPS=2 bash tools/ab_libs_multi.sh $O/ab > $O/ab.txt 2>&1 || { tail -5 $O/ab.txt; exit 1; }
+cat $O/ab.txt
