@@ -1993,6 +1993,14 @@ __global__ __launch_bounds__(1024) void k_chunk_order_xcd_seq(const int4* __rest
 #ifndef GSMPM_CHUNK_XCD
 #define GSMPM_CHUNK_XCD 1
 #endif
+// GSMPM_CHUNK_XCD_SEQ=1 (A/B, off): the multi-round placement above.  Measured
+// on bicycle D (profiles/r06/ab_chunk_xcd_seq_r06z.txt): k_fused unchanged
+// (98.2 against 98.5 us) and the frame 1.3 % slower -- the one-workgroup
+// ordering pass over ~30,000 chunks at every re-binning costs more than the
+// placement returns -- so multi-round grids keep the tile order.
+#ifndef GSMPM_CHUNK_XCD_SEQ
+#define GSMPM_CHUNK_XCD_SEQ 0
+#endif
 static int order_chunks_f(gsmpm_mpm* h, int c, hipStream_t st) {
   if (!h->chunk_order) {
     // multi-round grids: the XCD placement alone (tile order within each XCD)
@@ -2738,7 +2746,7 @@ int gsmpm_mpm_create(const gsmpm_mpm_params* prm, gsmpm_mpm** out) {
       // (later rounds are placed as CUs free up, not by position): lego and B'
       // gain, bicycle's 5 rounds lost 1 % (profiles/r06/ab_chunk_order_r06n.txt)
       h->chunk_order = rounds == 1;
-      h->chunk_xcd_seq = rounds > 1 && GSMPM_CHUNK_XCD && kGridGroup > 0 && h->fused_wgs % 8 == 0;
+      h->chunk_xcd_seq = GSMPM_CHUNK_XCD_SEQ && rounds > 1 && GSMPM_CHUNK_XCD && kGridGroup > 0 && h->fused_wgs % 8 == 0;
     }
     if (const char* fw = std::getenv("GSMPM_FUSED_WGS")) h->fused_wgs = std::max(1, std::atoi(fw));
     if (const char* co = std::getenv("GSMPM_CHUNK_ORDER")) h->chunk_order = co[0] != '0';
