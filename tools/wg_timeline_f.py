@@ -59,6 +59,17 @@ same = {}
 for i in np.nonzero(ok)[0]:
     same.setdefault(int(cu[i]), []).append(int(i))
 print("  WG sets sharing a CU (sample):", list(same.values())[:8])
+# the SIMD of each workgroup's wave 0 (HW_ID simd_id [5:4]): are the three
+# workgroups of a CU starting on the same SIMD (small chunks' only wave
+# stacked on it) or spread?
+simd0 = (hw >> 4) & 3
+print("  wave-0 SIMD histogram (WGs with a chunk):", np.bincount(simd0[ok], minlength=4).tolist())
+tuples = {}
+for c_, idx in same.items():
+    if len(idx) == 3:
+        key = tuple(sorted(int(simd0[i]) for i in idx))
+        tuples[key] = tuples.get(key, 0) + 1
+print("  wave-0 SIMDs of the 3 WGs of a CU (count):", sorted(tuples.items(), key=lambda kv: -kv[1])[:8])
 # second-chunk WGs (grid-stride): count WGs whose end - start >> single chunk
 ms2 = sim.time_kernels(sa.substep_dt, masks[203], reps=20)
 print('time_kernels K/grid/bins', ms2)
